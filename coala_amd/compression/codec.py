@@ -1,0 +1,274 @@
+"""Update codec over state_dicts: flatten -> HIP encode -> picklable carrier -> HIP decode -> module.
+
+This is the host-side mirror of what COALA's empty compression package would provide
+(/root/reference/coala/compression/__init__.py is 0 bytes). What the reference DOES pin, and this module
+honours:
+  * the carrier is whatever object the hook leaves in `self.model`; the reference deep-copies it and
+    pickles it into UploadContent.data (/root/reference/coala/client/base.py:363,
+    /root/reference/coala/protocol/codec.py:4-9), so CompressedUpdate pickles to a compact blob;
+  * the server hands the decoded object to FedAvg, which iterates `state_dict()` of full modules
+    including int64 `num_batches_tracked` buffers (/root/reference/coala/server/strategies.py:57-90),
+    so decode returns a full nn.Module; non-fp32 entries travel raw (passthrough);
+  * `calculate_model_size` calls `.parameters()` on whatever is in `self.model`
+    (/root/reference/coala/client/base.py:155,474-487), so the carrier has a parameters() that reports
+    its real payload size.
+"""
+import copy
+import math
+import threading
+from collections import OrderedDict
+
+import numpy as np
+import torch
+from torch import nn
+
+from . import wire
+from .plan import CodecPlan, Encoded
+from .spec import ALIGN, RAW_BITS, VALID_BITS, align_up
+
+MODES = ("delta", "weights")
+
+
+class HipBackend:
+    """Default backend: hand-written HIP kernels behind the C ABI (coala_amd/csrc/coalac.hip)."""
+
+    name = "hip"
+
+    def make_plan(self, sizes, ratio, bits, device):
+        if device.type != "cuda":
+            raise RuntimeError(f"the HIP codec runs on GPU tensors only; got tensors on {device} "
+                               "(there is no CPU fallback)")
+        return CodecPlan(sizes, ratio, bits, clients=1, device=device)
+
+
+class FlatState:
+    """A state_dict split into one aligned flat fp32 buffer (segments) plus raw passthrough entries."""
+
+    def __init__(self, entries, flat, raw):
+        self.entries = entries  # list of dicts: name, dtype, shape, kind, (seg, off, n) | ()
+        self.flat = flat        # fp32 [span] on device (None if no fp32 entry)
+        self.raw = raw          # OrderedDict name -> tensor
+
+
+def layout_of(state):
+    """[(name, dtype str, shape)] of a state_dict — what must match between encoder and decoder."""
+    return [(k, str(v.dtype).replace("torch.", ""), tuple(v.shape)) for k, v in state.items()]
+
+
+def flatten_state(state, device=None):
+    """state_dict -> FlatState with every fp32 entry at an ALIGN-aligned offset of one flat buffer.
+
+    One torch.cat over the tensors and zero pads (a single device copy kernel), not one copy per entry.
+    """
+    entries, parts, raw = [], [], OrderedDict()
+    off = seg = 0
+    pad_src = None
+    for name, t in state.items():
+        e = {"name": name, "dtype": str(t.dtype).replace("torch.", ""), "shape": list(t.shape)}
+        if t.dtype == torch.float32 and t.numel() > 0:
+            if device is None:
+                device = t.device
+            n = t.numel()
+            e.update(kind="seg", seg=seg, off=off, n=n)
+            parts.append(t.detach().reshape(-1).to(device))
+            pad = align_up(off + n) - (off + n)
+            if pad:
+                if pad_src is None:
+                    pad_src = torch.zeros(ALIGN, dtype=torch.float32, device=device)
+                parts.append(pad_src[:pad])
+            off += n + pad
+            seg += 1
+        else:
+            e.update(kind="raw")
+            raw[name] = t.detach().clone()
+        entries.append(e)
+    flat = torch.cat(parts) if parts else None
+    return FlatState(entries, flat, raw)
+
+
+class CompressedUpdate:
+    """Picklable carrier of one compressed client update (what `compression()` leaves in self.model).
+
+    Holds the encoded buffers (device tensors right after encode; CPU tensors after unpickling) and the
+    raw passthrough entries. Pickles to the COALAQ1 blob (wire.py).
+    """
+
+    def __init__(self, header, encoded, raw):
+        self.header = header
+        self.encoded = encoded
+        self.raw = raw
+
+    # -- size accounting (client/base.py:155, 474-487) -------------------------------------------
+    @property
+    def nbytes(self):
+        h = self.header
+        vb = 4 if h["bits"] == RAW_BITS else 1
+        raw_b = sum(t.numel() * t.element_size() for t in self.raw.values())
+        return 8 * h["n_segments"] + (4 + vb) * h["total_k"] + raw_b
+
+    def parameters(self):
+        """One meta tensor whose numel * 32 bit equals the payload size, so the reference's
+        calculate_model_size reports the real upload size even without the plugin's override."""
+        yield torch.empty(int(math.ceil(self.nbytes / 4)), device="meta")
+
+    # -- wire -------------------------------------------------------------------------------------
+    def to_bytes(self):
+        h = dict(self.header)
+        raw_entries, chunks, pos = [], [], 0
+        for e in h["entries"]:
+            if e["kind"] == "raw":
+                b = self.raw[e["name"]].cpu().contiguous().view(torch.uint8).numpy().tobytes() \
+                    if self.raw[e["name"]].numel() else b""
+                e = dict(e, off=pos, nbytes=len(b))
+                chunks.append(b)
+                pos += len(b)
+            raw_entries.append(e)
+        h["entries"] = raw_entries
+        enc = self.encoded
+        return wire.pack(h, enc.mn.cpu().numpy(), enc.scale.cpu().numpy(), enc.idx.cpu().numpy(),
+                         enc.vals.cpu().numpy(), b"".join(chunks))
+
+    @classmethod
+    def from_bytes(cls, blob):
+        h, mn, scale, idx, vals, rawb = wire.unpack(blob)
+        raw = OrderedDict()
+        for e in h["entries"]:
+            if e["kind"] == "raw":
+                dt = getattr(torch, e["dtype"])
+                buf = bytearray(rawb[e["off"]:e["off"] + e["nbytes"]])
+                t = torch.frombuffer(buf, dtype=dt) if buf else torch.empty(0, dtype=dt)
+                raw[e["name"]] = t.reshape(e["shape"]).clone()
+        enc = Encoded(torch.from_numpy(idx.copy()), torch.from_numpy(vals.copy()),
+                      torch.from_numpy(mn.copy()), torch.from_numpy(scale.copy()))
+        return cls(h, enc, raw)
+
+    def __getstate__(self):
+        return {"blob": self.to_bytes()}
+
+    def __setstate__(self, state):
+        other = CompressedUpdate.from_bytes(state["blob"])
+        self.__dict__.update(other.__dict__)
+
+    def __repr__(self):
+        h = self.header
+        return (f"CompressedUpdate(mode={h['mode']}, ratio={h['ratio']}, bits={h['bits']}, "
+                f"segments={h['n_segments']}, kept={h['total_k']}, bytes={self.nbytes})")
+
+
+class UpdateCodec:
+    """Encode / decode model updates with CodecSpec v1.
+
+    Args:
+        ratio: top-k ratio per tensor, (0, 1].
+        bits:  1..8 -> uint8 min/max codes; 32 -> raw fp32 values (lossless at ratio 1).
+        mode:  "delta" encodes w_local - w_global (decode adds w_global back, fused in the kernel);
+               "weights" encodes the weights themselves.
+        backend: object with make_plan(sizes, ratio, bits, device); default HipBackend.
+    """
+
+    def __init__(self, ratio=0.01, bits=8, mode="delta", backend=None):
+        if not (0.0 < float(ratio) <= 1.0):
+            raise ValueError(f"ratio must be in (0, 1], got {ratio}")
+        if bits not in VALID_BITS:
+            raise ValueError(f"bits must be one of {VALID_BITS}, got {bits}")
+        if mode not in MODES:
+            raise ValueError(f"mode must be one of {MODES}, got {mode}")
+        self.ratio, self.bits, self.mode = float(ratio), int(bits), mode
+        self.backend = backend if backend is not None else HipBackend()
+        self._plans = {}
+        self._lock = threading.Lock()
+
+    def plan_for(self, sizes, device, ratio=None, bits=None):
+        ratio = self.ratio if ratio is None else float(ratio)
+        bits = self.bits if bits is None else int(bits)
+        key = (tuple(sizes), ratio, bits, str(device))
+        with self._lock:
+            p = self._plans.get(key)
+            if p is None:
+                p = self.backend.make_plan(list(sizes), ratio, bits, device)
+                self._plans[key] = p
+        return p
+
+    # -- encode -----------------------------------------------------------------------------------
+    def encode(self, state, base=None):
+        """state_dict -> CompressedUpdate. `base` (delta mode): FlatState of w_global (same layout)."""
+        fs = flatten_state(state)
+        if self.mode == "delta" and base is None:
+            raise ValueError("delta mode needs the global-model snapshot (base)")
+        sizes = [e["n"] for e in fs.entries if e["kind"] == "seg"]
+        header = {"ratio": self.ratio, "bits": self.bits, "mode": self.mode, "n_segments": len(sizes),
+                  "entries": fs.entries}
+        if fs.flat is None:
+            header["total_k"] = 0
+            z = torch.zeros(0)
+            return CompressedUpdate(header, Encoded(z.int(), z.to(torch.uint8), z, z), fs.raw)
+        base_flat = None
+        if self.mode == "delta":
+            _check_same_layout(fs.entries, base.entries)
+            base_flat = base.flat
+        plan = self.plan_for(sizes, fs.flat.device)
+        enc = plan.encode(fs.flat, base=base_flat)
+        header["total_k"] = int(plan.table.total_k)
+        return CompressedUpdate(header, enc, fs.raw)
+
+    def snapshot(self, module_or_state):
+        """FlatState of a model (the w_global snapshot for delta mode)."""
+        state = module_or_state.state_dict() if isinstance(module_or_state, nn.Module) else module_or_state
+        return flatten_state(state)
+
+    # -- decode -----------------------------------------------------------------------------------
+    def decode_state(self, update, base=None, device=None):
+        """CompressedUpdate -> OrderedDict state (fp32 entries are views into one fresh flat buffer)."""
+        h = update.header  # self-describing: decode with the blob's own ratio/bits/mode
+        sizes = [e["n"] for e in h["entries"] if e["kind"] == "seg"]
+        state = OrderedDict()
+        flat = None
+        if sizes:
+            if h["mode"] == "delta":
+                if base is None:
+                    raise ValueError("delta-mode update needs the global model (base) to decode")
+                _check_same_layout(h["entries"], base.entries)
+                device = base.flat.device
+            elif device is None:
+                device = torch.device("cuda", torch.cuda.current_device())
+            plan = self.plan_for(sizes, device, ratio=h["ratio"], bits=h["bits"])
+            enc = update.encoded.to(device, non_blocking=True)
+            flat = plan.decode(enc, base=base.flat if h["mode"] == "delta" else None)
+        for e in h["entries"]:
+            if e["kind"] == "seg":
+                state[e["name"]] = flat[e["off"]:e["off"] + e["n"]].view(e["shape"])
+            else:
+                t = update.raw[e["name"]]
+                state[e["name"]] = t.to(device) if device is not None else t
+        return state
+
+    def decode_module(self, update, template, base=None):
+        """CompressedUpdate -> new nn.Module shaped like `template` holding the decoded state.
+
+        No parameter data is copied: the new module's parameters/buffers are views into the decode
+        output (deepcopy with a memo that pre-binds every tensor). `template` is never aliased.
+        """
+        state = self.decode_state(update, base=base)
+        return module_with_state(template, state)
+
+
+def module_with_state(template, state):
+    memo = {}
+    for name, p in template.named_parameters():
+        if name in state:
+            memo[id(p)] = nn.Parameter(state[name], requires_grad=p.requires_grad)
+    for name, b in template.named_buffers():
+        if name in state and b is not None:
+            memo[id(b)] = state[name]
+    return copy.deepcopy(template, memo)
+
+
+def _check_same_layout(entries, base_entries):
+    a = [(e["name"], e["dtype"], tuple(e["shape"])) for e in entries]
+    b = [(e["name"], e["dtype"], tuple(e["shape"])) for e in base_entries]
+    if a != b:
+        raise ValueError("update and base model have different state_dict layouts")
+
+
+def as_numpy(t):
+    return t.detach().cpu().numpy() if isinstance(t, torch.Tensor) else np.asarray(t)

@@ -1,0 +1,183 @@
+"""Device-side codec plan: one segment table (a model layout × clients) bound to one GPU.
+
+Thin typed wrapper over coalac_plan_create / coalac_encode / coalac_decode. Tensors are torch tensors
+used purely as device memory; streams are torch's current HIP stream unless one is passed. Every
+argument is checked against what the kernels assume (dtype, device, contiguity, length, 16-B
+alignment) BEFORE a launch.
+"""
+import ctypes
+from dataclasses import dataclass
+
+import torch
+
+from . import _lib
+from .spec import RAW_BITS, VALID_BITS, SegmentTable
+
+
+@dataclass
+class Encoded:
+    """Device buffers of one encode: idx int32[K], vals uint8[K] (fp32[K] when bits == 32),
+    mn fp32[T], scale fp32[T]."""
+    idx: torch.Tensor
+    vals: torch.Tensor
+    mn: torch.Tensor
+    scale: torch.Tensor
+
+    def to(self, device, non_blocking=False):
+        return Encoded(*(t.to(device, non_blocking=non_blocking) for t in (self.idx, self.vals, self.mn, self.scale)))
+
+
+def _ptr(t):
+    return ctypes.c_void_p(t.data_ptr()) if t is not None else ctypes.c_void_p(0)
+
+
+def _stream_handle(stream):
+    s = torch.cuda.current_stream() if stream is None else stream
+    return ctypes.c_void_p(s.cuda_stream)
+
+
+class CodecPlan:
+    """Plan for `clients` copies of a layout given by fp32 segment sizes.
+
+    Args:
+        sizes: element count of every fp32 segment of ONE client, in state_dict order.
+        ratio: top-k ratio in (0, 1].
+        bits:  1..8 (uint8 codes) or 32 (raw fp32 values).
+        clients: number of client updates batched into one launch sequence.
+        device: CUDA/HIP device (default: current).
+    """
+
+    def __init__(self, sizes, ratio, bits=8, clients=1, device=None):
+        if bits not in VALID_BITS:
+            raise ValueError(f"bits must be one of {VALID_BITS}, got {bits}")
+        self.table = SegmentTable(sizes, ratio, clients)
+        self.bits = int(bits)
+        self.device = torch.device("cuda", torch.cuda.current_device() if device is None
+                                   else torch.device(device).index or 0)
+        self._lib = _lib.load()
+        segs = self.table.segs
+        arr = (_lib.SegDesc * len(segs))()
+        for i, (a, b, c, d) in enumerate(segs.tolist()):
+            arr[i] = _lib.SegDesc(a, b, c, d)
+        h = ctypes.c_void_p()
+        with torch.cuda.device(self.device):
+            _lib.check(self._lib.coalac_plan_create(arr, len(segs), self.bits, ctypes.byref(h)),
+                       "coalac_plan_create")
+        self._h = h
+        ws, tk, span, nu = (ctypes.c_uint64() for _ in range(4))
+        _lib.check(self._lib.coalac_plan_query(h, ctypes.byref(ws), ctypes.byref(tk), ctypes.byref(span),
+                                               ctypes.byref(nu)), "coalac_plan_query")
+        self.ws_bytes, self.total_k, self.span, self.n_units = ws.value, tk.value, span.value, nu.value
+        if self.total_k != self.table.total_k:
+            raise _lib.CodecError(f"plan total_k {self.total_k} != table {self.table.total_k}")
+
+    # -- lifetime ---------------------------------------------------------------------------------
+    def close(self):
+        h, self._h = getattr(self, "_h", None), None
+        if h is not None and h.value:
+            with torch.cuda.device(self.device):
+                self._lib.coalac_plan_destroy(h)
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # -- buffers ----------------------------------------------------------------------------------
+    @property
+    def n_segments(self):
+        return self.table.n_segments
+
+    @property
+    def vals_dtype(self):
+        return torch.float32 if self.bits == RAW_BITS else torch.uint8
+
+    def empty_flat(self):
+        return torch.empty(self.span, dtype=torch.float32, device=self.device)
+
+    def empty_encoded(self):
+        d = self.device
+        return Encoded(torch.empty(self.total_k, dtype=torch.int32, device=d),
+                       torch.empty(self.total_k, dtype=self.vals_dtype, device=d),
+                       torch.empty(self.n_segments, dtype=torch.float32, device=d),
+                       torch.empty(self.n_segments, dtype=torch.float32, device=d))
+
+    def empty_workspace(self):
+        return torch.empty(self.ws_bytes, dtype=torch.uint8, device=self.device)
+
+    # -- checks -----------------------------------------------------------------------------------
+    def _check_flat(self, t, name):
+        if t is None:
+            return
+        if t.device != self.device or t.dtype != torch.float32 or not t.is_contiguous():
+            raise ValueError(f"{name}: need a contiguous float32 tensor on {self.device}, got "
+                             f"{t.dtype} on {t.device} (contiguous={t.is_contiguous()})")
+        if t.numel() < self.span:
+            raise ValueError(f"{name}: {t.numel()} elements < plan span {self.span}")
+        if t.data_ptr() % 16:
+            raise ValueError(f"{name}: storage must be 16-byte aligned")
+
+    def _check_encoded(self, e):
+        want = ((e.idx, torch.int32, self.total_k), (e.vals, self.vals_dtype, self.total_k),
+                (e.mn, torch.float32, self.n_segments), (e.scale, torch.float32, self.n_segments))
+        for t, dt, n in want:
+            if t.device != self.device or t.dtype != dt or not t.is_contiguous() or t.numel() < n:
+                raise ValueError(f"encoded buffer mismatch: need {dt}[{n}] on {self.device}, got "
+                                 f"{t.dtype}[{t.numel()}] on {t.device}")
+
+    # -- codec ------------------------------------------------------------------------------------
+    def encode(self, flat, base=None, out=None, workspace=None, flags=0, stream=None, events=None):
+        """Encode flat (fp32[span]) [- base] -> Encoded. Asynchronous on `stream`."""
+        self._check_flat(flat, "input")
+        self._check_flat(base, "base")
+        out = self.empty_encoded() if out is None else out
+        self._check_encoded(out)
+        ws = self.empty_workspace() if workspace is None else workspace
+        if ws.device != self.device or ws.numel() * ws.element_size() < self.ws_bytes:
+            raise ValueError(f"workspace: need {self.ws_bytes} bytes on {self.device}")
+        args = (self._h, _ptr(flat), _ptr(base), _ptr(out.idx), _ptr(out.vals), _ptr(out.mn),
+                _ptr(out.scale), _ptr(ws), ctypes.c_uint64(self.ws_bytes), ctypes.c_uint(flags),
+                _stream_handle(stream))
+        with torch.cuda.device(self.device):
+            if events is None:
+                rc = self._lib.coalac_encode(*args)
+            else:
+                rc = self._lib.coalac_encode_ev(*args, _event_array(events, 5))
+        _lib.check(rc, "coalac_encode")
+        return out
+
+    def decode(self, enc, base=None, out=None, stream=None, events=None):
+        """Decode Encoded -> dense flat fp32[span] (+ base, fused). Asynchronous on `stream`."""
+        self._check_encoded(enc)
+        self._check_flat(base, "base")
+        if out is None:
+            out = self.empty_flat() if base is None else torch.empty_like(base)
+        self._check_flat(out, "output")
+        args = (self._h, _ptr(enc.idx), _ptr(enc.vals), _ptr(enc.mn), _ptr(enc.scale), _ptr(base), _ptr(out),
+                _stream_handle(stream))
+        with torch.cuda.device(self.device):
+            if events is None:
+                rc = self._lib.coalac_decode(*args)
+            else:
+                rc = self._lib.coalac_decode_ev(*args, _event_array(events, 2))
+        _lib.check(rc, "coalac_decode")
+        return out
+
+    def fallbacks(self, workspace, stream=None):
+        """Segments of the last encode with this workspace whose sampled bracket missed (synchronises)."""
+        c = ctypes.c_int()
+        with torch.cuda.device(self.device):
+            _lib.check(self._lib.coalac_workspace_fallbacks(self._h, _ptr(workspace), _stream_handle(stream),
+                                                            ctypes.byref(c)), "coalac_workspace_fallbacks")
+        return c.value
+
+
+def _event_array(events, n):
+    """torch.cuda.Event list -> void*[n] of hipEvent_t (events must have been recorded once or be
+    created with enable_timing; torch creates the HIP event lazily on first record)."""
+    arr = (ctypes.c_void_p * n)()
+    for i, e in enumerate(events[:n]):
+        if e is not None:
+            arr[i] = ctypes.c_void_p(e.cuda_event)
+    return arr

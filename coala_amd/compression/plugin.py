@@ -1,0 +1,115 @@
+"""COALA compression plugin surface: client/server hook mixins with the reference's exact signatures.
+
+The reference exposes compression only as no-op hooks that users override in subclasses
+(/root/reference/docs/en/tutorials/customize_server_and_client.md:57-58,72-73,168-169):
+
+    BaseClient.decompression(self) -> None          coala/client/base.py:203-205   (called :141)
+    BaseClient.compression(self) -> None            coala/client/base.py:330-332   (called :153)
+    BaseServer.compression(self) -> None            coala/server/base.py:347-349   (called :196)
+    BaseServer.decompression(self, model) -> model  coala/server/base.py:558-560   (called :376,
+                                                    server/service.py:106,125)
+
+Usage (drop-in, nothing else in COALA changes):
+
+    from coala.client import BaseClient
+    from coala_amd.compression import CompressionClientMixin, CompressionServerMixin
+    class Client(CompressionClientMixin, BaseClient): pass
+    class Server(CompressionServerMixin, BaseServer): pass
+    coala.register_client(Client); coala.register_server(Server)   # coordinator.py:519-536
+
+Behaviour:
+  * client decompression(): runs right after set_model (base.py:138,141) — snapshots w_global for delta
+    mode; tolerates self.model being None (application/MAS/fl_client.py:23-26 pattern).
+  * client compression(): encodes the trained model (still on the training device, base.py:144-153) and
+    leaves a CompressedUpdate carrier in self.model, which construct_upload_request deep-copies and
+    pickles into UploadContent.data (base.py:363). post_upload() puts the trained module back so the
+    next round's set_model (base.py:197-201) works.
+  * calculate_model_size(): reports the real payload size for a carrier (base.py:155, 474-487).
+  * server decompression(model): CompressedUpdate -> a NEW nn.Module (never aliases self.model, which
+    aggregation overwrites, base.py:571) built on the pre-aggregation global model (delta mode: w_global
+    + decoded delta, fused in the decode kernel); anything else (plain modules, splitFL feature dicts,
+    server/service.py:124-131) passes through unchanged. Safe to call from several threads
+    (server/service.py:74 spawns one per upload).
+"""
+import threading
+
+from torch import nn
+
+from .codec import CompressedUpdate, UpdateCodec
+
+
+def _bit_to_megabyte(bits):
+    # same conversion as the reference tracker (coala/tracking/evaluation.py:16-17)
+    return bits / (8 * 1024 * 1024)
+
+
+class _CodecOwner:
+    codec_ratio = 0.01
+    codec_bits = 8
+    codec_mode = "delta"
+    codec_backend = None
+
+    def _codec(self):
+        c = self.__dict__.get("_update_codec")
+        if c is None:
+            c = UpdateCodec(self.codec_ratio, self.codec_bits, self.codec_mode, self.codec_backend)
+            self.__dict__["_update_codec"] = c
+        return c
+
+
+class CompressionClientMixin(_CodecOwner):
+    """Mix in before coala's BaseClient: `class Client(CompressionClientMixin, BaseClient)`."""
+
+    def decompression(self):
+        if getattr(self, "model", None) is None:
+            return
+        if isinstance(self.model, nn.Module) and self._codec().mode == "delta":
+            self._codec_base = self._codec().snapshot(self.model)
+
+    def compression(self):
+        model = getattr(self, "model", None)
+        if model is None or not isinstance(model, nn.Module):
+            return
+        codec = self._codec()
+        base = getattr(self, "_codec_base", None) if codec.mode == "delta" else None
+        update = codec.encode(model.state_dict(), base=base)
+        self._codec_trained_model = model
+        self.model = update
+
+    def post_upload(self):
+        trained = self.__dict__.pop("_codec_trained_model", None)
+        if trained is not None:
+            self.model = trained
+        parent = getattr(super(), "post_upload", None)
+        if parent is not None:
+            parent()
+
+    def calculate_model_size(self, model, param_size=32):
+        if isinstance(model, CompressedUpdate):
+            return _bit_to_megabyte(model.nbytes * 8)
+        parent = getattr(super(), "calculate_model_size", None)
+        if parent is not None:
+            return parent(model, param_size)
+        return _bit_to_megabyte(sum(p.numel() for p in model.parameters()) * param_size)
+
+
+class CompressionServerMixin(_CodecOwner):
+    """Mix in before coala's BaseServer: `class Server(CompressionServerMixin, BaseServer)`."""
+
+    def _global_snapshot(self):
+        """Flat fp32 copy of the current global model, rebuilt only when its tensors changed."""
+        lock = self.__dict__.setdefault("_codec_lock", threading.Lock())
+        with lock:
+            state = self.model.state_dict()
+            stamp = (id(self.model), tuple((id(t), t._version) for t in state.values()))
+            snap = self.__dict__.get("_codec_snapshot")
+            if snap is None or snap[0] != stamp:
+                snap = (stamp, self._codec().snapshot(state))
+                self.__dict__["_codec_snapshot"] = snap
+            return snap[1]
+
+    def decompression(self, model):
+        if isinstance(model, CompressedUpdate):
+            base = self._global_snapshot() if model.header["mode"] == "delta" else None
+            return self._codec().decode_module(model, self.model, base=base)
+        return model

@@ -1,0 +1,96 @@
+"""CodecSpec v1 host-side logic: kept-element counts and segment tables (no torch, no GPU).
+
+The spec itself is SURVEY.md §8(a) rows a3/a4; the kernels implementing it are coala_amd/csrc/coalac.hip.
+This module decides WHAT the kernels run on: one segment per fp32 state_dict entry, in the
+state_dict's insertion order (the order coala/server/strategies.py:57-90 iterates), laid out in one
+flat buffer with every segment start aligned to ALIGN elements (128 B), clients concatenated.
+"""
+import math
+
+import numpy as np
+
+ALIGN = 32          # elements; 128-byte aligned segment starts (float4 loads need >= 4)
+RAW_BITS = 32       # bits == 32: values stored as raw fp32 (lossless at ratio 1)
+VALID_BITS = tuple(range(1, 9)) + (RAW_BITS,)
+
+
+def k_for(n, ratio):
+    """Kept elements of a segment of n elements: max(1, min(n, ceil(n * ratio))), 0 for n == 0.
+
+    Computed in float64 on the host, as SURVEY.md §8(a) a3 specifies.
+    """
+    if not (ratio > 0.0):
+        raise ValueError(f"ratio must be > 0, got {ratio}")
+    n = int(n)
+    if n <= 0:
+        return 0
+    return max(1, min(n, int(math.ceil(float(n) * float(ratio)))))
+
+
+def align_up(x, a=ALIGN):
+    return (int(x) + a - 1) // a * a
+
+
+class SegmentTable:
+    """Segment table of `clients` copies of one layout (list of fp32 segment sizes).
+
+    segs: uint64 [clients * T, 4] rows (in_off, n, k, out_off) — the coalac_seg_t table.
+    span_per_client: flat elements per client (aligned); total_k_per_client: kept entries per client.
+    """
+
+    def __init__(self, sizes, ratio, clients=1, align=ALIGN):
+        self.sizes = [int(s) for s in sizes]
+        self.ratio = float(ratio)
+        self.clients = int(clients)
+        if self.clients < 1:
+            raise ValueError("clients must be >= 1")
+        offs, ks, oofs = [], [], []
+        off = oo = 0
+        for n in self.sizes:
+            offs.append(off)
+            k = k_for(n, ratio)
+            ks.append(k)
+            oofs.append(oo)
+            off = align_up(off + n, align)
+            oo += k
+        self.offsets = offs
+        self.ks = ks
+        self.out_offsets = oofs
+        self.span_per_client = max(off, align)
+        self.total_k_per_client = oo
+        T = len(self.sizes)
+        segs = np.zeros((self.clients * T, 4), dtype=np.uint64)
+        for c in range(self.clients):
+            for t in range(T):
+                segs[c * T + t] = (c * self.span_per_client + offs[t], self.sizes[t], ks[t],
+                                   c * self.total_k_per_client + oofs[t])
+        self.segs = segs
+
+    @property
+    def n_segments(self):
+        return len(self.segs)
+
+    @property
+    def span(self):
+        return self.clients * self.span_per_client
+
+    @property
+    def total_k(self):
+        return self.clients * self.total_k_per_client
+
+    @property
+    def n_elements(self):
+        return self.clients * sum(self.sizes)
+
+    def algorithmic_bytes(self, bits=8, delta=False):
+        """HBM bytes an ideal encode+decode moves: 8N + 10K + 32T for 8-bit codes.
+
+        Encode reads 4N, writes idx (4K) + codes (1K, or 4K raw) + mn/scale/k/off (16T); decode reads
+        those and writes 4N. Delta mode adds a 4N base read on each side.
+        """
+        N, K, T = self.n_elements, self.total_k, self.n_segments
+        vb = 4 if bits == RAW_BITS else 1
+        b = 8 * N + 2 * (4 + vb) * K + 32 * T
+        if delta:
+            b += 8 * N
+        return b

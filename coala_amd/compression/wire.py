@@ -1,0 +1,68 @@
+"""Self-describing wire format of a compressed update ("COALAQ1").
+
+The blob rides inside the pickled carrier that COALA puts into UploadContent.data
+(/root/reference/coala/client/base.py:363 -> protos/coala/pb/server_service.proto:13-24). It must be
+self-describing because remote clients never receive new config keys (OperateConfig has fixed fields,
+/root/reference/protos/coala/pb/client_service.proto:24-39).
+
+Layout (little-endian):
+    0   8B   magic b"COALAQ1\\0"
+    8   u32  format version (1)
+    12  u32  header length H
+    16  H    UTF-8 JSON header: ratio, bits, mode, n_segments, total_k, entries[]
+             entry = {"name", "dtype", "shape", "kind": "seg", "seg": i, "n", "k", "out_off"}
+                   | {"name", "dtype", "shape", "kind": "raw", "off", "nbytes"}
+    then, each section starting at a 16-byte boundary:
+         mn f32[T] | scale f32[T] | idx i32[K] | vals (u8[K], or f32[K] if bits == 32) | raw bytes
+"""
+import json
+import struct
+
+import numpy as np
+
+MAGIC = b"COALAQ1\0"
+VERSION = 1
+
+
+def _pad16(n):
+    return (16 - n % 16) % 16
+
+
+def pack(header, mn, scale, idx, vals, raw):
+    """numpy arrays + raw bytes -> blob (bytes)."""
+    h = json.dumps(header, separators=(",", ":"), sort_keys=True).encode()
+    parts = [MAGIC, struct.pack("<II", VERSION, len(h)), h]
+    size = 16 + len(h)
+    for arr in (np.ascontiguousarray(mn, "<f4"), np.ascontiguousarray(scale, "<f4"),
+                np.ascontiguousarray(idx, "<i4"), np.ascontiguousarray(vals)):
+        p = _pad16(size)
+        parts.append(b"\0" * p)
+        b = arr.tobytes()
+        parts.append(b)
+        size += p + len(b)
+    p = _pad16(size)
+    parts.append(b"\0" * p)
+    parts.append(bytes(raw))
+    return b"".join(parts)
+
+
+def unpack(blob):
+    """blob -> (header dict, mn, scale, idx, vals, raw bytes). Arrays are read-only views of blob."""
+    mv = memoryview(blob)
+    if bytes(mv[:8]) != MAGIC:
+        raise ValueError("not a COALAQ1 blob (bad magic)")
+    ver, hl = struct.unpack_from("<II", mv, 8)
+    if ver != VERSION:
+        raise ValueError(f"unsupported COALAQ1 version {ver}")
+    header = json.loads(bytes(mv[16:16 + hl]).decode())
+    T, K = int(header["n_segments"]), int(header["total_k"])
+    vdt = np.dtype("<f4") if int(header["bits"]) == 32 else np.dtype("u1")
+    pos = 16 + hl
+    out = []
+    for dt, n in ((np.dtype("<f4"), T), (np.dtype("<f4"), T), (np.dtype("<i4"), K), (vdt, K)):
+        pos += _pad16(pos)
+        out.append(np.frombuffer(mv, dtype=dt, count=n, offset=pos))
+        pos += n * dt.itemsize
+    pos += _pad16(pos)
+    raw = bytes(mv[pos:])
+    return (header, *out, raw)

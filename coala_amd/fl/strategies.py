@@ -1,0 +1,42 @@
+"""FedAvg over decoded modules — restatement of /root/reference/coala/server/strategies.py.
+
+federated_averaging: strategies.py:6-29 — weighted sum of EVERY state_dict entry (fp32 and int64
+buffers alike), then torch.div by the total weight (int64 entries become float, as in the reference).
+weighted_sum: strategies.py:57-90 — params *= w0, then += model_i[name] * w_i in client order.
+"""
+import copy
+
+import torch
+
+
+def weighted_sum(models, weights):
+    if not models or not weights:
+        return None, 0
+    total = sum(weights)
+    if total == 0:
+        weights = [1 for _ in models]
+    model = copy.deepcopy(models[0])
+    acc = copy.deepcopy(models[0].state_dict())
+    states = [dict(m.state_dict()) for m in models]
+    with torch.no_grad():
+        for name, params in acc.items():
+            params *= weights[0]
+            for i in range(1, len(models)):
+                params += states[i][name] * weights[i]
+            acc[name] = params
+    model.load_state_dict(acc)
+    return model, total
+
+
+def federated_averaging(models, weights):
+    if not models:
+        return None
+    if not weights or sum(weights) == 0:
+        weights = [1 for _ in models]
+    model, total = weighted_sum(models, weights)
+    state = model.state_dict()
+    with torch.no_grad():
+        for name, params in state.items():
+            state[name] = torch.div(params, total)
+    model.load_state_dict(state)
+    return model

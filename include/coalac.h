@@ -1,0 +1,110 @@
+/*
+ * coalac.h — C ABI of the MI355X (gfx950) model-update codec (CodecSpec v1: per-tensor top-k + 8-bit
+ * quantise). This is the drop-in boundary for COALA's compression plugin surface.
+ *
+ * The reference (SonyResearch/COALA) is 100 % Python and has NO codec and NO FFI: coala/compression/
+ * __init__.py is 0 bytes. The entry points below replace the work the reference's empty hooks would do:
+ *
+ *   coalac_encode  <- BaseClient.compression()          /root/reference/coala/client/base.py:330-332
+ *                     (called from run_train, base.py:153; its output rides in UploadContent.data via
+ *                      codec.marshal, base.py:363 / coala/protocol/codec.py:4-5)
+ *                     and BaseServer.compression()        /root/reference/coala/server/base.py:347-349
+ *   coalac_decode  <- BaseServer.decompression(model)   /root/reference/coala/server/base.py:558-560
+ *                     (called at server/base.py:376 and server/service.py:106,125)
+ *                     and BaseClient.decompression()      /root/reference/coala/client/base.py:203-205
+ *   coalac_plan_*  <- no counterpart: a tensor layout (segment table) is fixed for a whole FL task, so
+ *                     the device-side metadata is built once per layout and reused every round.
+ *
+ * Conventions
+ *   - Every d_* pointer is a DEVICE pointer owned by the caller (e.g. torch tensor storage).
+ *   - All work is enqueued on the caller's HIP stream (`stream`, a hipStream_t; NULL = default stream)
+ *     and returns immediately. No host synchronisation, no allocation inside encode/decode.
+ *   - Re-entrant: no global mutable state. A plan is immutable after creation and may be shared by
+ *     threads; each concurrent encode needs its own workspace.
+ *   - Errors: return value 0 = OK, negative = error code below; nothing throws across the ABI. The
+ *     message of the last failed call on the calling thread is in coalac_last_error().
+ */
+#ifndef COALAC_H
+#define COALAC_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define COALAC_ABI_VERSION 1
+
+enum {
+  COALAC_OK = 0,
+  COALAC_EINVAL = -1,      /* invalid argument (bad segment table, null pointer, misaligned offset) */
+  COALAC_EBITS = -2,       /* unsupported bit width (valid: 1..8, or 32 = raw fp32 values) */
+  COALAC_EWORKSPACE = -3,  /* workspace smaller than coalac_plan_query() says */
+  COALAC_EHIP = -4,        /* a HIP runtime call or kernel launch failed */
+  COALAC_EDEVICE = -5,     /* called with a different current device than the plan was created on */
+  COALAC_ENOMEM = -6       /* device allocation for the plan failed */
+};
+
+enum {
+  COALAC_FLAG_FORCE_EXACT = 1  /* test hook: take the exact (non-sampled) selection path everywhere */
+};
+
+/* One fp32 segment (= one flattened tensor of the state_dict). Offsets are in ELEMENTS.
+ *   in_off : start of the segment in the flat input / dense output buffer; must be a multiple of 4
+ *   n      : element count, 0 <= n < 2^31
+ *   k      : kept elements, 0 if n == 0 else 1 <= k <= n (host computes max(1, min(n, ceil(n*ratio))))
+ *   out_off: start of this segment's k entries in the idx / vals arrays                              */
+typedef struct coalac_seg {
+  uint64_t in_off;
+  uint64_t n;
+  uint64_t k;
+  uint64_t out_off;
+} coalac_seg_t;
+
+typedef struct coalac_plan* coalac_plan_t;
+
+int coalac_version(void);
+const char* coalac_last_error(void);
+
+/* Build the device metadata for a segment table (HOST pointer) on the current device.
+ * bits: 1..8 -> uint8 codes (vals is uint8_t[total_k]); 32 -> raw fp32 values (vals is float[total_k]). */
+int coalac_plan_create(const coalac_seg_t* h_segs, int nseg, int bits, coalac_plan_t* out);
+int coalac_plan_destroy(coalac_plan_t plan);
+
+/* ws_bytes: workspace coalac_encode needs; total_k: length of idx/vals; span: max(in_off + n) = the
+ * minimum length (elements) of the input/output flat buffers; n_units: 4096-element work units. */
+int coalac_plan_query(coalac_plan_t plan, uint64_t* ws_bytes, uint64_t* total_k, uint64_t* span,
+                      uint64_t* n_units);
+
+/* Encode d_in (fp32[span]) into idx (int32[total_k], segment-relative, ascending per segment),
+ * vals (uint8[total_k] codes or fp32[total_k]), mn (fp32[nseg]) and scale (fp32[nseg]).
+ * d_base != NULL selects delta mode: the codec encodes (d_in - d_base). */
+int coalac_encode(coalac_plan_t plan, const float* d_in, const float* d_base, int32_t* d_idx,
+                  void* d_vals, float* d_mn, float* d_scale, void* d_ws, uint64_t ws_bytes,
+                  unsigned flags, void* stream);
+
+/* Decode into the dense d_out (fp32[span]); only positions inside segments are written.
+ * d_base != NULL: d_out = d_base + decoded (fused; d_out may alias d_base). */
+int coalac_decode(coalac_plan_t plan, const int32_t* d_idx, const void* d_vals, const float* d_mn,
+                  const float* d_scale, const float* d_base, float* d_out, void* stream);
+
+/* Profiling variants: identical work, plus hipEventRecord(events[i], stream) between kernels.
+ * encode: events[0] before k_prep, [1] after k_prep, [2] after k_scan, [3] after k_select,
+ *         [4] after k_emit (recorded even if the plan has no large segment); decode: [0] before,
+ *         [1] after k_decode. NULL array or NULL entries are skipped. */
+int coalac_encode_ev(coalac_plan_t plan, const float* d_in, const float* d_base, int32_t* d_idx,
+                     void* d_vals, float* d_mn, float* d_scale, void* d_ws, uint64_t ws_bytes,
+                     unsigned flags, void* stream, void* const* events);
+int coalac_decode_ev(coalac_plan_t plan, const int32_t* d_idx, const void* d_vals, const float* d_mn,
+                     const float* d_scale, const float* d_base, float* d_out, void* stream,
+                     void* const* events);
+
+/* Diagnostics: number of segments whose sampled thresholds were rejected and re-selected exactly in
+ * the last encode that used workspace d_ws (synchronises `stream`). */
+int coalac_workspace_fallbacks(coalac_plan_t plan, const void* d_ws, void* stream, int* out);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* COALAC_H */

@@ -1,0 +1,37 @@
+"""Test-only codec backend that runs the CPU oracle behind the same plan interface as the HIP plan.
+
+Used by CPU tests (C1 plumbing, gloo sharding) to exercise the plugin/host logic without a GPU. The
+product never imports this (coala_amd has no CPU fallback); here the oracle is the checker.
+"""
+import numpy as np
+import torch
+
+from coala_amd.compression.plan import Encoded
+from coala_amd.compression.spec import RAW_BITS, SegmentTable
+from oracle import codec_oracle as O
+
+
+class OraclePlan:
+    def __init__(self, sizes, ratio, bits, clients=1):
+        self.table = SegmentTable(sizes, ratio, clients)
+        self.bits = bits
+
+    def encode(self, flat, base=None, **_):
+        x = flat.detach().cpu().numpy()
+        b = None if base is None else base.detach().cpu().numpy()
+        idx, vals, mn, sc = O.encode(x, self.table.segs.astype(np.int64), self.bits, base=b)
+        return Encoded(torch.from_numpy(idx), torch.from_numpy(vals), torch.from_numpy(mn), torch.from_numpy(sc))
+
+    def decode(self, enc, base=None, **_):
+        b = None if base is None else base.detach().cpu().numpy()
+        out = np.zeros(self.table.span, dtype=np.float32) if b is None else b.copy()
+        O.decode(enc.idx.numpy(), enc.vals.numpy(), enc.mn.numpy(), enc.scale.numpy(),
+                 self.table.segs.astype(np.int64), self.bits, self.table.span, base=b, out=out)
+        return torch.from_numpy(out)
+
+
+class OracleBackend:
+    name = "oracle"
+
+    def make_plan(self, sizes, ratio, bits, device):
+        return OraclePlan(sizes, ratio, bits)

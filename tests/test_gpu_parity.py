@@ -1,0 +1,211 @@
+"""GPU parity: HIP kernels (through the C ABI) vs the CPU oracle, bit-exact.
+
+Tolerance (written here as the bar): indices, codes, mn, scale and decoded values must be BIT-IDENTICAL
+to oracle/codec_oracle.py (both follow the same fp32 op order with no FMA). The spec's guaranteed bound,
+if a rounding-boundary case ever differed, would be one quantisation step; we do not
+use it — any difference fails.
+"""
+import numpy as np
+import pytest
+import torch
+
+from coala_amd.compression import CodecPlan, SegmentTable
+from coala_amd.compression._lib import COALAC_FLAG_FORCE_EXACT
+from coala_amd.layouts import fp32_sizes
+from coala_amd.workload import synth_batch
+from oracle import codec_oracle as O
+
+pytestmark = pytest.mark.gpu
+
+
+def to_flat(table, xs):
+    flat = np.zeros(table.span, dtype=np.float32)
+    for c in range(table.clients):
+        for t, (off, n) in enumerate(zip(table.offsets, table.sizes)):
+            o = c * table.span_per_client + off
+            flat[o:o + n] = xs[c][t]
+    return flat
+
+
+def run_both(sizes, ratio, bits, xs, bases=None, flags=0, clients=1):
+    plan = CodecPlan(sizes, ratio, bits, clients=clients)
+    table = plan.table
+    flat = to_flat(table, xs)
+    base = None if bases is None else to_flat(table, bases)
+    d_flat = torch.from_numpy(flat).cuda()
+    d_base = None if base is None else torch.from_numpy(base).cuda()
+    ws = plan.empty_workspace()
+    enc = plan.encode(d_flat, base=d_base, workspace=ws, flags=flags)
+    dec = plan.decode(enc, base=d_base)
+    torch.cuda.synchronize()
+    g = dict(idx=enc.idx.cpu().numpy(), vals=enc.vals.cpu().numpy(), mn=enc.mn.cpu().numpy(),
+             scale=enc.scale.cpu().numpy(), dec=dec.cpu().numpy(), fallbacks=plan.fallbacks(ws))
+    segs = table.segs.astype(np.int64)
+    idx, vals, mn, sc = O.encode(flat, segs, bits, base=base)
+    ref_dec = O.decode(idx, vals, mn, sc, segs, bits, table.span, base=base)
+    r = dict(idx=idx, vals=vals, mn=mn, scale=sc, dec=ref_dec)
+    return plan, g, r
+
+
+def assert_same(plan, g, r):
+    t = plan.table
+    np.testing.assert_array_equal(g["idx"], r["idx"])
+    np.testing.assert_array_equal(g["vals"].view(np.uint8), r["vals"].view(np.uint8))
+    np.testing.assert_array_equal(g["mn"].view(np.uint32), r["mn"].view(np.uint32))
+    np.testing.assert_array_equal(g["scale"].view(np.uint32), r["scale"].view(np.uint32))
+    for (off, n, k, oo) in t.segs.astype(np.int64):
+        np.testing.assert_array_equal(g["dec"][off:off + n].view(np.uint32), r["dec"][off:off + n].view(np.uint32))
+
+
+def gauss(rng, sizes, lo=-4, hi=-2):
+    return [(rng.standard_normal(n) * 10 ** rng.uniform(lo, hi)).astype(np.float32) for n in sizes]
+
+
+# -- edge cases ---------------------------------------------------------------------------------------
+def edge_segments(rng):
+    segs = []
+    segs.append(np.array([3.0], np.float32))                                    # n = 1
+    segs.append(np.array([-0.0, 0.0, -0.0, 0.0, 0.0], np.float32))              # signed zeros, all ties
+    segs.append(np.full(37, 0.25, np.float32))                                  # constant -> scale 0
+    segs.append(np.array([1, -1, 1, -1, 2, -2, 2, -2, 0.5], np.float32))        # equal magnitudes, signs
+    segs.append(np.array([1e-40, -1e-41, 3e-39, 0, 1e-45, -1e-45], np.float32))  # denormals
+    segs.append(np.array([np.inf, -1.0, 2.0, 0.5, -np.inf, 3.0], np.float32))   # infinities
+    segs.append(np.array([np.nan, 1.0, -2.0, 0.25, 7.0, -7.0, np.nan], np.float32))  # NaN keys sort on top
+    segs.append(np.zeros(8192, np.float32))                                     # all zero, SMALL_MAX
+    x = rng.standard_normal(8193).astype(np.float32)                            # smallest large segment
+    segs.append(x)
+    x = np.round(rng.standard_normal(50000) * 4).astype(np.float32) / 4         # heavy ties, large
+    segs.append(x)
+    segs.append(np.zeros(20000, np.float32))                                    # all-zero large
+    x = rng.standard_normal(4096 * 3 + 5).astype(np.float32)                    # ragged tail unit
+    segs.append(x)
+    segs.append(rng.standard_normal(3).astype(np.float32))
+    return segs
+
+
+@pytest.mark.parametrize("bits", [8, 4, 1, 32])
+@pytest.mark.parametrize("ratio", [0.001, 0.01, 0.1, 0.5, 1.0])
+def test_edge_cases(cuda, bits, ratio):
+    rng = np.random.default_rng(7)
+    segs = edge_segments(rng)
+    plan, g, r = run_both([s.size for s in segs], ratio, bits, [segs])
+    assert_same(plan, g, r)
+
+
+@pytest.mark.parametrize("flags", [0, COALAC_FLAG_FORCE_EXACT])
+@pytest.mark.parametrize("delta", [False, True])
+def test_random_layout_resnet18(cuda, flags, delta):
+    rng = np.random.default_rng(11)
+    sizes = fp32_sizes("resnet18")
+    xs = [gauss(rng, sizes)]
+    bases = [gauss(rng, sizes, -2, -1)] if delta else None
+    plan, g, r = run_both(sizes, 0.01, 8, xs, bases, flags)
+    assert_same(plan, g, r)
+    if flags:
+        assert g["fallbacks"] == plan.table.n_segments - sum(1 for s in sizes if s <= 8192)
+
+
+@pytest.mark.parametrize("ratio", [0.001, 0.01, 0.1])
+def test_batched_clients_resnet50_layout(cuda, ratio):
+    rng = np.random.default_rng(int(ratio * 1e4))
+    sizes = fp32_sizes("resnet50_tv")
+    xs = [gauss(rng, sizes) for _ in range(2)]
+    plan, g, r = run_both(sizes, ratio, 8, xs, clients=2)
+    assert_same(plan, g, r)
+    assert g["fallbacks"] == 0
+
+
+@pytest.mark.parametrize("name", ["lenet", "vit_b16", "resnet18_split_cut4", "simple_cnn_split_cut2"])
+def test_layouts(cuda, name):
+    rng = np.random.default_rng(3)
+    sizes = fp32_sizes(name)
+    plan, g, r = run_both(sizes, 0.01, 8, [gauss(rng, sizes)])
+    assert_same(plan, g, r)
+
+
+def _hash32(x):
+    x = np.uint64(x) & np.uint64(0xFFFFFFFF)
+    x ^= x >> np.uint64(16)
+    x = (x * np.uint64(0x7FEB352D)) & np.uint64(0xFFFFFFFF)
+    x ^= x >> np.uint64(15)
+    x = (x * np.uint64(0x846CA68B)) & np.uint64(0xFFFFFFFF)
+    x ^= x >> np.uint64(16)
+    return int(x)
+
+
+def sampled_positions(n, seg_index):
+    """Positions the sampler reads for a large segment (restates sample_thresholds in coalac.hip)."""
+    R = max(64, min(512, n // 512)) & ~63
+    stride = n // R
+    room = stride - 16
+    pos = np.zeros(n, bool)
+    for run in range(R):
+        h = _hash32(((run * 0x9E3779B9) & 0xFFFFFFFF) ^ (((seg_index + 1) * 0x85EBCA6B) & 0xFFFFFFFF))
+        start = (run * stride + h % (room + 1)) & ~3
+        pos[start:start + 16] = True
+    return pos
+
+
+def test_bracket_miss_forces_exact_reselection(cuda):
+    """Adversarial input: the large values sit exactly where the sampler does not look, so the sampled
+    bracket misses (count(A) > k) and the in-launch exact re-selection branch must produce the result."""
+    n = 1 << 20
+    rng = np.random.default_rng(5)
+    x = (rng.standard_normal(n) * 1e-3).astype(np.float32)
+    seen = sampled_positions(n, 0)
+    unseen = np.flatnonzero(~seen)
+    big = rng.choice(unseen, size=30000, replace=False)
+    x[big] = (rng.standard_normal(big.size) * 10).astype(np.float32)
+    plan, g, r = run_both([n], 0.01, 8, [[x]])
+    assert g["fallbacks"] == 1
+    assert_same(plan, g, r)
+
+
+def test_full_size_properties_resnet50_x16(cuda):
+    """Full C3-per-GPU size (16 ResNet-50 clients, 409.8 M elements): size-independent properties
+    against the input itself (the oracle would take minutes at this size)."""
+    sizes = fp32_sizes("resnet50_tv")
+    plan = CodecPlan(sizes, 0.01, 8, clients=16)
+    t = plan.table
+    flat = synth_batch(t, cuda)
+    enc = plan.encode(flat)
+    dec = plan.decode(enc)
+    torch.cuda.synchronize()
+    key = flat.view(torch.int32) & 0x7FFFFFFF
+    for c in (0, 7, 15):
+        for (off, n, k, oo) in t.segs.astype(np.int64)[c * len(sizes):(c + 1) * len(sizes)]:
+            idx = enc.idx[oo:oo + k].long()
+            assert bool((idx[1:] > idx[:-1]).all()) and int(idx[0]) >= 0 and int(idx[-1]) < n
+            kk = key[off:off + n]
+            mask = torch.zeros(n, dtype=torch.bool, device=cuda)
+            mask[idx] = True
+            sel_min = int(kk[mask].min())
+            if k < n:
+                rest_max = int(kk[~mask].max())
+                assert sel_min >= rest_max
+                if sel_min == rest_max:  # ties at the threshold: kept ones have the lower indices
+                    tie_sel = torch.nonzero(mask & (kk == sel_min)).max()
+                    tie_rest = torch.nonzero(~mask & (kk == sel_min)).min()
+                    assert int(tie_sel) < int(tie_rest)
+            d = dec[off:off + n]
+            assert bool((d[~mask] == 0).all())
+    # quantisation error bound on every segment of client 0: |xhat - x| <= scale/2 + 2 ulp
+    segs0 = t.segs.astype(np.int64)[:len(sizes)]
+    for si, (off, n, k, oo) in enumerate(segs0):
+        idx = enc.idx[oo:oo + k].long()
+        x = flat[off:off + n][idx]
+        xh = dec[off:off + n][idx]
+        bound = enc.scale[si].item() / 2 + 2 * torch.finfo(torch.float32).eps * x.abs().max().item()
+        assert (xh - x).abs().max().item() <= bound + 1e-30
+
+
+def test_raw_bits_idempotent(cuda):
+    """bits = 32: decode(encode(x)) is x masked to its top-k, and re-encoding it is a fixed point."""
+    sizes = fp32_sizes("resnet18")
+    plan = CodecPlan(sizes, 0.05, 32, clients=2)
+    flat = synth_batch(plan.table, cuda)
+    e1 = plan.encode(flat)
+    d1 = plan.decode(e1)
+    e2 = plan.encode(d1)
+    torch.cuda.synchronize()
+    assert torch.equal(e1.idx, e2.idx) and torch.equal(e1.vals, e2.vals)
