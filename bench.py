@@ -37,6 +37,9 @@ def parse():
     p.add_argument("--ratio", type=float, default=0.01)
     p.add_argument("--bits", type=int, default=8)
     p.add_argument("--mode", choices=["weights", "delta"], default="weights")
+    p.add_argument("--streams", type=int, default=1,
+                   help="split each GPU's clients into this many sub-batches, one HIP stream each")
+    p.add_argument("--flags", type=int, default=0, help="coalac encode flags (test hooks; 0 for the bench)")
     p.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline time budget")
     p.add_argument("--no-cpu-baseline", action="store_true")
     return p.parse_args()
@@ -62,7 +65,7 @@ def cpu_baseline(layout, ratio, bits, budget_s):
     segs = t.segs.astype(np.int64)
     N = sum(sizes)
     done, el = 0, 0.0
-    while el < budget_s and done < 8:
+    while el < budget_s and done < 64:
         rng = np.random.default_rng(1234 + done)
         flat = np.zeros(t.span, np.float32)
         for off, n in zip(t.offsets, sizes):
@@ -83,6 +86,7 @@ def main():
     import torch.distributed as dist
 
     from coala_amd.compression import CodecPlan
+    from coala_amd.compression.spec import SMALL_MAX
     from coala_amd.layouts import fp32_sizes
     from coala_amd.workload import synth_batch
 
@@ -97,32 +101,51 @@ def main():
         dist.init_process_group("nccl", device_id=dev)
 
     sizes = fp32_sizes(a.layout)
-    plan = CodecPlan(sizes, a.ratio, a.bits, clients=a.clients, device=dev)
-    t = plan.table
-    ids = range(rank * a.clients, (rank + 1) * a.clients)
-    flat = synth_batch(t, dev, client_ids=ids)
-    base = synth_batch(t, dev, client_ids=[10_000 + i for i in ids]) if a.mode == "delta" else None
-    enc = plan.empty_encoded()
-    ws = plan.empty_workspace()
-    out = plan.empty_flat()
+    if a.clients % a.streams:
+        raise SystemExit("--clients must be a multiple of --streams")
+    per = a.clients // a.streams
+    lanes = []  # one independent sub-batch per stream: plan, buffers, stream, events
+    for si in range(a.streams):
+        plan = CodecPlan(sizes, a.ratio, a.bits, clients=per, device=dev)
+        ids = range(rank * a.clients + si * per, rank * a.clients + (si + 1) * per)
+        flat = synth_batch(plan.table, dev, client_ids=ids)
+        base = synth_batch(plan.table, dev, client_ids=[10_000 + i for i in ids]) if a.mode == "delta" else None
+        lanes.append(dict(plan=plan, flat=flat, base=base, enc=plan.empty_encoded(), ws=plan.empty_workspace(),
+                          out=plan.empty_flat(), dws=plan.empty_decode_workspace(),
+                          stream=torch.cuda.current_stream() if a.streams == 1 else torch.cuda.Stream(dev)))
+    from coala_amd.compression import SegmentTable
+    t = SegmentTable(sizes, a.ratio, a.clients)
     torch.cuda.synchronize()
 
-    def step(ev_e=None, ev_d=None):
-        plan.encode(flat, base=base, out=enc, workspace=ws, events=ev_e)
-        plan.decode(enc, base=base, out=out, events=ev_d)
+    def step(i=None):
+        main = torch.cuda.current_stream()
+        for L in lanes:
+            if a.streams > 1:
+                L["stream"].wait_stream(main)
+            with torch.cuda.stream(L["stream"]):
+                ev_e = None if i is None else L["ev_e"][i]
+                ev_d = None if i is None else L["ev_d"][i]
+                L["plan"].encode(L["flat"], base=L["base"], out=L["enc"], workspace=L["ws"], events=ev_e,
+                                 flags=a.flags)
+                L["plan"].decode(L["enc"], base=L["base"], out=L["out"], workspace=L["dws"], events=ev_d)
+        if a.streams > 1:
+            for L in lanes:
+                main.wait_stream(L["stream"])
 
     for _ in range(a.warmup):
         step()
-    fallbacks = plan.fallbacks(ws)
-    ev_e = [make_events(torch, 5) for _ in range(a.steps)]
-    ev_d = [make_events(torch, 2) for _ in range(a.steps)]
+    fallbacks = sum(L["plan"].fallbacks(L["ws"], stream=L["stream"]) for L in lanes)
+    for L in lanes:
+        with torch.cuda.stream(L["stream"]):
+            L["ev_e"] = [make_events(torch, 5) for _ in range(a.steps)]
+            L["ev_d"] = [make_events(torch, 3) for _ in range(a.steps)]
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for i in range(a.steps):
-        step(ev_e[i], ev_d[i])
+        step(i)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -132,23 +155,23 @@ def main():
         dist.all_reduce(x, op=dist.ReduceOp.MAX)
         el = x.item()
 
-    # per-kernel mean durations (ms) from the HIP events recorded on the launch stream
+    # per-kernel mean durations (ms) from the HIP events recorded on each launch stream; with several
+    # streams, kernels overlap and each duration includes the co-running work of the other streams
     def mean(pairs):
         return sum(s.elapsed_time(e) for s, e in pairs) / len(pairs)
-    stages = {
-        "k_prep": mean([(e[0], e[1]) for e in ev_e]),
-        "k_scan": mean([(e[1], e[2]) for e in ev_e]),
-        "k_select": mean([(e[2], e[3]) for e in ev_e]),
-        "k_emit": mean([(e[3], e[4]) for e in ev_e]),
-        "k_decode": mean([(d[0], d[1]) for d in ev_d]),
-    }
+    stages = {}
+    for name, (which, i0, i1) in {"k_sample": ("ev_e", 0, 1), "k_scan": ("ev_e", 1, 2), "k_select": ("ev_e", 2, 3),
+                                  "k_emit": ("ev_e", 3, 4), "k_bounds": ("ev_d", 0, 1),
+                                  "k_decode": ("ev_d", 1, 2)}.items():
+        stages[name] = mean([(e[i0], e[i1]) for L in lanes for e in L[which]])
     N, K, T = t.n_elements, t.total_k, t.n_segments
     delta = a.mode == "delta"
     vb = 4 if a.bits == 32 else 1
-    large_elems = a.clients * sum(n for n in sizes if n > 8192)
+    large_elems = per * sum(n for n in sizes if n > SMALL_MAX)
+    Np, Kp, Tp = N // a.streams, K // a.streams, T // a.streams  # per launch (one sub-batch)
     alg = {  # algorithmic HBM bytes per launch
         "k_scan": 4 * large_elems * (2 if delta else 1),
-        "k_decode": 4 * N * (2 if delta else 1) + (4 + vb) * K + 8 * T,
+        "k_decode": 4 * Np * (2 if delta else 1) + (4 + vb) * Kp + 8 * Tp,
     }
     dom = max(alg, key=lambda k: stages[k])
     ach = alg[dom] / (stages[dom] * 1e-3) / 1e9
@@ -165,7 +188,8 @@ def main():
                                    f"{a.ratio}, {a.bits}-bit codes, {a.mode} mode, encode+decode batched",
                        "layout": a.layout, "clients_per_gpu": a.clients, "global_clients": a.clients * world,
                        "elements_per_client": sum(sizes), "segments_per_client": len(sizes),
-                       "ratio": a.ratio, "bits": a.bits, "mode": a.mode, "parallelism": f"replicas{world}"},
+                       "ratio": a.ratio, "bits": a.bits, "mode": a.mode, "streams_per_gpu": a.streams,
+                       "parallelism": f"replicas{world}"},
             "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None,
                          "alg_bytes_per_launch": alg[dom]},

@@ -10,6 +10,7 @@ import threading
 from .. import _build
 
 COALAC_FLAG_FORCE_EXACT = 1
+COALAC_FLAG_GENERIC_SELECT = 2
 
 ERRORS = {
     -1: "COALAC_EINVAL",
@@ -30,11 +31,11 @@ SIGNATURES = [
     ("coalac_plan_create", _I, [_P, _I, _I, ctypes.POINTER(_P)]),
     ("coalac_plan_destroy", _I, [_P]),
     ("coalac_plan_query", _I, [_P, ctypes.POINTER(_U64), ctypes.POINTER(_U64), ctypes.POINTER(_U64),
-                               ctypes.POINTER(_U64)]),
+                               ctypes.POINTER(_U64), ctypes.POINTER(_U64)]),
     ("coalac_encode", _I, [_P, _P, _P, _P, _P, _P, _P, _P, _U64, ctypes.c_uint, _P]),
-    ("coalac_decode", _I, [_P, _P, _P, _P, _P, _P, _P, _P]),
+    ("coalac_decode", _I, [_P, _P, _P, _P, _P, _P, _P, _P, _U64, _P]),
     ("coalac_encode_ev", _I, [_P, _P, _P, _P, _P, _P, _P, _P, _U64, ctypes.c_uint, _P, _P]),
-    ("coalac_decode_ev", _I, [_P, _P, _P, _P, _P, _P, _P, _P, _P]),
+    ("coalac_decode_ev", _I, [_P, _P, _P, _P, _P, _P, _P, _P, _U64, _P, _P]),
     ("coalac_workspace_fallbacks", _I, [_P, _P, _P, ctypes.POINTER(_I)]),
 ]
 

@@ -64,10 +64,11 @@ class CodecPlan:
             _lib.check(self._lib.coalac_plan_create(arr, len(segs), self.bits, ctypes.byref(h)),
                        "coalac_plan_create")
         self._h = h
-        ws, tk, span, nu = (ctypes.c_uint64() for _ in range(4))
-        _lib.check(self._lib.coalac_plan_query(h, ctypes.byref(ws), ctypes.byref(tk), ctypes.byref(span),
-                                               ctypes.byref(nu)), "coalac_plan_query")
-        self.ws_bytes, self.total_k, self.span, self.n_units = ws.value, tk.value, span.value, nu.value
+        ws, dws, tk, span, nu = (ctypes.c_uint64() for _ in range(5))
+        _lib.check(self._lib.coalac_plan_query(h, ctypes.byref(ws), ctypes.byref(dws), ctypes.byref(tk),
+                                               ctypes.byref(span), ctypes.byref(nu)), "coalac_plan_query")
+        self.ws_bytes, self.dec_ws_bytes = ws.value, dws.value
+        self.total_k, self.span, self.n_units = tk.value, span.value, nu.value
         if self.total_k != self.table.total_k:
             raise _lib.CodecError(f"plan total_k {self.total_k} != table {self.table.total_k}")
 
@@ -105,6 +106,9 @@ class CodecPlan:
 
     def empty_workspace(self):
         return torch.empty(self.ws_bytes, dtype=torch.uint8, device=self.device)
+
+    def empty_decode_workspace(self):
+        return torch.empty(self.dec_ws_bytes, dtype=torch.uint8, device=self.device)
 
     # -- checks -----------------------------------------------------------------------------------
     def _check_flat(self, t, name):
@@ -147,20 +151,23 @@ class CodecPlan:
         _lib.check(rc, "coalac_encode")
         return out
 
-    def decode(self, enc, base=None, out=None, stream=None, events=None):
+    def decode(self, enc, base=None, out=None, workspace=None, stream=None, events=None):
         """Decode Encoded -> dense flat fp32[span] (+ base, fused). Asynchronous on `stream`."""
         self._check_encoded(enc)
         self._check_flat(base, "base")
         if out is None:
             out = self.empty_flat() if base is None else torch.empty_like(base)
         self._check_flat(out, "output")
+        ws = self.empty_decode_workspace() if workspace is None else workspace
+        if ws.device != self.device or ws.numel() * ws.element_size() < self.dec_ws_bytes:
+            raise ValueError(f"decode workspace: need {self.dec_ws_bytes} bytes on {self.device}")
         args = (self._h, _ptr(enc.idx), _ptr(enc.vals), _ptr(enc.mn), _ptr(enc.scale), _ptr(base), _ptr(out),
-                _stream_handle(stream))
+                _ptr(ws), ctypes.c_uint64(self.dec_ws_bytes), _stream_handle(stream))
         with torch.cuda.device(self.device):
             if events is None:
                 rc = self._lib.coalac_decode(*args)
             else:
-                rc = self._lib.coalac_decode_ev(*args, _event_array(events, 2))
+                rc = self._lib.coalac_decode_ev(*args, _event_array(events, 3))
         _lib.check(rc, "coalac_decode")
         return out
 

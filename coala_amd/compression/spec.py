@@ -11,6 +11,8 @@ import numpy as np
 
 ALIGN = 32          # elements; 128-byte aligned segment starts (float4 loads need >= 4)
 RAW_BITS = 32       # bits == 32: values stored as raw fp32 (lossless at ratio 1)
+SMALL_MAX = 4096    # mirrors coalac.hip: segments up to this size are encoded by one block, no sampling
+UNIT = 4096         # mirrors coalac.hip: elements per wave work unit
 VALID_BITS = tuple(range(1, 9)) + (RAW_BITS,)
 
 

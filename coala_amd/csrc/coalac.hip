@@ -17,12 +17,15 @@
 //
 //   Work unit = 4096 contiguous elements of one segment, owned by ONE wave64: ordered compaction is
 //   done with wave ballots + mbcnt, so the streaming pass has no LDS traffic and no block barriers.
-//   Segments of <= 8192 elements are encoded whole by one 256-thread block in LDS.
+//   Every per-unit quantity is indexed by the unit's own index, so a wave reaches all it needs in one
+//   dependent round trip. Segments of <= 8192 elements are encoded whole by one block in LDS.
 //
-//   Kernels (encode): k_prep (small segments end to end; large segments: sample -> T_lo/T_hi),
-//   k_scan (streaming classify + compaction), k_select (exact k-th key, tie quotas, per-unit output
-//   offsets, min/max -> scale), k_emit (sorted idx + codes). Decode: k_decode (one wave per unit:
-//   wave-cooperative 64-ary search of the sorted index list, LDS tile scatter, dense float4 stores).
+//   Kernels (encode): k_sample (large segments: sample -> T_lo/T_hi), k_scan (small segments end to
+//   end in its first blocks, overlapping the streaming classify + compaction of the large units),
+//   k_select (exact k-th key inside B, tie quota, per-unit output offsets, min/max -> scale; 1024
+//   threads per segment), k_emit (sorted idx + codes via an LDS bitmap).
+//   Decode: k_bounds (first kept entry of every unit, one streaming pass over the sorted idx lists),
+//   k_decode (one wave per unit, no LDS: dense float4 background stores, then the kept values).
 //
 // Numerics: built with -ffp-contract=off; fp32 sub/div/mul/add are separate IEEE ops, rintf is
 // round-half-even — the same op sequence as the oracle, so decoded values are bit-identical.
@@ -44,23 +47,38 @@ namespace {
 
 constexpr int BLOCK = 256;
 constexpr int WAVES = BLOCK / 64;
-constexpr uint32_t UNIT = 4096;        // elements per wave work unit
+constexpr uint32_t UNIT = 4096;           // elements per wave work unit
+constexpr uint32_t UNIT_SHIFT = 12;
 constexpr uint32_t UNIT_IT = UNIT / 256;  // float4 loads per lane per unit
-constexpr uint32_t SMALL_MAX = 8192;   // segments up to this size are encoded whole in one block
+constexpr uint32_t SMALL_MAX = 4096;      // segments up to this size are encoded whole in one block
+constexpr uint32_t SAMPLE_MAX = 8192;     // sampled keys per large segment
+constexpr int SEL_NT = 512;               // threads of a k_select block
+constexpr uint32_t BCHUNK = 4096;         // idx entries per k_bounds block
+constexpr uint32_t STAGE_CAP = 512;       // candidate records staged in LDS per k_scan wave
+constexpr uint32_t A_FLAG = 0x80000000u;  // candidate record flag: key > T_hi (kept for sure)
 constexpr uint32_t KEY_MAX = 0x7FFFFFFFu;
 constexpr int HIST_BINS = 2048;
+constexpr uint32_t UCAP = 2048;           // units per k_select chunk (8.4 M elements)
+constexpr uint32_t WB = 4;                // in-window LDS slots per k_select thread (fast path)
+constexpr uint32_t NONE = 0xFFFFFFFFu;
 
 struct SegDev {
   uint64_t in_off;
-  uint32_t n, k;
   uint64_t out_off;
-  uint32_t unit_begin, unit_end;
+  uint32_t n, k;
+  uint32_t unit_begin, unit_end;  // range in the all-units table (decode)
+  uint32_t lu_begin, pad;         // first large-unit index (large segments)
 };
-static_assert(sizeof(SegDev) == 32, "SegDev layout");
 
 struct UnitDev {
+  uint64_t off;      // element offset of the unit in the flat buffer (= seg.in_off + start)
+  uint64_t out_off;  // the segment's out_off
   uint32_t seg, start;
+  uint32_t k;        // the segment's k
+  uint16_t len;      // elements in this unit (<= UNIT)
+  uint16_t last;     // 1 if this is the segment's last unit
 };
+static_assert(sizeof(UnitDev) == 32, "UnitDev layout");
 
 struct Params {
   // encode / decode operands
@@ -77,19 +95,21 @@ struct Params {
   float* out;
   // plan metadata
   const SegDev* segs;
-  const UnitDev* units;
+  const UnitDev* units;   // all units (decode)
+  const UnitDev* lunits;  // units of large segments (encode)
   const uint32_t* small_list;
   const uint32_t* large_list;
-  const uint32_t* lunits;
-  uint32_t n_small, n_large, n_units, n_lunits;
+  uint32_t nseg, n_small, n_large, n_units, n_lunits;
   float levels;
   unsigned flags;
-  // workspace
-  uint32_t *tlo, *thi, *tstar, *status;
-  uint32_t *cntA, *cntB, *gtB, *eqB, *fpos, *fneg, *quota, *outoff;
-  float *minA, *maxA;
-  int32_t *aI, *bI;
-  float *aV, *bV;
+  // encode workspace: per segment
+  uint32_t *tstar, *rtie, *status;
+  // per large unit
+  uint32_t *tlo, *thi, *cntA, *cntC, *gtC, *eqC, *eqpre, *outoff;
+  uint2* cand;  // candidate records {index | A_FLAG, value bits}, UNIT slots per large unit
+
+  // decode workspace
+  uint32_t* ustart;
 };
 
 // ------------------------------------------------------------------------------------------------
@@ -103,6 +123,7 @@ DEV uint32_t fkey(float x) { return __float_as_uint(x) & KEY_MAX; }
 // end (+ 0.0f), which makes the reduction order-independent.
 DEV float fmin_nan(float a, float b) { return (a != a) ? b : ((b != b) ? a : ((b < a) ? b : a)); }
 DEV float fmax_nan(float a, float b) { return (a != a) ? b : ((b != b) ? a : ((b > a) ? b : a)); }
+DEV float qnan() { return __int_as_float(0x7FC00000); }
 
 DEV uint32_t lane_id() { return __lane_id(); }
 
@@ -121,12 +142,6 @@ DEV uint32_t wave_incl_scan(uint32_t v) {
   return v;
 }
 
-DEV uint32_t wave_sum(uint32_t v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-  return v;
-}
-
 DEV float wave_min(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v = fmin_nan(v, __shfl_xor(v, o, 64));
@@ -139,9 +154,16 @@ DEV float wave_max(float v) {
   return v;
 }
 
-// Block-wide exclusive scan (BLOCK threads). sh needs >= WAVES words. Returns the exclusive prefix and
+DEV void wave_fence() {
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+}
+
+// Block-wide exclusive scan over NT threads. sh needs >= NT/64 words. Returns the exclusive prefix and
 // the block total. Contains barriers: call from all threads.
+template <int NT>
 DEV uint32_t block_excl_scan(uint32_t v, uint32_t* sh, uint32_t& total) {
+  constexpr int NW = NT / 64;
   const uint32_t lane = lane_id(), w = threadIdx.x >> 6;
   uint32_t inc = wave_incl_scan(v);
   __syncthreads();
@@ -149,7 +171,7 @@ DEV uint32_t block_excl_scan(uint32_t v, uint32_t* sh, uint32_t& total) {
   __syncthreads();
   uint32_t off = 0, tot = 0;
 #pragma unroll
-  for (int i = 0; i < WAVES; ++i) {
+  for (int i = 0; i < NW; ++i) {
     uint32_t s = sh[i];
     if ((uint32_t)i < w) off += s;
     tot += s;
@@ -158,27 +180,31 @@ DEV uint32_t block_excl_scan(uint32_t v, uint32_t* sh, uint32_t& total) {
   return off + inc - v;
 }
 
+template <int NT>
 DEV uint32_t block_sum(uint32_t v, uint32_t* sh) {
   uint32_t t;
-  block_excl_scan(v, sh, t);
+  block_excl_scan<NT>(v, sh, t);
   return t;
 }
 
+// shf needs >= 2 * NT/64 floats
+template <int NT>
 DEV void block_minmax(float& mn, float& mx, float* shf) {
+  constexpr int NW = NT / 64;
   const uint32_t lane = lane_id(), w = threadIdx.x >> 6;
   mn = wave_min(mn);
   mx = wave_max(mx);
   __syncthreads();
   if (lane == 0) {
     shf[w] = mn;
-    shf[WAVES + w] = mx;
+    shf[NW + w] = mx;
   }
   __syncthreads();
-  float a = shf[0], b = shf[WAVES];
+  float a = shf[0], b = shf[NW];
 #pragma unroll
-  for (int i = 1; i < WAVES; ++i) {
+  for (int i = 1; i < NW; ++i) {
     a = fmin_nan(a, shf[i]);
-    b = fmax_nan(b, shf[WAVES + i]);
+    b = fmax_nan(b, shf[NW + i]);
   }
   mn = a;
   mx = b;
@@ -186,57 +212,59 @@ DEV void block_minmax(float& mn, float& mx, float* shf) {
 
 // Exact selection of the r-th largest key (1-based) among the keys in [lo, hi] that `for_each`
 // enumerates (each thread enumerates its own share; the union is the key multiset). Returns T with
-// count(key in (T, hi]) < r <= count(key in [T, hi]). Radix narrowing with 2048-bin LDS histograms:
-// at most 3 passes over the keys for a full 31-bit range.
-template <class ForEach>
-DEV uint32_t block_select(ForEach&& for_each, uint32_t lo, uint32_t hi, uint32_t r, uint32_t* hist,
+// count(key in (T, hi]) < r <= count(key in [T, hi]) and leaves in r the number of keys == T to take
+// (r - count(key in (T, hi])). Radix narrowing with 2048-bin LDS histograms: at most 3 passes over the
+// keys for a full 31-bit range. sh needs >= 64 words (broadcast slots sh[40], sh[41]).
+template <int NT, class ForEach>
+DEV uint32_t block_select(ForEach&& for_each, uint32_t lo, uint32_t hi, uint32_t& r, uint32_t* hist,
                           uint32_t* sh) {
+  constexpr int BPT = HIST_BINS / NT;  // bins per thread
   const uint32_t t = threadIdx.x;
   while (lo < hi) {
     const uint32_t w = hi - lo;
     const int bl = 32 - __clz(w);
     const int shift = bl > 11 ? bl - 11 : 0;
-    for (uint32_t i = t; i < HIST_BINS; i += BLOCK) hist[i] = 0;
+    for (uint32_t i = t; i < HIST_BINS; i += NT) hist[i] = 0;
     __syncthreads();
     const uint32_t l0 = lo, h0 = hi;
     for_each([&](uint32_t key) {
       if (key >= l0 && key <= h0) atomicAdd(&hist[(key - l0) >> shift], 1u);
     });
     __syncthreads();
-    uint32_t c[HIST_BINS / BLOCK];
+    uint32_t c[BPT];
     uint32_t s = 0;
 #pragma unroll
-    for (int j = 0; j < HIST_BINS / BLOCK; ++j) {
-      c[j] = hist[t * (HIST_BINS / BLOCK) + j];
+    for (int j = 0; j < BPT; ++j) {
+      c[j] = hist[t * BPT + j];
       s += c[j];
     }
     uint32_t total;
-    const uint32_t ex = block_excl_scan(s, sh, total);
+    const uint32_t ex = block_excl_scan<NT>(s, sh, total);
     const uint32_t above = total - ex - s;  // keys in bins above this thread's bins
     if (t == 0) {
-      sh[8] = 0xFFFFFFFFu;
-      sh[9] = r;
+      sh[40] = NONE;
+      sh[41] = r;
     }
     __syncthreads();
     if (above < r && r <= above + s) {
       uint32_t acc = above;
-      int b = (int)(t * (HIST_BINS / BLOCK));
+      int b = (int)(t * BPT);
 #pragma unroll
-      for (int j = HIST_BINS / BLOCK - 1; j >= 0; --j) {
+      for (int j = BPT - 1; j >= 0; --j) {
         if (acc + c[j] >= r) {
-          b = (int)(t * (HIST_BINS / BLOCK)) + j;
+          b = (int)(t * BPT) + j;
           break;
         }
         acc += c[j];
       }
-      sh[8] = (uint32_t)b;
-      sh[9] = r - acc;
+      sh[40] = (uint32_t)b;
+      sh[41] = r - acc;
     }
     __syncthreads();
-    const uint32_t b = sh[8];
-    r = sh[9];
+    const uint32_t b = sh[40];
+    r = sh[41];
     __syncthreads();
-    if (b == 0xFFFFFFFFu) return lo;  // precondition violated (cannot happen for valid inputs)
+    if (b == NONE) return lo;  // precondition violated (cannot happen for valid inputs)
     lo = lo + (b << shift);
     const uint32_t nhi = lo + ((1u << shift) - 1u);
     hi = nhi < hi ? nhi : hi;
@@ -284,6 +312,32 @@ DEV float4 load_x4(const Params& P, uint64_t off) {
   return v;
 }
 
+typedef float f4v __attribute__((ext_vector_type(4)));
+
+// histogram shift of the sampled band [tlo, thi]: HIST_BINS bins of 2^shift keys cover it. k_scan
+// (band histogram) and k_select (bin -> key window) must agree, so both use this.
+DEV int band_shift(uint32_t tlo, uint32_t thi) {
+  const uint32_t w = thi - tlo;
+  if (w == 0) return 0;
+  const int bl = 32 - __clz(w);
+  return bl > 11 ? bl - 11 : 0;
+}
+
+// non-temporal (read-once) 16-byte load of x (or x - base)
+template <bool DELTA>
+DEV float4 load_x4_nt(const Params& P, uint64_t off) {
+  const f4v a = __builtin_nontemporal_load(reinterpret_cast<const f4v*>(P.in + off));
+  float4 v = make_float4(a.x, a.y, a.z, a.w);
+  if (DELTA) {
+    const f4v b = __builtin_nontemporal_load(reinterpret_cast<const f4v*>(P.base + off));
+    v.x = v.x - b.x;
+    v.y = v.y - b.y;
+    v.z = v.z - b.z;
+    v.w = v.w - b.w;
+  }
+  return v;
+}
+
 template <bool DELTA>
 DEV float load_x1(const Params& P, uint64_t off) {
   float v = P.in[off];
@@ -301,99 +355,95 @@ DEV uint32_t hash32(uint32_t x) {
 }
 
 // ------------------------------------------------------------------------------------------------
-// streaming classify + ordered compaction of one unit by one wave (k_scan, and the exact fallback)
-// A: key > thi (kept for sure), B: tlo <= key <= thi (maybe). Both written in index order.
+// streaming classify + ordered compaction of one large unit by one wave (k_scan, exact fallback)
+// Candidates (key >= tlo) are written in index order as 8-byte records {index | A_FLAG, value}; A_FLAG
+// marks key > thi (kept for sure). With `stage` (k_scan) the first STAGE_CAP records go to a per-wave
+// LDS buffer and leave in coalesced 512-byte stores at the end; scattered per-lane global stores were
+// measured 28 % slower (tools/scan_ablate.hip). Input loads are non-temporal: the update is read once.
+// The unit is loaded in NB batches of UNIT_IT/NB float4 per lane: NB = 1 for the streaming pass (all
+// loads in flight at once), more for the register-lean fallback inside k_select.
 // ------------------------------------------------------------------------------------------------
-template <bool DELTA>
-DEV void scan_unit(const Params& P, uint32_t u, uint32_t tlo, uint32_t thi) {
+template <bool DELTA, int NB>
+DEV void scan_unit(const Params& P, uint32_t lu, const UnitDev& L, uint32_t tlo, uint32_t thi, uint2* stage) {
+  constexpr uint32_t IT = UNIT_IT / NB;
   const uint32_t lane = lane_id();
-  const UnitDev ud = P.units[u];
-  const SegDev sd = P.segs[ud.seg];
-  const uint32_t len = min(UNIT, sd.n - ud.start);
-  const uint64_t off = sd.in_off + ud.start;
-  int32_t* aI = P.aI + off;
-  float* aV = P.aV + off;
-  int32_t* bI = P.bI + off;
-  float* bV = P.bV + off;
+  const uint32_t len = L.len;
+  const uint64_t off = L.off;
+  uint2* R = P.cand + (uint64_t)lu * UNIT;
+  uint32_t cC = 0, cA = 0;
 
-  float4 v[UNIT_IT];
-  if (len == UNIT) {
+  for (uint32_t nb = 0; nb < (uint32_t)NB; ++nb) {
+    float4 v[IT];
+    if (len == UNIT) {
 #pragma unroll
-    for (uint32_t it = 0; it < UNIT_IT; ++it) v[it] = load_x4<DELTA>(P, off + (it * 64 + lane) * 4);
-  } else {
+      for (uint32_t i = 0; i < IT; ++i) v[i] = load_x4_nt<DELTA>(P, off + ((nb * IT + i) * 64 + lane) * 4);
+    } else {
 #pragma unroll
-    for (uint32_t it = 0; it < UNIT_IT; ++it) {
-      const uint32_t e = (it * 64 + lane) * 4;
-      if (e + 3 < len) {
-        v[it] = load_x4<DELTA>(P, off + e);
-      } else {
-        v[it].x = e + 0 < len ? load_x1<DELTA>(P, off + e + 0) : 0.0f;
-        v[it].y = e + 1 < len ? load_x1<DELTA>(P, off + e + 1) : 0.0f;
-        v[it].z = e + 2 < len ? load_x1<DELTA>(P, off + e + 2) : 0.0f;
-        v[it].w = e + 3 < len ? load_x1<DELTA>(P, off + e + 3) : 0.0f;
+      for (uint32_t i = 0; i < IT; ++i) {
+        const uint32_t e = ((nb * IT + i) * 64 + lane) * 4;
+        if (e + 3 < len) {
+          v[i] = load_x4<DELTA>(P, off + e);
+        } else {
+          v[i].x = e + 0 < len ? load_x1<DELTA>(P, off + e + 0) : 0.0f;
+          v[i].y = e + 1 < len ? load_x1<DELTA>(P, off + e + 1) : 0.0f;
+          v[i].z = e + 2 < len ? load_x1<DELTA>(P, off + e + 2) : 0.0f;
+          v[i].w = e + 3 < len ? load_x1<DELTA>(P, off + e + 3) : 0.0f;
+        }
+      }
+    }
+#pragma unroll
+    for (uint32_t i = 0; i < IT; ++i) {
+      const uint32_t e0 = ((nb * IT + i) * 64 + lane) * 4;
+      const float xs[4] = {v[i].x, v[i].y, v[i].z, v[i].w};
+      bool fc[4], fa[4];
+      bool any = false;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const uint32_t key = fkey(xs[j]);
+        fc[j] = e0 + j < len && key >= tlo;
+        fa[j] = fc[j] && key > thi;
+        any = any || fc[j];
+      }
+      if (!__any(any)) continue;
+      uint64_t bc[4];
+      uint32_t pc = cC;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        bc[j] = __ballot(fc[j]);
+        pc += mbcnt(bc[j]);
+        cA += (uint32_t)__popcll(__ballot(fa[j]));
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        if (fc[j]) {
+          const uint2 rec = make_uint2((L.start + e0 + j) | (fa[j] ? A_FLAG : 0u), __float_as_uint(xs[j]));
+          if (stage != nullptr && pc < STAGE_CAP)
+            stage[pc] = rec;
+          else
+            R[pc] = rec;
+          ++pc;
+        }
+        cC += (uint32_t)__popcll(bc[j]);
       }
     }
   }
-
-  uint32_t cA = 0, cB = 0;
-  float mnA = __int_as_float(0x7FC00000), mxA = __int_as_float(0x7FC00000);
-#pragma unroll
-  for (uint32_t it = 0; it < UNIT_IT; ++it) {
-    const uint32_t e0 = (it * 64 + lane) * 4;
-    const float xs[4] = {v[it].x, v[it].y, v[it].z, v[it].w};
-    bool fa[4], fb[4];
-    bool any = false;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const uint32_t key = fkey(xs[j]);
-      const bool valid = e0 + j < len;
-      fa[j] = valid && key > thi;
-      fb[j] = valid && !fa[j] && key >= tlo;
-      any = any || fa[j] || fb[j];
-    }
-    if (!__any(any)) continue;
-    uint64_t ba[4], bb[4];
-    uint32_t pa = cA, pb = cB;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      ba[j] = __ballot(fa[j]);
-      bb[j] = __ballot(fb[j]);
-      pa += mbcnt(ba[j]);
-      pb += mbcnt(bb[j]);
-    }
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      if (fa[j]) {
-        aI[pa] = (int32_t)(ud.start + e0 + j);
-        aV[pa] = xs[j];
-        ++pa;
-        mnA = fmin_nan(mnA, xs[j]);
-        mxA = fmax_nan(mxA, xs[j]);
-      }
-      if (fb[j]) {
-        bI[pb] = (int32_t)(ud.start + e0 + j);
-        bV[pb] = xs[j];
-        ++pb;
-      }
-      cA += (uint32_t)__popcll(ba[j]);
-      cB += (uint32_t)__popcll(bb[j]);
-    }
+  if (stage != nullptr) {
+    wave_fence();
+    for (uint32_t i = lane; i < cC && i < STAGE_CAP; i += 64) R[i] = stage[i];
   }
-  mnA = wave_min(mnA);
-  mxA = wave_max(mxA);
   if (lane == 0) {
-    P.cntA[u] = cA;
-    P.cntB[u] = cB;
-    P.minA[u] = mnA;
-    P.maxA[u] = mxA;
+    P.cntA[lu] = cA;
+    P.cntC[lu] = cC;
   }
 }
 
 // ------------------------------------------------------------------------------------------------
-// k_prep: small segments end to end; large segments: sampled thresholds
+// small segments (n <= SMALL_MAX): one 256-thread block, values in LDS, exact radix select, ordered
+// compaction, min/max, codes. Runs as the first blocks of k_scan so its latency hides under streaming.
 // ------------------------------------------------------------------------------------------------
 template <bool DELTA, bool RAW>
 DEV void small_encode(const Params& P, uint32_t s, float* vals, uint32_t* hist, uint32_t* sh) {
+  constexpr int NT = BLOCK;
   const uint32_t t = threadIdx.x;
   const SegDev sd = P.segs[s];
   const uint32_t n = sd.n, k = sd.k;
@@ -404,7 +454,7 @@ DEV void small_encode(const Params& P, uint32_t s, float* vals, uint32_t* hist, 
     }
     return;
   }
-  for (uint32_t i = t * 4; i < n; i += BLOCK * 4) {
+  for (uint32_t i = t * 4; i < n; i += NT * 4) {
     if (i + 3 < n) {
       const float4 v = load_x4<DELTA>(P, sd.in_off + i);
       vals[i + 0] = v.x;
@@ -416,14 +466,15 @@ DEV void small_encode(const Params& P, uint32_t s, float* vals, uint32_t* hist, 
     }
   }
   __syncthreads();
-  const uint32_t T = block_select(
+  uint32_t rt = k;
+  const uint32_t T = block_select<NT>(
       [&](auto&& f) {
-        for (uint32_t i = t; i < n; i += BLOCK) f(fkey(vals[i]));
+        for (uint32_t i = t; i < n; i += NT) f(fkey(vals[i]));
       },
-      0u, KEY_MAX, k, hist, sh);
+      0u, KEY_MAX, rt, hist, sh);
 
-  // ordered ownership: thread t owns the contiguous range [b0, b1)
-  const uint32_t E = (n + BLOCK - 1) / BLOCK;
+  // ordered ownership: thread t owns the contiguous range [b0, b1); the first rt ties are kept
+  const uint32_t E = (n + NT - 1) / NT;
   const uint32_t b0 = min(n, t * E), b1 = min(n, b0 + E);
   uint32_t gt = 0, eq = 0;
   for (uint32_t i = b0; i < b1; ++i) {
@@ -431,17 +482,15 @@ DEV void small_encode(const Params& P, uint32_t s, float* vals, uint32_t* hist, 
     gt += key > T;
     eq += key == T;
   }
-  uint32_t gtot, eqtot;
-  block_excl_scan(gt, sh, gtot);
-  const uint32_t eqpre = block_excl_scan(eq, sh, eqtot);
-  const uint32_t rt = k - gtot;
+  uint32_t eqtot;
+  const uint32_t eqpre = block_excl_scan<NT>(eq, sh, eqtot);
   const uint32_t quota = eqpre >= rt ? 0u : min(eq, rt - eqpre);
   uint32_t seltot;
-  const uint32_t opre = block_excl_scan(gt + quota, sh, seltot);
+  const uint32_t opre = block_excl_scan<NT>(gt + quota, sh, seltot);
 
   float mn = 0.0f, scale = 0.0f;
   if (!RAW) {
-    float a = __int_as_float(0x7FC00000), b = __int_as_float(0x7FC00000);
+    float a = qnan(), b = qnan();
     uint32_t eqseen = 0;
     for (uint32_t i = b0; i < b1; ++i) {
       const float x = vals[i];
@@ -452,7 +501,7 @@ DEV void small_encode(const Params& P, uint32_t s, float* vals, uint32_t* hist, 
         b = fmax_nan(b, x);
       }
     }
-    block_minmax(a, b, reinterpret_cast<float*>(sh));
+    block_minmax<NT>(a, b, reinterpret_cast<float*>(sh));
     a = a + 0.0f;
     b = b + 0.0f;
     mn = a;
@@ -476,17 +525,25 @@ DEV void small_encode(const Params& P, uint32_t s, float* vals, uint32_t* hist, 
   }
 }
 
+// ------------------------------------------------------------------------------------------------
+// k_sample: per large segment, sampled thresholds [T_lo, T_hi] for every unit of the segment
+// ------------------------------------------------------------------------------------------------
 template <bool DELTA>
-DEV void sample_thresholds(const Params& P, uint32_t s, uint32_t* keys, uint32_t* hist, uint32_t* sh) {
+__global__ __launch_bounds__(BLOCK) void k_sample(Params P) {
+  constexpr int NT = BLOCK;
+  __shared__ uint32_t keys[SAMPLE_MAX];
+  __shared__ uint32_t hist[HIST_BINS];
+  __shared__ uint32_t sh[64];
   const uint32_t t = threadIdx.x;
+  const uint32_t s = P.large_list[blockIdx.x];
   const SegDev sd = P.segs[s];
   const uint32_t n = sd.n, k = sd.k;
   // R runs of 16 contiguous elements, one per stratum of n / R elements, jittered inside it.
   uint32_t R = n / 512;
-  R = R < 64 ? 64 : (R > 512 ? 512 : R);
+  R = R < 64 ? 64 : (R > SAMPLE_MAX / 16 ? SAMPLE_MAX / 16 : R);
   R &= ~63u;
   const uint32_t m = R * 16;
-  const uint32_t stride = n / R;  // >= 16 because n > SMALL_MAX
+  const uint32_t stride = n / R;  // >= 16 because n > SMALL_MAX >= 1024
   const uint32_t room = stride - 16;
   for (uint32_t it = 0; it < R / 64; ++it) {
     const uint32_t run = it * 64 + (t >> 2), q = t & 3;
@@ -505,184 +562,431 @@ DEV void sample_thresholds(const Params& P, uint32_t s, uint32_t* keys, uint32_t
   const double d = 6.0 * sqrt(se) + 8.0;
   const double rlo = ceil(se + d), rhi = floor(se - d);
   auto each = [&](auto&& f) {
-    for (uint32_t i = t; i < m; i += BLOCK) f(keys[i]);
+    for (uint32_t i = t; i < m; i += NT) f(keys[i]);
   };
-  const uint32_t tlo = rlo >= (double)m ? 0u : block_select(each, 0u, KEY_MAX, (uint32_t)rlo, hist, sh);
-  const uint32_t thi = rhi < 1.0 ? KEY_MAX : block_select(each, 0u, KEY_MAX, (uint32_t)rhi, hist, sh);
-  if (t == 0) {
-    P.tlo[s] = tlo;
-    P.thi[s] = thi;
-    P.status[s] = 0;
+  uint32_t r1 = (uint32_t)rlo, r2 = (uint32_t)rhi;
+  const uint32_t tlo = rlo >= (double)m ? 0u : block_select<NT>(each, 0u, KEY_MAX, r1, hist, sh);
+  const uint32_t thi = rhi < 1.0 ? KEY_MAX : block_select<NT>(each, 0u, KEY_MAX, r2, hist, sh);
+  const uint32_t nu = sd.unit_end - sd.unit_begin;
+  for (uint32_t i = t; i < nu; i += NT) {
+    P.tlo[sd.lu_begin + i] = tlo;
+    P.thi[sd.lu_begin + i] = thi;
   }
+  if (t == 0) P.status[s] = 0;
 }
 
+// k_scan: blocks [0, n_small) encode the small segments; the rest stream the large units, one wave each.
 template <bool DELTA, bool RAW>
-__global__ __launch_bounds__(BLOCK) void k_prep(Params P) {
-  __shared__ uint32_t buf[SMALL_MAX];
-  __shared__ uint32_t hist[HIST_BINS];
-  __shared__ uint32_t sh[16];
-  const uint32_t b = blockIdx.x;
-  if (b < P.n_small)
-    small_encode<DELTA, RAW>(P, P.small_list[b], reinterpret_cast<float*>(buf), hist, sh);
-  else
-    sample_thresholds<DELTA>(P, P.large_list[b - P.n_small], buf, hist, sh);
-}
-
-template <bool DELTA>
 __global__ __launch_bounds__(BLOCK) void k_scan(Params P) {
-  const uint32_t gw = blockIdx.x * WAVES + (threadIdx.x >> 6);
-  if (gw >= P.n_lunits) return;
-  const uint32_t u = P.lunits[gw];
-  const uint32_t s = P.units[u].seg;
-  scan_unit<DELTA>(P, u, P.tlo[s], P.thi[s]);
+  // one LDS arena: small-segment blocks use it as values + histogram, streaming blocks as candidate
+  // staging (WAVES x STAGE_CAP records)
+  constexpr size_t SMALL_BYTES = (SMALL_MAX + HIST_BINS + 64) * 4;
+  constexpr size_t STAGE_BYTES = WAVES * STAGE_CAP * sizeof(uint2);
+  __shared__ __attribute__((aligned(16))) uint8_t arena[SMALL_BYTES > STAGE_BYTES ? SMALL_BYTES : STAGE_BYTES];
+  if (blockIdx.x < P.n_small) {
+    float* sbuf = reinterpret_cast<float*>(arena);
+    uint32_t* hist = reinterpret_cast<uint32_t*>(arena) + SMALL_MAX;
+    uint32_t* sh = hist + HIST_BINS;
+    small_encode<DELTA, RAW>(P, P.small_list[blockIdx.x], sbuf, hist, sh);
+    return;
+  }
+  const uint32_t wv = threadIdx.x >> 6;
+  const uint32_t lu = (blockIdx.x - P.n_small) * WAVES + wv;
+  if (lu >= P.n_lunits) return;
+  const UnitDev L = P.lunits[lu];
+  scan_unit<DELTA, 1>(P, lu, L, P.tlo[lu], P.thi[lu], reinterpret_cast<uint2*>(arena) + wv * STAGE_CAP);
 }
 
 // ------------------------------------------------------------------------------------------------
-// k_select: per large segment — validate the bracket (or re-select exactly), exact k-th key inside B,
-// tie quotas, per-unit output offsets, min/max -> scale.
+// k_select: per large segment, SEL_NT threads
 // ------------------------------------------------------------------------------------------------
-template <bool DELTA, bool RAW>
-__global__ __launch_bounds__(BLOCK) void k_select(Params P) {
-  __shared__ uint32_t hist[HIST_BINS];
-  __shared__ uint32_t sh[16];
-  __shared__ float shf[2 * WAVES];
-  const uint32_t t = threadIdx.x, lane = lane_id(), wv = t >> 6;
-  const uint32_t s = P.large_list[blockIdx.x];
-  const SegDev sd = P.segs[s];
-  const uint32_t ub = sd.unit_begin, ue = sd.unit_end, k = sd.k;
-
-  uint32_t sa = 0, sb = 0;
-  for (uint32_t u = ub + t; u < ue; u += BLOCK) {
-    sa += P.cntA[u];
-    sb += P.cntB[u];
+// Exclusive prefix of cnt[0..cn) into upre[0..cn] (upre[cn] = total). Barriers inside.
+template <int NT>
+DEV uint32_t chunk_prefix(const uint32_t* cnt, uint32_t cn, uint32_t* upre, uint32_t* sh) {
+  const uint32_t t = threadIdx.x;
+  uint32_t carry = 0;
+  for (uint32_t c0 = 0; c0 < cn; c0 += NT) {
+    const uint32_t i = c0 + t;
+    const uint32_t v = i < cn ? cnt[i] : 0u;
+    uint32_t tot;
+    const uint32_t ex = block_excl_scan<NT>(v, sh, tot);
+    if (i < cn) upre[i] = carry + ex;
+    carry += tot;
   }
-  sa = block_sum(sa, sh);
-  sb = block_sum(sb, sh);
-  uint32_t tlo = P.tlo[s], thi = P.thi[s];
+  if (t == 0) upre[cn] = carry;
+  __syncthreads();
+  return carry;
+}
 
-  if ((P.flags & COALAC_FLAG_FORCE_EXACT) || !(sa <= k && k <= sa + sb)) {
+// Visit the candidate records j in [j0, j1) of a chunk (concatenated lists of units lu0 .. lu0+cn-1,
+// in unit order, so j order = index order) calling f(x, unit_in_chunk). Loads are issued SB at a time.
+template <class F>
+DEV void sweep_run(const uint2* cand, uint32_t lu0, const uint32_t* upre, uint32_t cn, uint32_t j0, uint32_t j1,
+                   F&& f) {
+  constexpr int SB = 16;
+  if (j0 >= j1) return;
+  uint32_t lo = 0, hi = cn;  // upre[lo] <= j0 < upre[hi]
+  while (hi - lo > 1) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (upre[mid] <= j0)
+      lo = mid;
+    else
+      hi = mid;
+  }
+  uint32_t ul = lo, cur = upre[ul], nxt = upre[ul + 1];
+  for (uint32_t j = j0; j < j1; j += SB) {
+    float xs[SB];
+    uint32_t us[SB];
+#pragma unroll
+    for (int q = 0; q < SB; ++q) {
+      const uint32_t jj = j + q;
+      us[q] = NONE;
+      xs[q] = 0.0f;
+      if (jj < j1) {
+        while (jj >= nxt) {
+          ++ul;
+          cur = nxt;
+          nxt = upre[ul + 1];
+        }
+        us[q] = ul;
+        xs[q] = __uint_as_float(cand[(uint64_t)(lu0 + ul) * UNIT + (jj - cur)].y);
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < SB; ++q)
+      if (us[q] != NONE) f(xs[q], us[q]);
+  }
+}
+
+// Pick the bin of a HIST_BINS histogram (LDS) holding the r-th largest key: returns the bin, leaves in
+// r the rank inside that bin. sh needs >= 64 words.
+template <int NT>
+DEV uint32_t hist_pick(const uint32_t* hist, uint32_t& r, uint32_t* sh) {
+  constexpr int BPT = HIST_BINS / NT;
+  const uint32_t t = threadIdx.x;
+  uint32_t c[BPT];
+  uint32_t s = 0;
+#pragma unroll
+  for (int j = 0; j < BPT; ++j) {
+    c[j] = hist[t * BPT + j];
+    s += c[j];
+  }
+  uint32_t total;
+  const uint32_t ex = block_excl_scan<NT>(s, sh, total);
+  const uint32_t above = total - ex - s;
+  if (t == 0) {
+    sh[40] = NONE;
+    sh[41] = r;
+  }
+  __syncthreads();
+  if (above < r && r <= above + s) {
+    uint32_t acc = above;
+    int b = (int)(t * BPT);
+#pragma unroll
+    for (int j = BPT - 1; j >= 0; --j) {
+      if (acc + c[j] >= r) {
+        b = (int)(t * BPT) + j;
+        break;
+      }
+      acc += c[j];
+    }
+    sh[40] = (uint32_t)b;
+    sh[41] = r - acc;
+  }
+  __syncthreads();
+  const uint32_t b = sh[40];
+  r = sh[41];
+  __syncthreads();
+  return b;
+}
+
+// LDS scratch of k_select
+struct SelSmem {
+  uint32_t hist[HIST_BINS];
+  uint32_t upre[UCAP + 1];
+  uint32_t ugt[UCAP];
+  uint32_t ueq[UCAP];
+  uint32_t slot_val[SEL_NT * WB];   // per-thread in-window slots (value bits, unit)
+  uint32_t slot_unit[SEL_NT * WB];
+  uint32_t lst_val[SEL_NT * WB];    // in-window entries in index order
+  uint32_t lst_unit[SEL_NT * WB];
+  uint32_t sh[64];
+  float shf[2 * (SEL_NT / 64)];
+};
+
+// Fast path (two sweeps): a histogram sweep over the band [tlo, thi] locates the bin of the k-th key;
+// one more sweep counts, per unit, the keys above that bin and collects the (few) keys inside it into
+// an ordered LDS list, where the exact key and the ties are resolved. Returns false (nothing written)
+// if the bin's entries do not fit the LDS slots (heavy ties); the caller then takes the generic path.
+template <int NT>
+DEV bool select_fast(const Params& P, uint32_t lb, uint32_t nu, uint32_t tlo, uint32_t thi,
+                     uint32_t r, SelSmem& S, uint32_t& T_out, uint32_t& rt_out, uint32_t& fp, uint32_t& fn,
+                     float& gmn, float& gmx) {
+  const uint32_t t = threadIdx.x;
+  const int shift = band_shift(tlo, thi);
+  for (uint32_t i = t; i < HIST_BINS; i += NT) S.hist[i] = 0;
+  for (uint32_t i = t; i < nu; i += NT) {
+    S.ugt[i] = 0;
+    S.ueq[i] = 0;
+  }
+  const uint32_t total = chunk_prefix<NT>(P.cntC + lb, nu, S.upre, S.sh);  // barrier inside
+  const uint32_t E = (total + NT - 1) / NT;
+  const uint32_t j0 = min(total, t * E), j1 = min(total, j0 + E);
+  sweep_run(P.cand, lb, S.upre, nu, j0, j1, [&](float x, uint32_t) {
+    const uint32_t key = fkey(x);
+    if (key >= tlo && key <= thi) atomicAdd(&S.hist[(key - tlo) >> shift], 1u);
+  });
+  __syncthreads();
+  uint32_t rw = r;
+  const uint32_t b = hist_pick<NT>(S.hist, rw, S.sh);
+  if (b == NONE) return false;
+  const uint32_t wlo = tlo + (b << shift);
+  const uint32_t whi = min(thi, wlo + ((1u << shift) - 1u));
+  uint32_t wc = 0, cu = NONE, cg = 0;
+  float lmn = qnan(), lmx = qnan();
+  sweep_run(P.cand, lb, S.upre, nu, j0, j1, [&](float x, uint32_t u) {
+    const uint32_t key = fkey(x);
+    if (key > whi) {
+      if (u != cu) {
+        if (cu != NONE) atomicAdd(&S.ugt[cu], cg);
+        cu = u;
+        cg = 0;
+      }
+      ++cg;
+      lmn = fmin_nan(lmn, x);
+      lmx = fmax_nan(lmx, x);
+    } else if (key >= wlo) {
+      if (wc < WB) {
+        S.slot_val[t * WB + wc] = __float_as_uint(x);
+        S.slot_unit[t * WB + wc] = u;
+      }
+      ++wc;
+    }
+  });
+  if (cu != NONE) atomicAdd(&S.ugt[cu], cg);
+  const uint32_t over = block_sum<NT>(wc > WB ? 1u : 0u, S.sh);
+  if (over) return false;  // uniform: every thread sees the same block sum
+  uint32_t W;
+  const uint32_t wpre = block_excl_scan<NT>(wc, S.sh, W);
+  for (uint32_t q = 0; q < wc; ++q) {
+    S.lst_val[wpre + q] = S.slot_val[t * WB + q];
+    S.lst_unit[wpre + q] = S.slot_unit[t * WB + q];
+  }
+  __syncthreads();
+  // exact k-th key inside the window: the rw-th largest of the W listed keys
+  uint32_t rt = rw;
+  const uint32_t T = block_select<NT>(
+      [&](auto&& f) {
+        for (uint32_t i = t; i < W; i += NT) f(S.lst_val[i] & KEY_MAX);
+      },
+      wlo, whi, rt, S.hist, S.sh);
+  // per-unit counts of the window entries; tie ranks in list (= index) order
+  const uint32_t q0 = min(W, t * WB), q1 = min(W, q0 + WB);
+  uint32_t leq = 0, lfp = NONE, lfn = NONE;
+  for (uint32_t q = q0; q < q1; ++q) {
+    const uint32_t vb = S.lst_val[q];
+    const uint32_t key = vb & KEY_MAX;
+    if (key > T) {
+      atomicAdd(&S.ugt[S.lst_unit[q]], 1u);
+      lmn = fmin_nan(lmn, __uint_as_float(vb));
+      lmx = fmax_nan(lmx, __uint_as_float(vb));
+    } else if (key == T) {
+      atomicAdd(&S.ueq[S.lst_unit[q]], 1u);
+      const bool neg = (vb >> 31) != 0;
+      lfp = min(lfp, neg ? NONE : leq);
+      lfn = min(lfn, neg ? leq : NONE);
+      ++leq;
+    }
+  }
+  uint32_t teq;
+  const uint32_t ex = block_excl_scan<NT>(leq, S.sh, teq);
+  if (t == 0) {
+    S.sh[42] = NONE;
+    S.sh[43] = NONE;
+  }
+  __syncthreads();
+  if (lfp != NONE) atomicMin(&S.sh[42], ex + lfp);
+  if (lfn != NONE) atomicMin(&S.sh[43], ex + lfn);
+  __syncthreads();
+  for (uint32_t i = t; i < nu; i += NT) {
+    P.gtC[lb + i] = S.ugt[i];
+    P.eqC[lb + i] = S.ueq[i];
+  }
+  T_out = T;
+  rt_out = rt;
+  fp = S.sh[42];
+  fn = S.sh[43];
+  gmn = lmn;
+  gmx = lmx;
+  __syncthreads();
+  return true;
+}
+
+// Generic path: radix select over all candidates (1-3 sweeps) + a counts sweep; handles any number
+// of ties and segments of any size (units in chunks of UCAP).
+template <int NT>
+DEV void select_generic(const Params& P, uint32_t lb, uint32_t nu, uint32_t tlo, uint32_t thi, uint32_t r,
+                        SelSmem& S, uint32_t& T_out, uint32_t& rt_out, uint32_t& fp, uint32_t& fn, float& gmn,
+                        float& gmx) {
+  const uint32_t t = threadIdx.x;
+  uint32_t rt = r;
+  auto forC = [&](auto&& f) {
+    for (uint32_t c0 = 0; c0 < nu; c0 += UCAP) {
+      const uint32_t cn = min(UCAP, nu - c0);
+      const uint32_t total = chunk_prefix<NT>(P.cntC + lb + c0, cn, S.upre, S.sh);
+      const uint32_t E = (total + NT - 1) / NT;
+      const uint32_t j0 = min(total, t * E), j1 = min(total, j0 + E);
+      sweep_run(P.cand, lb + c0, S.upre, cn, j0, j1, [&](float x, uint32_t) { f(fkey(x)); });
+      __syncthreads();
+    }
+  };
+  const uint32_t T = rt == 0 ? thi : block_select<NT>(forC, tlo, thi, rt, S.hist, S.sh);
+
+  // counts sweep: per-unit gt/eq, global tie rank of the first positive / negative tie, min/max of
+  // the values with key > T (all of them are kept).
+  float lmn = qnan(), lmx = qnan();
+  uint32_t carry_eq = 0;
+  if (t == 0) {
+    S.sh[42] = NONE;
+    S.sh[43] = NONE;
+  }
+  for (uint32_t c0 = 0; c0 < nu; c0 += UCAP) {
+    const uint32_t cn = min(UCAP, nu - c0);
+    for (uint32_t i = t; i < cn; i += NT) {
+      S.ugt[i] = 0;
+      S.ueq[i] = 0;
+    }
+    const uint32_t total = chunk_prefix<NT>(P.cntC + lb + c0, cn, S.upre, S.sh);
+    const uint32_t E = (total + NT - 1) / NT;
+    const uint32_t j0 = min(total, t * E), j1 = min(total, j0 + E);
+    uint32_t leq = 0, lfp = NONE, lfn = NONE, cu = NONE, cg = 0, ce = 0;
+    sweep_run(P.cand, lb + c0, S.upre, cn, j0, j1, [&](float x, uint32_t u) {
+      if (u != cu) {
+        if (cu != NONE) {
+          if (cg) atomicAdd(&S.ugt[cu], cg);
+          if (ce) atomicAdd(&S.ueq[cu], ce);
+        }
+        cu = u;
+        cg = ce = 0;
+      }
+      const uint32_t key = fkey(x);
+      if (key > T) {
+        ++cg;
+        lmn = fmin_nan(lmn, x);
+        lmx = fmax_nan(lmx, x);
+      } else if (key == T) {
+        const bool neg = (__float_as_uint(x) >> 31) != 0;
+        lfp = min(lfp, neg ? NONE : leq);  // leq only grows: min keeps the first (branch-free)
+        lfn = min(lfn, neg ? leq : NONE);
+        ++leq;
+        ++ce;
+      }
+    });
+    if (cu != NONE) {
+      if (cg) atomicAdd(&S.ugt[cu], cg);
+      if (ce) atomicAdd(&S.ueq[cu], ce);
+    }
+    uint32_t teq;
+    const uint32_t ex = block_excl_scan<NT>(leq, S.sh, teq) + carry_eq;
+    if (lfp != NONE) atomicMin(&S.sh[42], ex + lfp);
+    if (lfn != NONE) atomicMin(&S.sh[43], ex + lfn);
+    carry_eq += teq;
+    for (uint32_t i = t; i < cn; i += NT) {
+      P.gtC[lb + c0 + i] = S.ugt[i];
+      P.eqC[lb + c0 + i] = S.ueq[i];
+    }
+    __syncthreads();
+  }
+  T_out = T;
+  rt_out = rt;
+  fp = S.sh[42];
+  fn = S.sh[43];
+  gmn = lmn;
+  gmx = lmx;
+  __syncthreads();
+}
+
+template <bool DELTA, bool RAW>
+__global__ __launch_bounds__(SEL_NT) void k_select(Params P) {
+  constexpr int NT = SEL_NT;
+  constexpr int NW = NT / 64;
+  __shared__ SelSmem S;
+  const uint32_t t = threadIdx.x, wv = t >> 6;
+  const uint32_t li = blockIdx.x;
+  const uint32_t s = P.large_list[li];
+  const SegDev sd = P.segs[s];
+  const uint32_t lb = sd.lu_begin, nu = sd.unit_end - sd.unit_begin, k = sd.k;
+
+  uint32_t sa = 0, sc = 0;
+  for (uint32_t i = t; i < nu; i += NT) {
+    sa += P.cntA[lb + i];
+    sc += P.cntC[lb + i];
+  }
+  sa = block_sum<NT>(sa, S.sh);
+  sc = block_sum<NT>(sc, S.sh);
+  uint32_t tlo = P.tlo[lb], thi = P.thi[lb];
+  bool exact = false;
+
+  if ((P.flags & COALAC_FLAG_FORCE_EXACT) || !(sa <= k && k <= sc)) {
     // Exact re-selection over the raw segment (rare path): T* of the whole segment, then rewrite the
     // candidate lists with tlo = thi = T*.
     const uint32_t n = sd.n;
-    const uint32_t T = block_select(
+    uint32_t rk = k;
+    const uint32_t T = block_select<NT>(
         [&](auto&& f) {
-          for (uint32_t i = t; i < n; i += BLOCK) f(fkey(load_x1<DELTA>(P, sd.in_off + i)));
+          for (uint32_t i = t; i < n; i += NT) f(fkey(load_x1<DELTA>(P, sd.in_off + i)));
         },
-        0u, KEY_MAX, k, hist, sh);
-    for (uint32_t u = ub + wv; u < ue; u += WAVES) scan_unit<DELTA>(P, u, T, T);
+        0u, KEY_MAX, rk, S.hist, S.sh);
+    for (uint32_t i = wv; i < nu; i += NW) scan_unit<DELTA, 4>(P, lb + i, P.lunits[lb + i], T, T, nullptr);
     __syncthreads();
     sa = 0;
-    sb = 0;
-    for (uint32_t u = ub + t; u < ue; u += BLOCK) {
-      sa += P.cntA[u];
-      sb += P.cntB[u];
-    }
-    sa = block_sum(sa, sh);
-    sb = block_sum(sb, sh);
+    for (uint32_t i = t; i < nu; i += NT) sa += P.cntA[lb + i];
+    sa = block_sum<NT>(sa, S.sh);
     tlo = thi = T;
+    exact = true;
     if (t == 0) P.status[s] = 1;
   }
 
-  const uint32_t r = k - sa;  // rank of the k-th key inside B (0: nothing from B)
-  const uint64_t seg_off = sd.in_off;
-  uint32_t T;
-  if (r == 0) {
-    T = thi;
-  } else {
-    T = block_select(
-        [&](auto&& f) {
-          for (uint32_t u = ub + wv; u < ue; u += WAVES) {
-            const uint64_t reg = seg_off + (uint64_t)(u - ub) * UNIT;
-            const uint32_t nb = P.cntB[u];
-            for (uint32_t i = lane; i < nb; i += 64) f(fkey(P.bV[reg + i]));
-          }
-        },
-        tlo, thi, r, hist, sh);
-  }
+  // rank of the k-th key among candidates with key <= thi (0: none of them)
+  const uint32_t r = k - sa;
+  uint32_t T, rt, fp_rank, fn_rank;
+  float gmn, gmx;
+  bool done = false;
+  if (r > 0 && !exact && nu <= UCAP && !(P.flags & COALAC_FLAG_GENERIC_SELECT))
+    done = select_fast<NT>(P, lb, nu, tlo, thi, r, S, T, rt, fp_rank, fn_rank, gmn, gmx);
+  if (!done) select_generic<NT>(P, lb, nu, tlo, thi, r, S, T, rt, fp_rank, fn_rank, gmn, gmx);
 
-  // counts over B per unit: gt / eq, first positive / negative tie rank; min/max of kept B values
-  float gmn = __int_as_float(0x7FC00000), gmx = __int_as_float(0x7FC00000);
-  uint32_t gsum = 0;
-  for (uint32_t u = ub + wv; u < ue; u += WAVES) {
-    const uint64_t reg = seg_off + (uint64_t)(u - ub) * UNIT;
-    const uint32_t nb = P.cntB[u];
-    uint32_t gt = 0, eq = 0, fp = 0xFFFFFFFFu, fn = 0xFFFFFFFFu;
-    for (uint32_t i0 = 0; i0 < nb; i0 += 64) {
-      const uint32_t i = i0 + lane;
-      const bool valid = i < nb;
-      const float x = valid ? P.bV[reg + i] : 0.0f;
-      const uint32_t key = fkey(x);
-      const bool g = valid && key > T;
-      const bool e = valid && key == T;
-      const uint64_t eb = __ballot(e);
-      gt += (uint32_t)__popcll(__ballot(g));
-      const bool neg = (__float_as_uint(x) >> 31) != 0;
-      const uint64_t pm = __ballot(e && !neg), nm = __ballot(e && neg);
-      if (fp == 0xFFFFFFFFu && pm) {
-        const int fl = __ffsll((long long)pm) - 1;
-        fp = eq + (uint32_t)__popcll(eb & ((1ull << fl) - 1ull));
-      }
-      if (fn == 0xFFFFFFFFu && nm) {
-        const int fl = __ffsll((long long)nm) - 1;
-        fn = eq + (uint32_t)__popcll(eb & ((1ull << fl) - 1ull));
-      }
-      eq += (uint32_t)__popcll(eb);
-      if (g) {
-        gmn = fmin_nan(gmn, x);
-        gmx = fmax_nan(gmx, x);
-      }
-    }
-    if (lane == 0) {
-      P.gtB[u] = gt;
-      P.eqB[u] = eq;
-      P.fpos[u] = fp;
-      P.fneg[u] = fn;
-      gsum += gt;
-    }
-  }
-  for (uint32_t u = ub + t; u < ue; u += BLOCK) {
-    gmn = fmin_nan(gmn, P.minA[u]);
-    gmx = fmax_nan(gmx, P.maxA[u]);
-  }
-  gsum = block_sum(gsum, sh);  // barrier: per-unit counts of all waves are now visible in the block
-  const uint32_t rt = r - gsum;  // ties to keep
-
-  // in-order scan over the units: tie quotas and output offsets
-  uint32_t carry_eq = 0, carry_sel = 0;
-  uint32_t tie_pos = 0, tie_neg = 0;
-  for (uint32_t c0 = ub; c0 < ue; c0 += BLOCK) {
-    const uint32_t u = c0 + t;
-    const bool valid = u < ue;
-    const uint32_t e = valid ? P.eqB[u] : 0u;
+  // in-order scan over the units: global tie prefix and output offsets
+  uint32_t carry_e = 0, carry_sel = 0;
+  for (uint32_t c0 = 0; c0 < nu; c0 += NT) {
+    const uint32_t i = c0 + t;
+    const bool valid = i < nu;
+    const uint32_t e = valid ? P.eqC[lb + i] : 0u;
     uint32_t tot;
-    const uint32_t ex = block_excl_scan(e, sh, tot) + carry_eq;
-    carry_eq += tot;
+    const uint32_t ex = block_excl_scan<NT>(e, S.sh, tot) + carry_e;
+    carry_e += tot;
     const uint32_t quota = !valid ? 0u : (ex >= rt ? 0u : min(e, rt - ex));
-    const uint32_t sel = valid ? P.cntA[u] + P.gtB[u] + quota : 0u;
+    const uint32_t sel = valid ? P.gtC[lb + i] + quota : 0u;
     uint32_t tot2;
-    const uint32_t so = block_excl_scan(sel, sh, tot2) + carry_sel;
+    const uint32_t so = block_excl_scan<NT>(sel, S.sh, tot2) + carry_sel;
     carry_sel += tot2;
     if (valid) {
-      P.quota[u] = quota;
-      P.outoff[u] = so;
-      if (quota > 0) {
-        tie_pos |= P.fpos[u] < quota;
-        tie_neg |= P.fneg[u] < quota;
-      }
+      P.eqpre[lb + i] = ex;
+      P.outoff[lb + i] = so;
     }
   }
   float mn = 0.0f, scale = 0.0f;
   if (!RAW) {
     const float tv = __uint_as_float(T);
-    if (tie_pos) {
+    if (t == 0 && fp_rank < rt) {
       gmn = fmin_nan(gmn, tv);
       gmx = fmax_nan(gmx, tv);
     }
-    if (tie_neg) {
+    if (t == 0 && fn_rank < rt) {
       gmn = fmin_nan(gmn, -tv);
       gmx = fmax_nan(gmx, -tv);
     }
-    block_minmax(gmn, gmx, shf);
+    block_minmax<NT>(gmn, gmx, S.shf);
     gmn = gmn + 0.0f;
     gmx = gmx + 0.0f;
     mn = gmn;
@@ -690,146 +994,140 @@ __global__ __launch_bounds__(BLOCK) void k_select(Params P) {
   }
   if (t == 0) {
     P.tstar[s] = T;
+    P.rtie[s] = rt;
     P.mn[s] = mn;
     P.scale[s] = scale;
   }
 }
 
 // ------------------------------------------------------------------------------------------------
-// k_emit: per large unit (one wave) — merge A and the kept part of B in index order through an LDS
-// tile + bitmap, write sorted idx and codes.
+// k_emit: per large unit (one wave) — the candidate list is already in index order: keep key > T and
+// the ties whose segment-wide tie rank is < rt, compact with ballots, write idx + code. No LDS.
 // ------------------------------------------------------------------------------------------------
 template <bool RAW>
 __global__ __launch_bounds__(BLOCK) void k_emit(Params P) {
-  __shared__ float tile[WAVES][UNIT];
-  __shared__ unsigned long long bm[WAVES][64];
   const uint32_t lane = lane_id(), wv = threadIdx.x >> 6;
-  const uint32_t gw = blockIdx.x * WAVES + wv;
-  if (gw >= P.n_lunits) return;
-  const uint32_t u = P.lunits[gw];
-  const UnitDev ud = P.units[u];
-  const SegDev sd = P.segs[ud.seg];
-  const uint64_t reg = sd.in_off + ud.start;
-  const uint32_t nA = P.cntA[u], nB = P.cntB[u];
-  if (nA == 0 && nB == 0) return;
-  const uint32_t T = P.tstar[ud.seg], quota = P.quota[u];
-  float* tl = tile[wv];
-  bm[wv][lane] = 0ull;
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  for (uint32_t i = lane; i < nA; i += 64) {
-    const uint32_t pos = (uint32_t)P.aI[reg + i] - ud.start;
-    tl[pos] = P.aV[reg + i];
-    atomicOr(&bm[wv][pos >> 6], 1ull << (pos & 63));
-  }
-  uint32_t eqc = 0;
-  for (uint32_t i0 = 0; i0 < nB; i0 += 64) {
+  const uint32_t lu = blockIdx.x * WAVES + wv;
+  if (lu >= P.n_lunits) return;
+  const uint32_t nC = P.cntC[lu];
+  if (nC == 0) return;
+  const UnitDev L = P.lunits[lu];
+  const uint32_t eqp = P.eqpre[lu], oo = P.outoff[lu];
+  const uint32_t T = P.tstar[L.seg], rt = P.rtie[L.seg];
+  const float mn = RAW ? 0.0f : P.mn[L.seg];
+  const float scale = RAW ? 0.0f : P.scale[L.seg];
+  const uint2* R = P.cand + (uint64_t)lu * UNIT;
+  const uint64_t obase = L.out_off + oo;
+  uint32_t eqc = 0, outc = 0;
+  for (uint32_t i0 = 0; i0 < nC; i0 += 64) {
     const uint32_t i = i0 + lane;
-    const bool valid = i < nB;
-    const float x = valid ? P.bV[reg + i] : 0.0f;
+    const bool valid = i < nC;
+    const uint2 rec = valid ? R[i] : make_uint2(0u, 0u);
+    const float x = __uint_as_float(rec.y);
     const uint32_t key = fkey(x);
     const bool e = valid && key == T;
     const uint64_t eb = __ballot(e);
-    const uint32_t rank = eqc + mbcnt(eb);
+    const uint32_t rank = eqp + eqc + mbcnt(eb);
     eqc += (uint32_t)__popcll(eb);
-    const bool sel = (valid && key > T) || (e && rank < quota);
+    const bool sel = valid && (key > T || (e && rank < rt));
+    const uint64_t sb = __ballot(sel);
     if (sel) {
-      const uint32_t pos = (uint32_t)P.bI[reg + i] - ud.start;
-      tl[pos] = x;
-      atomicOr(&bm[wv][pos >> 6], 1ull << (pos & 63));
+      const uint64_t o = obase + outc + mbcnt(sb);
+      P.idx[o] = (int32_t)(rec.x & ~A_FLAG);
+      store_val<RAW>(P, o, x, mn, scale);
     }
-  }
-  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  unsigned long long word = bm[wv][lane];
-  const uint32_t c = (uint32_t)__popcll(word);
-  const uint32_t pre = wave_incl_scan(c) - c;
-  const float mn = RAW ? 0.0f : P.mn[ud.seg];
-  const float scale = RAW ? 0.0f : P.scale[ud.seg];
-  uint64_t o = sd.out_off + P.outoff[u] + pre;
-  while (word) {
-    const int b = __ffsll((long long)word) - 1;
-    word &= word - 1ull;
-    const uint32_t pos = lane * 64 + (uint32_t)b;
-    P.idx[o] = (int32_t)(ud.start + pos);
-    store_val<RAW>(P, o, tl[pos], mn, scale);
-    ++o;
+    outc += (uint32_t)__popcll(sb);
   }
 }
 
 // ------------------------------------------------------------------------------------------------
 // decode
 // ------------------------------------------------------------------------------------------------
-// first position in L[lo, hi) with L[pos] >= target (hi if none); the whole wave cooperates: 64-ary
-// search, one probe per lane per round.
-DEV uint32_t wave_lower_bound(const int32_t* L, uint32_t lo, uint32_t hi, int32_t target) {
-  const uint32_t lane = lane_id();
-  while (hi - lo > 64) {
-    const uint32_t step = (hi - lo + 63) / 64;
-    const uint32_t p = lo + lane * step;
-    const bool pred = lane > 0 && p < hi && L[p] >= target;
-    const uint64_t m = __ballot(pred);
-    const uint32_t f = m ? (uint32_t)(__ffsll((long long)m) - 1) : 64u;
-    const uint32_t jmax = (hi - 1 - lo) / step;
-    const uint32_t nlo = lo + min(f - 1, jmax) * step;
-    const uint32_t nhi = f < 64 ? lo + f * step : hi;
-    lo = nlo;
-    hi = nhi;
+// k_bounds: ustart[u] = first kept entry whose index falls in unit u or later. One block per chunk of
+// <= BCHUNK entries of one segment's sorted idx list, 16 consecutive entries per thread (loads batched).
+// Indices are range-checked (the list may come from an untrusted blob): a corrupt list can only
+// mis-decode, never write out of bounds.
+struct BChunk {
+  uint32_t seg, e0, e1, pad;
+};
+
+__global__ __launch_bounds__(BLOCK) void k_bounds(Params P, const BChunk* chunks) {
+  constexpr uint32_t EPT = BCHUNK / BLOCK;
+  const BChunk C = chunks[blockIdx.x];
+  const SegDev sd = P.segs[C.seg];
+  const uint32_t nu = sd.unit_end - sd.unit_begin, k = sd.k;
+  const int32_t* L = P.cidx + sd.out_off;
+  uint32_t* us = P.ustart + sd.unit_begin;
+  const uint32_t e0 = C.e0 + threadIdx.x * EPT;
+  if (e0 >= C.e1) return;
+  uint32_t ix[EPT + 1];
+#pragma unroll
+  for (uint32_t q = 0; q <= EPT; ++q) {
+    const uint32_t e = e0 + q - 1;  // q = 0: the entry before e0
+    ix[q] = (q == 0 && e0 == 0) ? 0u : (e < C.e1 ? (uint32_t)L[e] : 0u);
   }
-  const bool pred = lo + lane < hi && L[lo + lane] >= target;
-  const uint64_t m = __ballot(pred);
-  return m ? lo + (uint32_t)(__ffsll((long long)m) - 1) : hi;
+#pragma unroll
+  for (uint32_t q = 1; q <= EPT; ++q) {
+    const uint32_t e = e0 + q - 1;
+    if (e < C.e1) {
+      const uint32_t u = min(ix[q] >> UNIT_SHIFT, nu - 1);
+      const uint32_t v0 = e == 0 ? 0u : min(ix[q - 1] >> UNIT_SHIFT, nu - 1) + 1;
+      for (uint32_t v = v0; v <= u; ++v) us[v] = e;
+      if (e == k - 1)
+        for (uint32_t v = u + 1; v < nu; ++v) us[v] = k;
+    }
+  }
 }
 
+// k_decode: one wave per unit, no LDS. Store the unit's dense background (zeros, or base + 0.0f), wait
+// until those stores are complete (s_waitcnt vmcnt(0): later stores to the same addresses are then
+// ordered after them), then scatter the kept values. The scattered lines are still dirty in L2, so HBM
+// sees each line written once.
 template <bool RAW, bool HASBASE>
 __global__ __launch_bounds__(BLOCK) void k_decode(Params P) {
-  __shared__ float4 tile[WAVES][UNIT / 4];
   const uint32_t lane = lane_id(), wv = threadIdx.x >> 6;
   const uint32_t u = blockIdx.x * WAVES + wv;
   if (u >= P.n_units) return;
-  const UnitDev ud = P.units[u];
-  const SegDev sd = P.segs[ud.seg];
-  const uint32_t len = min(UNIT, sd.n - ud.start);
-  const uint64_t off = sd.in_off + ud.start;
-  float4* tl = tile[wv];
-  const float4 z = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-#pragma unroll
-  for (uint32_t it = 0; it < UNIT_IT; ++it) tl[it * 64 + lane] = z;
-
-  const int32_t* L = P.cidx + sd.out_off;
-  const uint32_t lo = wave_lower_bound(L, 0u, sd.k, (int32_t)ud.start);
-  const uint32_t hi = wave_lower_bound(L, lo, sd.k, (int32_t)(ud.start + len));
-  const float mn = RAW ? 0.0f : P.cmn[ud.seg];
-  const float scale = RAW ? 0.0f : P.cscale[ud.seg];
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  float* tf = reinterpret_cast<float*>(tl);
-  for (uint32_t e = lo + lane; e < hi; e += 64) {
-    const uint32_t pos = (uint32_t)L[e] - ud.start;
-    tf[pos] = load_val<RAW>(P, sd.out_off + e, mn, scale);
-  }
-  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-  __builtin_amdgcn_wave_barrier();
+  const UnitDev U = P.units[u];
+  // clamp: ustart comes from a possibly untrusted idx list
+  const uint32_t lo = min(P.ustart[u], U.k);
+  const uint32_t hi = min(U.last ? U.k : P.ustart[u + 1], U.k);
+  const float mn = RAW ? 0.0f : P.cmn[U.seg];
+  const float scale = RAW ? 0.0f : P.cscale[U.seg];
+  const uint32_t len = U.len;
+  const int32_t* Lx = P.cidx + U.out_off;
+  // first batch of kept entries, loaded before the background stores
+  const uint32_t e = lo + lane;
+  const bool has = e < hi;
+  const uint32_t pos0 = has ? (uint32_t)Lx[e] - U.start : NONE;
+  const float v0 = has ? load_val<RAW>(P, U.out_off + e, mn, scale) : 0.0f;
+  float* out = P.out + U.off;
+  const float* bs = HASBASE ? P.base + U.off : nullptr;
   if (len == UNIT) {
+    float4 bv[UNIT_IT];
 #pragma unroll
     for (uint32_t it = 0; it < UNIT_IT; ++it) {
-      const uint32_t e = (it * 64 + lane) * 4;
-      float4 v = tl[it * 64 + lane];
       if (HASBASE) {
-        const float4 b = *reinterpret_cast<const float4*>(P.base + off + e);
-        v.x = b.x + v.x;
-        v.y = b.y + v.y;
-        v.z = b.z + v.z;
-        v.w = b.w + v.w;
+        bv[it] = *reinterpret_cast<const float4*>(bs + (it * 64 + lane) * 4);
+        bv[it].x = bv[it].x + 0.0f;
+        bv[it].y = bv[it].y + 0.0f;
+        bv[it].z = bv[it].z + 0.0f;
+        bv[it].w = bv[it].w + 0.0f;
+      } else {
+        bv[it] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
       }
-      *reinterpret_cast<float4*>(P.out + off + e) = v;
     }
+#pragma unroll
+    for (uint32_t it = 0; it < UNIT_IT; ++it) *reinterpret_cast<float4*>(out + (it * 64 + lane) * 4) = bv[it];
   } else {
-    for (uint32_t e = lane; e < len; e += 64) {
-      float v = tf[e];
-      if (HASBASE) v = P.base[off + e] + v;
-      P.out[off + e] = v;
-    }
+    for (uint32_t i = lane; i < len; i += 64) out[i] = HASBASE ? bs[i] + 0.0f : 0.0f;
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if (pos0 < len) out[pos0] = HASBASE ? bs[pos0] + v0 : v0;
+  for (uint32_t e2 = lo + 64 + lane; e2 < hi; e2 += 64) {
+    const uint32_t pos = (uint32_t)Lx[e2] - U.start;
+    const float v = load_val<RAW>(P, U.out_off + e2, mn, scale);
+    if (pos < len) out[pos] = HASBASE ? bs[pos] + v : v;
   }
 }
 
@@ -848,22 +1146,22 @@ int fail(int code, const char* fmt, ...) {
   return code;
 }
 
-#define HIP_CHECK(expr)                                                                   \
-  do {                                                                                    \
-    hipError_t e_ = (expr);                                                               \
+#define HIP_CHECK(expr)                                                                             \
+  do {                                                                                              \
+    hipError_t e_ = (expr);                                                                         \
     if (e_ != hipSuccess) return fail(COALAC_EHIP, "%s failed: %s", #expr, hipGetErrorString(e_)); \
   } while (0)
 
 size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 
 struct WsLayout {
-  size_t tlo, thi, tstar, status;
-  size_t cntA, cntB, gtB, eqB, fpos, fneg, quota, outoff, minA, maxA;
-  size_t aI, aV, bI, bV;
+  size_t tstar, rtie, status;
+  size_t tlo, thi, cntA, cntC, gtC, eqC, eqpre, outoff;
+  size_t cand;
   size_t total;
 };
 
-WsLayout ws_layout(size_t S, size_t U, size_t span) {
+WsLayout ws_layout(size_t S, size_t LU) {
   WsLayout L{};
   size_t o = 0;
   auto take = [&](size_t bytes) {
@@ -871,24 +1169,18 @@ WsLayout ws_layout(size_t S, size_t U, size_t span) {
     o = align_up(o + bytes, 256);
     return r;
   };
-  L.tlo = take(4 * S);
-  L.thi = take(4 * S);
   L.tstar = take(4 * S);
+  L.rtie = take(4 * S);
   L.status = take(4 * S);
-  L.cntA = take(4 * U);
-  L.cntB = take(4 * U);
-  L.gtB = take(4 * U);
-  L.eqB = take(4 * U);
-  L.fpos = take(4 * U);
-  L.fneg = take(4 * U);
-  L.quota = take(4 * U);
-  L.outoff = take(4 * U);
-  L.minA = take(4 * U);
-  L.maxA = take(4 * U);
-  L.aI = take(4 * span);
-  L.aV = take(4 * span);
-  L.bI = take(4 * span);
-  L.bV = take(4 * span);
+  L.tlo = take(4 * LU);
+  L.thi = take(4 * LU);
+  L.cntA = take(4 * LU);
+  L.cntC = take(4 * LU);
+  L.gtC = take(4 * LU);
+  L.eqC = take(4 * LU);
+  L.eqpre = take(4 * LU);
+  L.outoff = take(4 * LU);
+  L.cand = take(sizeof(uint2) * UNIT * LU);
   L.total = std::max<size_t>(o, 256);
   return L;
 }
@@ -904,13 +1196,18 @@ struct coalac_plan {
   void* meta = nullptr;
   SegDev* segs = nullptr;
   UnitDev* units = nullptr;
+  UnitDev* lunits = nullptr;
   uint32_t* small_list = nullptr;
   uint32_t* large_list = nullptr;
-  uint32_t* lunits = nullptr;
+  BChunk* bchunks = nullptr;
+  uint32_t n_bchunks = 0;
   WsLayout ws{};
+  size_t dec_ws = 0;
 };
 
-static int check_device(coalac_plan_t plan) {
+namespace {
+
+int check_device(coalac_plan_t plan) {
   int dev = -1;
   HIP_CHECK(hipGetDevice(&dev));
   if (dev != plan->device)
@@ -918,12 +1215,13 @@ static int check_device(coalac_plan_t plan) {
   return COALAC_OK;
 }
 
-static void fill_meta(Params& P, coalac_plan_t plan) {
+void fill_meta(Params& P, coalac_plan_t plan) {
   P.segs = plan->segs;
   P.units = plan->units;
+  P.lunits = plan->lunits;
   P.small_list = plan->small_list;
   P.large_list = plan->large_list;
-  P.lunits = plan->lunits;
+  P.nseg = (uint32_t)plan->nseg;
   P.n_small = plan->n_small;
   P.n_large = plan->n_large;
   P.n_units = plan->n_units;
@@ -931,24 +1229,25 @@ static void fill_meta(Params& P, coalac_plan_t plan) {
   P.levels = plan->bits == 32 ? 0.0f : (float)((1u << plan->bits) - 1u);
 }
 
-static void record(void* const* ev, int i, hipStream_t st) {
+void record(void* const* ev, int i, hipStream_t st) {
   if (ev && ev[i]) (void)hipEventRecord(static_cast<hipEvent_t>(ev[i]), st);
 }
 
 template <bool DELTA, bool RAW>
-static void launch_encode(const Params& P, coalac_plan_t plan, hipStream_t st, void* const* ev) {
-  const uint32_t g1 = plan->n_small + plan->n_large;
-  record(ev, 0, st);
-  if (g1) hipLaunchKernelGGL((k_prep<DELTA, RAW>), dim3(g1), dim3(BLOCK), 0, st, P);
-  record(ev, 1, st);
+void launch_encode(const Params& P, coalac_plan_t plan, hipStream_t st, void* const* ev) {
   const uint32_t gu = (plan->n_lunits + WAVES - 1) / WAVES;
-  if (plan->n_large) hipLaunchKernelGGL((k_scan<DELTA>), dim3(gu), dim3(BLOCK), 0, st, P);
+  record(ev, 0, st);
+  if (plan->n_large) hipLaunchKernelGGL((k_sample<DELTA>), dim3(plan->n_large), dim3(BLOCK), 0, st, P);
+  record(ev, 1, st);
+  if (plan->n_small + gu) hipLaunchKernelGGL((k_scan<DELTA, RAW>), dim3(plan->n_small + gu), dim3(BLOCK), 0, st, P);
   record(ev, 2, st);
-  if (plan->n_large) hipLaunchKernelGGL((k_select<DELTA, RAW>), dim3(plan->n_large), dim3(BLOCK), 0, st, P);
+  if (plan->n_large) hipLaunchKernelGGL((k_select<DELTA, RAW>), dim3(plan->n_large), dim3(SEL_NT), 0, st, P);
   record(ev, 3, st);
   if (plan->n_large) hipLaunchKernelGGL((k_emit<RAW>), dim3(gu), dim3(BLOCK), 0, st, P);
   record(ev, 4, st);
 }
+
+}  // namespace
 
 extern "C" {
 
@@ -963,31 +1262,44 @@ int coalac_plan_create(const coalac_seg_t* h_segs, int nseg, int bits, coalac_pl
   if (!((bits >= 1 && bits <= 8) || bits == 32)) return fail(COALAC_EBITS, "unsupported bits=%d (1..8 or 32)", bits);
 
   std::vector<SegDev> segs(nseg);
-  std::vector<UnitDev> units;
-  std::vector<uint32_t> small_list, large_list, lunits;
+  std::vector<UnitDev> units, lunits;
+  std::vector<BChunk> bchunks;
+  std::vector<uint32_t> small_list, large_list;
   uint64_t span = 0, total_k = 0;
   std::vector<std::pair<uint64_t, uint64_t>> in_r, out_r;
   for (int s = 0; s < nseg; ++s) {
     const coalac_seg_t& g = h_segs[s];
     if (g.n >= (1ull << 31)) return fail(COALAC_EINVAL, "segment %d: n=%llu >= 2^31", s, (unsigned long long)g.n);
-    if (g.in_off % 4) return fail(COALAC_EINVAL, "segment %d: in_off=%llu not a multiple of 4", s, (unsigned long long)g.in_off);
+    if (g.in_off % 4)
+      return fail(COALAC_EINVAL, "segment %d: in_off=%llu not a multiple of 4", s, (unsigned long long)g.in_off);
     if (g.n == 0 ? g.k != 0 : (g.k < 1 || g.k > g.n))
-      return fail(COALAC_EINVAL, "segment %d: k=%llu invalid for n=%llu", s, (unsigned long long)g.k, (unsigned long long)g.n);
+      return fail(COALAC_EINVAL, "segment %d: k=%llu invalid for n=%llu", s, (unsigned long long)g.k,
+                  (unsigned long long)g.n);
     if (g.in_off > (1ull << 46) || g.out_off > (1ull << 46)) return fail(COALAC_EINVAL, "segment %d: offset too large", s);
     SegDev d{};
     d.in_off = g.in_off;
+    d.out_off = g.out_off;
     d.n = (uint32_t)g.n;
     d.k = (uint32_t)g.k;
-    d.out_off = g.out_off;
     d.unit_begin = (uint32_t)units.size();
-    for (uint64_t st = 0; st < g.n; st += UNIT) units.push_back(UnitDev{(uint32_t)s, (uint32_t)st});
-    d.unit_end = (uint32_t)units.size();
-    if (g.n <= SMALL_MAX) {
-      small_list.push_back((uint32_t)s);
-    } else {
-      large_list.push_back((uint32_t)s);
-      for (uint32_t u = d.unit_begin; u < d.unit_end; ++u) lunits.push_back(u);
+    const bool large = g.n > SMALL_MAX;
+    d.lu_begin = large ? (uint32_t)lunits.size() : 0u;
+    for (uint64_t st = 0; st < g.n; st += UNIT) {
+      UnitDev u{};
+      u.off = g.in_off + st;
+      u.out_off = g.out_off;
+      u.seg = (uint32_t)s;
+      u.start = (uint32_t)st;
+      u.k = (uint32_t)g.k;
+      u.len = (uint16_t)std::min<uint64_t>(UNIT, g.n - st);
+      u.last = st + UNIT >= g.n ? 1 : 0;
+      units.push_back(u);
+      if (large) lunits.push_back(u);
     }
+    d.unit_end = (uint32_t)units.size();
+    (large ? large_list : small_list).push_back((uint32_t)s);
+    for (uint64_t e0 = 0; e0 < g.k; e0 += BCHUNK)
+      bchunks.push_back(BChunk{(uint32_t)s, (uint32_t)e0, (uint32_t)std::min<uint64_t>(g.k, e0 + BCHUNK), 0u});
     segs[s] = d;
     if (g.n) {
       span = std::max<uint64_t>(span, g.in_off + g.n);
@@ -996,6 +1308,7 @@ int coalac_plan_create(const coalac_seg_t* h_segs, int nseg, int bits, coalac_pl
       out_r.push_back({g.out_off, g.out_off + g.k});
     }
   }
+  if (lunits.size() >= (1ull << 32) / UNIT) return fail(COALAC_EINVAL, "plan too large (%zu large units)", lunits.size());
   auto overlaps = [](std::vector<std::pair<uint64_t, uint64_t>>& r) {
     std::sort(r.begin(), r.end());
     for (size_t i = 1; i < r.size(); ++i)
@@ -1015,22 +1328,26 @@ int coalac_plan_create(const coalac_seg_t* h_segs, int nseg, int bits, coalac_pl
   p->n_large = (uint32_t)large_list.size();
   p->n_units = (uint32_t)units.size();
   p->n_lunits = (uint32_t)lunits.size();
+  p->n_bchunks = (uint32_t)bchunks.size();
   p->span = span;
   p->total_k = total_k;
-  p->ws = ws_layout((size_t)nseg, units.size(), (size_t)span);
+  p->ws = ws_layout((size_t)nseg, lunits.size());
+  p->dec_ws = align_up(4 * (units.size() + 1), 256);
 
-  size_t o_segs = 0;
-  size_t o_units = align_up(o_segs + sizeof(SegDev) * segs.size(), 256);
-  size_t o_small = align_up(o_units + sizeof(UnitDev) * units.size(), 256);
-  size_t o_large = align_up(o_small + 4 * small_list.size(), 256);
-  size_t o_lunits = align_up(o_large + 4 * large_list.size(), 256);
-  size_t bytes = align_up(o_lunits + 4 * lunits.size(), 256) + 256;
+  const size_t o_segs = 0;
+  const size_t o_units = align_up(o_segs + sizeof(SegDev) * segs.size(), 256);
+  const size_t o_lunits = align_up(o_units + sizeof(UnitDev) * units.size(), 256);
+  const size_t o_small = align_up(o_lunits + sizeof(UnitDev) * lunits.size(), 256);
+  const size_t o_large = align_up(o_small + 4 * small_list.size(), 256);
+  const size_t o_bch = align_up(o_large + 4 * large_list.size(), 256);
+  const size_t bytes = align_up(o_bch + sizeof(BChunk) * bchunks.size(), 256) + 256;
   std::vector<uint8_t> host(bytes, 0);
   if (!segs.empty()) memcpy(host.data() + o_segs, segs.data(), sizeof(SegDev) * segs.size());
   if (!units.empty()) memcpy(host.data() + o_units, units.data(), sizeof(UnitDev) * units.size());
+  if (!lunits.empty()) memcpy(host.data() + o_lunits, lunits.data(), sizeof(UnitDev) * lunits.size());
   if (!small_list.empty()) memcpy(host.data() + o_small, small_list.data(), 4 * small_list.size());
   if (!large_list.empty()) memcpy(host.data() + o_large, large_list.data(), 4 * large_list.size());
-  if (!lunits.empty()) memcpy(host.data() + o_lunits, lunits.data(), 4 * lunits.size());
+  if (!bchunks.empty()) memcpy(host.data() + o_bch, bchunks.data(), sizeof(BChunk) * bchunks.size());
   hipError_t e = hipMalloc(&p->meta, bytes);
   if (e != hipSuccess) {
     delete p;
@@ -1045,9 +1362,10 @@ int coalac_plan_create(const coalac_seg_t* h_segs, int nseg, int bits, coalac_pl
   uint8_t* m = static_cast<uint8_t*>(p->meta);
   p->segs = reinterpret_cast<SegDev*>(m + o_segs);
   p->units = reinterpret_cast<UnitDev*>(m + o_units);
+  p->lunits = reinterpret_cast<UnitDev*>(m + o_lunits);
   p->small_list = reinterpret_cast<uint32_t*>(m + o_small);
   p->large_list = reinterpret_cast<uint32_t*>(m + o_large);
-  p->lunits = reinterpret_cast<uint32_t*>(m + o_lunits);
+  p->bchunks = reinterpret_cast<BChunk*>(m + o_bch);
   *out = p;
   return COALAC_OK;
 }
@@ -1063,21 +1381,15 @@ int coalac_plan_destroy(coalac_plan_t plan) {
   return COALAC_OK;
 }
 
-int coalac_plan_query(coalac_plan_t plan, uint64_t* ws_bytes, uint64_t* total_k, uint64_t* span,
-                      uint64_t* n_units) {
+int coalac_plan_query(coalac_plan_t plan, uint64_t* ws_bytes, uint64_t* dec_ws_bytes, uint64_t* total_k,
+                      uint64_t* span, uint64_t* n_units) {
   if (!plan) return fail(COALAC_EINVAL, "coalac_plan_query: plan is NULL");
   if (ws_bytes) *ws_bytes = plan->ws.total;
+  if (dec_ws_bytes) *dec_ws_bytes = plan->dec_ws;
   if (total_k) *total_k = plan->total_k;
   if (span) *span = plan->span;
   if (n_units) *n_units = plan->n_units;
   return COALAC_OK;
-}
-
-int coalac_encode(coalac_plan_t plan, const float* d_in, const float* d_base, int32_t* d_idx,
-                  void* d_vals, float* d_mn, float* d_scale, void* d_ws, uint64_t ws_bytes,
-                  unsigned flags, void* stream) {
-  return coalac_encode_ev(plan, d_in, d_base, d_idx, d_vals, d_mn, d_scale, d_ws, ws_bytes, flags, stream,
-                          nullptr);
 }
 
 int coalac_encode_ev(coalac_plan_t plan, const float* d_in, const float* d_base, int32_t* d_idx,
@@ -1106,24 +1418,18 @@ int coalac_encode_ev(coalac_plan_t plan, const float* d_in, const float* d_base,
   P.flags = flags;
   uint8_t* w = static_cast<uint8_t*>(d_ws);
   const WsLayout& L = plan->ws;
+  P.tstar = reinterpret_cast<uint32_t*>(w + L.tstar);
+  P.rtie = reinterpret_cast<uint32_t*>(w + L.rtie);
+  P.status = reinterpret_cast<uint32_t*>(w + L.status);
   P.tlo = reinterpret_cast<uint32_t*>(w + L.tlo);
   P.thi = reinterpret_cast<uint32_t*>(w + L.thi);
-  P.tstar = reinterpret_cast<uint32_t*>(w + L.tstar);
-  P.status = reinterpret_cast<uint32_t*>(w + L.status);
   P.cntA = reinterpret_cast<uint32_t*>(w + L.cntA);
-  P.cntB = reinterpret_cast<uint32_t*>(w + L.cntB);
-  P.gtB = reinterpret_cast<uint32_t*>(w + L.gtB);
-  P.eqB = reinterpret_cast<uint32_t*>(w + L.eqB);
-  P.fpos = reinterpret_cast<uint32_t*>(w + L.fpos);
-  P.fneg = reinterpret_cast<uint32_t*>(w + L.fneg);
-  P.quota = reinterpret_cast<uint32_t*>(w + L.quota);
+  P.cntC = reinterpret_cast<uint32_t*>(w + L.cntC);
+  P.gtC = reinterpret_cast<uint32_t*>(w + L.gtC);
+  P.eqC = reinterpret_cast<uint32_t*>(w + L.eqC);
+  P.eqpre = reinterpret_cast<uint32_t*>(w + L.eqpre);
   P.outoff = reinterpret_cast<uint32_t*>(w + L.outoff);
-  P.minA = reinterpret_cast<float*>(w + L.minA);
-  P.maxA = reinterpret_cast<float*>(w + L.maxA);
-  P.aI = reinterpret_cast<int32_t*>(w + L.aI);
-  P.aV = reinterpret_cast<float*>(w + L.aV);
-  P.bI = reinterpret_cast<int32_t*>(w + L.bI);
-  P.bV = reinterpret_cast<float*>(w + L.bV);
+  P.cand = reinterpret_cast<uint2*>(w + L.cand);
   hipStream_t st = static_cast<hipStream_t>(stream);
   const bool delta = d_base != nullptr, raw = plan->bits == 32;
   if (delta && raw)
@@ -1138,14 +1444,15 @@ int coalac_encode_ev(coalac_plan_t plan, const float* d_in, const float* d_base,
   return COALAC_OK;
 }
 
-int coalac_decode(coalac_plan_t plan, const int32_t* d_idx, const void* d_vals, const float* d_mn,
-                  const float* d_scale, const float* d_base, float* d_out, void* stream) {
-  return coalac_decode_ev(plan, d_idx, d_vals, d_mn, d_scale, d_base, d_out, stream, nullptr);
+int coalac_encode(coalac_plan_t plan, const float* d_in, const float* d_base, int32_t* d_idx, void* d_vals,
+                  float* d_mn, float* d_scale, void* d_ws, uint64_t ws_bytes, unsigned flags, void* stream) {
+  return coalac_encode_ev(plan, d_in, d_base, d_idx, d_vals, d_mn, d_scale, d_ws, ws_bytes, flags, stream,
+                          nullptr);
 }
 
 int coalac_decode_ev(coalac_plan_t plan, const int32_t* d_idx, const void* d_vals, const float* d_mn,
-                     const float* d_scale, const float* d_base, float* d_out, void* stream,
-                     void* const* events) {
+                     const float* d_scale, const float* d_base, float* d_out, void* d_ws, uint64_t ws_bytes,
+                     void* stream, void* const* events) {
   if (!plan) return fail(COALAC_EINVAL, "coalac_decode: plan is NULL");
   if (plan->n_units == 0) return COALAC_OK;
   if (!d_out) return fail(COALAC_EINVAL, "coalac_decode: output pointer is NULL");
@@ -1153,6 +1460,9 @@ int coalac_decode_ev(coalac_plan_t plan, const int32_t* d_idx, const void* d_val
   if (plan->bits != 32 && (!d_mn || !d_scale)) return fail(COALAC_EINVAL, "coalac_decode: mn/scale pointers are NULL");
   if ((reinterpret_cast<uintptr_t>(d_out) | reinterpret_cast<uintptr_t>(d_base)) & 15)
     return fail(COALAC_EINVAL, "coalac_decode: output/base must be 16-byte aligned");
+  if (!d_ws || ws_bytes < plan->dec_ws)
+    return fail(COALAC_EWORKSPACE, "coalac_decode: workspace %llu < required %llu", (unsigned long long)ws_bytes,
+                (unsigned long long)plan->dec_ws);
   int rc = check_device(plan);
   if (rc) return rc;
   Params P{};
@@ -1163,10 +1473,13 @@ int coalac_decode_ev(coalac_plan_t plan, const int32_t* d_idx, const void* d_val
   P.cscale = d_scale;
   P.base = d_base;
   P.out = d_out;
+  P.ustart = static_cast<uint32_t*>(d_ws);
   hipStream_t st = static_cast<hipStream_t>(stream);
   const uint32_t g = (plan->n_units + WAVES - 1) / WAVES;
   const bool raw = plan->bits == 32, hb = d_base != nullptr;
   record(events, 0, st);
+  if (plan->n_bchunks) hipLaunchKernelGGL(k_bounds, dim3(plan->n_bchunks), dim3(BLOCK), 0, st, P, plan->bchunks);
+  record(events, 1, st);
   if (raw && hb)
     hipLaunchKernelGGL((k_decode<true, true>), dim3(g), dim3(BLOCK), 0, st, P);
   else if (raw)
@@ -1175,9 +1488,15 @@ int coalac_decode_ev(coalac_plan_t plan, const int32_t* d_idx, const void* d_val
     hipLaunchKernelGGL((k_decode<false, true>), dim3(g), dim3(BLOCK), 0, st, P);
   else
     hipLaunchKernelGGL((k_decode<false, false>), dim3(g), dim3(BLOCK), 0, st, P);
-  record(events, 1, st);
+  record(events, 2, st);
   HIP_CHECK(hipGetLastError());
   return COALAC_OK;
+}
+
+int coalac_decode(coalac_plan_t plan, const int32_t* d_idx, const void* d_vals, const float* d_mn,
+                  const float* d_scale, const float* d_base, float* d_out, void* d_ws, uint64_t ws_bytes,
+                  void* stream) {
+  return coalac_decode_ev(plan, d_idx, d_vals, d_mn, d_scale, d_base, d_out, d_ws, ws_bytes, stream, nullptr);
 }
 
 int coalac_workspace_fallbacks(coalac_plan_t plan, const void* d_ws, void* stream, int* out) {

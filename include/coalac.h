@@ -46,7 +46,8 @@ enum {
 };
 
 enum {
-  COALAC_FLAG_FORCE_EXACT = 1  /* test hook: take the exact (non-sampled) selection path everywhere */
+  COALAC_FLAG_FORCE_EXACT = 1,    /* test hook: re-select every large segment exactly (no sampling) */
+  COALAC_FLAG_GENERIC_SELECT = 2  /* test hook: resolve the k-th key with the multi-pass select only */
 };
 
 /* One fp32 segment (= one flattened tensor of the state_dict). Offsets are in ELEMENTS.
@@ -71,10 +72,11 @@ const char* coalac_last_error(void);
 int coalac_plan_create(const coalac_seg_t* h_segs, int nseg, int bits, coalac_plan_t* out);
 int coalac_plan_destroy(coalac_plan_t plan);
 
-/* ws_bytes: workspace coalac_encode needs; total_k: length of idx/vals; span: max(in_off + n) = the
- * minimum length (elements) of the input/output flat buffers; n_units: 4096-element work units. */
-int coalac_plan_query(coalac_plan_t plan, uint64_t* ws_bytes, uint64_t* total_k, uint64_t* span,
-                      uint64_t* n_units);
+/* ws_bytes / dec_ws_bytes: workspace coalac_encode / coalac_decode need; total_k: length of idx/vals;
+ * span: max(in_off + n) = the minimum length (elements) of the input/output flat buffers;
+ * n_units: 4096-element work units. Any output pointer may be NULL. */
+int coalac_plan_query(coalac_plan_t plan, uint64_t* ws_bytes, uint64_t* dec_ws_bytes, uint64_t* total_k,
+                      uint64_t* span, uint64_t* n_units);
 
 /* Encode d_in (fp32[span]) into idx (int32[total_k], segment-relative, ascending per segment),
  * vals (uint8[total_k] codes or fp32[total_k]), mn (fp32[nseg]) and scale (fp32[nseg]).
@@ -84,20 +86,23 @@ int coalac_encode(coalac_plan_t plan, const float* d_in, const float* d_base, in
                   unsigned flags, void* stream);
 
 /* Decode into the dense d_out (fp32[span]); only positions inside segments are written.
- * d_base != NULL: d_out = d_base + decoded (fused; d_out may alias d_base). */
+ * d_base != NULL: d_out = d_base + decoded (fused; d_out may alias d_base). The encoded arrays may come
+ * from an untrusted blob: out-of-range or unsorted indices can mis-decode but never write outside the
+ * segment (still, validate blobs on the host; coala_amd/compression/wire.py does). */
 int coalac_decode(coalac_plan_t plan, const int32_t* d_idx, const void* d_vals, const float* d_mn,
-                  const float* d_scale, const float* d_base, float* d_out, void* stream);
+                  const float* d_scale, const float* d_base, float* d_out, void* d_ws, uint64_t ws_bytes,
+                  void* stream);
 
 /* Profiling variants: identical work, plus hipEventRecord(events[i], stream) between kernels.
  * encode: events[0] before k_prep, [1] after k_prep, [2] after k_scan, [3] after k_select,
- *         [4] after k_emit (recorded even if the plan has no large segment); decode: [0] before,
- *         [1] after k_decode. NULL array or NULL entries are skipped. */
+ *         [4] after k_emit (recorded even if the plan has no large segment); decode: [0] before
+ *         k_bounds, [1] after k_bounds, [2] after k_decode. NULL array or NULL entries are skipped. */
 int coalac_encode_ev(coalac_plan_t plan, const float* d_in, const float* d_base, int32_t* d_idx,
                      void* d_vals, float* d_mn, float* d_scale, void* d_ws, uint64_t ws_bytes,
                      unsigned flags, void* stream, void* const* events);
 int coalac_decode_ev(coalac_plan_t plan, const int32_t* d_idx, const void* d_vals, const float* d_mn,
-                     const float* d_scale, const float* d_base, float* d_out, void* stream,
-                     void* const* events);
+                     const float* d_scale, const float* d_base, float* d_out, void* d_ws,
+                     uint64_t ws_bytes, void* stream, void* const* events);
 
 /* Diagnostics: number of segments whose sampled thresholds were rejected and re-selected exactly in
  * the last encode that used workspace d_ws (synchronises `stream`). */
