@@ -7,11 +7,12 @@ Public surface:
   CodecPlan, Encoded                               — batched device-level API over the C ABI (plan.py)
   k_for, SegmentTable                              — CodecSpec v1 host logic (spec.py)
 """
+from . import wire
 from .codec import CompressedUpdate, FlatState, HipBackend, UpdateCodec, flatten_state, module_with_state
 from .plan import CodecPlan, Encoded
 from .plugin import CompressionClientMixin, CompressionServerMixin
 from .spec import ALIGN, RAW_BITS, SegmentTable, k_for
 
-__all__ = ["CompressedUpdate", "FlatState", "HipBackend", "UpdateCodec", "flatten_state", "module_with_state",
+__all__ = ["wire", "CompressedUpdate", "FlatState", "HipBackend", "UpdateCodec", "flatten_state", "module_with_state",
            "CodecPlan", "Encoded", "CompressionClientMixin", "CompressionServerMixin", "ALIGN", "RAW_BITS",
            "SegmentTable", "k_for"]

@@ -24,7 +24,7 @@ from torch import nn
 
 from . import wire
 from .plan import CodecPlan, Encoded
-from .spec import ALIGN, RAW_BITS, VALID_BITS, align_up
+from .spec import ALIGN, RAW_BITS, VALID_BITS, align_up, k_for
 
 MODES = ("delta", "weights")
 
@@ -33,6 +33,9 @@ class HipBackend:
     """Default backend: hand-written HIP kernels behind the C ABI (coala_amd/csrc/coalac.hip)."""
 
     name = "hip"
+
+    def default_device(self):
+        return torch.device("cuda", torch.cuda.current_device())
 
     def make_plan(self, sizes, ratio, bits, device):
         if device.type != "cuda":
@@ -117,7 +120,7 @@ class CompressedUpdate:
         raw_entries, chunks, pos = [], [], 0
         for e in h["entries"]:
             if e["kind"] == "raw":
-                b = self.raw[e["name"]].cpu().contiguous().view(torch.uint8).numpy().tobytes() \
+                b = self.raw[e["name"]].cpu().contiguous().reshape(-1).view(torch.uint8).numpy().tobytes() \
                     if self.raw[e["name"]].numel() else b""
                 e = dict(e, off=pos, nbytes=len(b))
                 chunks.append(b)
@@ -131,6 +134,7 @@ class CompressedUpdate:
     @classmethod
     def from_bytes(cls, blob):
         h, mn, scale, idx, vals, rawb = wire.unpack(blob)
+        validate(h, idx)
         raw = OrderedDict()
         for e in h["entries"]:
             if e["kind"] == "raw":
@@ -153,6 +157,33 @@ class CompressedUpdate:
         h = self.header
         return (f"CompressedUpdate(mode={h['mode']}, ratio={h['ratio']}, bits={h['bits']}, "
                 f"segments={h['n_segments']}, kept={h['total_k']}, bytes={self.nbytes})")
+
+
+def validate(header, idx):
+    """Check an (untrusted) blob's index lists: per fp32 segment, k = k_for(n, ratio) entries, strictly
+    increasing, inside [0, n). The decode kernels are bounds-safe anyway; this turns a corrupt upload
+    into an error instead of a silently wrong model."""
+    if header.get("bits") not in VALID_BITS or header.get("mode") not in MODES:
+        raise ValueError("COALAQ1: bad bits/mode")
+    segs = [e for e in header["entries"] if e["kind"] == "seg"]
+    if len(segs) != int(header["n_segments"]):
+        raise ValueError("COALAQ1: segment count mismatch")
+    ks = np.array([k_for(e["n"], header["ratio"]) for e in segs], dtype=np.int64)
+    if int(ks.sum()) != int(header["total_k"]) or idx.size != int(header["total_k"]):
+        raise ValueError("COALAQ1: kept-entry count mismatch")
+    if not ks.size:
+        return
+    ns = np.array([e["n"] for e in segs], dtype=np.int64)
+    seg_of = np.repeat(np.arange(ks.size), ks)
+    i64 = idx.astype(np.int64)
+    if np.any(i64 < 0) or np.any(i64 >= ns[seg_of]):
+        raise ValueError("COALAQ1: index out of range")
+    first = np.zeros(idx.size, dtype=bool)
+    first[np.cumsum(ks)[:-1][ks[1:] > 0] if ks.size > 1 else []] = True
+    first[0] = True
+    d = np.diff(i64, prepend=-1)
+    if np.any((d <= 0) & ~first):
+        raise ValueError("COALAQ1: indices not strictly increasing")
 
 
 class UpdateCodec:
@@ -230,7 +261,7 @@ class UpdateCodec:
                 _check_same_layout(h["entries"], base.entries)
                 device = base.flat.device
             elif device is None:
-                device = torch.device("cuda", torch.cuda.current_device())
+                device = self.backend.default_device()
             plan = self.plan_for(sizes, device, ratio=h["ratio"], bits=h["bits"])
             enc = update.encoded.to(device, non_blocking=True)
             flat = plan.decode(enc, base=base.flat if h["mode"] == "delta" else None)

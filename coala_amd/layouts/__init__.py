@@ -31,3 +31,32 @@ def fp32_sizes(name):
                 n *= d
             out.append(n)
     return out
+
+
+def build_module(name, seed=0, device="cpu"):
+    """An nn.Module whose state_dict has exactly the layout of reference model `name` (same names,
+    shapes, dtypes, order): fp32 weights as Parameters, BatchNorm running stats and int64 counters as
+    buffers. Values are seeded random (no checkpoints offline)."""
+    import torch
+    from torch import nn
+
+    g = torch.Generator().manual_seed(seed)
+    root = nn.Module()
+    for e in load(name)["entries"]:
+        path = e["name"].split(".")
+        mod = root
+        for p in path[:-1]:
+            if not hasattr(mod, p):
+                mod.add_module(p, nn.Module())
+            mod = getattr(mod, p)
+        dt = getattr(torch, e["dtype"])
+        leaf = path[-1]
+        if dt == torch.float32:
+            t = torch.randn(e["shape"], generator=g) * 0.05
+            if leaf in ("running_mean", "running_var"):
+                mod.register_buffer(leaf, t.abs() if leaf == "running_var" else t)
+            else:
+                mod.register_parameter(leaf, nn.Parameter(t))
+        else:
+            mod.register_buffer(leaf, torch.zeros(e["shape"], dtype=dt))
+    return root.to(device)

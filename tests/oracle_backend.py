@@ -33,5 +33,8 @@ class OraclePlan:
 class OracleBackend:
     name = "oracle"
 
+    def default_device(self):
+        return torch.device("cpu")
+
     def make_plan(self, sizes, ratio, bits, device):
         return OraclePlan(sizes, ratio, bits)

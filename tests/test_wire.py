@@ -1,0 +1,74 @@
+"""COALAQ1 wire format and the picklable carrier (no GPU: tensors on CPU)."""
+import pickle
+
+import numpy as np
+import pytest
+import torch
+
+from coala_amd.compression import CompressedUpdate, Encoded, wire
+
+
+def _update():
+    header = {"ratio": 0.25, "bits": 8, "mode": "delta", "n_segments": 2, "total_k": 3,
+              "entries": [{"name": "w", "dtype": "float32", "shape": [2, 3], "kind": "seg", "seg": 0, "off": 0,
+                           "n": 6},
+                          {"name": "steps", "dtype": "int64", "shape": [], "kind": "raw"},
+                          {"name": "b", "dtype": "float32", "shape": [4], "kind": "seg", "seg": 1, "off": 32,
+                           "n": 4}]}
+    enc = Encoded(torch.tensor([1, 4, 2], dtype=torch.int32), torch.tensor([0, 255, 7], dtype=torch.uint8),
+                  torch.tensor([-0.5, 0.0]), torch.tensor([0.01, 0.0]))
+    return CompressedUpdate(header, enc, {"steps": torch.tensor(41, dtype=torch.int64)})
+
+
+def test_pack_unpack_roundtrip():
+    h = {"bits": 8, "n_segments": 2, "total_k": 3, "x": [1, 2]}
+    blob = wire.pack(h, np.array([1, 2], np.float32), np.array([3, 4], np.float32), np.array([5, 6, 7], np.int32),
+                     np.array([8, 9, 10], np.uint8), b"raw!")
+    h2, mn, sc, idx, vals, raw = wire.unpack(blob)
+    assert h2 == h and raw == b"raw!"
+    assert mn.tolist() == [1, 2] and sc.tolist() == [3, 4] and idx.tolist() == [5, 6, 7] and vals.tolist() == [8, 9, 10]
+
+
+def test_carrier_pickles_to_blob_and_back():
+    u = _update()
+    data = pickle.dumps(u)
+    assert b"COALAQ1" in data
+    v = pickle.loads(data)
+    assert v.header["mode"] == "delta" and v.header["total_k"] == 3
+    assert torch.equal(v.encoded.idx, u.encoded.idx) and torch.equal(v.encoded.vals, u.encoded.vals)
+    assert torch.equal(v.encoded.mn, u.encoded.mn) and torch.equal(v.encoded.scale, u.encoded.scale)
+    assert v.raw["steps"].item() == 41 and v.raw["steps"].dtype == torch.int64
+
+
+def test_deepcopy_then_marshal_like_reference():
+    import copy
+    u = _update()
+    v = pickle.loads(pickle.dumps(copy.deepcopy(u)))  # client/base.py:363 then server/base.py:376
+    assert torch.equal(v.encoded.idx, u.encoded.idx)
+
+
+def test_payload_size_accounting():
+    u = _update()
+    assert u.nbytes == 8 * 2 + 5 * 3 + 8
+    p = list(u.parameters())
+    assert len(p) == 1 and p[0].device.type == "meta" and p[0].numel() * 4 >= u.nbytes
+
+
+def test_bad_magic_and_version():
+    with pytest.raises(ValueError):
+        wire.unpack(b"NOTCOALA" + b"\0" * 16)
+    blob = bytearray(pickle.loads(pickle.dumps(_update())).to_bytes())
+    blob[8] = 99
+    with pytest.raises(ValueError):
+        wire.unpack(bytes(blob))
+
+
+def test_validate_rejects_corrupt_indices():
+    u = _update()
+    blob = u.to_bytes()
+    h, mn, sc, idx, vals, raw = wire.unpack(blob)
+    bad = idx.copy()
+    bad[0] = 99  # out of range for a 6-element segment
+    blob2 = wire.pack(h, mn, sc, bad, vals, raw)
+    with pytest.raises(ValueError):
+        CompressedUpdate.from_bytes(blob2)
