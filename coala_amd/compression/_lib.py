@@ -11,6 +11,7 @@ from .. import _build
 
 COALAC_FLAG_FORCE_EXACT = 1
 COALAC_FLAG_GENERIC_SELECT = 2
+COALAC_FLAG_STAMPS = 4
 
 ERRORS = {
     -1: "COALAC_EINVAL",
@@ -37,6 +38,7 @@ SIGNATURES = [
     ("coalac_encode_ev", _I, [_P, _P, _P, _P, _P, _P, _P, _P, _U64, ctypes.c_uint, _P, _P]),
     ("coalac_decode_ev", _I, [_P, _P, _P, _P, _P, _P, _P, _P, _U64, _P, _P]),
     ("coalac_workspace_fallbacks", _I, [_P, _P, _P, ctypes.POINTER(_I)]),
+    ("coalac_debug_stamps", _I, [_P, _P, _P, ctypes.POINTER(ctypes.c_uint64), _I]),
 ]
 
 ABI_VERSION = 1

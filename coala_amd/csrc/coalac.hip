@@ -55,19 +55,23 @@ constexpr uint32_t SAMPLE_MAX = 8192;     // sampled keys per large segment
 constexpr int SEL_NT = 512;               // threads of a k_select block
 constexpr uint32_t BCHUNK = 4096;         // idx entries per k_bounds block
 constexpr uint32_t STAGE_CAP = 512;       // candidate records staged in LDS per k_scan wave
+constexpr uint32_t GU = 32;               // units per select group (k_ghist / k_gwin block)
+constexpr uint32_t HB2 = 512;             // bins of the per-group band histograms
+constexpr uint32_t GCAP = 256;            // in-window entries a group may hand to k_select
 constexpr uint32_t A_FLAG = 0x80000000u;  // candidate record flag: key > T_hi (kept for sure)
 constexpr uint32_t KEY_MAX = 0x7FFFFFFFu;
 constexpr int HIST_BINS = 2048;
 constexpr uint32_t UCAP = 2048;           // units per k_select chunk (8.4 M elements)
-constexpr uint32_t WB = 4;                // in-window LDS slots per k_select thread (fast path)
 constexpr uint32_t NONE = 0xFFFFFFFFu;
+constexpr int NSTAMP = 16;
 
 struct SegDev {
   uint64_t in_off;
   uint64_t out_off;
   uint32_t n, k;
   uint32_t unit_begin, unit_end;  // range in the all-units table (decode)
-  uint32_t lu_begin, pad;         // first large-unit index (large segments)
+  uint32_t lu_begin;              // first large-unit index (large segments)
+  uint32_t g_begin;               // first select group (large segments)
 };
 
 struct UnitDev {
@@ -107,9 +111,20 @@ struct Params {
   // per large unit
   uint32_t *tlo, *thi, *cntA, *cntC, *gtC, *eqC, *eqpre, *outoff;
   uint2* cand;  // candidate records {index | A_FLAG, value bits}, UNIT slots per large unit
+  // parallel select (groups of GU units of one large segment)
+  const uint4* groups;     // {large-segment index, first large unit, units, segment}
+  uint32_t n_groups;
+  uint32_t* ghist;         // [n_groups][HB2]
+  uint32_t* gcnt;          // [n_groups] in-window entries found by the group
+  uint2* glist;            // [n_groups][GCAP] {value bits, unit index within the segment}
+  float* gmm;              // [n_groups][2] min/max of the group's values above the window
+  uint4* sstate;           // [n_large] {wlo, whi, rank inside the window, path: 0 fast / 1 generic}
+  uint32_t* shhi;          // [n_large] histogram upper bound: min(T_hi, largest sampled key)
 
   // decode workspace
   uint32_t* ustart;
+  // diagnostics: per-block phase timestamps (COALAC_FLAG_STAMPS), NSTAMP per block, 100 MHz ticks
+  uint64_t* stamps;
 };
 
 // ------------------------------------------------------------------------------------------------
@@ -119,10 +134,18 @@ struct Params {
 
 DEV uint32_t fkey(float x) { return __float_as_uint(x) & KEY_MAX; }
 
-// NaN-ignoring min/max (NaN only if both are NaN). The sign of a zero result is canonicalised at the
-// end (+ 0.0f), which makes the reduction order-independent.
-DEV float fmin_nan(float a, float b) { return (a != a) ? b : ((b != b) ? a : ((b < a) ? b : a)); }
-DEV float fmax_nan(float a, float b) { return (a != a) ? b : ((b != b) ? a : ((b > a) ? b : a)); }
+// diagnostics only: thread 0 records the 100 MHz real-time counter for phase i of this block
+#define STAMP(P, i)                                                                                 \
+  do {                                                                                              \
+    if ((P).stamps != nullptr && threadIdx.x == 0)                                                  \
+      (P).stamps[(uint64_t)blockIdx.x * NSTAMP + (i)] = __builtin_amdgcn_s_memrealtime();          \
+  } while (0)
+
+// NaN-ignoring min/max (NaN only if both are NaN) = IEEE minNum/maxNum: one v_min_f32 / v_max_f32
+// (hipcc quiets signalling NaNs first, so a NaN operand is always ignored). The sign of a zero result is
+// canonicalised at the end (+ 0.0f), which makes the reduction order-independent.
+DEV float fmin_nan(float a, float b) { return __builtin_fminf(a, b); }
+DEV float fmax_nan(float a, float b) { return __builtin_fmaxf(a, b); }
 DEV float qnan() { return __int_as_float(0x7FC00000); }
 
 DEV uint32_t lane_id() { return __lane_id(); }
@@ -316,11 +339,11 @@ typedef float f4v __attribute__((ext_vector_type(4)));
 
 // histogram shift of the sampled band [tlo, thi]: HIST_BINS bins of 2^shift keys cover it. k_scan
 // (band histogram) and k_select (bin -> key window) must agree, so both use this.
-DEV int band_shift(uint32_t tlo, uint32_t thi) {
+DEV int band_shift(uint32_t tlo, uint32_t thi, int bin_bits = 11) {
   const uint32_t w = thi - tlo;
   if (w == 0) return 0;
   const int bl = 32 - __clz(w);
-  return bl > 11 ? bl - 11 : 0;
+  return bl > bin_bits ? bl - bin_bits : 0;
 }
 
 // non-temporal (read-once) 16-byte load of x (or x - base)
@@ -525,6 +548,48 @@ DEV void small_encode(const Params& P, uint32_t s, float* vals, uint32_t* hist, 
   }
 }
 
+// Pick the bin of a HIST_BINS histogram (LDS) holding the r-th largest key: returns the bin, leaves in
+// r the rank inside that bin. sh needs >= 64 words.
+template <int NT, int NB = HIST_BINS>
+DEV uint32_t hist_pick(const uint32_t* hist, uint32_t& r, uint32_t* sh) {
+  constexpr int BPT = NB / NT;
+  const uint32_t t = threadIdx.x;
+  uint32_t c[BPT];
+  uint32_t s = 0;
+#pragma unroll
+  for (int j = 0; j < BPT; ++j) {
+    c[j] = hist[t * BPT + j];
+    s += c[j];
+  }
+  uint32_t total;
+  const uint32_t ex = block_excl_scan<NT>(s, sh, total);
+  const uint32_t above = total - ex - s;
+  if (t == 0) {
+    sh[40] = NONE;
+    sh[41] = r;
+  }
+  __syncthreads();
+  if (above < r && r <= above + s) {
+    uint32_t acc = above;
+    int b = (int)(t * BPT);
+#pragma unroll
+    for (int j = BPT - 1; j >= 0; --j) {
+      if (acc + c[j] >= r) {
+        b = (int)(t * BPT) + j;
+        break;
+      }
+      acc += c[j];
+    }
+    sh[40] = (uint32_t)b;
+    sh[41] = r - acc;
+  }
+  __syncthreads();
+  const uint32_t b = sh[40];
+  r = sh[41];
+  __syncthreads();
+  return b;
+}
+
 // ------------------------------------------------------------------------------------------------
 // k_sample: per large segment, sampled thresholds [T_lo, T_hi] for every unit of the segment
 // ------------------------------------------------------------------------------------------------
@@ -561,17 +626,46 @@ __global__ __launch_bounds__(BLOCK) void k_sample(Params P) {
   const double se = p * (double)m;
   const double d = 6.0 * sqrt(se) + 8.0;
   const double rlo = ceil(se + d), rhi = floor(se - d);
-  auto each = [&](auto&& f) {
-    for (uint32_t i = t; i < m; i += NT) f(keys[i]);
-  };
-  uint32_t r1 = (uint32_t)rlo, r2 = (uint32_t)rhi;
-  const uint32_t tlo = rlo >= (double)m ? 0u : block_select<NT>(each, 0u, KEY_MAX, r1, hist, sh);
-  const uint32_t thi = rhi < 1.0 ? KEY_MAX : block_select<NT>(each, 0u, KEY_MAX, r2, hist, sh);
+  // One histogram pass over the sample's own key range; thresholds are bin EDGES taken outward (lower
+  // edge for T_lo, upper edge for T_hi), which only widens the bracket.
+  if (t == 0) {
+    sh[44] = KEY_MAX;
+    sh[45] = 0u;
+  }
+  for (uint32_t i = t; i < HIST_BINS; i += NT) hist[i] = 0;
+  __syncthreads();
+  uint32_t kmn = KEY_MAX, kmx = 0;
+  for (uint32_t i = t; i < m; i += NT) {
+    kmn = min(kmn, keys[i]);
+    kmx = max(kmx, keys[i]);
+  }
+  atomicMin(&sh[44], kmn);
+  atomicMax(&sh[45], kmx);
+  __syncthreads();
+  const uint32_t kmin = sh[44], kmax = sh[45];
+  const int shift = band_shift(kmin, kmax);
+  for (uint32_t i = t; i < m; i += NT) atomicAdd(&hist[(keys[i] - kmin) >> shift], 1u);
+  __syncthreads();
+  uint32_t tlo = 0u, thi = KEY_MAX;
+  if (rlo < (double)m) {
+    uint32_t r1 = (uint32_t)rlo;
+    const uint32_t b = hist_pick<NT>(hist, r1, sh);
+    tlo = kmin + (b << shift);
+  }
+  if (rhi >= 1.0) {
+    uint32_t r2 = (uint32_t)rhi;
+    const uint32_t b = hist_pick<NT>(hist, r2, sh);
+    const uint64_t edge = (uint64_t)kmin + (((uint64_t)b + 1) << shift) - 1;
+    thi = (uint32_t)min<uint64_t>(edge, kmax);
+  }
   const uint32_t nu = sd.unit_end - sd.unit_begin;
   for (uint32_t i = t; i < nu; i += NT) {
     P.tlo[sd.lu_begin + i] = tlo;
     P.thi[sd.lu_begin + i] = thi;
   }
+  // The band histograms of the parallel select span [T_lo, min(T_hi, max sampled key)] (keys above go
+  // to the last bin): with T_hi = KEY_MAX a full-range histogram would be too coarse.
+  if (t == 0) P.shhi[blockIdx.x] = max(tlo, min(thi, kmax));
   if (t == 0) P.status[s] = 0;
 }
 
@@ -618,170 +712,346 @@ DEV uint32_t chunk_prefix(const uint32_t* cnt, uint32_t cn, uint32_t* upre, uint
   return carry;
 }
 
-// Visit the candidate records j in [j0, j1) of a chunk (concatenated lists of units lu0 .. lu0+cn-1,
-// in unit order, so j order = index order) calling f(x, unit_in_chunk). Loads are issued SB at a time.
-template <class F>
-DEV void sweep_run(const uint2* cand, uint32_t lu0, const uint32_t* upre, uint32_t cn, uint32_t j0, uint32_t j1,
-                   F&& f) {
-  constexpr int SB = 16;
-  if (j0 >= j1) return;
-  uint32_t lo = 0, hi = cn;  // upre[lo] <= j0 < upre[hi]
-  while (hi - lo > 1) {
-    const uint32_t mid = (lo + hi) >> 1;
-    if (upre[mid] <= j0)
-      lo = mid;
-    else
-      hi = mid;
-  }
-  uint32_t ul = lo, cur = upre[ul], nxt = upre[ul + 1];
-  for (uint32_t j = j0; j < j1; j += SB) {
-    float xs[SB];
-    uint32_t us[SB];
+// Wave w owns the units whose first record index (upre[u]) lies in [w*total/NW, (w+1)*total/NW):
+// contiguous unit ranges balanced by record count, so segment order = (wave, unit, lane) order. A wave
+// reads one unit at a time from its contiguous region (coalesced, trivial addressing, the unit is
+// wave-uniform so per-unit counts are ballot popcounts), G units per batch with 2 records per lane per
+// unit in flight. f(x, valid, u) is called by ALL lanes (ballots allowed); fend(u) after each unit.
+template <int NW, int G, class F, class FE>
+DEV void unit_sweep(const uint2* cand, uint32_t lu0, const uint32_t* upre, uint32_t cn, uint32_t total, F&& f,
+                    FE&& fend) {
+  const uint32_t lane = lane_id(), w = threadIdx.x >> 6;
+  const uint32_t J0 = (uint32_t)((uint64_t)total * w / NW), J1 = (uint32_t)((uint64_t)total * (w + 1) / NW);
+  auto lower = [&](uint32_t key) {  // first u in [0, cn] with upre[u] >= key
+    uint32_t lo = 0, hi = cn;
+    while (lo < hi) {
+      const uint32_t mid = (lo + hi) >> 1;
+      if (upre[mid] < key)
+        lo = mid + 1;
+      else
+        hi = mid;
+    }
+    return lo;
+  };
+  const uint32_t U0 = w == 0 ? 0u : lower(J0);
+  const uint32_t U1 = w == NW - 1 ? cn : lower(J1);
+  for (uint32_t u = U0; u < U1; u += G) {
+    uint32_t x0[G], x1[G], nn[G];
 #pragma unroll
-    for (int q = 0; q < SB; ++q) {
-      const uint32_t jj = j + q;
-      us[q] = NONE;
-      xs[q] = 0.0f;
-      if (jj < j1) {
-        while (jj >= nxt) {
-          ++ul;
-          cur = nxt;
-          nxt = upre[ul + 1];
+    for (int g = 0; g < G; ++g) {
+      const uint32_t uu = min(u + g, U1 - 1);
+      const uint32_t n = upre[uu + 1] - upre[uu];
+      const uint32_t last = n ? n - 1 : 0u;  // region slot 0 always exists; read it when n == 0
+      const uint2* R = cand + (uint64_t)(lu0 + uu) * UNIT;
+      nn[g] = n;
+      x0[g] = R[min(lane, last)].y;
+      x1[g] = R[min(lane + 64, last)].y;
+    }
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      if (u + g < U1) {
+        const uint32_t uu = u + g, n = nn[g];
+        f(__uint_as_float(x0[g]), lane < n, uu);
+        if (n > 64) f(__uint_as_float(x1[g]), lane + 64 < n, uu);
+        if (n > 128) {
+          const uint2* R = cand + (uint64_t)(lu0 + uu) * UNIT;
+          for (uint32_t i0 = 128; i0 < n; i0 += 64) f(__uint_as_float(R[min(i0 + lane, n - 1)].y), i0 + lane < n, uu);
         }
-        us[q] = ul;
-        xs[q] = __uint_as_float(cand[(uint64_t)(lu0 + ul) * UNIT + (jj - cur)].y);
+        fend(uu);
       }
     }
-#pragma unroll
-    for (int q = 0; q < SB; ++q)
-      if (us[q] != NONE) f(xs[q], us[q]);
   }
-}
-
-// Pick the bin of a HIST_BINS histogram (LDS) holding the r-th largest key: returns the bin, leaves in
-// r the rank inside that bin. sh needs >= 64 words.
-template <int NT>
-DEV uint32_t hist_pick(const uint32_t* hist, uint32_t& r, uint32_t* sh) {
-  constexpr int BPT = HIST_BINS / NT;
-  const uint32_t t = threadIdx.x;
-  uint32_t c[BPT];
-  uint32_t s = 0;
-#pragma unroll
-  for (int j = 0; j < BPT; ++j) {
-    c[j] = hist[t * BPT + j];
-    s += c[j];
-  }
-  uint32_t total;
-  const uint32_t ex = block_excl_scan<NT>(s, sh, total);
-  const uint32_t above = total - ex - s;
-  if (t == 0) {
-    sh[40] = NONE;
-    sh[41] = r;
-  }
-  __syncthreads();
-  if (above < r && r <= above + s) {
-    uint32_t acc = above;
-    int b = (int)(t * BPT);
-#pragma unroll
-    for (int j = BPT - 1; j >= 0; --j) {
-      if (acc + c[j] >= r) {
-        b = (int)(t * BPT) + j;
-        break;
-      }
-      acc += c[j];
-    }
-    sh[40] = (uint32_t)b;
-    sh[41] = r - acc;
-  }
-  __syncthreads();
-  const uint32_t b = sh[40];
-  r = sh[41];
-  __syncthreads();
-  return b;
 }
 
 // LDS scratch of k_select
+constexpr uint32_t WLIST = 2048;               // in-window entries the fast path can hold
+constexpr uint32_t WSLOT = WLIST / (SEL_NT / 64);  // per-wave share while sweeping
 struct SelSmem {
   uint32_t hist[HIST_BINS];
   uint32_t upre[UCAP + 1];
   uint32_t ugt[UCAP];
   uint32_t ueq[UCAP];
-  uint32_t slot_val[SEL_NT * WB];   // per-thread in-window slots (value bits, unit)
-  uint32_t slot_unit[SEL_NT * WB];
-  uint32_t lst_val[SEL_NT * WB];    // in-window entries in index order
-  uint32_t lst_unit[SEL_NT * WB];
+  uint32_t slot_val[WLIST];   // per-wave in-window slots (value bits, unit), wave w at [w * WSLOT, ...)
+  uint32_t slot_unit[WLIST];
+  uint32_t lst_val[WLIST];    // in-window entries, all waves concatenated = index order
+  uint32_t lst_unit[WLIST];
+  uint32_t wcnt[SEL_NT / 64];
   uint32_t sh[64];
   float shf[2 * (SEL_NT / 64)];
 };
 
-// Fast path (two sweeps): a histogram sweep over the band [tlo, thi] locates the bin of the k-th key;
-// one more sweep counts, per unit, the keys above that bin and collects the (few) keys inside it into
-// an ordered LDS list, where the exact key and the ties are resolved. Returns false (nothing written)
-// if the bin's entries do not fit the LDS slots (heavy ties); the caller then takes the generic path.
+// Generic path: radix select over all candidates (1-3 coalesced sweeps) + a counts sweep; handles any
+// number of ties and segments of any size (units in chunks of UCAP).
 template <int NT>
-DEV bool select_fast(const Params& P, uint32_t lb, uint32_t nu, uint32_t tlo, uint32_t thi,
-                     uint32_t r, SelSmem& S, uint32_t& T_out, uint32_t& rt_out, uint32_t& fp, uint32_t& fn,
-                     float& gmn, float& gmx) {
+DEV void select_generic(const Params& P, uint32_t lb, uint32_t nu, uint32_t tlo, uint32_t thi, uint32_t r,
+                        SelSmem& S, uint32_t& T_out, uint32_t& rt_out, uint32_t& fp, uint32_t& fn, float& gmn,
+                        float& gmx) {
+  constexpr int NW = NT / 64;
+  const uint32_t t = threadIdx.x, lane = lane_id(), wv = t >> 6;
+  uint32_t rt = r;
+  auto forC = [&](auto&& f) {
+    for (uint32_t c0 = 0; c0 < nu; c0 += UCAP) {
+      const uint32_t cn = min(UCAP, nu - c0);
+      const uint32_t total = chunk_prefix<NT>(P.cntC + lb + c0, cn, S.upre, S.sh);
+      unit_sweep<NW, 16>(
+          P.cand, lb + c0, S.upre, cn, total,
+          [&](float x, bool valid, uint32_t) {
+            if (valid) f(fkey(x));
+          },
+          [&](uint32_t) {});
+      __syncthreads();
+    }
+  };
+  const uint32_t T = rt == 0 ? thi : block_select<NT>(forC, tlo, thi, rt, S.hist, S.sh);
+
+  // counts sweep: per-unit gt/eq, segment-wide tie rank of the first positive / negative tie, min/max
+  // of the values with key > T (all of them are kept).
+  float lmn = qnan(), lmx = qnan();
+  uint32_t carry_eq = 0;
+  if (t == 0) {
+    S.sh[42] = NONE;
+    S.sh[43] = NONE;
+  }
+  for (uint32_t c0 = 0; c0 < nu; c0 += UCAP) {
+    const uint32_t cn = min(UCAP, nu - c0);
+    for (uint32_t i = t; i < cn; i += NT) {
+      S.ugt[i] = 0;
+      S.ueq[i] = 0;
+    }
+    const uint32_t total = chunk_prefix<NT>(P.cntC + lb + c0, cn, S.upre, S.sh);
+    uint32_t weq = 0, wfp = NONE, wfn = NONE, ug = 0, ue = 0;  // wave-uniform
+    unit_sweep<NW, 16>(
+        P.cand, lb + c0, S.upre, cn, total,
+        [&](float x, bool valid, uint32_t) {
+          const uint32_t key = fkey(x);
+          const bool g = valid && key > T;
+          const bool e = valid && key == T;
+          ug += (uint32_t)__popcll(__ballot(g));
+          const float xg = g ? x : qnan();
+          lmn = fmin_nan(lmn, xg);
+          lmx = fmax_nan(lmx, xg);
+          const uint64_t eb = __ballot(e);
+          if (eb) {
+            const bool neg = (__float_as_uint(x) >> 31) != 0;
+            const uint64_t pm = __ballot(e && !neg), nm = __ballot(e && neg);
+            if (wfp == NONE && pm) wfp = weq + (uint32_t)__popcll(eb & ((1ull << (__ffsll((long long)pm) - 1)) - 1ull));
+            if (wfn == NONE && nm) wfn = weq + (uint32_t)__popcll(eb & ((1ull << (__ffsll((long long)nm) - 1)) - 1ull));
+            weq += (uint32_t)__popcll(eb);
+            ue += (uint32_t)__popcll(eb);
+          }
+        },
+        [&](uint32_t u) {
+          if (lane == 0) {
+            S.ugt[u] = ug;
+            S.ueq[u] = ue;
+          }
+          ug = ue = 0;
+        });
+    if (lane == 0) S.wcnt[wv] = weq;
+    __syncthreads();
+    uint32_t wpre = carry_eq, tot = 0;
+#pragma unroll
+    for (int i = 0; i < NW; ++i) {
+      const uint32_t c = S.wcnt[i];
+      if ((uint32_t)i < wv) wpre += c;
+      tot += c;
+    }
+    if (lane == 0 && wfp != NONE) atomicMin(&S.sh[42], wpre + wfp);
+    if (lane == 0 && wfn != NONE) atomicMin(&S.sh[43], wpre + wfn);
+    carry_eq += tot;
+    __syncthreads();
+    for (uint32_t i = t; i < cn; i += NT) {
+      P.gtC[lb + c0 + i] = S.ugt[i];
+      P.eqC[lb + c0 + i] = S.ueq[i];
+    }
+    __syncthreads();
+  }
+  T_out = T;
+  rt_out = rt;
+  fp = S.sh[42];
+  fn = S.sh[43];
+  gmn = lmn;
+  gmx = lmx;
+  __syncthreads();
+}
+
+// ------------------------------------------------------------------------------------------------
+// parallel select, fast path: groups of GU units of one large segment, one 256-thread block each
+// ------------------------------------------------------------------------------------------------
+// Group-histogram geometry of a segment: bins of 2^shift keys over [tlo, hhi]; keys in (hhi, thi] are
+// clamped into the last bin, whose key window therefore ends at thi.
+struct Band {
+  uint32_t tlo, thi, hhi, last;
+  int shift;
+  DEV Band(uint32_t lo, uint32_t hi, uint32_t hh) : tlo(lo), thi(hi), hhi(hh) {
+    shift = band_shift(lo, hh, 9);
+    last = (hh - lo) >> shift;
+  }
+  DEV uint32_t bin(uint32_t key) const { return key > hhi ? last : (key - tlo) >> shift; }
+  DEV uint32_t wlo(uint32_t b) const { return tlo + (b << shift); }
+  DEV uint32_t whi(uint32_t b) const { return b == last ? thi : min(thi, wlo(b) + ((1u << shift) - 1u)); }
+};
+// k_ghist: the group's HB2-bin histogram of the band keys [tlo, thi] -> ghist[group]
+__global__ __launch_bounds__(BLOCK) void k_ghist(Params P) {
+  __shared__ uint32_t hist[HB2];
+  __shared__ uint32_t upre[GU + 1];
+  __shared__ uint32_t sh[64];
+  const uint4 G = P.groups[blockIdx.x];  // x: large-segment index, y: first large unit, z: units, w: segment
   const uint32_t t = threadIdx.x;
-  const int shift = band_shift(tlo, thi);
-  for (uint32_t i = t; i < HIST_BINS; i += NT) S.hist[i] = 0;
+  const uint32_t tlo = P.tlo[G.y], thi = P.thi[G.y];
+  const Band band(tlo, thi, P.shhi[G.x]);
+  for (uint32_t i = t; i < HB2; i += BLOCK) hist[i] = 0;
+  const uint32_t total = chunk_prefix<BLOCK>(P.cntC + G.y, G.z, upre, sh);  // barrier inside
+  unit_sweep<WAVES, 4>(
+      P.cand, G.y, upre, G.z, total,
+      [&](float x, bool valid, uint32_t) {
+        const uint32_t key = fkey(x);
+        if (valid && key >= tlo && key <= thi) atomicAdd(&hist[band.bin(key)], 1u);
+      },
+      [&](uint32_t) {});
+  __syncthreads();
+  for (uint32_t i = t; i < HB2; i += BLOCK) P.ghist[(uint64_t)blockIdx.x * HB2 + i] = hist[i];
+}
+
+// k_pick: per large segment — validate the sampled bracket, sum the group histograms, pick the bin of
+// the k-th key: sstate = {window lo, window hi, rank inside the window, 0}; {.., 1} routes the segment
+// to the generic single-block path (bracket miss, nothing to take from B, huge segment, test flags).
+__global__ __launch_bounds__(BLOCK) void k_pick(Params P) {
+  __shared__ uint32_t hist[HB2];
+  __shared__ uint32_t sh[64];
+  const uint32_t t = threadIdx.x, li = blockIdx.x;
+  const SegDev sd = P.segs[P.large_list[li]];
+  const uint32_t lb = sd.lu_begin, nu = sd.unit_end - sd.unit_begin, k = sd.k;
+  uint32_t sa = 0, sc = 0;
+  for (uint32_t i = t; i < nu; i += BLOCK) {
+    sa += P.cntA[lb + i];
+    sc += P.cntC[lb + i];
+  }
+  sa = block_sum<BLOCK>(sa, sh);
+  sc = block_sum<BLOCK>(sc, sh);
+  const bool generic = (P.flags & (COALAC_FLAG_FORCE_EXACT | COALAC_FLAG_GENERIC_SELECT)) || !(sa < k && k <= sc) ||
+                       nu > UCAP;
+  if (generic) {
+    if (t == 0) P.sstate[li] = make_uint4(0u, 0u, 0u, 1u);
+    return;
+  }
+  const uint32_t g0 = sd.g_begin, ng = (nu + GU - 1) / GU;
+  for (uint32_t b = t; b < HB2; b += BLOCK) {
+    uint32_t acc = 0;
+    for (uint32_t g = 0; g < ng; ++g) acc += P.ghist[(uint64_t)(g0 + g) * HB2 + b];
+    hist[b] = acc;
+  }
+  __syncthreads();
+  uint32_t r = k - sa;
+  const uint32_t b = hist_pick<BLOCK, HB2>(hist, r, sh);
+  if (t == 0) {
+    if (b == NONE) {
+      P.sstate[li] = make_uint4(0u, 0u, 0u, 1u);
+    } else {
+      const Band band(P.tlo[lb], P.thi[lb], P.shhi[li]);
+      P.sstate[li] = make_uint4(band.wlo(b), band.whi(b), r, 0u);
+    }
+  }
+}
+
+// k_gwin: per group — per-unit counts of keys above the window (-> gtC), the group's in-window entries
+// in index order (-> glist, count -> gcnt), min/max of the values above the window (-> gmm)
+__global__ __launch_bounds__(BLOCK) void k_gwin(Params P) {
+  __shared__ uint32_t upre[GU + 1];
+  __shared__ uint2 slots[WAVES][GCAP];
+  __shared__ uint32_t wcnt[WAVES];
+  __shared__ uint32_t sh[64];
+  __shared__ float shf[2 * WAVES];
+  const uint4 G = P.groups[blockIdx.x];
+  const uint4 st = P.sstate[G.x];
+  if (st.w != 0) return;
+  const uint32_t t = threadIdx.x, lane = lane_id(), wv = t >> 6;
+  const uint32_t wlo = st.x, whi = st.y;
+  const uint32_t useg0 = G.y - P.segs[G.w].lu_begin;  // unit index (within the segment) of the group's first unit
+  const uint32_t total = chunk_prefix<BLOCK>(P.cntC + G.y, G.z, upre, sh);
+  uint32_t wc = 0, ug = 0;
+  float lmn = qnan(), lmx = qnan();
+  unit_sweep<WAVES, 4>(
+      P.cand, G.y, upre, G.z, total,
+      [&](float x, bool valid, uint32_t u) {
+        const uint32_t key = fkey(x);
+        const bool g = valid && key > whi;
+        const bool in = valid && key >= wlo && key <= whi;
+        ug += (uint32_t)__popcll(__ballot(g));
+        const float xg = g ? x : qnan();
+        lmn = fmin_nan(lmn, xg);
+        lmx = fmax_nan(lmx, xg);
+        const uint64_t im = __ballot(in);
+        if (im) {
+          const uint32_t pos = wc + mbcnt(im);
+          if (in && pos < GCAP) slots[wv][pos] = make_uint2(__float_as_uint(x), useg0 + u);
+          wc += (uint32_t)__popcll(im);
+        }
+      },
+      [&](uint32_t u) {
+        if (lane == 0) {
+          P.gtC[G.y + u] = ug;
+          P.eqC[G.y + u] = 0;
+        }
+        ug = 0;
+      });
+  if (lane == 0) wcnt[wv] = wc;
+  __syncthreads();
+  uint32_t wpre = 0, W = 0;
+#pragma unroll
+  for (int i = 0; i < WAVES; ++i) {
+    const uint32_t c = wcnt[i];
+    if (i < (int)wv) wpre += c;
+    W += c;
+  }
+  for (uint32_t q = lane; q < wc && q < GCAP; q += 64)
+    if (wpre + q < GCAP) P.glist[(uint64_t)blockIdx.x * GCAP + wpre + q] = slots[wv][q];
+  block_minmax<BLOCK>(lmn, lmx, shf);
+  if (t == 0) {
+    P.gcnt[blockIdx.x] = W;
+    P.gmm[2 * blockIdx.x] = lmn;
+    P.gmm[2 * blockIdx.x + 1] = lmx;
+  }
+}
+
+// Fast-path resolution in k_select: gather the groups' in-window lists (group order = index order),
+// find the exact key inside the window, apply the window entries to the per-unit counts. Returns false
+// if a group's list overflowed (the caller then runs the generic path from scratch).
+template <int NT>
+DEV bool select_from_groups(const Params& P, const SegDev& sd, uint32_t lb, uint32_t nu, uint4 st, SelSmem& S,
+                            uint32_t& T_out, uint32_t& rt_out, uint32_t& fp, uint32_t& fn, float& gmn, float& gmx) {
+  const uint32_t t = threadIdx.x;
+  const uint32_t g0 = sd.g_begin, ng = (nu + GU - 1) / GU;  // ng <= UCAP / GU = 64 <= NT
+  const uint32_t c = t < ng ? P.gcnt[g0 + t] : 0u;
+  uint32_t W;
+  const uint32_t gpre = block_excl_scan<NT>(c, S.sh, W);
+  const uint32_t over = block_sum<NT>(c > GCAP ? 1u : 0u, S.sh);
+  if (over || W > WLIST) return false;
+  // offset of each group's entries, then copy them
+  if (t < ng) S.upre[t] = gpre;
+  __syncthreads();
+  for (uint32_t g = 0; g < ng; ++g) {
+    const uint32_t cg = min(P.gcnt[g0 + g], GCAP), base = S.upre[g];
+    for (uint32_t q = t; q < cg; q += NT) {
+      const uint2 e = P.glist[(uint64_t)(g0 + g) * GCAP + q];
+      S.lst_val[base + q] = e.x;
+      S.lst_unit[base + q] = e.y;
+    }
+  }
   for (uint32_t i = t; i < nu; i += NT) {
-    S.ugt[i] = 0;
+    S.ugt[i] = P.gtC[lb + i];
     S.ueq[i] = 0;
   }
-  const uint32_t total = chunk_prefix<NT>(P.cntC + lb, nu, S.upre, S.sh);  // barrier inside
-  const uint32_t E = (total + NT - 1) / NT;
-  const uint32_t j0 = min(total, t * E), j1 = min(total, j0 + E);
-  sweep_run(P.cand, lb, S.upre, nu, j0, j1, [&](float x, uint32_t) {
-    const uint32_t key = fkey(x);
-    if (key >= tlo && key <= thi) atomicAdd(&S.hist[(key - tlo) >> shift], 1u);
-  });
   __syncthreads();
-  uint32_t rw = r;
-  const uint32_t b = hist_pick<NT>(S.hist, rw, S.sh);
-  if (b == NONE) return false;
-  const uint32_t wlo = tlo + (b << shift);
-  const uint32_t whi = min(thi, wlo + ((1u << shift) - 1u));
-  uint32_t wc = 0, cu = NONE, cg = 0;
-  float lmn = qnan(), lmx = qnan();
-  sweep_run(P.cand, lb, S.upre, nu, j0, j1, [&](float x, uint32_t u) {
-    const uint32_t key = fkey(x);
-    if (key > whi) {
-      if (u != cu) {
-        if (cu != NONE) atomicAdd(&S.ugt[cu], cg);
-        cu = u;
-        cg = 0;
-      }
-      ++cg;
-      lmn = fmin_nan(lmn, x);
-      lmx = fmax_nan(lmx, x);
-    } else if (key >= wlo) {
-      if (wc < WB) {
-        S.slot_val[t * WB + wc] = __float_as_uint(x);
-        S.slot_unit[t * WB + wc] = u;
-      }
-      ++wc;
-    }
-  });
-  if (cu != NONE) atomicAdd(&S.ugt[cu], cg);
-  const uint32_t over = block_sum<NT>(wc > WB ? 1u : 0u, S.sh);
-  if (over) return false;  // uniform: every thread sees the same block sum
-  uint32_t W;
-  const uint32_t wpre = block_excl_scan<NT>(wc, S.sh, W);
-  for (uint32_t q = 0; q < wc; ++q) {
-    S.lst_val[wpre + q] = S.slot_val[t * WB + q];
-    S.lst_unit[wpre + q] = S.slot_unit[t * WB + q];
-  }
-  __syncthreads();
-  // exact k-th key inside the window: the rw-th largest of the W listed keys
-  uint32_t rt = rw;
+  uint32_t rt = st.z;
   const uint32_t T = block_select<NT>(
       [&](auto&& f) {
         for (uint32_t i = t; i < W; i += NT) f(S.lst_val[i] & KEY_MAX);
       },
-      wlo, whi, rt, S.hist, S.sh);
-  // per-unit counts of the window entries; tie ranks in list (= index) order
-  const uint32_t q0 = min(W, t * WB), q1 = min(W, q0 + WB);
+      st.x, st.y, rt, S.hist, S.sh);
+  constexpr uint32_t EPT = WLIST / NT;
+  const uint32_t q0 = min(W, t * EPT), q1 = min(W, q0 + EPT);
+  float lmn = qnan(), lmx = qnan();
   uint32_t leq = 0, lfp = NONE, lfn = NONE;
   for (uint32_t q = q0; q < q1; ++q) {
     const uint32_t vb = S.lst_val[q];
@@ -797,6 +1067,10 @@ DEV bool select_fast(const Params& P, uint32_t lb, uint32_t nu, uint32_t tlo, ui
       lfn = min(lfn, neg ? leq : NONE);
       ++leq;
     }
+  }
+  for (uint32_t g = t; g < ng; g += NT) {
+    lmn = fmin_nan(lmn, P.gmm[2 * (g0 + g)]);
+    lmx = fmax_nan(lmx, P.gmm[2 * (g0 + g) + 1]);
   }
   uint32_t teq;
   const uint32_t ex = block_excl_scan<NT>(leq, S.sh, teq);
@@ -822,90 +1096,6 @@ DEV bool select_fast(const Params& P, uint32_t lb, uint32_t nu, uint32_t tlo, ui
   return true;
 }
 
-// Generic path: radix select over all candidates (1-3 sweeps) + a counts sweep; handles any number
-// of ties and segments of any size (units in chunks of UCAP).
-template <int NT>
-DEV void select_generic(const Params& P, uint32_t lb, uint32_t nu, uint32_t tlo, uint32_t thi, uint32_t r,
-                        SelSmem& S, uint32_t& T_out, uint32_t& rt_out, uint32_t& fp, uint32_t& fn, float& gmn,
-                        float& gmx) {
-  const uint32_t t = threadIdx.x;
-  uint32_t rt = r;
-  auto forC = [&](auto&& f) {
-    for (uint32_t c0 = 0; c0 < nu; c0 += UCAP) {
-      const uint32_t cn = min(UCAP, nu - c0);
-      const uint32_t total = chunk_prefix<NT>(P.cntC + lb + c0, cn, S.upre, S.sh);
-      const uint32_t E = (total + NT - 1) / NT;
-      const uint32_t j0 = min(total, t * E), j1 = min(total, j0 + E);
-      sweep_run(P.cand, lb + c0, S.upre, cn, j0, j1, [&](float x, uint32_t) { f(fkey(x)); });
-      __syncthreads();
-    }
-  };
-  const uint32_t T = rt == 0 ? thi : block_select<NT>(forC, tlo, thi, rt, S.hist, S.sh);
-
-  // counts sweep: per-unit gt/eq, global tie rank of the first positive / negative tie, min/max of
-  // the values with key > T (all of them are kept).
-  float lmn = qnan(), lmx = qnan();
-  uint32_t carry_eq = 0;
-  if (t == 0) {
-    S.sh[42] = NONE;
-    S.sh[43] = NONE;
-  }
-  for (uint32_t c0 = 0; c0 < nu; c0 += UCAP) {
-    const uint32_t cn = min(UCAP, nu - c0);
-    for (uint32_t i = t; i < cn; i += NT) {
-      S.ugt[i] = 0;
-      S.ueq[i] = 0;
-    }
-    const uint32_t total = chunk_prefix<NT>(P.cntC + lb + c0, cn, S.upre, S.sh);
-    const uint32_t E = (total + NT - 1) / NT;
-    const uint32_t j0 = min(total, t * E), j1 = min(total, j0 + E);
-    uint32_t leq = 0, lfp = NONE, lfn = NONE, cu = NONE, cg = 0, ce = 0;
-    sweep_run(P.cand, lb + c0, S.upre, cn, j0, j1, [&](float x, uint32_t u) {
-      if (u != cu) {
-        if (cu != NONE) {
-          if (cg) atomicAdd(&S.ugt[cu], cg);
-          if (ce) atomicAdd(&S.ueq[cu], ce);
-        }
-        cu = u;
-        cg = ce = 0;
-      }
-      const uint32_t key = fkey(x);
-      if (key > T) {
-        ++cg;
-        lmn = fmin_nan(lmn, x);
-        lmx = fmax_nan(lmx, x);
-      } else if (key == T) {
-        const bool neg = (__float_as_uint(x) >> 31) != 0;
-        lfp = min(lfp, neg ? NONE : leq);  // leq only grows: min keeps the first (branch-free)
-        lfn = min(lfn, neg ? leq : NONE);
-        ++leq;
-        ++ce;
-      }
-    });
-    if (cu != NONE) {
-      if (cg) atomicAdd(&S.ugt[cu], cg);
-      if (ce) atomicAdd(&S.ueq[cu], ce);
-    }
-    uint32_t teq;
-    const uint32_t ex = block_excl_scan<NT>(leq, S.sh, teq) + carry_eq;
-    if (lfp != NONE) atomicMin(&S.sh[42], ex + lfp);
-    if (lfn != NONE) atomicMin(&S.sh[43], ex + lfn);
-    carry_eq += teq;
-    for (uint32_t i = t; i < cn; i += NT) {
-      P.gtC[lb + c0 + i] = S.ugt[i];
-      P.eqC[lb + c0 + i] = S.ueq[i];
-    }
-    __syncthreads();
-  }
-  T_out = T;
-  rt_out = rt;
-  fp = S.sh[42];
-  fn = S.sh[43];
-  gmn = lmn;
-  gmx = lmx;
-  __syncthreads();
-}
-
 template <bool DELTA, bool RAW>
 __global__ __launch_bounds__(SEL_NT) void k_select(Params P) {
   constexpr int NT = SEL_NT;
@@ -916,7 +1106,13 @@ __global__ __launch_bounds__(SEL_NT) void k_select(Params P) {
   const uint32_t s = P.large_list[li];
   const SegDev sd = P.segs[s];
   const uint32_t lb = sd.lu_begin, nu = sd.unit_end - sd.unit_begin, k = sd.k;
-
+  STAMP(P, 0);
+  uint32_t T, rt, fp_rank, fn_rank;
+  float gmn, gmx;
+  const uint4 st = P.sstate[li];
+  bool done = st.w == 0 && select_from_groups<NT>(P, sd, lb, nu, st, S, T, rt, fp_rank, fn_rank, gmn, gmx);
+  STAMP(P, 1);
+  if (!done) {
   uint32_t sa = 0, sc = 0;
   for (uint32_t i = t; i < nu; i += NT) {
     sa += P.cntA[lb + i];
@@ -949,12 +1145,10 @@ __global__ __launch_bounds__(SEL_NT) void k_select(Params P) {
 
   // rank of the k-th key among candidates with key <= thi (0: none of them)
   const uint32_t r = k - sa;
-  uint32_t T, rt, fp_rank, fn_rank;
-  float gmn, gmx;
-  bool done = false;
-  if (r > 0 && !exact && nu <= UCAP && !(P.flags & COALAC_FLAG_GENERIC_SELECT))
-    done = select_fast<NT>(P, lb, nu, tlo, thi, r, S, T, rt, fp_rank, fn_rank, gmn, gmx);
-  if (!done) select_generic<NT>(P, lb, nu, tlo, thi, r, S, T, rt, fp_rank, fn_rank, gmn, gmx);
+  (void)exact;
+  select_generic<NT>(P, lb, nu, tlo, thi, r, S, T, rt, fp_rank, fn_rank, gmn, gmx);
+  }
+  STAMP(P, 10);
 
   // in-order scan over the units: global tie prefix and output offsets
   uint32_t carry_e = 0, carry_sel = 0;
@@ -975,6 +1169,7 @@ __global__ __launch_bounds__(SEL_NT) void k_select(Params P) {
       P.outoff[lb + i] = so;
     }
   }
+  STAMP(P, 11);
   float mn = 0.0f, scale = 0.0f;
   if (!RAW) {
     const float tv = __uint_as_float(T);
@@ -998,6 +1193,7 @@ __global__ __launch_bounds__(SEL_NT) void k_select(Params P) {
     P.mn[s] = mn;
     P.scale[s] = scale;
   }
+  STAMP(P, 12);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -1022,7 +1218,7 @@ __global__ __launch_bounds__(BLOCK) void k_emit(Params P) {
   for (uint32_t i0 = 0; i0 < nC; i0 += 64) {
     const uint32_t i = i0 + lane;
     const bool valid = i < nC;
-    const uint2 rec = valid ? R[i] : make_uint2(0u, 0u);
+    const uint2 rec = R[min(i, nC - 1)];  // unconditional load (clamped index)
     const float x = __uint_as_float(rec.y);
     const uint32_t key = fkey(x);
     const bool e = valid && key == T;
@@ -1063,8 +1259,9 @@ __global__ __launch_bounds__(BLOCK) void k_bounds(Params P, const BChunk* chunks
   uint32_t ix[EPT + 1];
 #pragma unroll
   for (uint32_t q = 0; q <= EPT; ++q) {
-    const uint32_t e = e0 + q - 1;  // q = 0: the entry before e0
-    ix[q] = (q == 0 && e0 == 0) ? 0u : (e < C.e1 ? (uint32_t)L[e] : 0u);
+    // q = 0: the entry before e0; indices clamped so every load is unconditional
+    const uint32_t e = min(e0 + q - (e0 == 0 && q == 0 ? 0u : 1u), C.e1 - 1);
+    ix[q] = (uint32_t)L[e];
   }
 #pragma unroll
   for (uint32_t q = 1; q <= EPT; ++q) {
@@ -1097,10 +1294,13 @@ __global__ __launch_bounds__(BLOCK) void k_decode(Params P) {
   const uint32_t len = U.len;
   const int32_t* Lx = P.cidx + U.out_off;
   // first batch of kept entries, loaded before the background stores
+  // unconditional loads at a clamped index (k >= 1): guarded loads would each wait vmcnt(0)
   const uint32_t e = lo + lane;
   const bool has = e < hi;
-  const uint32_t pos0 = has ? (uint32_t)Lx[e] - U.start : NONE;
-  const float v0 = has ? load_val<RAW>(P, U.out_off + e, mn, scale) : 0.0f;
+  const uint32_t ec = min(e, U.k - 1);
+  const uint32_t pos0r = (uint32_t)Lx[ec] - U.start;
+  const float v0 = load_val<RAW>(P, U.out_off + ec, mn, scale);
+  const uint32_t pos0 = has ? pos0r : NONE;
   float* out = P.out + U.off;
   const float* bs = HASBASE ? P.base + U.off : nullptr;
   if (len == UNIT) {
@@ -1157,11 +1357,11 @@ size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 struct WsLayout {
   size_t tstar, rtie, status;
   size_t tlo, thi, cntA, cntC, gtC, eqC, eqpre, outoff;
-  size_t cand;
+  size_t cand, stamps, ghist, gcnt, glist, gmm, sstate, shhi;
   size_t total;
 };
 
-WsLayout ws_layout(size_t S, size_t LU) {
+WsLayout ws_layout(size_t S, size_t LU, size_t NG, size_t NL) {
   WsLayout L{};
   size_t o = 0;
   auto take = [&](size_t bytes) {
@@ -1181,6 +1381,13 @@ WsLayout ws_layout(size_t S, size_t LU) {
   L.eqpre = take(4 * LU);
   L.outoff = take(4 * LU);
   L.cand = take(sizeof(uint2) * UNIT * LU);
+  L.stamps = take(8 * NSTAMP * std::max<size_t>(S, 1));
+  L.ghist = take(4 * HB2 * NG);
+  L.gcnt = take(4 * NG);
+  L.glist = take(sizeof(uint2) * GCAP * NG);
+  L.gmm = take(8 * NG);
+  L.sstate = take(sizeof(uint4) * NL);
+  L.shhi = take(4 * NL);
   L.total = std::max<size_t>(o, 256);
   return L;
 }
@@ -1200,7 +1407,8 @@ struct coalac_plan {
   uint32_t* small_list = nullptr;
   uint32_t* large_list = nullptr;
   BChunk* bchunks = nullptr;
-  uint32_t n_bchunks = 0;
+  uint4* groups = nullptr;
+  uint32_t n_bchunks = 0, n_groups = 0;
   WsLayout ws{};
   size_t dec_ws = 0;
 };
@@ -1221,6 +1429,8 @@ void fill_meta(Params& P, coalac_plan_t plan) {
   P.lunits = plan->lunits;
   P.small_list = plan->small_list;
   P.large_list = plan->large_list;
+  P.groups = plan->groups;
+  P.n_groups = plan->n_groups;
   P.nseg = (uint32_t)plan->nseg;
   P.n_small = plan->n_small;
   P.n_large = plan->n_large;
@@ -1241,7 +1451,12 @@ void launch_encode(const Params& P, coalac_plan_t plan, hipStream_t st, void* co
   record(ev, 1, st);
   if (plan->n_small + gu) hipLaunchKernelGGL((k_scan<DELTA, RAW>), dim3(plan->n_small + gu), dim3(BLOCK), 0, st, P);
   record(ev, 2, st);
-  if (plan->n_large) hipLaunchKernelGGL((k_select<DELTA, RAW>), dim3(plan->n_large), dim3(SEL_NT), 0, st, P);
+  if (plan->n_large) {
+    hipLaunchKernelGGL(k_ghist, dim3(plan->n_groups), dim3(BLOCK), 0, st, P);
+    hipLaunchKernelGGL(k_pick, dim3(plan->n_large), dim3(BLOCK), 0, st, P);
+    hipLaunchKernelGGL(k_gwin, dim3(plan->n_groups), dim3(BLOCK), 0, st, P);
+    hipLaunchKernelGGL((k_select<DELTA, RAW>), dim3(plan->n_large), dim3(SEL_NT), 0, st, P);
+  }
   record(ev, 3, st);
   if (plan->n_large) hipLaunchKernelGGL((k_emit<RAW>), dim3(gu), dim3(BLOCK), 0, st, P);
   record(ev, 4, st);
@@ -1264,6 +1479,7 @@ int coalac_plan_create(const coalac_seg_t* h_segs, int nseg, int bits, coalac_pl
   std::vector<SegDev> segs(nseg);
   std::vector<UnitDev> units, lunits;
   std::vector<BChunk> bchunks;
+  std::vector<uint4> groups;
   std::vector<uint32_t> small_list, large_list;
   uint64_t span = 0, total_k = 0;
   std::vector<std::pair<uint64_t, uint64_t>> in_r, out_r;
@@ -1297,6 +1513,12 @@ int coalac_plan_create(const coalac_seg_t* h_segs, int nseg, int bits, coalac_pl
       if (large) lunits.push_back(u);
     }
     d.unit_end = (uint32_t)units.size();
+    if (large) {
+      d.g_begin = (uint32_t)groups.size();
+      const uint32_t nu = d.unit_end - d.unit_begin;
+      for (uint32_t g0 = 0; g0 < nu; g0 += GU)
+        groups.push_back(make_uint4((uint32_t)large_list.size(), d.lu_begin + g0, std::min(GU, nu - g0), (uint32_t)s));
+    }
     (large ? large_list : small_list).push_back((uint32_t)s);
     for (uint64_t e0 = 0; e0 < g.k; e0 += BCHUNK)
       bchunks.push_back(BChunk{(uint32_t)s, (uint32_t)e0, (uint32_t)std::min<uint64_t>(g.k, e0 + BCHUNK), 0u});
@@ -1329,9 +1551,10 @@ int coalac_plan_create(const coalac_seg_t* h_segs, int nseg, int bits, coalac_pl
   p->n_units = (uint32_t)units.size();
   p->n_lunits = (uint32_t)lunits.size();
   p->n_bchunks = (uint32_t)bchunks.size();
+  p->n_groups = (uint32_t)groups.size();
   p->span = span;
   p->total_k = total_k;
-  p->ws = ws_layout((size_t)nseg, lunits.size());
+  p->ws = ws_layout((size_t)nseg, lunits.size(), groups.size(), large_list.size());
   p->dec_ws = align_up(4 * (units.size() + 1), 256);
 
   const size_t o_segs = 0;
@@ -1340,7 +1563,8 @@ int coalac_plan_create(const coalac_seg_t* h_segs, int nseg, int bits, coalac_pl
   const size_t o_small = align_up(o_lunits + sizeof(UnitDev) * lunits.size(), 256);
   const size_t o_large = align_up(o_small + 4 * small_list.size(), 256);
   const size_t o_bch = align_up(o_large + 4 * large_list.size(), 256);
-  const size_t bytes = align_up(o_bch + sizeof(BChunk) * bchunks.size(), 256) + 256;
+  const size_t o_grp = align_up(o_bch + sizeof(BChunk) * bchunks.size(), 256);
+  const size_t bytes = align_up(o_grp + sizeof(uint4) * groups.size(), 256) + 256;
   std::vector<uint8_t> host(bytes, 0);
   if (!segs.empty()) memcpy(host.data() + o_segs, segs.data(), sizeof(SegDev) * segs.size());
   if (!units.empty()) memcpy(host.data() + o_units, units.data(), sizeof(UnitDev) * units.size());
@@ -1348,6 +1572,7 @@ int coalac_plan_create(const coalac_seg_t* h_segs, int nseg, int bits, coalac_pl
   if (!small_list.empty()) memcpy(host.data() + o_small, small_list.data(), 4 * small_list.size());
   if (!large_list.empty()) memcpy(host.data() + o_large, large_list.data(), 4 * large_list.size());
   if (!bchunks.empty()) memcpy(host.data() + o_bch, bchunks.data(), sizeof(BChunk) * bchunks.size());
+  if (!groups.empty()) memcpy(host.data() + o_grp, groups.data(), sizeof(uint4) * groups.size());
   hipError_t e = hipMalloc(&p->meta, bytes);
   if (e != hipSuccess) {
     delete p;
@@ -1366,6 +1591,7 @@ int coalac_plan_create(const coalac_seg_t* h_segs, int nseg, int bits, coalac_pl
   p->small_list = reinterpret_cast<uint32_t*>(m + o_small);
   p->large_list = reinterpret_cast<uint32_t*>(m + o_large);
   p->bchunks = reinterpret_cast<BChunk*>(m + o_bch);
+  p->groups = reinterpret_cast<uint4*>(m + o_grp);
   *out = p;
   return COALAC_OK;
 }
@@ -1430,6 +1656,13 @@ int coalac_encode_ev(coalac_plan_t plan, const float* d_in, const float* d_base,
   P.eqpre = reinterpret_cast<uint32_t*>(w + L.eqpre);
   P.outoff = reinterpret_cast<uint32_t*>(w + L.outoff);
   P.cand = reinterpret_cast<uint2*>(w + L.cand);
+  P.stamps = (flags & COALAC_FLAG_STAMPS) ? reinterpret_cast<uint64_t*>(w + L.stamps) : nullptr;
+  P.ghist = reinterpret_cast<uint32_t*>(w + L.ghist);
+  P.gcnt = reinterpret_cast<uint32_t*>(w + L.gcnt);
+  P.glist = reinterpret_cast<uint2*>(w + L.glist);
+  P.gmm = reinterpret_cast<float*>(w + L.gmm);
+  P.sstate = reinterpret_cast<uint4*>(w + L.sstate);
+  P.shhi = reinterpret_cast<uint32_t*>(w + L.shhi);
   hipStream_t st = static_cast<hipStream_t>(stream);
   const bool delta = d_base != nullptr, raw = plan->bits == 32;
   if (delta && raw)
@@ -1515,6 +1748,17 @@ int coalac_workspace_fallbacks(coalac_plan_t plan, const void* d_ws, void* strea
   for (uint32_t s2 : large) c += st[s2] == 1;
   *out = c;
   return COALAC_OK;
+}
+
+int coalac_debug_stamps(coalac_plan_t plan, const void* d_ws, void* stream, uint64_t* host, int n) {
+  if (!plan || !d_ws || !host || n < 0) return fail(COALAC_EINVAL, "coalac_debug_stamps: bad argument");
+  const size_t cap = (size_t)NSTAMP * std::max<size_t>(plan->nseg, 1);
+  const size_t cnt = std::min<size_t>((size_t)n, cap);
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  HIP_CHECK(hipMemcpyAsync(host, static_cast<const uint8_t*>(d_ws) + plan->ws.stamps, 8 * cnt,
+                           hipMemcpyDeviceToHost, s));
+  HIP_CHECK(hipStreamSynchronize(s));
+  return (int)cnt;
 }
 
 }  // extern "C"

@@ -47,7 +47,8 @@ enum {
 
 enum {
   COALAC_FLAG_FORCE_EXACT = 1,    /* test hook: re-select every large segment exactly (no sampling) */
-  COALAC_FLAG_GENERIC_SELECT = 2  /* test hook: resolve the k-th key with the multi-pass select only */
+  COALAC_FLAG_GENERIC_SELECT = 2, /* test hook: resolve the k-th key with the multi-pass select only */
+  COALAC_FLAG_STAMPS = 4          /* diagnostics: record per-block phase timestamps of k_select */
 };
 
 /* One fp32 segment (= one flattened tensor of the state_dict). Offsets are in ELEMENTS.
@@ -107,6 +108,11 @@ int coalac_decode_ev(coalac_plan_t plan, const int32_t* d_idx, const void* d_val
 /* Diagnostics: number of segments whose sampled thresholds were rejected and re-selected exactly in
  * the last encode that used workspace d_ws (synchronises `stream`). */
 int coalac_workspace_fallbacks(coalac_plan_t plan, const void* d_ws, void* stream, int* out);
+
+/* Diagnostics: copy up to n phase timestamps (16 per k_select block = per large segment, 100 MHz
+ * ticks; 0 = phase not reached) of the last COALAC_FLAG_STAMPS encode with d_ws to host (synchronises
+ * `stream`). Returns the count copied or a negative error. */
+int coalac_debug_stamps(coalac_plan_t plan, const void* d_ws, void* stream, uint64_t* host, int n);
 
 #ifdef __cplusplus
 }
