@@ -1,0 +1,25 @@
+#!/bin/bash
+# Profile the default bench workload on the GPU box (run through gpurun from the repo root):
+#   tools/profile_round.sh r01
+# Pass 1: kernel trace + stats (per-kernel average durations, must agree with bench.py's HIP events).
+# Pass 2/3: FETCH_SIZE and WRITE_SIZE in separate passes (they do not fit one TCC pass on gfx950),
+# no trace domains besides the kernel trace. Summaries land in gpurun_out/prof_<tag>/.
+set -e
+TAG=${1:-r01}
+OUT=gpurun_out/prof_${TAG}
+mkdir -p "$OUT"
+export TMPDIR=/tmp
+timeout -k 10 240 rocprofv3 --kernel-trace --stats -d "$OUT/trace" -o run --output-format csv \
+  -- python3 bench.py --steps 10 --warmup 3 --no-cpu-baseline > "$OUT/bench_trace.json" 2> "$OUT/trace.err"
+timeout -k 10 240 rocprofv3 --pmc FETCH_SIZE -d "$OUT/fetch" -o run --output-format csv \
+  -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline > "$OUT/bench_fetch.json" 2> "$OUT/fetch.err"
+timeout -k 10 240 rocprofv3 --pmc WRITE_SIZE -d "$OUT/write" -o run --output-format csv \
+  -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline > "$OUT/bench_write.json" 2> "$OUT/write.err"
+python3 tools/pmc_summary.py "$OUT" > "$OUT/summary.json"
+# keep the small summaries only (raw per-dispatch CSVs can exceed gpurun's 64 MiB pull limit)
+du -sh "$OUT"/trace "$OUT"/fetch "$OUT"/write || true
+for s in trace fetch write; do
+  find "$OUT/$s" -name '*kernel_stats.csv' -exec cp {} "$OUT/${s}_kernel_stats.csv" \; || true
+done
+rm -rf "$OUT/trace" "$OUT/fetch" "$OUT/write"
+ls -la "$OUT"
