@@ -161,7 +161,7 @@ def main():
         return sum(s.elapsed_time(e) for s, e in pairs) / len(pairs)
     stages = {}
     for name, (which, i0, i1) in {"k_sample": ("ev_e", 0, 1), "k_scan": ("ev_e", 1, 2), "k_select": ("ev_e", 2, 3),
-                                  "k_emit": ("ev_e", 3, 4), "k_bounds": ("ev_d", 0, 1),
+                                  "k_emit": ("ev_e", 3, 4),
                                   "k_decode": ("ev_d", 1, 2)}.items():
         stages[name] = mean([(e[i0], e[i1]) for L in lanes for e in L[which]])
     N, K, T = t.n_elements, t.total_k, t.n_segments

@@ -37,11 +37,11 @@ class HipBackend:
     def default_device(self):
         return torch.device("cuda", torch.cuda.current_device())
 
-    def make_plan(self, sizes, ratio, bits, device):
+    def make_plan(self, sizes, ratio, bits, device, clients=1):
         if device.type != "cuda":
             raise RuntimeError(f"the HIP codec runs on GPU tensors only; got tensors on {device} "
                                "(there is no CPU fallback)")
-        return CodecPlan(sizes, ratio, bits, clients=1, device=device)
+        return CodecPlan(sizes, ratio, bits, clients=clients, device=device)
 
 
 class FlatState:
@@ -209,14 +209,14 @@ class UpdateCodec:
         self._plans = {}
         self._lock = threading.Lock()
 
-    def plan_for(self, sizes, device, ratio=None, bits=None):
+    def plan_for(self, sizes, device, ratio=None, bits=None, clients=1):
         ratio = self.ratio if ratio is None else float(ratio)
         bits = self.bits if bits is None else int(bits)
-        key = (tuple(sizes), ratio, bits, str(device))
+        key = (tuple(sizes), ratio, bits, str(device), int(clients))
         with self._lock:
             p = self._plans.get(key)
             if p is None:
-                p = self.backend.make_plan(list(sizes), ratio, bits, device)
+                p = self.backend.make_plan(list(sizes), ratio, bits, device, clients=clients)
                 self._plans[key] = p
         return p
 
@@ -280,6 +280,60 @@ class UpdateCodec:
         output (deepcopy with a memo that pre-binds every tensor). `template` is never aliased.
         """
         state = self.decode_state(update, base=base)
+        return module_with_state(template, state)
+
+
+    # -- fused server-side aggregation ------------------------------------------------------------
+    def aggregate(self, updates, weights, template, base=None, mode="recip"):
+        """Fused decode + FedAvg of several CompressedUpdates of one layout -> new nn.Module.
+
+        Equivalent to decode_module() of every update followed by the reference's
+        strategies.federated_averaging(models, weights) (coala/server/strategies.py:6-29, 57-90), with
+        the fp32 entries decoded and averaged in ONE kernel (coalac_aggregate) instead of C dense
+        modules. mode "recip": torch-on-GPU division semantics (the decoded modules live on the GPU);
+        "div": torch-on-CPU. Non-fp32 entries (int64 BatchNorm counters) are averaged with the same
+        torch ops as the reference, on the output device. Weights follow federated_averaging: empty or
+        all-zero weights become 1 per update.
+        """
+        if not updates:
+            return None
+        weights = list(weights) if weights is not None else []
+        if not weights or sum(weights) == 0:
+            weights = [1 for _ in updates]
+        if len(weights) != len(updates):
+            raise ValueError("one weight per update")
+        total = sum(weights)
+        h0 = updates[0].header
+        for u in updates[1:]:
+            h = u.header
+            if (h["ratio"], h["bits"], h["mode"], h["entries"]) != (h0["ratio"], h0["bits"], h0["mode"], h0["entries"]):
+                raise ValueError("fused aggregation needs updates of one layout / ratio / bits / mode")
+        sizes = [e["n"] for e in h0["entries"] if e["kind"] == "seg"]
+        if h0["mode"] == "delta":
+            if base is None:
+                raise ValueError("delta-mode updates need the global model (base) to aggregate")
+            _check_same_layout(h0["entries"], base.entries)
+            device = base.flat.device if base.flat is not None else self.backend.default_device()
+        else:
+            device = self.backend.default_device()
+        state = OrderedDict()
+        flat = None
+        if sizes:
+            C = len(updates)
+            plan = self.plan_for(sizes, device, ratio=h0["ratio"], bits=h0["bits"], clients=C)
+            encs = [u.encoded.to(device, non_blocking=True) for u in updates]
+            batched = Encoded(*(torch.cat([getattr(e, f) for e in encs]) for f in ("idx", "vals", "mn", "scale")))
+            flat = plan.aggregate(batched, weights, total=total,
+                                  base=base.flat if h0["mode"] == "delta" else None, mode=mode)
+        for e in h0["entries"]:
+            if e["kind"] == "seg":
+                state[e["name"]] = flat[e["off"]:e["off"] + e["n"]].view(e["shape"])
+            else:  # restated weighted_sum + torch.div on the raw entries, then the dtype cast load_state_dict does
+                acc = updates[0].raw[e["name"]].to(device).clone()
+                acc *= weights[0]
+                for i in range(1, len(updates)):
+                    acc += updates[i].raw[e["name"]].to(device) * weights[i]
+                state[e["name"]] = torch.div(acc, total).to(acc.dtype)
         return module_with_state(template, state)
 
 

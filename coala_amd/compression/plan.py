@@ -111,14 +111,15 @@ class CodecPlan:
         return torch.empty(self.dec_ws_bytes, dtype=torch.uint8, device=self.device)
 
     # -- checks -----------------------------------------------------------------------------------
-    def _check_flat(self, t, name):
+    def _check_flat(self, t, name, need=None):
         if t is None:
             return
+        need = self.span if need is None else need
         if t.device != self.device or t.dtype != torch.float32 or not t.is_contiguous():
             raise ValueError(f"{name}: need a contiguous float32 tensor on {self.device}, got "
                              f"{t.dtype} on {t.device} (contiguous={t.is_contiguous()})")
-        if t.numel() < self.span:
-            raise ValueError(f"{name}: {t.numel()} elements < plan span {self.span}")
+        if t.numel() < need:
+            raise ValueError(f"{name}: {t.numel()} elements < required {need}")
         if t.data_ptr() % 16:
             raise ValueError(f"{name}: storage must be 16-byte aligned")
 
@@ -169,6 +170,45 @@ class CodecPlan:
             else:
                 rc = self._lib.coalac_decode_ev(*args, _event_array(events, 3))
         _lib.check(rc, "coalac_decode")
+        return out
+
+    def aggregate(self, enc, weights, total=None, base=None, out=None, workspace=None, mode="recip", stream=None,
+                  events=None):
+        """Fused decode + FedAvg of the plan's `clients` updates (coalac_aggregate).
+
+        enc: the batched Encoded of all clients (client-major, as encode() produces). weights: one
+        number per client (FedAvg weights, e.g. sample counts); total: their sum (default
+        sum(weights)). Returns out fp32[span_per_client] indexed like client 0's segments:
+        base + decoded_i averaged exactly as coala/server/strategies.py:6-29,57-90 would on the decoded
+        modules — mode "recip" reproduces torch on the GPU (division by a host scalar becomes a multiply
+        by its fp32 reciprocal), "div" torch on the CPU.
+        """
+        self._check_encoded(enc)
+        C = self.table.clients
+        if len(weights) != C:
+            raise ValueError(f"need {C} weights, got {len(weights)}")
+        if mode not in ("recip", "div"):
+            raise ValueError(f"mode must be 'recip' or 'div', got {mode!r}")
+        n_out = self.table.span_per_client
+        if base is not None:
+            self._check_flat(base, "base", n_out)
+        out = torch.empty(n_out, dtype=torch.float32, device=self.device) if out is None else out
+        self._check_flat(out, "output", n_out)
+        ws = self.empty_decode_workspace() if workspace is None else workspace
+        if ws.device != self.device or ws.numel() * ws.element_size() < self.dec_ws_bytes:
+            raise ValueError(f"aggregate workspace: need {self.dec_ws_bytes} bytes on {self.device}")
+        w = torch.tensor([float(x) for x in weights], dtype=torch.float64).to(torch.float32).to(self.device)
+        total = float(sum(weights)) if total is None else float(total)
+        args = (self._h, C, _ptr(enc.idx), _ptr(enc.vals), _ptr(enc.mn), _ptr(enc.scale), _ptr(w),
+                ctypes.c_float(total), _lib.COALAC_AGG_RECIP if mode == "recip" else _lib.COALAC_AGG_DIV,
+                _ptr(base), _ptr(out), _ptr(ws), ctypes.c_uint64(self.dec_ws_bytes), _stream_handle(stream))
+        with torch.cuda.device(self.device):
+            if events is None:
+                rc = self._lib.coalac_aggregate(*args)
+            else:
+                rc = self._lib.coalac_aggregate_ev(*args, _event_array(events, 3))
+        _lib.check(rc, "coalac_aggregate")
+        self._keepalive = w  # the weights buffer must outlive the asynchronous launch
         return out
 
     def fallbacks(self, workspace, stream=None):

@@ -37,6 +37,9 @@ from torch import nn
 
 from .codec import CompressedUpdate, UpdateCodec
 
+EQUAL_AVERAGE = "equal"                     # coala/server/base.py:37
+AGGREGATION_CONTENT_PARAMS = "parameters"   # coala/server/base.py:40
+
 
 def _bit_to_megabyte(bits):
     # same conversion as the reference tracker (coala/tracking/evaluation.py:16-17)
@@ -108,8 +111,42 @@ class CompressionServerMixin(_CodecOwner):
                 self.__dict__["_codec_snapshot"] = snap
             return snap[1]
 
+    codec_fused_aggregate = False
+
+    def _decode_upload(self, model):
+        base = self._global_snapshot() if model.header["mode"] == "delta" else None
+        return self._codec().decode_module(model, self.model, base=base)
+
     def decompression(self, model):
         if isinstance(model, CompressedUpdate):
-            base = self._global_snapshot() if model.header["mode"] == "delta" else None
-            return self._codec().decode_module(model, self.model, base=base)
+            if self.codec_fused_aggregate:
+                return model  # decoded together with the other uploads in aggregate()
+            return self._decode_upload(model)
         return model
+
+    def aggregate(self, models, weights):
+        conf = getattr(self, "conf", None)
+        server_conf = getattr(conf, "server", None)
+        distributed = bool(getattr(conf, "is_distributed", False))
+        params_only = getattr(server_conf, "aggregation_content", "all") == AGGREGATION_CONTENT_PARAMS
+        fusable = (self.codec_fused_aggregate and models and not distributed and not params_only
+                   and all(isinstance(m, CompressedUpdate) for m in models))
+        if fusable:
+            if getattr(server_conf, "aggregation_strategy", None) == EQUAL_AVERAGE:
+                weights = [1 for _ in models]
+            h0 = models[0].header
+            if all(m.header["entries"] == h0["entries"] and
+                   (m.header["ratio"], m.header["bits"], m.header["mode"]) == (h0["ratio"], h0["bits"], h0["mode"])
+                   for m in models):
+                base = self._global_snapshot() if h0["mode"] == "delta" else None
+                codec = self._codec()
+                dev = base.flat.device if base is not None and base.flat is not None else \
+                    codec.backend.default_device()
+                mode = "div" if dev.type == "cpu" else "recip"  # torch's division semantics on that device
+                return codec.aggregate(models, weights, self.model, base=base, mode=mode)
+        models = [self._decode_upload(m) if isinstance(m, CompressedUpdate) else m for m in models]
+        parent = getattr(super(), "aggregate", None)
+        if parent is not None:
+            return parent(models, weights)
+        from ..fl.strategies import federated_averaging
+        return federated_averaging(models, weights)

@@ -24,8 +24,8 @@
 //   end in its first blocks, overlapping the streaming classify + compaction of the large units),
 //   k_select (exact k-th key inside B, tie quota, per-unit output offsets, min/max -> scale; 1024
 //   threads per segment), k_emit (sorted idx + codes via an LDS bitmap).
-//   Decode: k_bounds (first kept entry of every unit, one streaming pass over the sorted idx lists),
-//   k_decode (one wave per unit, no LDS: dense float4 background stores, then the kept values).
+//   Decode: k_decode (one wave per unit, no LDS: dense float4 background stores, a wave-parallel search
+//   of the unit's range in the segment's sorted idx list, then the kept values).
 //
 // Numerics: built with -ffp-contract=off; fp32 sub/div/mul/add are separate IEEE ops, rintf is
 // round-half-even — the same op sequence as the oracle, so decoded values are bit-identical.
@@ -53,7 +53,6 @@ constexpr uint32_t UNIT_IT = UNIT / 256;  // float4 loads per lane per unit
 constexpr uint32_t SMALL_MAX = 4096;      // segments up to this size are encoded whole in one block
 constexpr uint32_t SAMPLE_MAX = 8192;     // sampled keys per large segment
 constexpr int SEL_NT = 512;               // threads of a k_select block
-constexpr uint32_t BCHUNK = 4096;         // idx entries per k_bounds block
 constexpr uint32_t STAGE_CAP = 512;       // candidate records staged in LDS per k_scan wave
 constexpr uint32_t GU = 32;               // units per select group (k_ghist / k_gwin block)
 constexpr uint32_t HB2 = 512;             // bins of the per-group band histograms
@@ -61,6 +60,7 @@ constexpr uint32_t GCAP = 256;            // in-window entries a group may hand 
 constexpr uint32_t A_FLAG = 0x80000000u;  // candidate record flag: key > T_hi (kept for sure)
 constexpr uint32_t KEY_MAX = 0x7FFFFFFFu;
 constexpr int HIST_BINS = 2048;
+constexpr uint32_t BCHUNK = 4096;         // idx entries per k_bounds block (aggregate)
 constexpr uint32_t UCAP = 2048;           // units per k_select chunk (8.4 M elements)
 constexpr uint32_t NONE = 0xFFFFFFFFu;
 constexpr int NSTAMP = 16;
@@ -120,9 +120,9 @@ struct Params {
   float* gmm;              // [n_groups][2] min/max of the group's values above the window
   uint4* sstate;           // [n_large] {wlo, whi, rank inside the window, path: 0 fast / 1 generic}
   uint32_t* shhi;          // [n_large] histogram upper bound: min(T_hi, largest sampled key)
+  uint32_t* arrive;        // [n_large][2] group blocks done in k_ghist / k_gwin (reset by k_sample)
 
   // decode workspace
-  uint32_t* ustart;
   // diagnostics: per-block phase timestamps (COALAC_FLAG_STAMPS), NSTAMP per block, 100 MHz ticks
   uint64_t* stamps;
 };
@@ -134,11 +134,11 @@ struct Params {
 
 DEV uint32_t fkey(float x) { return __float_as_uint(x) & KEY_MAX; }
 
-// diagnostics only: thread 0 records the 100 MHz real-time counter for phase i of this block
-#define STAMP(P, i)                                                                                 \
+// diagnostics only: thread 0 records the 100 MHz real-time counter for phase i of large segment li
+#define STAMP(P, li, i)                                                                             \
   do {                                                                                              \
     if ((P).stamps != nullptr && threadIdx.x == 0)                                                  \
-      (P).stamps[(uint64_t)blockIdx.x * NSTAMP + (i)] = __builtin_amdgcn_s_memrealtime();          \
+      (P).stamps[(uint64_t)(li) * NSTAMP + (i)] = __builtin_amdgcn_s_memrealtime();                \
   } while (0)
 
 // NaN-ignoring min/max (NaN only if both are NaN) = IEEE minNum/maxNum: one v_min_f32 / v_max_f32
@@ -665,11 +665,15 @@ __global__ __launch_bounds__(BLOCK) void k_sample(Params P) {
   }
   // The band histograms of the parallel select span [T_lo, min(T_hi, max sampled key)] (keys above go
   // to the last bin): with T_hi = KEY_MAX a full-range histogram would be too coarse.
-  if (t == 0) P.shhi[blockIdx.x] = max(tlo, min(thi, kmax));
+  if (t == 0) {
+    P.shhi[blockIdx.x] = max(tlo, min(thi, kmax));
+    P.arrive[2 * blockIdx.x] = 0;
+    P.arrive[2 * blockIdx.x + 1] = 0;
+  }
   if (t == 0) P.status[s] = 0;
 }
 
-// k_scan: blocks [0, n_small) encode the small segments; the rest stream the large units, one wave each.
+// k_scan: n_small blocks encode the small segments; the rest stream the large units, one wave each.
 template <bool DELTA, bool RAW>
 __global__ __launch_bounds__(BLOCK) void k_scan(Params P) {
   // one LDS arena: small-segment blocks use it as values + histogram, streaming blocks as candidate
@@ -677,22 +681,26 @@ __global__ __launch_bounds__(BLOCK) void k_scan(Params P) {
   constexpr size_t SMALL_BYTES = (SMALL_MAX + HIST_BINS + 64) * 4;
   constexpr size_t STAGE_BYTES = WAVES * STAGE_CAP * sizeof(uint2);
   __shared__ __attribute__((aligned(16))) uint8_t arena[SMALL_BYTES > STAGE_BYTES ? SMALL_BYTES : STAGE_BYTES];
-  if (blockIdx.x < P.n_small) {
+  // The compute-heavy small-segment blocks are spread evenly over the grid (block b is small iff
+  // floor((b+1)*ns/T) > floor(b*ns/T)), so they overlap the streaming blocks instead of delaying them.
+  const uint64_t b = blockIdx.x, T = gridDim.x, ns = P.n_small;
+  const uint32_t before = (uint32_t)(b * ns / T);
+  if ((uint32_t)((b + 1) * ns / T) != before) {
     float* sbuf = reinterpret_cast<float*>(arena);
     uint32_t* hist = reinterpret_cast<uint32_t*>(arena) + SMALL_MAX;
     uint32_t* sh = hist + HIST_BINS;
-    small_encode<DELTA, RAW>(P, P.small_list[blockIdx.x], sbuf, hist, sh);
+    small_encode<DELTA, RAW>(P, P.small_list[before], sbuf, hist, sh);
     return;
   }
   const uint32_t wv = threadIdx.x >> 6;
-  const uint32_t lu = (blockIdx.x - P.n_small) * WAVES + wv;
+  const uint32_t lu = ((uint32_t)b - before) * WAVES + wv;
   if (lu >= P.n_lunits) return;
   const UnitDev L = P.lunits[lu];
   scan_unit<DELTA, 1>(P, lu, L, P.tlo[lu], P.thi[lu], reinterpret_cast<uint2*>(arena) + wv * STAGE_CAP);
 }
 
 // ------------------------------------------------------------------------------------------------
-// k_select: per large segment, SEL_NT threads
+// per-segment select (run by the last group block of k_gwin)
 // ------------------------------------------------------------------------------------------------
 // Exclusive prefix of cnt[0..cn) into upre[0..cn] (upre[cn] = total). Barriers inside.
 template <int NT>
@@ -765,14 +773,11 @@ DEV void unit_sweep(const uint2* cand, uint32_t lu0, const uint32_t* upre, uint3
 
 // LDS scratch of k_select
 constexpr uint32_t WLIST = 2048;               // in-window entries the fast path can hold
-constexpr uint32_t WSLOT = WLIST / (SEL_NT / 64);  // per-wave share while sweeping
 struct SelSmem {
   uint32_t hist[HIST_BINS];
   uint32_t upre[UCAP + 1];
   uint32_t ugt[UCAP];
   uint32_t ueq[UCAP];
-  uint32_t slot_val[WLIST];   // per-wave in-window slots (value bits, unit), wave w at [w * WSLOT, ...)
-  uint32_t slot_unit[WLIST];
   uint32_t lst_val[WLIST];    // in-window entries, all waves concatenated = index order
   uint32_t lst_unit[WLIST];
   uint32_t wcnt[SEL_NT / 64];
@@ -891,7 +896,24 @@ struct Band {
   DEV uint32_t wlo(uint32_t b) const { return tlo + (b << shift); }
   DEV uint32_t whi(uint32_t b) const { return b == last ? thi : min(thi, wlo(b) + ((1u << shift) - 1u)); }
 };
-// k_ghist: the group's HB2-bin histogram of the band keys [tlo, thi] -> ghist[group]
+// Last-arriving-block pattern: every group block of a segment publishes its results (agent-scope
+// release), counts itself in; the block that arrives last (agent-scope acquire) does the per-segment
+// step. No block ever waits for another, so no co-residency assumption is made.
+DEV bool arrive_last(uint32_t* ctr, uint32_t expected, uint32_t* sh) {
+  __threadfence();
+  __syncthreads();
+  if (threadIdx.x == 0) sh[0] = atomicAdd(ctr, 1u);
+  __syncthreads();
+  const bool last = sh[0] == expected - 1;
+  __syncthreads();
+  if (last) __threadfence();
+  return last;
+}
+
+DEV void segment_pick(const Params& P, uint32_t li, uint32_t* hist, uint32_t* sh);
+
+// k_ghist: the group's HB2-bin histogram of the band keys [tlo, thi] -> ghist[group]; the segment's last
+// group block then picks the window (segment_pick)
 __global__ __launch_bounds__(BLOCK) void k_ghist(Params P) {
   __shared__ uint32_t hist[HB2];
   __shared__ uint32_t upre[GU + 1];
@@ -911,15 +933,16 @@ __global__ __launch_bounds__(BLOCK) void k_ghist(Params P) {
       [&](uint32_t) {});
   __syncthreads();
   for (uint32_t i = t; i < HB2; i += BLOCK) P.ghist[(uint64_t)blockIdx.x * HB2 + i] = hist[i];
+  const SegDev& sd = P.segs[G.w];
+  const uint32_t ng = (sd.unit_end - sd.unit_begin + GU - 1) / GU;
+  if (arrive_last(P.arrive + 2 * G.x, ng, sh)) segment_pick(P, G.x, hist, sh);
 }
 
-// k_pick: per large segment — validate the sampled bracket, sum the group histograms, pick the bin of
+// segment_pick: per large segment — validate the sampled bracket, sum the group histograms, pick the bin of
 // the k-th key: sstate = {window lo, window hi, rank inside the window, 0}; {.., 1} routes the segment
 // to the generic single-block path (bracket miss, nothing to take from B, huge segment, test flags).
-__global__ __launch_bounds__(BLOCK) void k_pick(Params P) {
-  __shared__ uint32_t hist[HB2];
-  __shared__ uint32_t sh[64];
-  const uint32_t t = threadIdx.x, li = blockIdx.x;
+DEV void segment_pick(const Params& P, uint32_t li, uint32_t* hist, uint32_t* sh) {
+  const uint32_t t = threadIdx.x;
   const SegDev sd = P.segs[P.large_list[li]];
   const uint32_t lb = sd.lu_begin, nu = sd.unit_end - sd.unit_begin, k = sd.k;
   uint32_t sa = 0, sc = 0;
@@ -955,16 +978,24 @@ __global__ __launch_bounds__(BLOCK) void k_pick(Params P) {
 }
 
 // k_gwin: per group — per-unit counts of keys above the window (-> gtC), the group's in-window entries
-// in index order (-> glist, count -> gcnt), min/max of the values above the window (-> gmm)
-__global__ __launch_bounds__(BLOCK) void k_gwin(Params P) {
-  __shared__ uint32_t upre[GU + 1];
-  __shared__ uint2 slots[WAVES][GCAP];
-  __shared__ uint32_t wcnt[WAVES];
-  __shared__ uint32_t sh[64];
-  __shared__ float shf[2 * WAVES];
-  const uint4 G = P.groups[blockIdx.x];
-  const uint4 st = P.sstate[G.x];
-  if (st.w != 0) return;
+// in index order (-> glist, count -> gcnt), min/max of the values above the window (-> gmm); the
+// segment's last group block then runs segment_select (also for segments routed to the generic path,
+// whose group blocks only count themselves in).
+struct GwinSmem {
+  uint32_t upre[GU + 1];
+  uint2 slots[WAVES][GCAP];
+  uint32_t wcnt[WAVES];
+  float shf[2 * WAVES];
+};
+
+template <int NT, bool DELTA, bool RAW>
+DEV void segment_select(const Params& P, uint32_t li, SelSmem& S);
+
+DEV void group_window(const Params& P, const uint4 G, const uint4 st, GwinSmem& W_, uint32_t* sh) {
+  uint32_t* upre = W_.upre;
+  auto& slots = W_.slots;
+  uint32_t* wcnt = W_.wcnt;
+  float* shf = W_.shf;
   const uint32_t t = threadIdx.x, lane = lane_id(), wv = t >> 6;
   const uint32_t wlo = st.x, whi = st.y;
   const uint32_t useg0 = G.y - P.segs[G.w].lu_begin;  // unit index (within the segment) of the group's first unit
@@ -1012,6 +1043,21 @@ __global__ __launch_bounds__(BLOCK) void k_gwin(Params P) {
     P.gmm[2 * blockIdx.x] = lmn;
     P.gmm[2 * blockIdx.x + 1] = lmx;
   }
+}
+
+template <bool DELTA, bool RAW>
+__global__ __launch_bounds__(BLOCK) void k_gwin(Params P) {
+  __shared__ union {
+    GwinSmem g;
+    SelSmem s;
+  } U;
+  __shared__ uint32_t sh[64];
+  const uint4 G = P.groups[blockIdx.x];
+  const uint4 st = P.sstate[G.x];
+  if (st.w == 0) group_window(P, G, st, U.g, sh);
+  const SegDev& sd = P.segs[G.w];
+  const uint32_t ng = (sd.unit_end - sd.unit_begin + GU - 1) / GU;
+  if (arrive_last(P.arrive + 2 * G.x + 1, ng, sh)) segment_select<BLOCK, DELTA, RAW>(P, G.x, U.s);
 }
 
 // Fast-path resolution in k_select: gather the groups' in-window lists (group order = index order),
@@ -1096,22 +1142,19 @@ DEV bool select_from_groups(const Params& P, const SegDev& sd, uint32_t lb, uint
   return true;
 }
 
-template <bool DELTA, bool RAW>
-__global__ __launch_bounds__(SEL_NT) void k_select(Params P) {
-  constexpr int NT = SEL_NT;
+template <int NT, bool DELTA, bool RAW>
+DEV void segment_select(const Params& P, uint32_t li, SelSmem& S) {
   constexpr int NW = NT / 64;
-  __shared__ SelSmem S;
   const uint32_t t = threadIdx.x, wv = t >> 6;
-  const uint32_t li = blockIdx.x;
   const uint32_t s = P.large_list[li];
   const SegDev sd = P.segs[s];
   const uint32_t lb = sd.lu_begin, nu = sd.unit_end - sd.unit_begin, k = sd.k;
-  STAMP(P, 0);
+  STAMP(P, li, 0);
   uint32_t T, rt, fp_rank, fn_rank;
   float gmn, gmx;
   const uint4 st = P.sstate[li];
   bool done = st.w == 0 && select_from_groups<NT>(P, sd, lb, nu, st, S, T, rt, fp_rank, fn_rank, gmn, gmx);
-  STAMP(P, 1);
+  STAMP(P, li, 1);
   if (!done) {
   uint32_t sa = 0, sc = 0;
   for (uint32_t i = t; i < nu; i += NT) {
@@ -1148,7 +1191,7 @@ __global__ __launch_bounds__(SEL_NT) void k_select(Params P) {
   (void)exact;
   select_generic<NT>(P, lb, nu, tlo, thi, r, S, T, rt, fp_rank, fn_rank, gmn, gmx);
   }
-  STAMP(P, 10);
+  STAMP(P, li, 10);
 
   // in-order scan over the units: global tie prefix and output offsets
   uint32_t carry_e = 0, carry_sel = 0;
@@ -1169,7 +1212,7 @@ __global__ __launch_bounds__(SEL_NT) void k_select(Params P) {
       P.outoff[lb + i] = so;
     }
   }
-  STAMP(P, 11);
+  STAMP(P, li, 11);
   float mn = 0.0f, scale = 0.0f;
   if (!RAW) {
     const float tv = __uint_as_float(T);
@@ -1193,7 +1236,7 @@ __global__ __launch_bounds__(SEL_NT) void k_select(Params P) {
     P.mn[s] = mn;
     P.scale[s] = scale;
   }
-  STAMP(P, 12);
+  STAMP(P, li, 12);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -1239,21 +1282,91 @@ __global__ __launch_bounds__(BLOCK) void k_emit(Params P) {
 // ------------------------------------------------------------------------------------------------
 // decode
 // ------------------------------------------------------------------------------------------------
+// k_decode: one wave per unit, no LDS. Store the unit's dense background (zeros, or base + 0.0f), wait
+// until those stores are complete (s_waitcnt vmcnt(0): later stores to the same addresses are then
+// ordered after them), then scatter the kept values. The scattered lines are still dirty in L2, so HBM
+// sees each line written once.
+template <bool RAW, bool HASBASE>
+__global__ __launch_bounds__(BLOCK) void k_decode(Params P) {
+  const uint32_t lane = lane_id(), wv = threadIdx.x >> 6;
+  const uint32_t u = blockIdx.x * WAVES + wv;
+  if (u >= P.n_units) return;
+  const UnitDev U = P.units[u];
+  const uint32_t len = U.len;
+  float* out = P.out + U.off;
+  const float* bs = HASBASE ? P.base + U.off : nullptr;
+  if (len == UNIT) {
+    float4 bv[UNIT_IT];
+#pragma unroll
+    for (uint32_t it = 0; it < UNIT_IT; ++it) {
+      if (HASBASE) {
+        bv[it] = *reinterpret_cast<const float4*>(bs + (it * 64 + lane) * 4);
+        bv[it].x = bv[it].x + 0.0f;
+        bv[it].y = bv[it].y + 0.0f;
+        bv[it].z = bv[it].z + 0.0f;
+        bv[it].w = bv[it].w + 0.0f;
+      } else {
+        bv[it] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+      }
+    }
+#pragma unroll
+    for (uint32_t it = 0; it < UNIT_IT; ++it) *reinterpret_cast<float4*>(out + (it * 64 + lane) * 4) = bv[it];
+  } else {
+    for (uint32_t i = lane; i < len; i += 64) out[i] = HASBASE ? bs[i] + 0.0f : 0.0f;
+  }
+  // The unit's kept entries are the range [lo, hi) of the segment's ascending idx list: lo = first entry
+  // >= start (lanes 0..31), hi = first entry >= start + len (lanes 32..63). Each round probes 32
+  // positions per target and shrinks [a, b] (answer inside, inclusive) ~32x; the loads overlap the
+  // background stores' drain. The list may come from an untrusted blob: every probe is in bounds, the
+  // range shrinks every round whatever the values, and a wrong range can only mis-decode (pos < len).
+  const int32_t* Lx = P.cidx + U.out_off;
+  const uint32_t half = lane >> 5, sl = lane & 31;
+  const uint32_t tgt = U.start + (half ? len : 0u);
+  uint32_t a = 0, b = U.k;
+  while (__any(a < b)) {
+    const uint32_t s = (b - a + 31) >> 5;
+    const uint32_t pr = min(a + sl * s + s - 1, b - 1);
+    const bool lt = a < b && (uint32_t)Lx[min(pr, U.k - 1)] < tgt;
+    const uint64_t m = __ballot(lt);
+    const uint32_t c = (uint32_t)__popcll(half ? (m >> 32) : (m & 0xFFFFFFFFull));
+    if (a < b) {
+      const uint32_t na = c ? min(a + (c - 1) * s + s - 1, b - 1) + 1 : a;
+      const uint32_t nb = c < 32 ? min(a + c * s + s - 1, b - 1) : b;
+      a = na;
+      b = max(na, nb);
+    }
+  }
+  const uint32_t lo = __builtin_amdgcn_readlane(a, 0);
+  const uint32_t hi = U.last ? U.k : max(lo, (uint32_t)__builtin_amdgcn_readlane(a, 32));
+  const float mn = RAW ? 0.0f : P.cmn[U.seg];
+  const float scale = RAW ? 0.0f : P.cscale[U.seg];
+  // background stores must be complete before the scatter writes the same lines
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  for (uint32_t e = lo + lane; e < hi; e += 64) {
+    const uint32_t pos = (uint32_t)Lx[e] - U.start;
+    const float v = load_val<RAW>(P, U.out_off + e, mn, scale);
+    if (pos < len) out[pos] = HASBASE ? bs[pos] + v : v;
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// aggregate: fused server-side decode + FedAvg of C client updates of one layout
+// ------------------------------------------------------------------------------------------------
 // k_bounds: ustart[u] = first kept entry whose index falls in unit u or later. One block per chunk of
 // <= BCHUNK entries of one segment's sorted idx list, 16 consecutive entries per thread (loads batched).
 // Indices are range-checked (the list may come from an untrusted blob): a corrupt list can only
-// mis-decode, never write out of bounds.
+// mis-aggregate, never write out of bounds.
 struct BChunk {
   uint32_t seg, e0, e1, pad;
 };
 
-__global__ __launch_bounds__(BLOCK) void k_bounds(Params P, const BChunk* chunks) {
+__global__ __launch_bounds__(BLOCK) void k_bounds(Params P, const BChunk* chunks, uint32_t* ustart) {
   constexpr uint32_t EPT = BCHUNK / BLOCK;
   const BChunk C = chunks[blockIdx.x];
   const SegDev sd = P.segs[C.seg];
   const uint32_t nu = sd.unit_end - sd.unit_begin, k = sd.k;
   const int32_t* L = P.cidx + sd.out_off;
-  uint32_t* us = P.ustart + sd.unit_begin;
+  uint32_t* us = ustart + sd.unit_begin;
   const uint32_t e0 = C.e0 + threadIdx.x * EPT;
   if (e0 >= C.e1) return;
   uint32_t ix[EPT + 1];
@@ -1276,58 +1389,159 @@ __global__ __launch_bounds__(BLOCK) void k_bounds(Params P, const BChunk* chunks
   }
 }
 
-// k_decode: one wave per unit, no LDS. Store the unit's dense background (zeros, or base + 0.0f), wait
-// until those stores are complete (s_waitcnt vmcnt(0): later stores to the same addresses are then
-// ordered after them), then scatter the kept values. The scattered lines are still dirty in L2, so HBM
-// sees each line written once.
-template <bool RAW, bool HASBASE>
-__global__ __launch_bounds__(BLOCK) void k_decode(Params P) {
+struct AggArgs {
+  const uint32_t* ustart;  // [n_units] from k_bounds
+  const float* weights;    // [clients] fp32 weights (float(w_i), as torch converts a Python scalar)
+  uint32_t clients, T, U0; // clients, segments per client, units per client
+  uint64_t Kc;             // kept entries per client (out_off stride between clients)
+  float total, inv_total;  // sum of weights; 1.0f / total (fp32 division)
+};
+
+template <bool RAW>
+DEV uint32_t load_code(const Params& P, uint64_t o) {
+  if (RAW) return __float_as_uint(static_cast<const float*>(P.cvals)[o]);
+  return static_cast<const uint8_t*>(P.cvals)[o];
+}
+
+template <bool RAW>
+DEV float code_value(uint32_t q, float mn, float scale) {
+  return RAW ? __uint_as_float(q) : dequantize((uint8_t)q, mn, scale);
+}
+
+// k_aggregate: one wave per 4096-element unit of the (client-0) layout. For client i in order:
+//   x_i = base + d_i   (d_i = decoded value where client i kept the element, +0.0f elsewhere: exactly
+//                       what coalac_decode with a base writes; without a base x_i = d_i)
+//   acc = x_0 * w_0, then acc = acc + (x_i * w_i)        (torch: params *= w0; params += s_i * w_i)
+//   out = acc / total (mode DIV, torch CPU division) or acc * (1.0f / total) (mode RECIP, torch GPU
+//   division by a host scalar)                       — coala/server/strategies.py:6-29, 57-90
+// d_i goes through a per-wave LDS tile: the client's kept values are scattered into the zeroed tile,
+// every lane reads its 64 elements back with ds_read_b128, then the same positions are re-zeroed.
+// Latency: every client's range / mn / scale / weight is fetched lane-parallel in one round (lane j =
+// client j of a 64-client chunk); the first 64 kept entries of client j+2 are in flight while client
+// j is accumulated (three rotating register slots). Clients are identical copies of one layout, so
+// client c's unit / segment / entry offsets are u + c*U0, seg + c*T, out_off + c*Kc (host-validated).
+template <bool RAW, bool HASBASE, int MODE>
+__global__ __launch_bounds__(BLOCK) void k_aggregate(Params P, AggArgs A) {
+  __shared__ float4 tiles[WAVES][UNIT / 4];
   const uint32_t lane = lane_id(), wv = threadIdx.x >> 6;
   const uint32_t u = blockIdx.x * WAVES + wv;
-  if (u >= P.n_units) return;
+  if (u >= A.U0) return;
   const UnitDev U = P.units[u];
-  // clamp: ustart comes from a possibly untrusted idx list
-  const uint32_t lo = min(P.ustart[u], U.k);
-  const uint32_t hi = min(U.last ? U.k : P.ustart[u + 1], U.k);
-  const float mn = RAW ? 0.0f : P.cmn[U.seg];
-  const float scale = RAW ? 0.0f : P.cscale[U.seg];
-  const uint32_t len = U.len;
-  const int32_t* Lx = P.cidx + U.out_off;
-  // first batch of kept entries, loaded before the background stores
-  // unconditional loads at a clamped index (k >= 1): guarded loads would each wait vmcnt(0)
-  const uint32_t e = lo + lane;
-  const bool has = e < hi;
-  const uint32_t ec = min(e, U.k - 1);
-  const uint32_t pos0r = (uint32_t)Lx[ec] - U.start;
-  const float v0 = load_val<RAW>(P, U.out_off + ec, mn, scale);
-  const uint32_t pos0 = has ? pos0r : NONE;
-  float* out = P.out + U.off;
-  const float* bs = HASBASE ? P.base + U.off : nullptr;
-  if (len == UNIT) {
-    float4 bv[UNIT_IT];
+  const uint32_t len = U.len, kseg = U.k;
+  float4* tile = tiles[wv];
+  float* tf = reinterpret_cast<float*>(tile);
 #pragma unroll
-    for (uint32_t it = 0; it < UNIT_IT; ++it) {
-      if (HASBASE) {
-        bv[it] = *reinterpret_cast<const float4*>(bs + (it * 64 + lane) * 4);
-        bv[it].x = bv[it].x + 0.0f;
-        bv[it].y = bv[it].y + 0.0f;
-        bv[it].z = bv[it].z + 0.0f;
-        bv[it].w = bv[it].w + 0.0f;
+  for (uint32_t it = 0; it < UNIT_IT; ++it) tile[it * 64 + lane] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+  float4 b[UNIT_IT], acc[UNIT_IT];
+  const float* bs = HASBASE ? P.base + U.off : nullptr;
+#pragma unroll
+  for (uint32_t it = 0; it < UNIT_IT; ++it) {
+    const uint32_t e = (it * 64 + lane) * 4;
+    if (HASBASE) {
+      if (len == UNIT) {
+        b[it] = *reinterpret_cast<const float4*>(bs + e);
       } else {
-        bv[it] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+        b[it].x = e + 0 < len ? bs[e + 0] : 0.0f;
+        b[it].y = e + 1 < len ? bs[e + 1] : 0.0f;
+        b[it].z = e + 2 < len ? bs[e + 2] : 0.0f;
+        b[it].w = e + 3 < len ? bs[e + 3] : 0.0f;
       }
     }
-#pragma unroll
-    for (uint32_t it = 0; it < UNIT_IT; ++it) *reinterpret_cast<float4*>(out + (it * 64 + lane) * 4) = bv[it];
-  } else {
-    for (uint32_t i = lane; i < len; i += 64) out[i] = HASBASE ? bs[i] + 0.0f : 0.0f;
+    acc[it] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
   }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  if (pos0 < len) out[pos0] = HASBASE ? bs[pos0] + v0 : v0;
-  for (uint32_t e2 = lo + 64 + lane; e2 < hi; e2 += 64) {
-    const uint32_t pos = (uint32_t)Lx[e2] - U.start;
-    const float v = load_val<RAW>(P, U.out_off + e2, mn, scale);
-    if (pos < len) out[pos] = HASBASE ? bs[pos] + v : v;
+  for (uint32_t c0 = 0; c0 < A.clients; c0 += 64) {
+    const uint32_t cn = min(64u, A.clients - c0);
+    // lane j: metadata of client c0 + j (unconditional loads at a clamped client index)
+    const uint32_t cl = c0 + min(lane, cn - 1);
+    const uint32_t ucl = u + cl * A.U0;
+    const uint32_t m_lo = min(A.ustart[ucl], kseg);
+    const uint32_t m_hi = max(m_lo, min(U.last ? kseg : A.ustart[min(ucl + 1, P.n_units - 1)], kseg));
+    const uint32_t sl = U.seg + cl * A.T;
+    const float m_mn = RAW ? 0.0f : P.cmn[sl];
+    const float m_sc = RAW ? 0.0f : P.cscale[sl];
+    const float m_w = A.weights[cl];
+    auto entries = [&](uint32_t j) -> uint64_t { return U.out_off + (uint64_t)(c0 + j) * A.Kc; };
+    auto fetch = [&](uint32_t j, uint32_t& pos, uint32_t& q) {
+      const uint32_t jj = min(j, cn - 1);
+      const uint32_t lo = __builtin_amdgcn_readlane(m_lo, jj), hi = __builtin_amdgcn_readlane(m_hi, jj);
+      const uint64_t oo = entries(jj);
+      const uint32_t e = min(lo + lane, hi > lo ? hi - 1 : lo);  // kseg >= 1: entry lo always exists
+      pos = (uint32_t)P.cidx[oo + min(e, kseg - 1)] - U.start;
+      q = load_code<RAW>(P, oo + min(e, kseg - 1));
+    };
+    auto process = [&](uint32_t j, uint32_t pos, uint32_t q) {
+      const uint32_t lo = __builtin_amdgcn_readlane(m_lo, j), hi = __builtin_amdgcn_readlane(m_hi, j);
+      const float mn = __uint_as_float(__builtin_amdgcn_readlane(__float_as_uint(m_mn), j));
+      const float sc = __uint_as_float(__builtin_amdgcn_readlane(__float_as_uint(m_sc), j));
+      const float w = __uint_as_float(__builtin_amdgcn_readlane(__float_as_uint(m_w), j));
+      const uint32_t ne = hi - lo;
+      const uint64_t oo = entries(j);
+      if (lane < ne && pos < len) tf[pos] = code_value<RAW>(q, mn, sc);
+      for (uint32_t e = lo + 64 + lane; e < hi; e += 64) {  // more than 64 kept entries in this unit
+        const uint32_t p2 = (uint32_t)P.cidx[oo + e] - U.start;
+        const float v2 = load_val<RAW>(P, oo + e, mn, sc);
+        if (p2 < len) tf[p2] = v2;
+      }
+      wave_fence();
+      const bool first = c0 + j == 0;
+#pragma unroll
+      for (uint32_t it = 0; it < UNIT_IT; ++it) {
+        const float4 d = tile[it * 64 + lane];
+        float4 x;
+        x.x = HASBASE ? b[it].x + d.x : d.x;
+        x.y = HASBASE ? b[it].y + d.y : d.y;
+        x.z = HASBASE ? b[it].z + d.z : d.z;
+        x.w = HASBASE ? b[it].w + d.w : d.w;
+        const float4 t = make_float4(x.x * w, x.y * w, x.z * w, x.w * w);
+        acc[it].x = first ? t.x : acc[it].x + t.x;
+        acc[it].y = first ? t.y : acc[it].y + t.y;
+        acc[it].z = first ? t.z : acc[it].z + t.z;
+        acc[it].w = first ? t.w : acc[it].w + t.w;
+      }
+      wave_fence();
+      if (ne > 64) {
+#pragma unroll
+        for (uint32_t it = 0; it < UNIT_IT; ++it) tile[it * 64 + lane] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+      } else if (lane < ne && pos < len) {
+        tf[pos] = 0.0f;
+      }
+      wave_fence();
+    };
+    uint32_t p0, q0, p1, q1, p2, q2;
+    fetch(0, p0, q0);
+    fetch(1, p1, q1);
+    for (uint32_t j = 0; j < cn; j += 3) {
+      fetch(j + 2, p2, q2);
+      process(j, p0, q0);
+      if (j + 1 < cn) {
+        fetch(j + 3, p0, q0);
+        process(j + 1, p1, q1);
+      }
+      if (j + 2 < cn) {
+        fetch(j + 4, p1, q1);
+        process(j + 2, p2, q2);
+      }
+    }
+  }
+  float* out = P.out + U.off;
+#pragma unroll
+  for (uint32_t it = 0; it < UNIT_IT; ++it) {
+    float4 o;
+    if (MODE == 0) {
+      o = make_float4(acc[it].x / A.total, acc[it].y / A.total, acc[it].z / A.total, acc[it].w / A.total);
+    } else {
+      o = make_float4(acc[it].x * A.inv_total, acc[it].y * A.inv_total, acc[it].z * A.inv_total,
+                      acc[it].w * A.inv_total);
+    }
+    const uint32_t e = (it * 64 + lane) * 4;
+    if (len == UNIT) {
+      *reinterpret_cast<float4*>(out + e) = o;
+    } else {
+      if (e + 0 < len) out[e + 0] = o.x;
+      if (e + 1 < len) out[e + 1] = o.y;
+      if (e + 2 < len) out[e + 2] = o.z;
+      if (e + 3 < len) out[e + 3] = o.w;
+    }
   }
 }
 
@@ -1357,7 +1571,7 @@ size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 struct WsLayout {
   size_t tstar, rtie, status;
   size_t tlo, thi, cntA, cntC, gtC, eqC, eqpre, outoff;
-  size_t cand, stamps, ghist, gcnt, glist, gmm, sstate, shhi;
+  size_t cand, stamps, ghist, gcnt, glist, gmm, sstate, shhi, arrive;
   size_t total;
 };
 
@@ -1388,6 +1602,7 @@ WsLayout ws_layout(size_t S, size_t LU, size_t NG, size_t NL) {
   L.gmm = take(8 * NG);
   L.sstate = take(sizeof(uint4) * NL);
   L.shhi = take(4 * NL);
+  L.arrive = take(8 * NL);
   L.total = std::max<size_t>(o, 256);
   return L;
 }
@@ -1406,9 +1621,11 @@ struct coalac_plan {
   UnitDev* lunits = nullptr;
   uint32_t* small_list = nullptr;
   uint32_t* large_list = nullptr;
-  BChunk* bchunks = nullptr;
   uint4* groups = nullptr;
-  uint32_t n_bchunks = 0, n_groups = 0;
+  uint32_t n_groups = 0;
+  BChunk* bchunks = nullptr;  // aggregate: k_bounds work list
+  uint32_t n_bchunks = 0;
+  std::vector<SegDev> hsegs;  // host copy (aggregate validates the client-copy structure)
   WsLayout ws{};
   size_t dec_ws = 0;
 };
@@ -1453,9 +1670,7 @@ void launch_encode(const Params& P, coalac_plan_t plan, hipStream_t st, void* co
   record(ev, 2, st);
   if (plan->n_large) {
     hipLaunchKernelGGL(k_ghist, dim3(plan->n_groups), dim3(BLOCK), 0, st, P);
-    hipLaunchKernelGGL(k_pick, dim3(plan->n_large), dim3(BLOCK), 0, st, P);
-    hipLaunchKernelGGL(k_gwin, dim3(plan->n_groups), dim3(BLOCK), 0, st, P);
-    hipLaunchKernelGGL((k_select<DELTA, RAW>), dim3(plan->n_large), dim3(SEL_NT), 0, st, P);
+    hipLaunchKernelGGL((k_gwin<DELTA, RAW>), dim3(plan->n_groups), dim3(BLOCK), 0, st, P);
   }
   record(ev, 3, st);
   if (plan->n_large) hipLaunchKernelGGL((k_emit<RAW>), dim3(gu), dim3(BLOCK), 0, st, P);
@@ -1478,9 +1693,9 @@ int coalac_plan_create(const coalac_seg_t* h_segs, int nseg, int bits, coalac_pl
 
   std::vector<SegDev> segs(nseg);
   std::vector<UnitDev> units, lunits;
-  std::vector<BChunk> bchunks;
   std::vector<uint4> groups;
   std::vector<uint32_t> small_list, large_list;
+  std::vector<BChunk> bchunks;
   uint64_t span = 0, total_k = 0;
   std::vector<std::pair<uint64_t, uint64_t>> in_r, out_r;
   for (int s = 0; s < nseg; ++s) {
@@ -1550,29 +1765,30 @@ int coalac_plan_create(const coalac_seg_t* h_segs, int nseg, int bits, coalac_pl
   p->n_large = (uint32_t)large_list.size();
   p->n_units = (uint32_t)units.size();
   p->n_lunits = (uint32_t)lunits.size();
-  p->n_bchunks = (uint32_t)bchunks.size();
   p->n_groups = (uint32_t)groups.size();
   p->span = span;
   p->total_k = total_k;
   p->ws = ws_layout((size_t)nseg, lunits.size(), groups.size(), large_list.size());
-  p->dec_ws = align_up(4 * (units.size() + 1), 256);
+  p->n_bchunks = (uint32_t)bchunks.size();
+  p->hsegs = segs;
+  p->dec_ws = align_up(4 * (units.size() + 1), 256);  // decode needs none; aggregate: per-unit bounds
 
   const size_t o_segs = 0;
   const size_t o_units = align_up(o_segs + sizeof(SegDev) * segs.size(), 256);
   const size_t o_lunits = align_up(o_units + sizeof(UnitDev) * units.size(), 256);
   const size_t o_small = align_up(o_lunits + sizeof(UnitDev) * lunits.size(), 256);
   const size_t o_large = align_up(o_small + 4 * small_list.size(), 256);
-  const size_t o_bch = align_up(o_large + 4 * large_list.size(), 256);
-  const size_t o_grp = align_up(o_bch + sizeof(BChunk) * bchunks.size(), 256);
-  const size_t bytes = align_up(o_grp + sizeof(uint4) * groups.size(), 256) + 256;
+  const size_t o_grp = align_up(o_large + 4 * large_list.size(), 256);
+  const size_t o_bch = align_up(o_grp + sizeof(uint4) * groups.size(), 256);
+  const size_t bytes = align_up(o_bch + sizeof(BChunk) * bchunks.size(), 256) + 256;
   std::vector<uint8_t> host(bytes, 0);
   if (!segs.empty()) memcpy(host.data() + o_segs, segs.data(), sizeof(SegDev) * segs.size());
   if (!units.empty()) memcpy(host.data() + o_units, units.data(), sizeof(UnitDev) * units.size());
   if (!lunits.empty()) memcpy(host.data() + o_lunits, lunits.data(), sizeof(UnitDev) * lunits.size());
   if (!small_list.empty()) memcpy(host.data() + o_small, small_list.data(), 4 * small_list.size());
   if (!large_list.empty()) memcpy(host.data() + o_large, large_list.data(), 4 * large_list.size());
-  if (!bchunks.empty()) memcpy(host.data() + o_bch, bchunks.data(), sizeof(BChunk) * bchunks.size());
   if (!groups.empty()) memcpy(host.data() + o_grp, groups.data(), sizeof(uint4) * groups.size());
+  if (!bchunks.empty()) memcpy(host.data() + o_bch, bchunks.data(), sizeof(BChunk) * bchunks.size());
   hipError_t e = hipMalloc(&p->meta, bytes);
   if (e != hipSuccess) {
     delete p;
@@ -1590,8 +1806,8 @@ int coalac_plan_create(const coalac_seg_t* h_segs, int nseg, int bits, coalac_pl
   p->lunits = reinterpret_cast<UnitDev*>(m + o_lunits);
   p->small_list = reinterpret_cast<uint32_t*>(m + o_small);
   p->large_list = reinterpret_cast<uint32_t*>(m + o_large);
-  p->bchunks = reinterpret_cast<BChunk*>(m + o_bch);
   p->groups = reinterpret_cast<uint4*>(m + o_grp);
+  p->bchunks = reinterpret_cast<BChunk*>(m + o_bch);
   *out = p;
   return COALAC_OK;
 }
@@ -1663,6 +1879,7 @@ int coalac_encode_ev(coalac_plan_t plan, const float* d_in, const float* d_base,
   P.gmm = reinterpret_cast<float*>(w + L.gmm);
   P.sstate = reinterpret_cast<uint4*>(w + L.sstate);
   P.shhi = reinterpret_cast<uint32_t*>(w + L.shhi);
+  P.arrive = reinterpret_cast<uint32_t*>(w + L.arrive);
   hipStream_t st = static_cast<hipStream_t>(stream);
   const bool delta = d_base != nullptr, raw = plan->bits == 32;
   if (delta && raw)
@@ -1693,7 +1910,7 @@ int coalac_decode_ev(coalac_plan_t plan, const int32_t* d_idx, const void* d_val
   if (plan->bits != 32 && (!d_mn || !d_scale)) return fail(COALAC_EINVAL, "coalac_decode: mn/scale pointers are NULL");
   if ((reinterpret_cast<uintptr_t>(d_out) | reinterpret_cast<uintptr_t>(d_base)) & 15)
     return fail(COALAC_EINVAL, "coalac_decode: output/base must be 16-byte aligned");
-  if (!d_ws || ws_bytes < plan->dec_ws)
+  if (plan->dec_ws && (!d_ws || ws_bytes < plan->dec_ws))
     return fail(COALAC_EWORKSPACE, "coalac_decode: workspace %llu < required %llu", (unsigned long long)ws_bytes,
                 (unsigned long long)plan->dec_ws);
   int rc = check_device(plan);
@@ -1706,13 +1923,11 @@ int coalac_decode_ev(coalac_plan_t plan, const int32_t* d_idx, const void* d_val
   P.cscale = d_scale;
   P.base = d_base;
   P.out = d_out;
-  P.ustart = static_cast<uint32_t*>(d_ws);
   hipStream_t st = static_cast<hipStream_t>(stream);
   const uint32_t g = (plan->n_units + WAVES - 1) / WAVES;
   const bool raw = plan->bits == 32, hb = d_base != nullptr;
   record(events, 0, st);
-  if (plan->n_bchunks) hipLaunchKernelGGL(k_bounds, dim3(plan->n_bchunks), dim3(BLOCK), 0, st, P, plan->bchunks);
-  record(events, 1, st);
+  record(events, 1, st);  // (events[0..1] bracketed the former unit-bounds pass; kept for ABI stability)
   if (raw && hb)
     hipLaunchKernelGGL((k_decode<true, true>), dim3(g), dim3(BLOCK), 0, st, P);
   else if (raw)
@@ -1730,6 +1945,85 @@ int coalac_decode(coalac_plan_t plan, const int32_t* d_idx, const void* d_vals, 
                   const float* d_scale, const float* d_base, float* d_out, void* d_ws, uint64_t ws_bytes,
                   void* stream) {
   return coalac_decode_ev(plan, d_idx, d_vals, d_mn, d_scale, d_base, d_out, d_ws, ws_bytes, stream, nullptr);
+}
+
+int coalac_aggregate_ev(coalac_plan_t plan, int clients, const int32_t* d_idx, const void* d_vals,
+                        const float* d_mn, const float* d_scale, const float* d_weights, float total, int mode,
+                        const float* d_base, float* d_out, void* d_ws, uint64_t ws_bytes, void* stream,
+                        void* const* events) {
+  if (!plan) return fail(COALAC_EINVAL, "coalac_aggregate: plan is NULL");
+  if (clients < 1 || plan->nseg % clients) return fail(COALAC_EINVAL, "coalac_aggregate: %d segments are not %d copies "
+                                                       "of one layout", plan->nseg, clients);
+  if (mode != COALAC_AGG_DIV && mode != COALAC_AGG_RECIP) return fail(COALAC_EINVAL, "coalac_aggregate: bad mode %d", mode);
+  if (plan->n_units == 0) return COALAC_OK;
+  if (!d_out || !d_weights) return fail(COALAC_EINVAL, "coalac_aggregate: output/weights pointer is NULL");
+  if (plan->total_k && (!d_idx || !d_vals)) return fail(COALAC_EINVAL, "coalac_aggregate: idx/vals pointers are NULL");
+  if (plan->bits != 32 && (!d_mn || !d_scale)) return fail(COALAC_EINVAL, "coalac_aggregate: mn/scale pointers are NULL");
+  if ((reinterpret_cast<uintptr_t>(d_out) | reinterpret_cast<uintptr_t>(d_base)) & 15)
+    return fail(COALAC_EINVAL, "coalac_aggregate: output/base must be 16-byte aligned");
+  if (!d_ws || ws_bytes < plan->dec_ws)
+    return fail(COALAC_EWORKSPACE, "coalac_aggregate: workspace %llu < required %llu", (unsigned long long)ws_bytes,
+                (unsigned long long)plan->dec_ws);
+  // the table must be `clients` copies of one layout at constant input / output strides
+  const uint32_t T = (uint32_t)(plan->nseg / clients);
+  const std::vector<SegDev>& H = plan->hsegs;
+  const uint32_t U0 = plan->n_units / (uint32_t)clients;
+  if (plan->n_units % (uint32_t)clients) return fail(COALAC_EINVAL, "coalac_aggregate: unit count not divisible");
+  const uint64_t S = clients > 1 ? H[T].in_off - H[0].in_off : 0, Kc = clients > 1 ? H[T].out_off - H[0].out_off : 0;
+  for (uint32_t c = 1; c < (uint32_t)clients; ++c)
+    for (uint32_t t = 0; t < T; ++t) {
+      const SegDev &a = H[t], &b = H[c * T + t];
+      if (b.n != a.n || b.k != a.k || b.in_off != a.in_off + c * S || b.out_off != a.out_off + c * Kc ||
+          b.unit_begin != a.unit_begin + c * U0)
+        return fail(COALAC_EINVAL, "coalac_aggregate: segment %u of client %u is not a copy of segment %u of client 0",
+                    c * T + t, c, t);
+    }
+  int rc = check_device(plan);
+  if (rc) return rc;
+  Params P{};
+  fill_meta(P, plan);
+  P.cidx = d_idx;
+  P.cvals = d_vals;
+  P.cmn = d_mn;
+  P.cscale = d_scale;
+  P.base = d_base;
+  P.out = d_out;
+  AggArgs A{};
+  A.ustart = static_cast<const uint32_t*>(d_ws);
+  A.weights = d_weights;
+  A.clients = (uint32_t)clients;
+  A.T = T;
+  A.U0 = U0;
+  A.Kc = Kc;
+  A.total = total;
+  A.inv_total = 1.0f / total;
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  record(events, 0, st);
+  if (plan->n_bchunks)
+    hipLaunchKernelGGL(k_bounds, dim3(plan->n_bchunks), dim3(BLOCK), 0, st, P, plan->bchunks,
+                       static_cast<uint32_t*>(d_ws));
+  record(events, 1, st);
+  const uint32_t g = (U0 + WAVES - 1) / WAVES;
+  const bool raw = plan->bits == 32, hb = d_base != nullptr, rc1 = mode == COALAC_AGG_RECIP;
+#define AGG(R, H, M) hipLaunchKernelGGL((k_aggregate<R, H, M>), dim3(g), dim3(BLOCK), 0, st, P, A)
+  if (raw) {
+    if (hb) { if (rc1) AGG(true, true, 1); else AGG(true, true, 0); }
+    else { if (rc1) AGG(true, false, 1); else AGG(true, false, 0); }
+  } else {
+    if (hb) { if (rc1) AGG(false, true, 1); else AGG(false, true, 0); }
+    else { if (rc1) AGG(false, false, 1); else AGG(false, false, 0); }
+  }
+#undef AGG
+  record(events, 2, st);
+  HIP_CHECK(hipGetLastError());
+  return COALAC_OK;
+}
+
+int coalac_aggregate(coalac_plan_t plan, int clients, const int32_t* d_idx, const void* d_vals, const float* d_mn,
+                     const float* d_scale, const float* d_weights, float total, int mode, const float* d_base,
+                     float* d_out, void* d_ws, uint64_t ws_bytes, void* stream) {
+  return coalac_aggregate_ev(plan, clients, d_idx, d_vals, d_mn, d_scale, d_weights, total, mode, d_base, d_out,
+                             d_ws, ws_bytes, stream, nullptr);
 }
 
 int coalac_workspace_fallbacks(coalac_plan_t plan, const void* d_ws, void* stream, int* out) {

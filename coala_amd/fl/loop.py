@@ -134,6 +134,9 @@ class LoopbackServer:
             model = self.decompression(unmarshal(req.content.data))
             self.uploaded[c.cid] = model
             self.weights[c.cid] = req.content.data_size
-        agg = federated_averaging(list(self.uploaded.values()), list(self.weights.values()))
-        self.model.load_state_dict(agg.state_dict())
+        agg = self.aggregate(list(self.uploaded.values()), list(self.weights.values()))
+        self.model.load_state_dict(agg.state_dict())  # set_model(load_dict=True), server/base.py:571
         return self.model
+
+    def aggregate(self, models, weights):  # server/base.py:573-601, non-distributed "all" branch
+        return federated_averaging(models, weights)

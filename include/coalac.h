@@ -73,7 +73,8 @@ const char* coalac_last_error(void);
 int coalac_plan_create(const coalac_seg_t* h_segs, int nseg, int bits, coalac_plan_t* out);
 int coalac_plan_destroy(coalac_plan_t plan);
 
-/* ws_bytes / dec_ws_bytes: workspace coalac_encode / coalac_decode need; total_k: length of idx/vals;
+/* ws_bytes: workspace coalac_encode needs; dec_ws_bytes: workspace of coalac_aggregate (coalac_decode
+ * needs none and accepts d_ws = NULL); total_k: length of idx/vals;
  * span: max(in_off + n) = the minimum length (elements) of the input/output flat buffers;
  * n_units: 4096-element work units. Any output pointer may be NULL. */
 int coalac_plan_query(coalac_plan_t plan, uint64_t* ws_bytes, uint64_t* dec_ws_bytes, uint64_t* total_k,
@@ -95,15 +96,38 @@ int coalac_decode(coalac_plan_t plan, const int32_t* d_idx, const void* d_vals, 
                   void* stream);
 
 /* Profiling variants: identical work, plus hipEventRecord(events[i], stream) between kernels.
- * encode: events[0] before k_prep, [1] after k_prep, [2] after k_scan, [3] after k_select,
- *         [4] after k_emit (recorded even if the plan has no large segment); decode: [0] before
- *         k_bounds, [1] after k_bounds, [2] after k_decode. NULL array or NULL entries are skipped. */
+ * encode: events[0] before k_sample, [1] after k_sample, [2] after k_scan, [3] after the select
+ *         kernels (k_ghist, k_pick, k_gwin, k_select), [4] after k_emit (recorded even if the plan has
+ *         no large segment); decode: [0] and [1] before k_decode (back to back), [2] after k_decode.
+ *         NULL array or NULL entries are skipped. */
 int coalac_encode_ev(coalac_plan_t plan, const float* d_in, const float* d_base, int32_t* d_idx,
                      void* d_vals, float* d_mn, float* d_scale, void* d_ws, uint64_t ws_bytes,
                      unsigned flags, void* stream, void* const* events);
 int coalac_decode_ev(coalac_plan_t plan, const int32_t* d_idx, const void* d_vals, const float* d_mn,
                      const float* d_scale, const float* d_base, float* d_out, void* d_ws,
                      uint64_t ws_bytes, void* stream, void* const* events);
+
+/* Fused server-side decode + FedAvg of the `clients` updates the plan batches.
+ * Replaces, on the server, decompression of every upload (coala/server/base.py:558-560, called :376)
+ * followed by strategies.federated_averaging (coala/server/strategies.py:6-29, 57-90) on the decoded
+ * modules, for the fp32 entries. The plan's table must be `clients` copies of one layout at constant
+ * input / output strides (client-major, as a batched encode uses). Per element of client 0's layout:
+ *   x_i = d_base + decoded_i   (decoded_i = +0.0f where client i did not keep the element; without a
+ *                               base x_i = decoded_i: exactly what coalac_decode writes)
+ *   acc = x_0 * w_0;  acc = acc + (x_i * w_i) for i = 1.. in client order (fp32, no FMA)
+ *   d_out = acc / total               (mode COALAC_AGG_DIV: torch's CPU division by a scalar)
+ *         = acc * (1.0f / total)      (mode COALAC_AGG_RECIP: torch's GPU division by a host scalar)
+ * d_weights: DEVICE fp32[clients] = float(w_i); total: float(sum of the weights). d_out / d_base are
+ * indexed like client 0's segments. Workspace: dec_ws_bytes of coalac_plan_query. Events (the _ev
+ * variant): [0] before the unit-bounds pass, [1] before k_aggregate, [2] after. */
+enum { COALAC_AGG_DIV = 0, COALAC_AGG_RECIP = 1 };
+int coalac_aggregate(coalac_plan_t plan, int clients, const int32_t* d_idx, const void* d_vals,
+                     const float* d_mn, const float* d_scale, const float* d_weights, float total, int mode,
+                     const float* d_base, float* d_out, void* d_ws, uint64_t ws_bytes, void* stream);
+int coalac_aggregate_ev(coalac_plan_t plan, int clients, const int32_t* d_idx, const void* d_vals,
+                        const float* d_mn, const float* d_scale, const float* d_weights, float total, int mode,
+                        const float* d_base, float* d_out, void* d_ws, uint64_t ws_bytes, void* stream,
+                        void* const* events);
 
 /* Diagnostics: number of segments whose sampled thresholds were rejected and re-selected exactly in
  * the last encode that used workspace d_ws (synchronises `stream`). */

@@ -165,3 +165,41 @@ def decode(idx, vals, mn, scale, segs, bits, span, base=None, out=None):
         b = None if base is None else base[off:off + n]
         out[off:off + n] = decode_segment(idx[oo:oo + k], vals[oo:oo + k], mn[s], scale[s], int(n), bits, b)
     return out
+
+
+AGG_DIV, AGG_RECIP = 0, 1
+
+
+def aggregate(idx, vals, mn, scale, segs, bits, clients, weights, total, mode, base=None, out_span=None):
+    """Fused decode + FedAvg restated: decode every client (decode_segment, i.e. coalac_decode with the
+    same base), then the reference's weighted average over the decoded fp32 entries, in client order:
+
+        params = s_0 * w_0; params += s_i * w_i          coala/server/strategies.py:57-90 (weighted_sum)
+        params = torch.div(params, total)                coala/server/strategies.py:6-29
+
+    torch evaluates the division as params / total on the CPU (mode AGG_DIV) and as
+    params * (1.0f / total) on a GPU, where a host scalar divisor becomes a reciprocal multiply (mode
+    AGG_RECIP). weights / total are taken as fp32 (torch converts the Python scalars to the tensor's
+    fp32 compute type). segs: [clients * T, 4] client-major copies of one layout; the output is
+    indexed like client 0's segments (positions outside them: 0).
+    """
+    segs = np.asarray(segs, dtype=np.int64).reshape(-1, 4)
+    T = len(segs) // clients
+    w = np.asarray(weights, dtype=np.float64).astype(F32)
+    tot = F32(total)
+    span = int(max(segs[t, 0] + segs[t, 1] for t in range(T))) if out_span is None else out_span
+    out = np.zeros(span, dtype=F32)
+    with np.errstate(all="ignore"):
+        for t in range(T):
+            off0, n = int(segs[t, 0]), int(segs[t, 1])
+            b = None if base is None else base[off0:off0 + n]
+            acc = None
+            for c in range(clients):
+                off, n_, k, oo = (int(v) for v in segs[c * T + t])
+                s = decode_segment(idx[oo:oo + k], vals[oo:oo + k], mn[c * T + t], scale[c * T + t], n, bits, b)
+                term = s * w[c]
+                acc = term if acc is None else acc + term
+            if acc is None:
+                continue
+            out[off0:off0 + n] = acc / tot if mode == AGG_DIV else acc * (F32(1.0) / tot)
+    return out

@@ -29,6 +29,15 @@ class OraclePlan:
                  self.table.segs.astype(np.int64), self.bits, self.table.span, base=b, out=out)
         return torch.from_numpy(out)
 
+    def aggregate(self, enc, weights, total=None, base=None, mode="div", **_):
+        total = float(sum(weights)) if total is None else float(total)
+        b = None if base is None else base.detach().cpu().numpy()
+        out = O.aggregate(enc.idx.numpy(), enc.vals.numpy(), enc.mn.numpy(), enc.scale.numpy(),
+                          self.table.segs.astype(np.int64), self.bits, self.table.clients, weights, total,
+                          O.AGG_DIV if mode == "div" else O.AGG_RECIP, base=b,
+                          out_span=self.table.span_per_client)
+        return torch.from_numpy(out)
+
 
 class OracleBackend:
     name = "oracle"
@@ -36,5 +45,5 @@ class OracleBackend:
     def default_device(self):
         return torch.device("cpu")
 
-    def make_plan(self, sizes, ratio, bits, device):
-        return OraclePlan(sizes, ratio, bits)
+    def make_plan(self, sizes, ratio, bits, device, clients=1):
+        return OraclePlan(sizes, ratio, bits, clients)

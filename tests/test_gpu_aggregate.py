@@ -1,0 +1,120 @@
+"""GPU parity of the fused server-side decode + FedAvg (coalac_aggregate).
+
+Bar: BIT-IDENTICAL to (a) the CPU oracle's restatement (oracle.codec_oracle.aggregate) in both division
+modes and (b) what the reference flow computes on the GPU: decompress every upload (coalac_decode) and
+run strategies.federated_averaging (coala/server/strategies.py:6-29, 57-90) on cuda tensors, i.e.
+params *= w0; params += s_i * w_i; torch.div(params, total).
+"""
+import copy
+
+import numpy as np
+import pytest
+import torch
+
+from coala_amd.compression import CodecPlan, CompressionClientMixin, CompressionServerMixin, UpdateCodec
+from coala_amd.compression._lib import CodecError
+from coala_amd.fl import LoopbackClient, LoopbackServer, federated_averaging
+from coala_amd.layouts import build_module, fp32_sizes
+from coala_amd.workload import synth_batch
+from oracle import codec_oracle as O
+
+pytestmark = pytest.mark.gpu
+
+
+def setup(layout, ratio, bits, clients, delta, seed=0):
+    sizes = fp32_sizes(layout)
+    plan = CodecPlan(sizes, ratio, bits, clients=clients)
+    dev = torch.device("cuda", 0)
+    flat = synth_batch(plan.table, dev, client_ids=[seed * 100 + i for i in range(clients)])
+    one = CodecPlan(sizes, ratio, bits, clients=1)
+    base = synth_batch(one.table, dev, client_ids=[seed * 100 + 99]) if delta else None
+    # every client's update is encoded against the same global model (base repeated per client)
+    base_rep = base.repeat(clients) if delta else None
+    enc = plan.encode(flat, base=base_rep)
+    return plan, one, enc, base
+
+
+@pytest.mark.parametrize("bits", [8, 32, 2])
+@pytest.mark.parametrize("ratio", [0.01, 0.1])
+@pytest.mark.parametrize("delta", [True, False])
+def test_aggregate_matches_oracle_both_modes(cuda, bits, ratio, delta):
+    C = 5
+    plan, one, enc, base = setup("resnet18", ratio, bits, C, delta, seed=bits)
+    weights = [17, 0, 5, 1000, 3]
+    segs = plan.table.segs.astype(np.int64)
+    h = [t.cpu().numpy() for t in (enc.idx, enc.vals, enc.mn, enc.scale)]
+    b = None if base is None else base.cpu().numpy()
+    for mode, om in (("recip", O.AGG_RECIP), ("div", O.AGG_DIV)):
+        out = plan.aggregate(enc, weights, base=base, mode=mode)
+        torch.cuda.synchronize()
+        ref = O.aggregate(*h, segs, bits, C, weights, sum(weights), om, base=b, out_span=plan.table.span_per_client)
+        g = out.cpu().numpy()
+        for off, n in zip(plan.table.offsets, plan.table.sizes):
+            np.testing.assert_array_equal(g[off:off + n].view(np.uint32), ref[off:off + n].view(np.uint32))
+
+
+@pytest.mark.parametrize("delta", [True, False])
+def test_aggregate_matches_torch_gpu_fedavg_on_decoded(cuda, delta):
+    """The reference flow on the GPU: decode each client, then weighted_sum + torch.div on cuda."""
+    C = 6
+    plan, one, enc, base = setup("resnet50_tv", 0.01, 8, C, delta, seed=3)
+    weights = [40, 12, 7, 0, 99, 1]
+    dense = plan.decode(enc, base=None if base is None else base.repeat(C))
+    S = plan.table.span_per_client
+    acc = dense[0:S].clone()
+    acc *= weights[0]
+    for i in range(1, C):
+        acc += dense[i * S:(i + 1) * S] * weights[i]
+    ref = torch.div(acc, sum(weights))
+    out = plan.aggregate(enc, weights, base=base, mode="recip")
+    torch.cuda.synchronize()
+    for off, n in zip(plan.table.offsets, plan.table.sizes):
+        assert torch.equal(out[off:off + n].view(torch.int32), ref[off:off + n].view(torch.int32))
+
+
+def test_aggregate_single_client_equals_decode_scaled(cuda):
+    plan, one, enc, base = setup("lenet", 0.05, 8, 1, True, seed=9)
+    out = plan.aggregate(enc, [4], base=base, mode="div")
+    dec = plan.decode(enc, base=base)
+    ref = torch.div(dec * 4, 4)
+    torch.cuda.synchronize()
+    for off, n in zip(plan.table.offsets, plan.table.sizes):
+        assert torch.equal(out[off:off + n], ref[off:off + n])
+
+
+def test_aggregate_rejects_non_copy_layouts(cuda):
+    import ctypes
+
+    from coala_amd.compression import _lib
+    plan = CodecPlan([5000, 300, 7000], 0.01, 8, clients=1)
+    # 3 segments cannot be 2 copies of one layout: refused before any launch
+    rc = plan._lib.coalac_aggregate(plan._h, 2, None, None, None, None, None, ctypes.c_float(1.0), 0, None,
+                                    None, None, ctypes.c_uint64(0), None)
+    with pytest.raises(CodecError, match="copies"):
+        _lib.check(rc, "coalac_aggregate")
+    with pytest.raises(ValueError):
+        plan.aggregate(plan.empty_encoded(), [1, 2])  # one weight per client
+
+
+def test_fused_server_end_to_end_on_gpu(cuda):
+    """Mixin with the HIP backend: fused aggregation == decompress-each + federated_averaging on the GPU."""
+    dev = torch.device("cuda", 0)
+
+    class Client(CompressionClientMixin, LoopbackClient):
+        codec_ratio, codec_bits, codec_mode = 0.02, 8, "delta"
+
+    class Plain(CompressionServerMixin, LoopbackServer):
+        codec_ratio, codec_bits, codec_mode = 0.02, 8, "delta"
+
+    class Fused(Plain):
+        codec_fused_aggregate = True
+
+    g0 = build_module("resnet18_split_cut4", seed=2, device=dev)
+    mk = lambda: [Client(f"c{i}", [11, 3, 30, 6][i], device=dev, step_seed=i) for i in range(4)]
+    plain, fused = Plain(copy.deepcopy(g0), mk()), Fused(copy.deepcopy(g0), mk())
+    for r in range(2):
+        plain.round(r)
+        fused.round(r)
+        for (k, a), b in zip(plain.model.state_dict().items(), fused.model.state_dict().values()):
+            assert a.dtype == b.dtype and torch.equal(a, b), k
+    assert federated_averaging is not None

@@ -211,3 +211,39 @@ def test_raw_bits_idempotent(cuda):
     e2 = plan.encode(d1)
     torch.cuda.synchronize()
     assert torch.equal(e1.idx, e2.idx) and torch.equal(e1.vals, e2.vals)
+
+
+@pytest.mark.parametrize("kind", ["random", "reversed", "out_of_range", "duplicates"])
+def test_decode_untrusted_idx_stays_in_bounds(cuda, kind):
+    """A corrupt idx list (the blob may be untrusted) can mis-decode but never write outside its
+    segment: the decode kernel's unit-range search and scatter are bounds-checked. Sentinels after the
+    span and in the alignment pads between segments must survive."""
+    sizes = [5000, 70, 9000, 4096 * 3 + 5]
+    plan = CodecPlan(sizes, 0.1, 8)
+    t = plan.table
+    rng = np.random.default_rng(11)
+    enc = plan.empty_encoded()
+    K = plan.total_k
+    if kind == "random":
+        idx = rng.integers(0, 20000, K, dtype=np.int64)
+    elif kind == "reversed":
+        idx = np.concatenate([np.arange(k)[::-1] for k in t.ks])
+    elif kind == "out_of_range":
+        idx = rng.integers(-(2 ** 31), 2 ** 31 - 1, K, dtype=np.int64)
+    else:
+        idx = np.zeros(K, np.int64)
+    enc.idx.copy_(torch.from_numpy(idx.astype(np.int32)))
+    enc.vals.copy_(torch.from_numpy(rng.integers(0, 256, K, dtype=np.uint8)))
+    enc.mn.fill_(1.0)
+    enc.scale.fill_(0.5)
+    sentinel = 12345.0
+    out = torch.full((t.span + 1024,), sentinel, dtype=torch.float32, device="cuda")
+    plan.decode(enc, out=out)
+    torch.cuda.synchronize()
+    o = out.cpu().numpy()
+    inside = np.zeros(o.size, bool)
+    for (off, n, k, oo) in t.segs.astype(np.int64):
+        inside[off:off + n] = True
+        seg = o[off:off + n]
+        assert np.all((seg == 0.0) | ((seg >= 1.0) & (seg <= 1.0 + 255 * 0.5)))
+    assert np.all(o[~inside] == sentinel)

@@ -174,3 +174,53 @@ def test_codec_rejects_mismatched_layouts_and_bad_args():
     b = build_module("simple_cnn_split_cut1")
     with pytest.raises(ValueError):
         codec.encode(a.state_dict(), base=codec.snapshot(b))
+
+
+@pytest.mark.parametrize("mode,bits,strategy", [("delta", 8, "FedAvg"), ("weights", 4, "FedAvg"),
+                                                 ("delta", 32, "equal")])
+def test_fused_aggregation_matches_decode_then_fedavg(mode, bits, strategy):
+    """codec_fused_aggregate: decode + FedAvg of all uploads in one call must leave the global model
+    bit-identical to decompressing every upload and running the reference federated_averaging
+    (here on the CPU: mode "div"), including int64 BatchNorm counters, over two rounds."""
+    Client, Server = make_classes(0.05, bits, mode)
+
+    class Fused(Server):
+        codec_fused_aggregate = True
+
+    class Conf:
+        class server:
+            aggregation_strategy = strategy
+            aggregation_content = "all"
+        is_distributed = False
+
+    g0 = build_module("resnet18_split_cut4", seed=7)
+    mk = lambda: [Client(f"c{i}", [13, 0, 7][i] if strategy == "FedAvg" else 5, step_seed=i) for i in range(3)]
+    plain, fused = Server(copy.deepcopy(g0), mk()), Fused(copy.deepcopy(g0), mk())
+    fused.conf = plain.conf = Conf
+    if strategy == "equal":  # the reference's EQUAL_AVERAGE branch (server/base.py:584-585)
+        plain.aggregate = lambda models, weights: federated_averaging(models, [1 for _ in models])
+    for r in range(2):
+        plain.round(r)
+        fused.round(r)
+        assert all(isinstance(m, CompressedUpdate) for m in fused.uploaded.values())
+        for (k, a), (k2, b) in zip(plain.model.state_dict().items(), fused.model.state_dict().items()):
+            assert k == k2 and a.dtype == b.dtype, k
+            assert torch.equal(a, b), k
+
+
+def test_fused_aggregation_zero_weights_and_oracle_modes():
+    """Weights summing to 0 become 1 per update (strategies.py:21-22); the two division modes of the
+    oracle restate torch's CPU (a / b) and GPU (a * (1 / b)) scalar division."""
+    codec = UpdateCodec(0.1, 8, "weights", backend=OracleBackend())
+    ms = [build_module("simple_cnn_split_cut2", seed=s) for s in range(3)]
+    ups = [codec.encode(m.state_dict()) for m in ms]
+    agg = codec.aggregate(ups, [0, 0, 0], ms[0], mode="div")
+    dec = [codec.decode_module(u, ms[0]) for u in ups]
+    ref = federated_averaging(dec, [0, 0, 0])
+    for a, b in zip(ref.state_dict().values(), agg.state_dict().values()):
+        assert torch.equal(a, b)
+    x = np.float32([1.0, 3.0, 10.0])
+    tot = np.float32(3.0)
+    assert np.array_equal(x / tot, torch.div(torch.from_numpy(x), 3).numpy())
+    r = x * (np.float32(1.0) / tot)
+    assert not np.array_equal(r, x / tot)  # 10 * (1/3) != 10 / 3 in fp32: the modes really differ

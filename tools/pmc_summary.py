@@ -11,6 +11,7 @@ import csv
 import glob
 import json
 import os
+import re
 import sys
 
 
@@ -23,10 +24,12 @@ def rows(pattern):
 
 
 def short(name):
-    name = name.split("(")[0]
-    for tok in ("void ", "__global__ "):
+    if name.startswith("_Z"):  # mangled: keep the kernel's base name
+        m = re.search(r"\d(k_[a-z]+)", name)
+        return m.group(1) if m else name
+    for tok in ("(anonymous namespace)::", "void ", "__global__ "):
         name = name.replace(tok, "")
-    return name.strip()
+    return name.split("(")[0].strip()
 
 
 def main(d):
