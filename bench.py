@@ -52,6 +52,24 @@ def make_events(torch, n):
     return evs
 
 
+def pmc_traffic(kernel, a):
+    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC summary of the default workload
+    (profiles/rNN_pmc_summary.json, written by tools/profile_round.sh + tools/pmc_summary.py): FETCH_SIZE
+    doubled (gfx950 reports half the bytes of wide coalesced streaming reads, MI355X_MICROARCH.md §HBM)
+    + WRITE_SIZE. Only reported for the default configuration the summary was collected on."""
+    import glob
+    default = (a.layout, a.clients, a.ratio, a.bits, a.mode, a.streams) == ("resnet50_tv", 16, 0.01, 8, "weights", 1)
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_summary.json")))
+    if not default or not files:
+        return None, None
+    with open(files[-1]) as f:
+        d = json.load(f)
+    for name, e in sorted(d.items()):
+        if name.split("<")[0] == kernel and "FETCH_SIZE_x2_bytes" in e and "WRITE_SIZE_bytes" in e:
+            return e["FETCH_SIZE_x2_bytes"] + e["WRITE_SIZE_bytes"], os.path.relpath(files[-1], ROOT)
+    return None, None
+
+
 def cpu_baseline(layout, ratio, bits, budget_s):
     """Oracle encode+decode of whole synthetic clients on the host, until ~budget_s elapsed."""
     import numpy as np
@@ -161,7 +179,7 @@ def main():
         return sum(s.elapsed_time(e) for s, e in pairs) / len(pairs)
     stages = {}
     for name, (which, i0, i1) in {"k_sample": ("ev_e", 0, 1), "k_scan": ("ev_e", 1, 2), "k_select": ("ev_e", 2, 3),
-                                  "k_emit": ("ev_e", 3, 4),
+                                  "k_emit": ("ev_e", 3, 4), "k_bounds": ("ev_d", 0, 1),
                                   "k_decode": ("ev_d", 1, 2)}.items():
         stages[name] = mean([(e[i0], e[i1]) for L in lanes for e in L[which]])
     N, K, T = t.n_elements, t.total_k, t.n_segments
@@ -175,6 +193,7 @@ def main():
     }
     dom = max(alg, key=lambda k: stages[k])
     ach = alg[dom] / (stages[dom] * 1e-3) / 1e9
+    traffic, traffic_src = pmc_traffic(dom, a)
     step_ms = el / a.steps * 1e3
     step_alg = t.algorithmic_bytes(a.bits, delta)
     value = 4.0 * N * world * a.steps / el / 1e9
@@ -191,8 +210,8 @@ def main():
                        "ratio": a.ratio, "bits": a.bits, "mode": a.mode, "streams_per_gpu": a.streams,
                        "parallelism": f"replicas{world}"},
             "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,
-                         "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None,
-                         "alg_bytes_per_launch": alg[dom]},
+                         "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": traffic,
+                         "traffic_source": traffic_src, "alg_bytes_per_launch": alg[dom]},
             "step_roofline": {"alg_bytes_per_step": step_alg,
                               "achieved_GBs": round(step_alg / (step_ms * 1e-3) / 1e9, 1),
                               "frac": round(step_alg / (step_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)},

@@ -120,9 +120,9 @@ struct Params {
   float* gmm;              // [n_groups][2] min/max of the group's values above the window
   uint4* sstate;           // [n_large] {wlo, whi, rank inside the window, path: 0 fast / 1 generic}
   uint32_t* shhi;          // [n_large] histogram upper bound: min(T_hi, largest sampled key)
-  uint32_t* arrive;        // [n_large][2] group blocks done in k_ghist / k_gwin (reset by k_sample)
 
   // decode workspace
+  const uint32_t* ustart;  // [n_units + 1] first kept entry of every unit (k_bounds)
   // diagnostics: per-block phase timestamps (COALAC_FLAG_STAMPS), NSTAMP per block, 100 MHz ticks
   uint64_t* stamps;
 };
@@ -320,6 +320,17 @@ template <bool RAW>
 DEV float load_val(const Params& P, uint64_t o, float mn, float scale) {
   if (RAW) return static_cast<const float*>(P.cvals)[o];
   return dequantize(static_cast<const uint8_t*>(P.cvals)[o], mn, scale);
+}
+
+template <bool RAW>
+DEV uint32_t load_code(const Params& P, uint64_t o) {
+  if (RAW) return __float_as_uint(static_cast<const float*>(P.cvals)[o]);
+  return static_cast<const uint8_t*>(P.cvals)[o];
+}
+
+template <bool RAW>
+DEV float code_value(uint32_t q, float mn, float scale) {
+  return RAW ? __uint_as_float(q) : dequantize((uint8_t)q, mn, scale);
 }
 
 template <bool DELTA>
@@ -665,15 +676,11 @@ __global__ __launch_bounds__(BLOCK) void k_sample(Params P) {
   }
   // The band histograms of the parallel select span [T_lo, min(T_hi, max sampled key)] (keys above go
   // to the last bin): with T_hi = KEY_MAX a full-range histogram would be too coarse.
-  if (t == 0) {
-    P.shhi[blockIdx.x] = max(tlo, min(thi, kmax));
-    P.arrive[2 * blockIdx.x] = 0;
-    P.arrive[2 * blockIdx.x + 1] = 0;
-  }
+  if (t == 0) P.shhi[blockIdx.x] = max(tlo, min(thi, kmax));
   if (t == 0) P.status[s] = 0;
 }
 
-// k_scan: n_small blocks encode the small segments; the rest stream the large units, one wave each.
+// k_scan: blocks [0, n_small) encode the small segments; the rest stream the large units, one wave each.
 template <bool DELTA, bool RAW>
 __global__ __launch_bounds__(BLOCK) void k_scan(Params P) {
   // one LDS arena: small-segment blocks use it as values + histogram, streaming blocks as candidate
@@ -681,26 +688,24 @@ __global__ __launch_bounds__(BLOCK) void k_scan(Params P) {
   constexpr size_t SMALL_BYTES = (SMALL_MAX + HIST_BINS + 64) * 4;
   constexpr size_t STAGE_BYTES = WAVES * STAGE_CAP * sizeof(uint2);
   __shared__ __attribute__((aligned(16))) uint8_t arena[SMALL_BYTES > STAGE_BYTES ? SMALL_BYTES : STAGE_BYTES];
-  // The compute-heavy small-segment blocks are spread evenly over the grid (block b is small iff
-  // floor((b+1)*ns/T) > floor(b*ns/T)), so they overlap the streaming blocks instead of delaying them.
-  const uint64_t b = blockIdx.x, T = gridDim.x, ns = P.n_small;
-  const uint32_t before = (uint32_t)(b * ns / T);
-  if ((uint32_t)((b + 1) * ns / T) != before) {
+  // The small-segment blocks come first: spreading them evenly over the grid measured slower (0.346 vs
+  // 0.322 ms for 16 ResNet-50 clients) — they then hold LDS while streaming blocks wait to be placed.
+  if (blockIdx.x < P.n_small) {
     float* sbuf = reinterpret_cast<float*>(arena);
     uint32_t* hist = reinterpret_cast<uint32_t*>(arena) + SMALL_MAX;
     uint32_t* sh = hist + HIST_BINS;
-    small_encode<DELTA, RAW>(P, P.small_list[before], sbuf, hist, sh);
+    small_encode<DELTA, RAW>(P, P.small_list[blockIdx.x], sbuf, hist, sh);
     return;
   }
   const uint32_t wv = threadIdx.x >> 6;
-  const uint32_t lu = ((uint32_t)b - before) * WAVES + wv;
+  const uint32_t lu = (blockIdx.x - P.n_small) * WAVES + wv;
   if (lu >= P.n_lunits) return;
   const UnitDev L = P.lunits[lu];
   scan_unit<DELTA, 1>(P, lu, L, P.tlo[lu], P.thi[lu], reinterpret_cast<uint2*>(arena) + wv * STAGE_CAP);
 }
 
 // ------------------------------------------------------------------------------------------------
-// per-segment select (run by the last group block of k_gwin)
+// per-segment select (k_select: one SEL_NT-thread block per large segment)
 // ------------------------------------------------------------------------------------------------
 // Exclusive prefix of cnt[0..cn) into upre[0..cn] (upre[cn] = total). Barriers inside.
 template <int NT>
@@ -896,24 +901,11 @@ struct Band {
   DEV uint32_t wlo(uint32_t b) const { return tlo + (b << shift); }
   DEV uint32_t whi(uint32_t b) const { return b == last ? thi : min(thi, wlo(b) + ((1u << shift) - 1u)); }
 };
-// Last-arriving-block pattern: every group block of a segment publishes its results (agent-scope
-// release), counts itself in; the block that arrives last (agent-scope acquire) does the per-segment
-// step. No block ever waits for another, so no co-residency assumption is made.
-DEV bool arrive_last(uint32_t* ctr, uint32_t expected, uint32_t* sh) {
-  __threadfence();
-  __syncthreads();
-  if (threadIdx.x == 0) sh[0] = atomicAdd(ctr, 1u);
-  __syncthreads();
-  const bool last = sh[0] == expected - 1;
-  __syncthreads();
-  if (last) __threadfence();
-  return last;
-}
-
 DEV void segment_pick(const Params& P, uint32_t li, uint32_t* hist, uint32_t* sh);
 
-// k_ghist: the group's HB2-bin histogram of the band keys [tlo, thi] -> ghist[group]; the segment's last
-// group block then picks the window (segment_pick)
+// k_ghist: the group's HB2-bin histogram of the band keys [tlo, thi] -> ghist[group]. (A fused variant in
+// which the segment's last-arriving group block ran segment_pick needed an agent-scope release fence in
+// every block — an L2 writeback on gfx950 — and was ~100x slower; kernel boundaries are cheaper.)
 __global__ __launch_bounds__(BLOCK) void k_ghist(Params P) {
   __shared__ uint32_t hist[HB2];
   __shared__ uint32_t upre[GU + 1];
@@ -933,9 +925,6 @@ __global__ __launch_bounds__(BLOCK) void k_ghist(Params P) {
       [&](uint32_t) {});
   __syncthreads();
   for (uint32_t i = t; i < HB2; i += BLOCK) P.ghist[(uint64_t)blockIdx.x * HB2 + i] = hist[i];
-  const SegDev& sd = P.segs[G.w];
-  const uint32_t ng = (sd.unit_end - sd.unit_begin + GU - 1) / GU;
-  if (arrive_last(P.arrive + 2 * G.x, ng, sh)) segment_pick(P, G.x, hist, sh);
 }
 
 // segment_pick: per large segment — validate the sampled bracket, sum the group histograms, pick the bin of
@@ -978,9 +967,7 @@ DEV void segment_pick(const Params& P, uint32_t li, uint32_t* hist, uint32_t* sh
 }
 
 // k_gwin: per group — per-unit counts of keys above the window (-> gtC), the group's in-window entries
-// in index order (-> glist, count -> gcnt), min/max of the values above the window (-> gmm); the
-// segment's last group block then runs segment_select (also for segments routed to the generic path,
-// whose group blocks only count themselves in).
+// in index order (-> glist, count -> gcnt), min/max of the values above the window (-> gmm)
 struct GwinSmem {
   uint32_t upre[GU + 1];
   uint2 slots[WAVES][GCAP];
@@ -1045,19 +1032,12 @@ DEV void group_window(const Params& P, const uint4 G, const uint4 st, GwinSmem& 
   }
 }
 
-template <bool DELTA, bool RAW>
 __global__ __launch_bounds__(BLOCK) void k_gwin(Params P) {
-  __shared__ union {
-    GwinSmem g;
-    SelSmem s;
-  } U;
+  __shared__ GwinSmem W;
   __shared__ uint32_t sh[64];
   const uint4 G = P.groups[blockIdx.x];
   const uint4 st = P.sstate[G.x];
-  if (st.w == 0) group_window(P, G, st, U.g, sh);
-  const SegDev& sd = P.segs[G.w];
-  const uint32_t ng = (sd.unit_end - sd.unit_begin + GU - 1) / GU;
-  if (arrive_last(P.arrive + 2 * G.x + 1, ng, sh)) segment_select<BLOCK, DELTA, RAW>(P, G.x, U.s);
+  if (st.w == 0) group_window(P, G, st, W, sh);
 }
 
 // Fast-path resolution in k_select: gather the groups' in-window lists (group order = index order),
@@ -1239,6 +1219,18 @@ DEV void segment_select(const Params& P, uint32_t li, SelSmem& S) {
   STAMP(P, li, 12);
 }
 
+__global__ __launch_bounds__(BLOCK) void k_pick(Params P) {
+  __shared__ uint32_t hist[HB2];
+  __shared__ uint32_t sh[64];
+  segment_pick(P, blockIdx.x, hist, sh);
+}
+
+template <bool DELTA, bool RAW>
+__global__ __launch_bounds__(SEL_NT) void k_select(Params P) {
+  __shared__ SelSmem S;
+  segment_select<SEL_NT, DELTA, RAW>(P, blockIdx.x, S);
+}
+
 // ------------------------------------------------------------------------------------------------
 // k_emit: per large unit (one wave) — the candidate list is already in index order: keep key > T and
 // the ties whose segment-wide tie rank is < rt, compact with ballots, write idx + code. No LDS.
@@ -1282,70 +1274,112 @@ __global__ __launch_bounds__(BLOCK) void k_emit(Params P) {
 // ------------------------------------------------------------------------------------------------
 // decode
 // ------------------------------------------------------------------------------------------------
-// k_decode: one wave per unit, no LDS. Store the unit's dense background (zeros, or base + 0.0f), wait
-// until those stores are complete (s_waitcnt vmcnt(0): later stores to the same addresses are then
-// ordered after them), then scatter the kept values. The scattered lines are still dirty in L2, so HBM
-// sees each line written once.
+// k_decode: DPW = 2 units per wave (1 in delta mode), all loads issued up front. Under a saturated write stream every load
+// round trip a wave waits on keeps its slot from issuing stores (tools/decode_ablate.hip: one unit per
+// wave with a dependent load = 4.6 TB/s, two units with hoisted loads + non-temporal stores = 5.7 TB/s,
+// above the 5.5 TB/s of plain zero stores). Round 1: both units' metadata and [lo, hi) bounds (k_bounds);
+// round 2: their first 64 kept entries (+ the base of the unit in delta mode). The kept values are merged
+// into the unit's registers (wave-uniform walk over the sorted entries, rows visited in order), so every
+// output line is written exactly once, with non-temporal float4 stores.
+// Values: out = base + v where kept, base + 0.0f elsewhere (delta), or v / 0.0f without a base: the
+// kept-mask (bit 4*row + component, per lane) tells the two apart.
+template <bool HASBASE>
+DEV void merge_entries(float4 (&b)[UNIT_IT], uint64_t& kept, uint32_t pos0, float v0, uint32_t cnt, uint32_t lane) {
+  uint32_t j = 0;
+#pragma unroll
+  for (uint32_t i = 0; i < UNIT_IT; ++i) {
+    while (j < cnt) {
+      const uint32_t pos = __builtin_amdgcn_readlane(pos0, j);
+      if ((pos >> 8) != i) break;  // sorted entries: the next row (or an out-of-unit / corrupt entry)
+      const float v = __uint_as_float(__builtin_amdgcn_readlane(__float_as_uint(v0), j));
+      if (((pos >> 2) & 63u) == lane) {
+        const uint32_t c = pos & 3u;
+        b[i].x = c == 0 ? (HASBASE ? b[i].x + v : v) : b[i].x;
+        b[i].y = c == 1 ? (HASBASE ? b[i].y + v : v) : b[i].y;
+        b[i].z = c == 2 ? (HASBASE ? b[i].z + v : v) : b[i].z;
+        b[i].w = c == 3 ? (HASBASE ? b[i].w + v : v) : b[i].w;
+        kept |= 1ull << (i * 4 + c);
+      }
+      ++j;
+    }
+  }
+}
+
+// units per wave of k_decode: 1 with a base (its 16 float4 of base per unit would double the registers)
+template <bool HASBASE>
+constexpr uint32_t decode_dpw() { return HASBASE ? 1u : 2u; }
+
 template <bool RAW, bool HASBASE>
 __global__ __launch_bounds__(BLOCK) void k_decode(Params P) {
+  constexpr uint32_t DPW = decode_dpw<HASBASE>();
   const uint32_t lane = lane_id(), wv = threadIdx.x >> 6;
-  const uint32_t u = blockIdx.x * WAVES + wv;
-  if (u >= P.n_units) return;
-  const UnitDev U = P.units[u];
-  const uint32_t len = U.len;
-  float* out = P.out + U.off;
-  const float* bs = HASBASE ? P.base + U.off : nullptr;
-  if (len == UNIT) {
-    float4 bv[UNIT_IT];
+  const uint32_t u0 = (blockIdx.x * WAVES + wv) * DPW;
+  if (u0 >= P.n_units) return;
+  UnitDev U[DPW];
+  uint32_t lo[DPW], hi[DPW];
+#pragma unroll
+  for (uint32_t r = 0; r < DPW; ++r) {
+    const uint32_t uu = min(u0 + r, P.n_units - 1);
+    U[r] = P.units[uu];
+    lo[r] = P.ustart[uu];
+    hi[r] = P.ustart[uu + 1];  // ustart has n_units + 1 entries
+  }
+  uint32_t pos[DPW], q[DPW];
+  float mn[DPW], sc[DPW];
+#pragma unroll
+  for (uint32_t r = 0; r < DPW; ++r) {
+    // clamp: the bounds come from a possibly untrusted idx list (k >= 1 for every unit)
+    lo[r] = min(lo[r], U[r].k);
+    hi[r] = max(lo[r], min(U[r].last ? U[r].k : hi[r], U[r].k));
+    const uint64_t e = U[r].out_off + min(lo[r] + lane, U[r].k - 1);
+    pos[r] = (uint32_t)P.cidx[e] - U[r].start;
+    q[r] = load_code<RAW>(P, e);
+    mn[r] = RAW ? 0.0f : P.cmn[U[r].seg];
+    sc[r] = RAW ? 0.0f : P.cscale[U[r].seg];
+  }
+#pragma unroll
+  for (uint32_t r = 0; r < DPW; ++r) {
+    if (u0 + r >= P.n_units) break;
+    const uint32_t len = U[r].len;
+    const float* bs = HASBASE ? P.base + U[r].off : nullptr;
+    float* out = P.out + U[r].off;
+    if (len != UNIT) {
+      // a segment's last, partial unit (one per segment): background, then scatter after the stores
+      for (uint32_t i = lane; i < len; i += 64) out[i] = HASBASE ? bs[i] + 0.0f : 0.0f;
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      for (uint32_t e = lo[r] + lane; e < hi[r]; e += 64) {
+        const uint64_t o = U[r].out_off + e;
+        const uint32_t p2 = (uint32_t)P.cidx[o] - U[r].start;
+        const float v2 = code_value<RAW>(load_code<RAW>(P, o), mn[r], sc[r]);
+        if (p2 < len) out[p2] = HASBASE ? bs[p2] + v2 : v2;
+      }
+      continue;
+    }
+    float4 b[UNIT_IT];
+#pragma unroll
+    for (uint32_t it = 0; it < UNIT_IT; ++it)
+      b[it] = HASBASE ? *reinterpret_cast<const float4*>(bs + (it * 64 + lane) * 4) : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    uint64_t kept = 0;
+    const uint32_t cnt = hi[r] - lo[r];
+    merge_entries<HASBASE>(b, kept, pos[r], code_value<RAW>(q[r], mn[r], sc[r]), min(cnt, 64u), lane);
+    for (uint32_t e0 = lo[r] + 64; e0 < hi[r]; e0 += 64) {  // more than 64 kept entries in the unit
+      const uint64_t e = U[r].out_off + min(e0 + lane, hi[r] - 1);
+      const uint32_t p2 = (uint32_t)P.cidx[e] - U[r].start;
+      const float v2 = code_value<RAW>(load_code<RAW>(P, e), mn[r], sc[r]);
+      merge_entries<HASBASE>(b, kept, p2, v2, min(hi[r] - e0, 64u), lane);
+    }
 #pragma unroll
     for (uint32_t it = 0; it < UNIT_IT; ++it) {
-      if (HASBASE) {
-        bv[it] = *reinterpret_cast<const float4*>(bs + (it * 64 + lane) * 4);
-        bv[it].x = bv[it].x + 0.0f;
-        bv[it].y = bv[it].y + 0.0f;
-        bv[it].z = bv[it].z + 0.0f;
-        bv[it].w = bv[it].w + 0.0f;
-      } else {
-        bv[it] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+      if (HASBASE) {  // base + 0.0f where nothing was kept (-0 -> +0, as the oracle's base + dense)
+        const uint32_t m = (uint32_t)(kept >> (it * 4)) & 15u;
+        b[it].x = (m & 1u) ? b[it].x : b[it].x + 0.0f;
+        b[it].y = (m & 2u) ? b[it].y : b[it].y + 0.0f;
+        b[it].z = (m & 4u) ? b[it].z : b[it].z + 0.0f;
+        b[it].w = (m & 8u) ? b[it].w : b[it].w + 0.0f;
       }
+      const f4v t = {b[it].x, b[it].y, b[it].z, b[it].w};
+      __builtin_nontemporal_store(t, reinterpret_cast<f4v*>(out + (it * 64 + lane) * 4));
     }
-#pragma unroll
-    for (uint32_t it = 0; it < UNIT_IT; ++it) *reinterpret_cast<float4*>(out + (it * 64 + lane) * 4) = bv[it];
-  } else {
-    for (uint32_t i = lane; i < len; i += 64) out[i] = HASBASE ? bs[i] + 0.0f : 0.0f;
-  }
-  // The unit's kept entries are the range [lo, hi) of the segment's ascending idx list: lo = first entry
-  // >= start (lanes 0..31), hi = first entry >= start + len (lanes 32..63). Each round probes 32
-  // positions per target and shrinks [a, b] (answer inside, inclusive) ~32x; the loads overlap the
-  // background stores' drain. The list may come from an untrusted blob: every probe is in bounds, the
-  // range shrinks every round whatever the values, and a wrong range can only mis-decode (pos < len).
-  const int32_t* Lx = P.cidx + U.out_off;
-  const uint32_t half = lane >> 5, sl = lane & 31;
-  const uint32_t tgt = U.start + (half ? len : 0u);
-  uint32_t a = 0, b = U.k;
-  while (__any(a < b)) {
-    const uint32_t s = (b - a + 31) >> 5;
-    const uint32_t pr = min(a + sl * s + s - 1, b - 1);
-    const bool lt = a < b && (uint32_t)Lx[min(pr, U.k - 1)] < tgt;
-    const uint64_t m = __ballot(lt);
-    const uint32_t c = (uint32_t)__popcll(half ? (m >> 32) : (m & 0xFFFFFFFFull));
-    if (a < b) {
-      const uint32_t na = c ? min(a + (c - 1) * s + s - 1, b - 1) + 1 : a;
-      const uint32_t nb = c < 32 ? min(a + c * s + s - 1, b - 1) : b;
-      a = na;
-      b = max(na, nb);
-    }
-  }
-  const uint32_t lo = __builtin_amdgcn_readlane(a, 0);
-  const uint32_t hi = U.last ? U.k : max(lo, (uint32_t)__builtin_amdgcn_readlane(a, 32));
-  const float mn = RAW ? 0.0f : P.cmn[U.seg];
-  const float scale = RAW ? 0.0f : P.cscale[U.seg];
-  // background stores must be complete before the scatter writes the same lines
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  for (uint32_t e = lo + lane; e < hi; e += 64) {
-    const uint32_t pos = (uint32_t)Lx[e] - U.start;
-    const float v = load_val<RAW>(P, U.out_off + e, mn, scale);
-    if (pos < len) out[pos] = HASBASE ? bs[pos] + v : v;
   }
 }
 
@@ -1396,17 +1430,6 @@ struct AggArgs {
   uint64_t Kc;             // kept entries per client (out_off stride between clients)
   float total, inv_total;  // sum of weights; 1.0f / total (fp32 division)
 };
-
-template <bool RAW>
-DEV uint32_t load_code(const Params& P, uint64_t o) {
-  if (RAW) return __float_as_uint(static_cast<const float*>(P.cvals)[o]);
-  return static_cast<const uint8_t*>(P.cvals)[o];
-}
-
-template <bool RAW>
-DEV float code_value(uint32_t q, float mn, float scale) {
-  return RAW ? __uint_as_float(q) : dequantize((uint8_t)q, mn, scale);
-}
 
 // k_aggregate: one wave per 4096-element unit of the (client-0) layout. For client i in order:
 //   x_i = base + d_i   (d_i = decoded value where client i kept the element, +0.0f elsewhere: exactly
@@ -1571,7 +1594,7 @@ size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 struct WsLayout {
   size_t tstar, rtie, status;
   size_t tlo, thi, cntA, cntC, gtC, eqC, eqpre, outoff;
-  size_t cand, stamps, ghist, gcnt, glist, gmm, sstate, shhi, arrive;
+  size_t cand, stamps, ghist, gcnt, glist, gmm, sstate, shhi;
   size_t total;
 };
 
@@ -1602,7 +1625,6 @@ WsLayout ws_layout(size_t S, size_t LU, size_t NG, size_t NL) {
   L.gmm = take(8 * NG);
   L.sstate = take(sizeof(uint4) * NL);
   L.shhi = take(4 * NL);
-  L.arrive = take(8 * NL);
   L.total = std::max<size_t>(o, 256);
   return L;
 }
@@ -1670,7 +1692,9 @@ void launch_encode(const Params& P, coalac_plan_t plan, hipStream_t st, void* co
   record(ev, 2, st);
   if (plan->n_large) {
     hipLaunchKernelGGL(k_ghist, dim3(plan->n_groups), dim3(BLOCK), 0, st, P);
-    hipLaunchKernelGGL((k_gwin<DELTA, RAW>), dim3(plan->n_groups), dim3(BLOCK), 0, st, P);
+    hipLaunchKernelGGL(k_pick, dim3(plan->n_large), dim3(BLOCK), 0, st, P);
+    hipLaunchKernelGGL(k_gwin, dim3(plan->n_groups), dim3(BLOCK), 0, st, P);
+    hipLaunchKernelGGL((k_select<DELTA, RAW>), dim3(plan->n_large), dim3(SEL_NT), 0, st, P);
   }
   record(ev, 3, st);
   if (plan->n_large) hipLaunchKernelGGL((k_emit<RAW>), dim3(gu), dim3(BLOCK), 0, st, P);
@@ -1771,7 +1795,7 @@ int coalac_plan_create(const coalac_seg_t* h_segs, int nseg, int bits, coalac_pl
   p->ws = ws_layout((size_t)nseg, lunits.size(), groups.size(), large_list.size());
   p->n_bchunks = (uint32_t)bchunks.size();
   p->hsegs = segs;
-  p->dec_ws = align_up(4 * (units.size() + 1), 256);  // decode needs none; aggregate: per-unit bounds
+  p->dec_ws = align_up(4 * (units.size() + 1), 256);  // decode / aggregate: per-unit bounds
 
   const size_t o_segs = 0;
   const size_t o_units = align_up(o_segs + sizeof(SegDev) * segs.size(), 256);
@@ -1879,7 +1903,6 @@ int coalac_encode_ev(coalac_plan_t plan, const float* d_in, const float* d_base,
   P.gmm = reinterpret_cast<float*>(w + L.gmm);
   P.sstate = reinterpret_cast<uint4*>(w + L.sstate);
   P.shhi = reinterpret_cast<uint32_t*>(w + L.shhi);
-  P.arrive = reinterpret_cast<uint32_t*>(w + L.arrive);
   hipStream_t st = static_cast<hipStream_t>(stream);
   const bool delta = d_base != nullptr, raw = plan->bits == 32;
   if (delta && raw)
@@ -1910,7 +1933,7 @@ int coalac_decode_ev(coalac_plan_t plan, const int32_t* d_idx, const void* d_val
   if (plan->bits != 32 && (!d_mn || !d_scale)) return fail(COALAC_EINVAL, "coalac_decode: mn/scale pointers are NULL");
   if ((reinterpret_cast<uintptr_t>(d_out) | reinterpret_cast<uintptr_t>(d_base)) & 15)
     return fail(COALAC_EINVAL, "coalac_decode: output/base must be 16-byte aligned");
-  if (plan->dec_ws && (!d_ws || ws_bytes < plan->dec_ws))
+  if (!d_ws || ws_bytes < plan->dec_ws)
     return fail(COALAC_EWORKSPACE, "coalac_decode: workspace %llu < required %llu", (unsigned long long)ws_bytes,
                 (unsigned long long)plan->dec_ws);
   int rc = check_device(plan);
@@ -1923,11 +1946,16 @@ int coalac_decode_ev(coalac_plan_t plan, const int32_t* d_idx, const void* d_val
   P.cscale = d_scale;
   P.base = d_base;
   P.out = d_out;
+  P.ustart = static_cast<const uint32_t*>(d_ws);
   hipStream_t st = static_cast<hipStream_t>(stream);
-  const uint32_t g = (plan->n_units + WAVES - 1) / WAVES;
   const bool raw = plan->bits == 32, hb = d_base != nullptr;
+  const uint32_t upb = WAVES * (hb ? decode_dpw<true>() : decode_dpw<false>());  // units per block
+  const uint32_t g = (plan->n_units + upb - 1) / upb;
   record(events, 0, st);
-  record(events, 1, st);  // (events[0..1] bracketed the former unit-bounds pass; kept for ABI stability)
+  if (plan->n_bchunks)
+    hipLaunchKernelGGL(k_bounds, dim3(plan->n_bchunks), dim3(BLOCK), 0, st, P, plan->bchunks,
+                       static_cast<uint32_t*>(d_ws));
+  record(events, 1, st);
   if (raw && hb)
     hipLaunchKernelGGL((k_decode<true, true>), dim3(g), dim3(BLOCK), 0, st, P);
   else if (raw)

@@ -73,8 +73,8 @@ const char* coalac_last_error(void);
 int coalac_plan_create(const coalac_seg_t* h_segs, int nseg, int bits, coalac_plan_t* out);
 int coalac_plan_destroy(coalac_plan_t plan);
 
-/* ws_bytes: workspace coalac_encode needs; dec_ws_bytes: workspace of coalac_aggregate (coalac_decode
- * needs none and accepts d_ws = NULL); total_k: length of idx/vals;
+/* ws_bytes / dec_ws_bytes: workspace coalac_encode / coalac_decode (and coalac_aggregate) need;
+ * total_k: length of idx/vals;
  * span: max(in_off + n) = the minimum length (elements) of the input/output flat buffers;
  * n_units: 4096-element work units. Any output pointer may be NULL. */
 int coalac_plan_query(coalac_plan_t plan, uint64_t* ws_bytes, uint64_t* dec_ws_bytes, uint64_t* total_k,
@@ -98,7 +98,7 @@ int coalac_decode(coalac_plan_t plan, const int32_t* d_idx, const void* d_vals, 
 /* Profiling variants: identical work, plus hipEventRecord(events[i], stream) between kernels.
  * encode: events[0] before k_sample, [1] after k_sample, [2] after k_scan, [3] after the select
  *         kernels (k_ghist, k_pick, k_gwin, k_select), [4] after k_emit (recorded even if the plan has
- *         no large segment); decode: [0] and [1] before k_decode (back to back), [2] after k_decode.
+ *         no large segment); decode: [0] before k_bounds, [1] after k_bounds, [2] after k_decode.
  *         NULL array or NULL entries are skipped. */
 int coalac_encode_ev(coalac_plan_t plan, const float* d_in, const float* d_base, int32_t* d_idx,
                      void* d_vals, float* d_mn, float* d_scale, void* d_ws, uint64_t ws_bytes,

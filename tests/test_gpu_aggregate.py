@@ -59,8 +59,9 @@ def test_aggregate_matches_torch_gpu_fedavg_on_decoded(cuda, delta):
     C = 6
     plan, one, enc, base = setup("resnet50_tv", 0.01, 8, C, delta, seed=3)
     weights = [40, 12, 7, 0, 99, 1]
-    dense = plan.decode(enc, base=None if base is None else base.repeat(C))
     S = plan.table.span_per_client
+    dense = torch.empty(C * S, dtype=torch.float32, device="cuda")
+    plan.decode(enc, base=None if base is None else base.repeat(C), out=dense)
     acc = dense[0:S].clone()
     acc *= weights[0]
     for i in range(1, C):

@@ -9,6 +9,9 @@
 //   5 3 with 4 units per wave
 //   6 zero stores, grid-stride persistent (2048 blocks)           (reference ceiling, like hbm_probe)
 //   7 3 with nontemporal stores
+//   8 UPW=4 units per wave, every unit's metadata + entries loaded up front (one latency for 4 units)
+//   9 8 with UPW=8
+//  10 9 with nontemporal stores
 #include <hip/hip_runtime.h>
 #include <cstdio>
 #include <cstdint>
@@ -99,6 +102,66 @@ __global__ __launch_bounds__(256) void dec(float* out, const Unit* units, uint32
   }
 }
 
+// merge up to 64 sorted entries (pos in lane j, value v) into the wave's registers b[16] (row = pos >> 8)
+__device__ __forceinline__ void merge64(float4 (&b)[16], uint32_t pos0, float v0, uint32_t cnt, uint32_t lane) {
+  uint32_t j = 0;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    while (j < cnt) {
+      const uint32_t pos = __builtin_amdgcn_readlane(pos0, j);
+      if ((pos >> 8) != (uint32_t)i) break;
+      const float v = __uint_as_float(__builtin_amdgcn_readlane(__float_as_uint(v0), j));
+      if (((pos >> 2) & 63) == lane) {
+        const uint32_t c = pos & 3;
+        b[i].x = c == 0 ? v : b[i].x;
+        b[i].y = c == 1 ? v : b[i].y;
+        b[i].z = c == 2 ? v : b[i].z;
+        b[i].w = c == 3 ? v : b[i].w;
+      }
+      ++j;
+    }
+  }
+}
+
+template <int UPW, bool NTS>
+__global__ __launch_bounds__(256) void dec_batch(float* out, const Unit* units, uint32_t nunits, const int32_t* idx,
+                                                 const float* vals) {
+  const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const uint32_t u0 = (blockIdx.x * 4 + wv) * UPW;
+  if (u0 >= nunits) return;
+  Unit U[UPW];
+#pragma unroll
+  for (int r = 0; r < UPW; ++r) U[r] = units[min(u0 + r, nunits - 1)];
+  uint32_t pos[UPW];
+  float v[UPW];
+#pragma unroll
+  for (int r = 0; r < UPW; ++r) {
+    const uint32_t e = U[r].lo + lane;
+    const uint32_t ec = min(e, U[r].hi > U[r].lo ? U[r].hi - 1 : U[r].lo);
+    pos[r] = (uint32_t)idx[ec];
+    v[r] = vals[ec];
+  }
+#pragma unroll
+  for (int r = 0; r < UPW; ++r) {
+    if (u0 + r >= nunits) break;
+    float4 b[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) b[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+    const uint32_t cnt = min(U[r].hi - U[r].lo, 64u);
+    merge64(b, pos[r], v[r], cnt, lane);
+    float* o = out + U[r].off;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      if (NTS) {
+        f4v t = {b[i].x, b[i].y, b[i].z, b[i].w};
+        __builtin_nontemporal_store(t, reinterpret_cast<f4v*>(o + (i * 64 + lane) * 4));
+      } else {
+        *reinterpret_cast<float4*>(o + (i * 64 + lane) * 4) = b[i];
+      }
+    }
+  }
+}
+
 __global__ __launch_bounds__(256) void persist(float* out, size_t n4) {
   float4* o = reinterpret_cast<float4*>(out);
   for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n4; i += (size_t)gridDim.x * 256)
@@ -171,6 +234,13 @@ int main() {
   RUN(3, 4, g4, "5_merge_4upw", true);
   run("6_persistent_2048", [&] { hipLaunchKernelGGL(persist, dim3(2048), dim3(256), 0, 0, out, n / 4); }, false);
   RUN(7, 1, g, "7_merge_nt_stores", true);
+  run("8_hoisted_4upw", [&] { hipLaunchKernelGGL((dec_batch<4, false>), dim3(g4), dim3(256), 0, 0, out, units, nunits, idx, vals); }, true);
+  const uint32_t g8 = (nunits + 31) / 32;
+  run("9_hoisted_8upw", [&] { hipLaunchKernelGGL((dec_batch<8, false>), dim3(g8), dim3(256), 0, 0, out, units, nunits, idx, vals); }, true);
+  run("10_hoisted_8upw_nt", [&] { hipLaunchKernelGGL((dec_batch<8, true>), dim3(g8), dim3(256), 0, 0, out, units, nunits, idx, vals); }, true);
+  run("11_hoisted_4upw_nt", [&] { hipLaunchKernelGGL((dec_batch<4, true>), dim3(g4), dim3(256), 0, 0, out, units, nunits, idx, vals); }, true);
+  const uint32_t g2 = (nunits + 7) / 8;
+  run("12_hoisted_2upw_nt", [&] { hipLaunchKernelGGL((dec_batch<2, true>), dim3(g2), dim3(256), 0, 0, out, units, nunits, idx, vals); }, true);
   RUN(0, 1, g, "0_zero_stores_again", false);
   return 0;
 }

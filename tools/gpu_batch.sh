@@ -14,3 +14,4 @@ if [ -n "$PROFILE" ]; then
   bash tools/profile_round.sh "$PROFILE"
   timeout -k 10 200 python tools/host_rate.py > gpurun_out/prof_$PROFILE/host_rate.jsonl 2> gpurun_out/prof_$PROFILE/host_rate.err
 fi
+timeout -k 10 120 python tools/bench_aggregate.py > gpurun_out/bench_aggregate.log 2>&1

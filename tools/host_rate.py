@@ -30,14 +30,15 @@ def run(clients, steps, warmup, layout, ratio, bits):
     flat_d = synth_batch(plan.table, dev, client_ids=range(clients))
     flat_h = flat_d.cpu().pin_memory()
     out_h = torch.empty_like(flat_h).pin_memory()
-    enc_d, ws, dws, out_d = plan.empty_encoded(), plan.empty_workspace(), plan.empty_decode_workspace(), plan.empty_flat()
+    enc_d, ws, dws = plan.empty_encoded(), plan.empty_workspace(), plan.empty_decode_workspace()
+    out_d = torch.empty_like(flat_d)
     enc_h = [torch.empty_like(t, device="cpu").pin_memory() for t in (enc_d.idx, enc_d.vals, enc_d.mn, enc_d.scale)]
     enc_r = plan.empty_encoded()  # server-side device copy of the received payload
     in_d = torch.empty_like(flat_d)
 
     def device_step():
         plan.encode(in_d, out=enc_d, workspace=ws)
-        plan.decode(enc_r, out=out_d, workspace=dws)
+        plan.decode(enc_d, out=out_d, workspace=dws)
 
     def host_step():
         in_d.copy_(flat_h, non_blocking=True)
