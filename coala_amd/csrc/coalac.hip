@@ -3,7 +3,8 @@
 //
 // Reference context: SonyResearch/COALA has no codec (coala/compression/__init__.py is 0 bytes); the
 // hooks this replaces are coala/client/base.py:330-332 (encode) and coala/server/base.py:558-560
-// (decode). The spec is SURVEY.md §8(a) a3/a4; the CPU oracle restating it is oracle/codec_oracle.py.
+// (decode), and strategies.federated_averaging on the decoded uploads (aggregate).
+// The spec is SURVEY.md §8(a) a3/a4; the CPU oracle restating it is oracle/codec_oracle.py.
 //
 // Design (DESIGN.md has the full rationale):
 //   The path is HBM-bound integer/byte work: no MFMA. Encode must read the input ONCE from HBM, so the
@@ -16,16 +17,24 @@
 //   round trip), so results are always exact.
 //
 //   Work unit = 4096 contiguous elements of one segment, owned by ONE wave64: ordered compaction is
-//   done with wave ballots + mbcnt, so the streaming pass has no LDS traffic and no block barriers.
-//   Every per-unit quantity is indexed by the unit's own index, so a wave reaches all it needs in one
-//   dependent round trip. Segments of <= 8192 elements are encoded whole by one block in LDS.
+//   done with wave ballots + mbcnt (records staged in the wave's LDS slice, flushed coalesced), so the
+//   streaming pass has no block barriers. Segments of <= 4096 elements ("small") are encoded whole by
+//   one block in LDS.
 //
-//   Kernels (encode): k_sample (large segments: sample -> T_lo/T_hi), k_scan (small segments end to
-//   end in its first blocks, overlapping the streaming classify + compaction of the large units),
-//   k_select (exact k-th key inside B, tie quota, per-unit output offsets, min/max -> scale; 1024
-//   threads per segment), k_emit (sorted idx + codes via an LDS bitmap).
-//   Decode: k_decode (one wave per unit, no LDS: dense float4 background stores, a wave-parallel search
-//   of the unit's range in the segment's sorted idx list, then the kept values).
+//   Encode kernels, in stream order:
+//     k_sample  one block per large segment: stratified sample -> [T_lo, T_hi]; then one block per
+//               small segment: the whole segment in LDS (latency-bound work placed where CUs idle)
+//     k_scan    one wave per large unit: single HBM read, classify A / B, 8-byte records in index order
+//     k_ghist   one block per 32-unit group: band histogram of the group's B records
+//     k_pick    one block per large segment: sum the group histograms -> key window of the k-th key
+//     k_gwin    one block per group: per-unit counts above the window + the in-window entries
+//     k_select  one 512-thread block per large segment: exact k-th key + tie quota from the window
+//               lists (generic multi-pass select / exact re-select on a bracket miss), per-unit output
+//               offsets, min / max -> scale
+//     k_emit    one wave per large unit: kept records -> ascending idx + codes
+//   Decode: k_bounds (first kept entry of every unit) and k_decode (two units per wave, hoisted loads,
+//   kept values merged in registers, one non-temporal write per output line).
+//   Aggregate (fused decode + FedAvg, server side): k_bounds + k_aggregate.
 //
 // Numerics: built with -ffp-contract=off; fp32 sub/div/mul/add are separate IEEE ops, rintf is
 // round-half-even — the same op sequence as the oracle, so decoded values are bit-identical.
@@ -38,6 +47,7 @@
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -104,6 +114,7 @@ struct Params {
   const uint32_t* small_list;
   const uint32_t* large_list;
   uint32_t nseg, n_small, n_large, n_units, n_lunits;
+  uint32_t scan_small;  // small segments encoded by k_scan's first blocks (0 when forked to k_small)
   float levels;
   unsigned flags;
   // encode workspace: per segment
@@ -471,9 +482,53 @@ DEV void scan_unit(const Params& P, uint32_t lu, const UnitDev& L, uint32_t tlo,
   }
 }
 
+
+// Pick the bin of a HIST_BINS histogram (LDS) holding the r-th largest key: returns the bin, leaves in
+// r the rank inside that bin. sh needs >= 64 words.
+template <int NT, int NB = HIST_BINS>
+DEV uint32_t hist_pick(const uint32_t* hist, uint32_t& r, uint32_t* sh) {
+  constexpr int BPT = NB / NT;
+  const uint32_t t = threadIdx.x;
+  uint32_t c[BPT];
+  uint32_t s = 0;
+#pragma unroll
+  for (int j = 0; j < BPT; ++j) {
+    c[j] = hist[t * BPT + j];
+    s += c[j];
+  }
+  uint32_t total;
+  const uint32_t ex = block_excl_scan<NT>(s, sh, total);
+  const uint32_t above = total - ex - s;
+  if (t == 0) {
+    sh[40] = NONE;
+    sh[41] = r;
+  }
+  __syncthreads();
+  if (above < r && r <= above + s) {
+    uint32_t acc = above;
+    int b = (int)(t * BPT);
+#pragma unroll
+    for (int j = BPT - 1; j >= 0; --j) {
+      if (acc + c[j] >= r) {
+        b = (int)(t * BPT) + j;
+        break;
+      }
+      acc += c[j];
+    }
+    sh[40] = (uint32_t)b;
+    sh[41] = r - acc;
+  }
+  __syncthreads();
+  const uint32_t b = sh[40];
+  r = sh[41];
+  __syncthreads();
+  return b;
+}
+
 // ------------------------------------------------------------------------------------------------
 // small segments (n <= SMALL_MAX): one 256-thread block, values in LDS, exact radix select, ordered
-// compaction, min/max, codes. Runs as the first blocks of k_scan so its latency hides under streaming.
+// compaction, min/max, codes. Runs as its own kernel (k_small) on the plan's side stream, concurrently
+// with k_sample / k_scan, so its latency hides under the HBM streaming.
 // ------------------------------------------------------------------------------------------------
 template <bool DELTA, bool RAW>
 DEV void small_encode(const Params& P, uint32_t s, float* vals, uint32_t* hist, uint32_t* sh) {
@@ -559,55 +614,21 @@ DEV void small_encode(const Params& P, uint32_t s, float* vals, uint32_t* hist, 
   }
 }
 
-// Pick the bin of a HIST_BINS histogram (LDS) holding the r-th largest key: returns the bin, leaves in
-// r the rank inside that bin. sh needs >= 64 words.
-template <int NT, int NB = HIST_BINS>
-DEV uint32_t hist_pick(const uint32_t* hist, uint32_t& r, uint32_t* sh) {
-  constexpr int BPT = NB / NT;
-  const uint32_t t = threadIdx.x;
-  uint32_t c[BPT];
-  uint32_t s = 0;
-#pragma unroll
-  for (int j = 0; j < BPT; ++j) {
-    c[j] = hist[t * BPT + j];
-    s += c[j];
-  }
-  uint32_t total;
-  const uint32_t ex = block_excl_scan<NT>(s, sh, total);
-  const uint32_t above = total - ex - s;
-  if (t == 0) {
-    sh[40] = NONE;
-    sh[41] = r;
-  }
-  __syncthreads();
-  if (above < r && r <= above + s) {
-    uint32_t acc = above;
-    int b = (int)(t * BPT);
-#pragma unroll
-    for (int j = BPT - 1; j >= 0; --j) {
-      if (acc + c[j] >= r) {
-        b = (int)(t * BPT) + j;
-        break;
-      }
-      acc += c[j];
-    }
-    sh[40] = (uint32_t)b;
-    sh[41] = r - acc;
-  }
-  __syncthreads();
-  const uint32_t b = sh[40];
-  r = sh[41];
-  __syncthreads();
-  return b;
+template <bool DELTA, bool RAW>
+__global__ __launch_bounds__(BLOCK) void k_small(Params P) {
+  __shared__ __attribute__((aligned(16))) float vals[SMALL_MAX];
+  __shared__ uint32_t hist[HIST_BINS];
+  __shared__ uint32_t sh[64];
+  small_encode<DELTA, RAW>(P, P.small_list[blockIdx.x], vals, hist, sh);
 }
 
 // ------------------------------------------------------------------------------------------------
 // k_sample: per large segment, sampled thresholds [T_lo, T_hi] for every unit of the segment
 // ------------------------------------------------------------------------------------------------
-template <bool DELTA>
+template <bool DELTA, bool RAW>
 __global__ __launch_bounds__(BLOCK) void k_sample(Params P) {
   constexpr int NT = BLOCK;
-  __shared__ uint32_t keys[SAMPLE_MAX];
+  __shared__ __attribute__((aligned(16))) uint32_t keys[SAMPLE_MAX];
   __shared__ uint32_t hist[HIST_BINS];
   __shared__ uint32_t sh[64];
   const uint32_t t = threadIdx.x;
@@ -680,28 +701,26 @@ __global__ __launch_bounds__(BLOCK) void k_sample(Params P) {
   if (t == 0) P.status[s] = 0;
 }
 
-// k_scan: blocks [0, n_small) encode the small segments; the rest stream the large units, one wave each.
+// k_scan: streams the large units, one wave each. Blocks [0, scan_small) first encode the small
+// segments when they are not forked to the side stream (small plans: the fork costs more than it hides).
 template <bool DELTA, bool RAW>
 __global__ __launch_bounds__(BLOCK) void k_scan(Params P) {
-  // one LDS arena: small-segment blocks use it as values + histogram, streaming blocks as candidate
-  // staging (WAVES x STAGE_CAP records)
+  // one LDS arena: candidate staging (WAVES x STAGE_CAP records) or a small segment's values + histogram
   constexpr size_t SMALL_BYTES = (SMALL_MAX + HIST_BINS + 64) * 4;
   constexpr size_t STAGE_BYTES = WAVES * STAGE_CAP * sizeof(uint2);
   __shared__ __attribute__((aligned(16))) uint8_t arena[SMALL_BYTES > STAGE_BYTES ? SMALL_BYTES : STAGE_BYTES];
-  // The small-segment blocks come first: spreading them evenly over the grid measured slower (0.346 vs
-  // 0.322 ms for 16 ResNet-50 clients) — they then hold LDS while streaming blocks wait to be placed.
-  if (blockIdx.x < P.n_small) {
-    float* sbuf = reinterpret_cast<float*>(arena);
+  if (blockIdx.x < P.scan_small) {
+    float* vals = reinterpret_cast<float*>(arena);
     uint32_t* hist = reinterpret_cast<uint32_t*>(arena) + SMALL_MAX;
-    uint32_t* sh = hist + HIST_BINS;
-    small_encode<DELTA, RAW>(P, P.small_list[blockIdx.x], sbuf, hist, sh);
+    small_encode<DELTA, RAW>(P, P.small_list[blockIdx.x], vals, hist, hist + HIST_BINS);
     return;
   }
+  uint2* stage = reinterpret_cast<uint2*>(arena);
   const uint32_t wv = threadIdx.x >> 6;
-  const uint32_t lu = (blockIdx.x - P.n_small) * WAVES + wv;
+  const uint32_t lu = (blockIdx.x - P.scan_small) * WAVES + wv;
   if (lu >= P.n_lunits) return;
   const UnitDev L = P.lunits[lu];
-  scan_unit<DELTA, 1>(P, lu, L, P.tlo[lu], P.thi[lu], reinterpret_cast<uint2*>(arena) + wv * STAGE_CAP);
+  scan_unit<DELTA, 1>(P, lu, L, P.tlo[lu], P.thi[lu], stage + wv * STAGE_CAP);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -1648,6 +1667,10 @@ struct coalac_plan {
   BChunk* bchunks = nullptr;  // aggregate: k_bounds work list
   uint32_t n_bchunks = 0;
   std::vector<SegDev> hsegs;  // host copy (aggregate validates the client-copy structure)
+  // encode fork/join: k_small runs on `side`, concurrently with k_sample / k_scan on the caller's stream
+  hipStream_t side = nullptr;
+  hipEvent_t fork = nullptr, join = nullptr;
+  std::mutex mu;  // serialises the (asynchronous) enqueue sequences that use side / fork / join
   WsLayout ws{};
   size_t dec_ws = 0;
 };
@@ -1683,12 +1706,23 @@ void record(void* const* ev, int i, hipStream_t st) {
 }
 
 template <bool DELTA, bool RAW>
-void launch_encode(const Params& P, coalac_plan_t plan, hipStream_t st, void* const* ev) {
+int launch_encode(const Params& P, coalac_plan_t plan, hipStream_t st, void* const* ev) {
   const uint32_t gu = (plan->n_lunits + WAVES - 1) / WAVES;
+  const bool fork = plan->n_small && plan->side != nullptr;
+  Params Q = P;
+  Q.scan_small = fork ? 0u : plan->n_small;
+  std::unique_lock<std::mutex> lk(plan->mu, std::defer_lock);
+  if (fork) lk.lock();
   record(ev, 0, st);
-  if (plan->n_large) hipLaunchKernelGGL((k_sample<DELTA>), dim3(plan->n_large), dim3(BLOCK), 0, st, P);
+  if (fork) {
+    HIP_CHECK(hipEventRecord(plan->fork, st));
+    HIP_CHECK(hipStreamWaitEvent(plan->side, plan->fork, 0));
+    hipLaunchKernelGGL((k_small<DELTA, RAW>), dim3(plan->n_small), dim3(BLOCK), 0, plan->side, P);
+    HIP_CHECK(hipEventRecord(plan->join, plan->side));
+  }
+  if (plan->n_large) hipLaunchKernelGGL((k_sample<DELTA, RAW>), dim3(plan->n_large), dim3(BLOCK), 0, st, P);
   record(ev, 1, st);
-  if (plan->n_small + gu) hipLaunchKernelGGL((k_scan<DELTA, RAW>), dim3(plan->n_small + gu), dim3(BLOCK), 0, st, P);
+  if (gu + Q.scan_small) hipLaunchKernelGGL((k_scan<DELTA, RAW>), dim3(gu + Q.scan_small), dim3(BLOCK), 0, st, Q);
   record(ev, 2, st);
   if (plan->n_large) {
     hipLaunchKernelGGL(k_ghist, dim3(plan->n_groups), dim3(BLOCK), 0, st, P);
@@ -1698,7 +1732,9 @@ void launch_encode(const Params& P, coalac_plan_t plan, hipStream_t st, void* co
   }
   record(ev, 3, st);
   if (plan->n_large) hipLaunchKernelGGL((k_emit<RAW>), dim3(gu), dim3(BLOCK), 0, st, P);
+  if (fork) HIP_CHECK(hipStreamWaitEvent(st, plan->join, 0));
   record(ev, 4, st);
+  return COALAC_OK;
 }
 
 }  // namespace
@@ -1832,6 +1868,17 @@ int coalac_plan_create(const coalac_seg_t* h_segs, int nseg, int bits, coalac_pl
   p->large_list = reinterpret_cast<uint32_t*>(m + o_large);
   p->groups = reinterpret_cast<uint4*>(m + o_grp);
   p->bchunks = reinterpret_cast<BChunk*>(m + o_bch);
+  // Small segments overlap the large ones' pipeline on a side stream once the batch is big enough for
+  // the fork / join (~10-20 us) to pay off (>= 16384 large units, ~3 ResNet-50 updates).
+  if (p->n_small && p->n_lunits >= 16384) {
+    if (hipStreamCreateWithFlags(&p->side, hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreateWithFlags(&p->fork, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&p->join, hipEventDisableTiming) != hipSuccess) {
+      const hipError_t ce = hipGetLastError();
+      coalac_plan_destroy(p);
+      return fail(COALAC_EHIP, "creating the plan's side stream / events failed: %s", hipGetErrorString(ce));
+    }
+  }
   *out = p;
   return COALAC_OK;
 }
@@ -1841,6 +1888,9 @@ int coalac_plan_destroy(coalac_plan_t plan) {
   int cur = 0;
   if (hipGetDevice(&cur) == hipSuccess && cur != plan->device) (void)hipSetDevice(plan->device);
   hipError_t e = hipFree(plan->meta);
+  if (plan->side) (void)hipStreamDestroy(plan->side);
+  if (plan->fork) (void)hipEventDestroy(plan->fork);
+  if (plan->join) (void)hipEventDestroy(plan->join);
   if (cur != plan->device) (void)hipSetDevice(cur);
   delete plan;
   if (e != hipSuccess) return fail(COALAC_EHIP, "hipFree failed: %s", hipGetErrorString(e));
@@ -1906,13 +1956,14 @@ int coalac_encode_ev(coalac_plan_t plan, const float* d_in, const float* d_base,
   hipStream_t st = static_cast<hipStream_t>(stream);
   const bool delta = d_base != nullptr, raw = plan->bits == 32;
   if (delta && raw)
-    launch_encode<true, true>(P, plan, st, events);
+    rc = launch_encode<true, true>(P, plan, st, events);
   else if (delta)
-    launch_encode<true, false>(P, plan, st, events);
+    rc = launch_encode<true, false>(P, plan, st, events);
   else if (raw)
-    launch_encode<false, true>(P, plan, st, events);
+    rc = launch_encode<false, true>(P, plan, st, events);
   else
-    launch_encode<false, false>(P, plan, st, events);
+    rc = launch_encode<false, false>(P, plan, st, events);
+  if (rc) return rc;
   HIP_CHECK(hipGetLastError());
   return COALAC_OK;
 }

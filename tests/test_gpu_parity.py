@@ -117,6 +117,19 @@ def test_batched_clients_resnet50_layout(cuda, ratio):
     assert g["fallbacks"] == 0
 
 
+@pytest.mark.parametrize("delta", [False, True])
+def test_forked_small_segments_resnet50_x3(cuda, delta):
+    """>= 16384 large units: the small segments are encoded by k_small on the plan's side stream,
+    concurrently with k_sample / k_scan, and joined back before the encode returns."""
+    rng = np.random.default_rng(33 + delta)
+    sizes = fp32_sizes("resnet50_tv")
+    xs = [gauss(rng, sizes) for _ in range(3)]
+    bases = [gauss(rng, sizes) for _ in range(3)] if delta else None
+    plan, g, r = run_both(sizes, 0.01, 8, xs, bases=bases, clients=3)
+    assert plan.n_units - sum(1 for n in sizes if 0 < n <= SMALL_MAX) * 3 >= 16384
+    assert_same(plan, g, r)
+
+
 @pytest.mark.parametrize("name", ["lenet", "vit_b16", "resnet18_split_cut4", "simple_cnn_split_cut2"])
 def test_layouts(cuda, name):
     rng = np.random.default_rng(3)
