@@ -25,6 +25,7 @@ sys.path.insert(0, ROOT)
 
 METRIC = "encode+decode GB/s over fp32 weight updates (device-resident), 1/2/4/8 GPU"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md: 8.0 TB/s)
+LANES = 2  # default pipeline lanes per GPU
 
 
 def parse():
@@ -37,8 +38,10 @@ def parse():
     p.add_argument("--ratio", type=float, default=0.01)
     p.add_argument("--bits", type=int, default=8)
     p.add_argument("--mode", choices=["weights", "delta"], default="weights")
-    p.add_argument("--streams", type=int, default=1,
-                   help="split each GPU's clients into this many sub-batches, one HIP stream each")
+    p.add_argument("--lanes", type=int, default=LANES,
+                   help="pipeline lanes per GPU (coala_amd/compression/pipeline.py): the batch's segments "
+                        "cut into this many contiguous ranges, one HIP stream each, streaming kernels "
+                        "serialised across lanes")
     p.add_argument("--flags", type=int, default=0, help="coalac encode flags (test hooks; 0 for the bench)")
     p.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline time budget")
     p.add_argument("--no-cpu-baseline", action="store_true")
@@ -58,7 +61,7 @@ def pmc_traffic(kernel, a):
     doubled (gfx950 reports half the bytes of wide coalesced streaming reads, MI355X_MICROARCH.md §HBM)
     + WRITE_SIZE. Only reported for the default configuration the summary was collected on."""
     import glob
-    default = (a.layout, a.clients, a.ratio, a.bits, a.mode, a.streams) == ("resnet50_tv", 16, 0.01, 8, "weights", 1)
+    default = (a.layout, a.clients, a.ratio, a.bits, a.mode, a.lanes) == ("resnet50_tv", 16, 0.01, 8, "weights", LANES)
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_summary.json")))
     if not default or not files:
         return None, None
@@ -103,7 +106,7 @@ def main():
     import torch
     import torch.distributed as dist
 
-    from coala_amd.compression import CodecPlan
+    from coala_amd.compression import LanePipeline, SegmentTable
     from coala_amd.compression.spec import SMALL_MAX
     from coala_amd.layouts import fp32_sizes
     from coala_amd.workload import synth_batch
@@ -119,44 +122,39 @@ def main():
         dist.init_process_group("nccl", device_id=dev)
 
     sizes = fp32_sizes(a.layout)
-    if a.clients % a.streams:
-        raise SystemExit("--clients must be a multiple of --streams")
-    per = a.clients // a.streams
-    lanes = []  # one independent sub-batch per stream: plan, buffers, stream, events
-    for si in range(a.streams):
-        plan = CodecPlan(sizes, a.ratio, a.bits, clients=per, device=dev)
-        ids = range(rank * a.clients + si * per, rank * a.clients + (si + 1) * per)
-        flat = synth_batch(plan.table, dev, client_ids=ids)
-        base = synth_batch(plan.table, dev, client_ids=[10_000 + i for i in ids]) if a.mode == "delta" else None
-        lanes.append(dict(plan=plan, flat=flat, base=base, enc=plan.empty_encoded(), ws=plan.empty_workspace(),
-                          out=plan.empty_flat(), dws=plan.empty_decode_workspace(),
-                          stream=torch.cuda.current_stream() if a.streams == 1 else torch.cuda.Stream(dev)))
-    from coala_amd.compression import SegmentTable
     t = SegmentTable(sizes, a.ratio, a.clients)
+    ids = range(rank * a.clients, (rank + 1) * a.clients)
+    flat = synth_batch(t, dev, client_ids=ids)
+    base = synth_batch(t, dev, client_ids=[10_000 + i for i in ids]) if a.mode == "delta" else None
+    pipe = LanePipeline(t, a.bits, lanes=a.lanes, device=dev, flags=a.flags)
+    enc, out = pipe.empty_encoded(), pipe.empty_flat()
     torch.cuda.synchronize()
 
     def step(i=None):
-        main = torch.cuda.current_stream()
-        for L in lanes:
-            if a.streams > 1:
-                L["stream"].wait_stream(main)
-            with torch.cuda.stream(L["stream"]):
-                ev_e = None if i is None else L["ev_e"][i]
-                ev_d = None if i is None else L["ev_d"][i]
-                L["plan"].encode(L["flat"], base=L["base"], out=L["enc"], workspace=L["ws"], events=ev_e,
-                                 flags=a.flags)
-                L["plan"].decode(L["enc"], base=L["base"], out=L["out"], workspace=L["dws"], events=ev_d)
-        if a.streams > 1:
-            for L in lanes:
-                main.wait_stream(L["stream"])
+        # the pipeline's streaming stream as the current stream: back-to-back steps need no join hops
+        with torch.cuda.stream(pipe.stream):
+            pipe.roundtrip(flat, base=base, enc=enc, out=out, enc_events=None if i is None else ev_e[i],
+                           dec_events=None if i is None else ev_d[i])
 
     for _ in range(a.warmup):
         step()
-    fallbacks = sum(L["plan"].fallbacks(L["ws"], stream=L["stream"]) for L in lanes)
-    for L in lanes:
-        with torch.cuda.stream(L["stream"]):
-            L["ev_e"] = [make_events(torch, 5) for _ in range(a.steps)]
-            L["ev_d"] = [make_events(torch, 3) for _ in range(a.steps)]
+    fallbacks = pipe.fallbacks()
+    # Timing events only at the streaming kernels' boundaries, and as few as possible: every recorded
+    # event costs ~6 us of dispatch gap (rocprofv3 trace, profiles/). The streaming kernels run back to
+    # back on one stream, so lane 0 records before and after its kernel and every later lane only
+    # after; a lane's interval is [previous lane's end, its end]. The latency-bound stages are timed
+    # by rocprofv3 (profiles/) instead.
+    def lane_events(n):
+        evs = []
+        for li in range(pipe.n_lanes):
+            ev = [None] * n
+            ev[2] = make_events(torch, 1)[0]
+            if li == 0:
+                ev[1] = make_events(torch, 1)[0]
+            evs.append(ev)
+        return evs
+    ev_e = [lane_events(5) for _ in range(a.steps)]
+    ev_d = [lane_events(3) for _ in range(a.steps)]
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -173,23 +171,25 @@ def main():
         dist.all_reduce(x, op=dist.ReduceOp.MAX)
         el = x.item()
 
-    # per-kernel mean durations (ms) from the HIP events recorded on each launch stream; with several
-    # streams, kernels overlap and each duration includes the co-running work of the other streams
+    # Per-kernel mean durations (ms per launch, averaged over lanes and steps) from the HIP events each
+    # lane records on its own stream at the stage boundaries. With several lanes a stage's interval can
+    # include co-running latency-bound kernels of other lanes (never another streaming kernel: the
+    # pipeline serialises k_scan / k_decode across lanes), i.e. it is the kernel's wall-clock time.
     def mean(pairs):
         return sum(s.elapsed_time(e) for s, e in pairs) / len(pairs)
     stages = {}
-    for name, (which, i0, i1) in {"k_sample": ("ev_e", 0, 1), "k_scan": ("ev_e", 1, 2), "k_select": ("ev_e", 2, 3),
-                                  "k_emit": ("ev_e", 3, 4), "k_bounds": ("ev_d", 0, 1),
-                                  "k_decode": ("ev_d", 1, 2)}.items():
-        stages[name] = mean([(e[i0], e[i1]) for L in lanes for e in L[which]])
+    for name, which in {"k_scan": ev_e, "k_decode": ev_d}.items():
+        stages[name] = mean([(lanes[li][1] if li == 0 else lanes[li - 1][2], lanes[li][2])
+                             for lanes in which for li in range(pipe.n_lanes)])
     N, K, T = t.n_elements, t.total_k, t.n_segments
     delta = a.mode == "delta"
     vb = 4 if a.bits == 32 else 1
-    large_elems = per * sum(n for n in sizes if n > SMALL_MAX)
-    Np, Kp, Tp = N // a.streams, K // a.streams, T // a.streams  # per launch (one sub-batch)
-    alg = {  # algorithmic HBM bytes per launch
-        "k_scan": 4 * large_elems * (2 if delta else 1),
-        "k_decode": 4 * Np * (2 if delta else 1) + (4 + vb) * Kp + 8 * Tp,
+    nl = pipe.n_lanes
+    segs = t.segs.astype("int64")
+    large_elems = int(segs[segs[:, 1] > SMALL_MAX, 1].sum())
+    alg = {  # algorithmic HBM bytes per launch, averaged over the lanes' launches
+        "k_scan": 4 * large_elems * (2 if delta else 1) / nl,
+        "k_decode": (4 * N * (2 if delta else 1) + (4 + vb) * K + 8 * T) / nl,
     }
     dom = max(alg, key=lambda k: stages[k])
     ach = alg[dom] / (stages[dom] * 1e-3) / 1e9
@@ -207,11 +207,11 @@ def main():
                                    f"{a.ratio}, {a.bits}-bit codes, {a.mode} mode, encode+decode batched",
                        "layout": a.layout, "clients_per_gpu": a.clients, "global_clients": a.clients * world,
                        "elements_per_client": sum(sizes), "segments_per_client": len(sizes),
-                       "ratio": a.ratio, "bits": a.bits, "mode": a.mode, "streams_per_gpu": a.streams,
+                       "ratio": a.ratio, "bits": a.bits, "mode": a.mode, "lanes_per_gpu": pipe.n_lanes,
                        "parallelism": f"replicas{world}"},
             "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": traffic,
-                         "traffic_source": traffic_src, "alg_bytes_per_launch": alg[dom]},
+                         "traffic_source": traffic_src, "alg_bytes_per_launch": int(alg[dom])},
             "step_roofline": {"alg_bytes_per_step": step_alg,
                               "achieved_GBs": round(step_alg / (step_ms * 1e-3) / 1e9, 1),
                               "frac": round(step_alg / (step_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)},

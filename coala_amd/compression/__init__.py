@@ -9,10 +9,11 @@ Public surface:
 """
 from . import wire
 from .codec import CompressedUpdate, FlatState, HipBackend, UpdateCodec, flatten_state, module_with_state
+from .pipeline import LanePipeline, split_lanes
 from .plan import CodecPlan, Encoded
 from .plugin import CompressionClientMixin, CompressionServerMixin
-from .spec import ALIGN, RAW_BITS, SegmentTable, k_for
+from .spec import ALIGN, RAW_BITS, SegmentTable, SubTable, k_for
 
-__all__ = ["wire", "CompressedUpdate", "FlatState", "HipBackend", "UpdateCodec", "flatten_state", "module_with_state",
+__all__ = ["wire", "LanePipeline", "split_lanes", "SubTable", "CompressedUpdate", "FlatState", "HipBackend", "UpdateCodec", "flatten_state", "module_with_state",
            "CodecPlan", "Encoded", "CompressionClientMixin", "CompressionServerMixin", "ALIGN", "RAW_BITS",
            "SegmentTable", "k_for"]

@@ -12,6 +12,9 @@ from .. import _build
 COALAC_FLAG_FORCE_EXACT = 1
 COALAC_FLAG_GENERIC_SELECT = 2
 COALAC_FLAG_STAMPS = 4
+# stages of a split encode / decode (coalac_sched_t.stages; 0 = all)
+COALAC_STAGE_SAMPLE, COALAC_STAGE_SCAN, COALAC_STAGE_SELECT, COALAC_STAGE_SMALL = 1, 2, 4, 8
+COALAC_STAGE_BOUNDS, COALAC_STAGE_DECODE = 1, 2
 COALAC_AGG_DIV = 0     # acc / total            (torch CPU division by a scalar)
 COALAC_AGG_RECIP = 1   # acc * (1.0f / total)   (torch GPU division by a host scalar)
 
@@ -39,6 +42,8 @@ SIGNATURES = [
     ("coalac_decode", _I, [_P, _P, _P, _P, _P, _P, _P, _P, _U64, _P]),
     ("coalac_encode_ev", _I, [_P, _P, _P, _P, _P, _P, _P, _P, _U64, ctypes.c_uint, _P, _P]),
     ("coalac_decode_ev", _I, [_P, _P, _P, _P, _P, _P, _P, _P, _U64, _P, _P]),
+    ("coalac_encode_sched", _I, [_P, _P, _P, _P, _P, _P, _P, _P, _U64, ctypes.c_uint, _P, _P]),
+    ("coalac_decode_sched", _I, [_P, _P, _P, _P, _P, _P, _P, _P, _U64, _P, _P]),
     ("coalac_aggregate", _I, [_P, _I, _P, _P, _P, _P, _P, ctypes.c_float, _I, _P, _P, _P, _U64, _P]),
     ("coalac_aggregate_ev", _I, [_P, _I, _P, _P, _P, _P, _P, ctypes.c_float, _I, _P, _P, _P, _U64, _P, _P]),
     ("coalac_workspace_fallbacks", _I, [_P, _P, _P, ctypes.POINTER(_I)]),
@@ -54,6 +59,11 @@ class CodecError(RuntimeError):
 
 class SegDesc(ctypes.Structure):
     _fields_ = [("in_off", _U64), ("n", _U64), ("k", _U64), ("out_off", _U64)]
+
+
+class Sched(ctypes.Structure):
+    """coalac_sched_t: per stage boundary, an event to wait for and an event to record (hipEvent_t)."""
+    _fields_ = [("wait", _P * 5), ("record", _P * 5), ("stages", ctypes.c_uint)]
 
 
 _lock = threading.Lock()

@@ -11,7 +11,7 @@ from dataclasses import dataclass
 import torch
 
 from . import _lib
-from .spec import RAW_BITS, VALID_BITS, SegmentTable
+from .spec import RAW_BITS, VALID_BITS, SegmentTable, SubTable
 
 
 @dataclass
@@ -47,10 +47,10 @@ class CodecPlan:
         device: CUDA/HIP device (default: current).
     """
 
-    def __init__(self, sizes, ratio, bits=8, clients=1, device=None):
+    def __init__(self, sizes, ratio, bits=8, clients=1, device=None, table=None):
         if bits not in VALID_BITS:
             raise ValueError(f"bits must be one of {VALID_BITS}, got {bits}")
-        self.table = SegmentTable(sizes, ratio, clients)
+        self.table = SegmentTable(sizes, ratio, clients) if table is None else table
         self.bits = int(bits)
         self.device = torch.device("cuda", torch.cuda.current_device() if device is None
                                    else torch.device(device).index or 0)
@@ -71,6 +71,13 @@ class CodecPlan:
         self.total_k, self.span, self.n_units = tk.value, span.value, nu.value
         if self.total_k != self.table.total_k:
             raise _lib.CodecError(f"plan total_k {self.total_k} != table {self.table.total_k}")
+
+    @classmethod
+    def from_segments(cls, segs, bits=8, device=None):
+        """Plan over explicit coalac_seg_t rows (in_off, n, k, out_off), offsets absolute: e.g. a
+        contiguous slice of a SegmentTable, whose results land in the buffers of the whole table
+        (LanePipeline). mn / scale of such a plan are indexed by row of `segs`."""
+        return cls(None, None, bits, device=device, table=SubTable(segs))
 
     # -- lifetime ---------------------------------------------------------------------------------
     def close(self):
@@ -132,8 +139,11 @@ class CodecPlan:
                                  f"{t.dtype}[{t.numel()}] on {t.device}")
 
     # -- codec ------------------------------------------------------------------------------------
-    def encode(self, flat, base=None, out=None, workspace=None, flags=0, stream=None, events=None):
-        """Encode flat (fp32[span]) [- base] -> Encoded. Asynchronous on `stream`."""
+    def encode(self, flat, base=None, out=None, workspace=None, flags=0, stream=None, events=None, sched=None):
+        """Encode flat (fp32[span]) [- base] -> Encoded. Asynchronous on `stream`.
+
+        events: 5 timing events recorded at the stage boundaries (coalac_encode_ev); sched: (wait,
+        record[, stages]) — lists of 5 events (or None) and a COALAC_STAGE_* mask (coalac_encode_sched)."""
         self._check_flat(flat, "input")
         self._check_flat(base, "base")
         out = self.empty_encoded() if out is None else out
@@ -145,15 +155,19 @@ class CodecPlan:
                 _ptr(out.scale), _ptr(ws), ctypes.c_uint64(self.ws_bytes), ctypes.c_uint(flags),
                 _stream_handle(stream))
         with torch.cuda.device(self.device):
-            if events is None:
+            if sched is not None:
+                rc = self._lib.coalac_encode_sched(*args, ctypes.byref(_sched(sched, 5)))
+            elif events is None:
                 rc = self._lib.coalac_encode(*args)
             else:
                 rc = self._lib.coalac_encode_ev(*args, _event_array(events, 5))
         _lib.check(rc, "coalac_encode")
         return out
 
-    def decode(self, enc, base=None, out=None, workspace=None, stream=None, events=None):
-        """Decode Encoded -> dense flat fp32[span] (+ base, fused). Asynchronous on `stream`."""
+    def decode(self, enc, base=None, out=None, workspace=None, stream=None, events=None, sched=None):
+        """Decode Encoded -> dense flat fp32[span] (+ base, fused). Asynchronous on `stream`.
+
+        events / sched: as encode(), 3 boundaries (coalac_decode_ev / coalac_decode_sched)."""
         self._check_encoded(enc)
         self._check_flat(base, "base")
         if out is None:
@@ -165,7 +179,9 @@ class CodecPlan:
         args = (self._h, _ptr(enc.idx), _ptr(enc.vals), _ptr(enc.mn), _ptr(enc.scale), _ptr(base), _ptr(out),
                 _ptr(ws), ctypes.c_uint64(self.dec_ws_bytes), _stream_handle(stream))
         with torch.cuda.device(self.device):
-            if events is None:
+            if sched is not None:
+                rc = self._lib.coalac_decode_sched(*args, ctypes.byref(_sched(sched, 3)))
+            elif events is None:
                 rc = self._lib.coalac_decode(*args)
             else:
                 rc = self._lib.coalac_decode_ev(*args, _event_array(events, 3))
@@ -228,3 +244,19 @@ def _event_array(events, n):
         if e is not None:
             arr[i] = ctypes.c_void_p(e.cuda_event)
     return arr
+
+
+def _sched(sched, n):
+    """(wait, record[, stages]) — lists of torch.cuda.Event or None, and a COALAC_STAGE_* mask (0 = all)
+    -> coalac_sched_t. Events must exist: recorded once, since torch creates the HIP event lazily."""
+    wait, record = sched[0], sched[1]
+    s = _lib.Sched()
+    s.stages = int(sched[2]) if len(sched) > 2 else 0
+    for i in range(n):
+        for arr, evs in ((s.wait, wait), (s.record, record)):
+            e = evs[i] if evs is not None and i < len(evs) else None
+            if e is not None:
+                if not e.cuda_event:
+                    raise ValueError("sched: event has no HIP event yet (record it once first)")
+                arr[i] = e.cuda_event
+    return s

@@ -96,3 +96,30 @@ class SegmentTable:
         if delta:
             b += 8 * N
         return b
+
+
+class SubTable:
+    """Explicit segment rows (in_off, n, k, out_off) with ABSOLUTE offsets, e.g. a contiguous slice of a
+    SegmentTable (one lane of coala_amd/compression/pipeline.py). total_k / span are the buffer extents
+    the rows need (max out_off + k, max in_off + n), not their sums."""
+
+    clients = None  # not a copies-of-one-layout table: no fused aggregation over it
+
+    def __init__(self, segs):
+        self.segs = np.ascontiguousarray(np.asarray(segs, dtype=np.uint64).reshape(-1, 4))
+
+    @property
+    def n_segments(self):
+        return len(self.segs)
+
+    @property
+    def total_k(self):
+        return int((self.segs[:, 3] + self.segs[:, 2]).max()) if len(self.segs) else 0
+
+    @property
+    def span(self):
+        return int((self.segs[:, 0] + self.segs[:, 1]).max()) if len(self.segs) else 0
+
+    @property
+    def n_elements(self):
+        return int(self.segs[:, 1].sum())

@@ -26,8 +26,9 @@
 //               small segment: the whole segment in LDS (latency-bound work placed where CUs idle)
 //     k_scan    one wave per large unit: single HBM read, classify A / B, 8-byte records in index order
 //     k_ghist   one block per 32-unit group: band histogram of the group's B records
-//     k_pick    one block per large segment: sum the group histograms -> key window of the k-th key
-//     k_gwin    one block per group: per-unit counts above the window + the in-window entries
+//     k_gwin    one block per group: sum the segment's group histograms -> key window of the k-th key
+//               (every group block of the segment, redundantly); per-unit counts above the window + the
+//               group's in-window entries
 //     k_select  one 512-thread block per large segment: exact k-th key + tie quota from the window
 //               lists (generic multi-pass select / exact re-select on a bracket miss), per-unit output
 //               offsets, min / max -> scale
@@ -703,13 +704,14 @@ __global__ __launch_bounds__(BLOCK) void k_sample(Params P) {
 
 // k_scan: streams the large units, one wave each. Blocks [0, scan_small) first encode the small
 // segments when they are not forked to the side stream (small plans: the fork costs more than it hides).
-template <bool DELTA, bool RAW>
+template <bool DELTA, bool RAW, bool WITH_SMALL>
 __global__ __launch_bounds__(BLOCK) void k_scan(Params P) {
   // one LDS arena: candidate staging (WAVES x STAGE_CAP records) or a small segment's values + histogram
-  constexpr size_t SMALL_BYTES = (SMALL_MAX + HIST_BINS + 64) * 4;
+  // (WITH_SMALL only: without it the block needs 16 KB of LDS instead of 24.8 KB)
+  constexpr size_t SMALL_BYTES = WITH_SMALL ? (SMALL_MAX + HIST_BINS + 64) * 4 : 0;
   constexpr size_t STAGE_BYTES = WAVES * STAGE_CAP * sizeof(uint2);
   __shared__ __attribute__((aligned(16))) uint8_t arena[SMALL_BYTES > STAGE_BYTES ? SMALL_BYTES : STAGE_BYTES];
-  if (blockIdx.x < P.scan_small) {
+  if (WITH_SMALL && blockIdx.x < P.scan_small) {
     float* vals = reinterpret_cast<float*>(arena);
     uint32_t* hist = reinterpret_cast<uint32_t*>(arena) + SMALL_MAX;
     small_encode<DELTA, RAW>(P, P.small_list[blockIdx.x], vals, hist, hist + HIST_BINS);
@@ -920,7 +922,6 @@ struct Band {
   DEV uint32_t wlo(uint32_t b) const { return tlo + (b << shift); }
   DEV uint32_t whi(uint32_t b) const { return b == last ? thi : min(thi, wlo(b) + ((1u << shift) - 1u)); }
 };
-DEV void segment_pick(const Params& P, uint32_t li, uint32_t* hist, uint32_t* sh);
 
 // k_ghist: the group's HB2-bin histogram of the band keys [tlo, thi] -> ghist[group]. (A fused variant in
 // which the segment's last-arriving group block ran segment_pick needed an agent-scope release fence in
@@ -947,42 +948,50 @@ __global__ __launch_bounds__(BLOCK) void k_ghist(Params P) {
 }
 
 // segment_pick: per large segment — validate the sampled bracket, sum the group histograms, pick the bin of
-// the k-th key: sstate = {window lo, window hi, rank inside the window, 0}; {.., 1} routes the segment
-// to the generic single-block path (bracket miss, nothing to take from B, huge segment, test flags).
-DEV void segment_pick(const Params& P, uint32_t li, uint32_t* hist, uint32_t* sh) {
+// the k-th key: {window lo, window hi, rank inside the window, 0}; {.., 1} routes the segment to the
+// generic single-block path (bracket miss, nothing to take from B, huge segment, test flags). Every group
+// block of the segment computes it (identically) at the start of k_gwin — cheaper than a launch of its
+// own between k_ghist and k_gwin. Returned to every thread.
+DEV uint4 segment_pick(const Params& P, uint32_t li, uint32_t* hist, uint32_t* sh) {
   const uint32_t t = threadIdx.x;
   const SegDev sd = P.segs[P.large_list[li]];
   const uint32_t lb = sd.lu_begin, nu = sd.unit_end - sd.unit_begin, k = sd.k;
+  const uint32_t g0 = sd.g_begin, ng = (nu + GU - 1) / GU;
+  // the group histograms: both of this thread's bins, 8 groups' loads in flight at a time
+  static_assert(HB2 == 2 * BLOCK, "two histogram bins per thread");
+  uint32_t h0 = 0, h1 = 0;
+  for (uint32_t g = 0; g < ng; g += 8) {
+    uint32_t v0[8], v1[8];
+#pragma unroll
+    for (uint32_t j = 0; j < 8; ++j) {
+      const uint64_t row = (uint64_t)(g0 + min(g + j, ng - 1)) * HB2;
+      v0[j] = P.ghist[row + t];
+      v1[j] = P.ghist[row + BLOCK + t];
+    }
+#pragma unroll
+    for (uint32_t j = 0; j < 8; ++j) {
+      h0 += g + j < ng ? v0[j] : 0u;
+      h1 += g + j < ng ? v1[j] : 0u;
+    }
+  }
   uint32_t sa = 0, sc = 0;
   for (uint32_t i = t; i < nu; i += BLOCK) {
     sa += P.cntA[lb + i];
     sc += P.cntC[lb + i];
   }
-  sa = block_sum<BLOCK>(sa, sh);
+  hist[t] = h0;
+  hist[BLOCK + t] = h1;
+  sa = block_sum<BLOCK>(sa, sh);  // barriers inside (also publish hist)
   sc = block_sum<BLOCK>(sc, sh);
   const bool generic = (P.flags & (COALAC_FLAG_FORCE_EXACT | COALAC_FLAG_GENERIC_SELECT)) || !(sa < k && k <= sc) ||
                        nu > UCAP;
-  if (generic) {
-    if (t == 0) P.sstate[li] = make_uint4(0u, 0u, 0u, 1u);
-    return;
-  }
-  const uint32_t g0 = sd.g_begin, ng = (nu + GU - 1) / GU;
-  for (uint32_t b = t; b < HB2; b += BLOCK) {
-    uint32_t acc = 0;
-    for (uint32_t g = 0; g < ng; ++g) acc += P.ghist[(uint64_t)(g0 + g) * HB2 + b];
-    hist[b] = acc;
-  }
+  if (generic) return make_uint4(0u, 0u, 0u, 1u);
   __syncthreads();
   uint32_t r = k - sa;
   const uint32_t b = hist_pick<BLOCK, HB2>(hist, r, sh);
-  if (t == 0) {
-    if (b == NONE) {
-      P.sstate[li] = make_uint4(0u, 0u, 0u, 1u);
-    } else {
-      const Band band(P.tlo[lb], P.thi[lb], P.shhi[li]);
-      P.sstate[li] = make_uint4(band.wlo(b), band.whi(b), r, 0u);
-    }
-  }
+  if (b == NONE) return make_uint4(0u, 0u, 0u, 1u);
+  const Band band(P.tlo[lb], P.thi[lb], P.shhi[li]);
+  return make_uint4(band.wlo(b), band.whi(b), r, 0u);
 }
 
 // k_gwin: per group — per-unit counts of keys above the window (-> gtC), the group's in-window entries
@@ -1053,9 +1062,11 @@ DEV void group_window(const Params& P, const uint4 G, const uint4 st, GwinSmem& 
 
 __global__ __launch_bounds__(BLOCK) void k_gwin(Params P) {
   __shared__ GwinSmem W;
+  __shared__ uint32_t hist[HB2];
   __shared__ uint32_t sh[64];
   const uint4 G = P.groups[blockIdx.x];
-  const uint4 st = P.sstate[G.x];
+  const uint4 st = segment_pick(P, G.x, hist, sh);
+  if (threadIdx.x == 0 && G.y == P.segs[G.w].lu_begin) P.sstate[G.x] = st;  // the segment's first group
   if (st.w == 0) group_window(P, G, st, W, sh);
 }
 
@@ -1072,15 +1083,33 @@ DEV bool select_from_groups(const Params& P, const SegDev& sd, uint32_t lb, uint
   const uint32_t gpre = block_excl_scan<NT>(c, S.sh, W);
   const uint32_t over = block_sum<NT>(c > GCAP ? 1u : 0u, S.sh);
   if (over || W > WLIST) return false;
-  // offset of each group's entries, then copy them
+  // offset of each group's entries, then gather them: entry e belongs to the last group g with
+  // upre[g] <= e (binary search in LDS); all of a thread's loads are issued before any is used
   if (t < ng) S.upre[t] = gpre;
   __syncthreads();
-  for (uint32_t g = 0; g < ng; ++g) {
-    const uint32_t cg = min(P.gcnt[g0 + g], GCAP), base = S.upre[g];
-    for (uint32_t q = t; q < cg; q += NT) {
-      const uint2 e = P.glist[(uint64_t)(g0 + g) * GCAP + q];
-      S.lst_val[base + q] = e.x;
-      S.lst_unit[base + q] = e.y;
+  {
+    constexpr uint32_t EPT = WLIST / NT;
+    uint2 v[EPT];
+#pragma unroll
+    for (uint32_t j = 0; j < EPT; ++j) {
+      const uint32_t e = min(t + j * NT, W > 0 ? W - 1 : 0u);
+      uint32_t lo = 0, hi = ng - 1;  // ng >= 1
+      while (lo < hi) {
+        const uint32_t mid = (lo + hi + 1) >> 1;
+        if (S.upre[mid] <= e)
+          lo = mid;
+        else
+          hi = mid - 1;
+      }
+      v[j] = P.glist[(uint64_t)(g0 + lo) * GCAP + min(e - S.upre[lo], GCAP - 1)];
+    }
+#pragma unroll
+    for (uint32_t j = 0; j < EPT; ++j) {
+      const uint32_t e = t + j * NT;
+      if (e < W) {
+        S.lst_val[e] = v[j].x;
+        S.lst_unit[e] = v[j].y;
+      }
     }
   }
   for (uint32_t i = t; i < nu; i += NT) {
@@ -1127,11 +1156,7 @@ DEV bool select_from_groups(const Params& P, const SegDev& sd, uint32_t lb, uint
   if (lfp != NONE) atomicMin(&S.sh[42], ex + lfp);
   if (lfn != NONE) atomicMin(&S.sh[43], ex + lfn);
   __syncthreads();
-  for (uint32_t i = t; i < nu; i += NT) {
-    P.gtC[lb + i] = S.ugt[i];
-    P.eqC[lb + i] = S.ueq[i];
-  }
-  T_out = T;
+  T_out = T;  // per-unit counts stay in S.ugt / S.ueq for the caller's in-order scan
   rt_out = rt;
   fp = S.sh[42];
   fn = S.sh[43];
@@ -1197,12 +1222,12 @@ DEV void segment_select(const Params& P, uint32_t li, SelSmem& S) {
   for (uint32_t c0 = 0; c0 < nu; c0 += NT) {
     const uint32_t i = c0 + t;
     const bool valid = i < nu;
-    const uint32_t e = valid ? P.eqC[lb + i] : 0u;
+    const uint32_t e = valid ? (done ? S.ueq[i] : P.eqC[lb + i]) : 0u;  // fast path: counts in LDS
     uint32_t tot;
     const uint32_t ex = block_excl_scan<NT>(e, S.sh, tot) + carry_e;
     carry_e += tot;
     const uint32_t quota = !valid ? 0u : (ex >= rt ? 0u : min(e, rt - ex));
-    const uint32_t sel = valid ? P.gtC[lb + i] + quota : 0u;
+    const uint32_t sel = valid ? (done ? S.ugt[i] : P.gtC[lb + i]) + quota : 0u;
     uint32_t tot2;
     const uint32_t so = block_excl_scan<NT>(sel, S.sh, tot2) + carry_sel;
     carry_sel += tot2;
@@ -1236,12 +1261,6 @@ DEV void segment_select(const Params& P, uint32_t li, SelSmem& S) {
     P.scale[s] = scale;
   }
   STAMP(P, li, 12);
-}
-
-__global__ __launch_bounds__(BLOCK) void k_pick(Params P) {
-  __shared__ uint32_t hist[HB2];
-  __shared__ uint32_t sh[64];
-  segment_pick(P, blockIdx.x, hist, sh);
 }
 
 template <bool DELTA, bool RAW>
@@ -1293,7 +1312,8 @@ __global__ __launch_bounds__(BLOCK) void k_emit(Params P) {
 // ------------------------------------------------------------------------------------------------
 // decode
 // ------------------------------------------------------------------------------------------------
-// k_decode: DPW = 2 units per wave (1 in delta mode), all loads issued up front. Under a saturated write stream every load
+// k_decode: DPW = 2 units per wave (1 in delta mode), all loads issued up front. Partial units (a
+// segment's last, len < 4096) take the same register path with masked stores. Under a saturated write stream every load
 // round trip a wave waits on keeps its slot from issuing stores (tools/decode_ablate.hip: one unit per
 // wave with a dependent load = 4.6 TB/s, two units with hoisted loads + non-temporal stores = 5.7 TB/s,
 // above the 5.5 TB/s of plain zero stores). Round 1: both units' metadata and [lo, hi) bounds (k_bounds);
@@ -1360,24 +1380,24 @@ __global__ __launch_bounds__(BLOCK) void k_decode(Params P) {
   for (uint32_t r = 0; r < DPW; ++r) {
     if (u0 + r >= P.n_units) break;
     const uint32_t len = U[r].len;
+    const bool full = len == UNIT;  // else a segment's last, partial unit: same path, masked
     const float* bs = HASBASE ? P.base + U[r].off : nullptr;
     float* out = P.out + U[r].off;
-    if (len != UNIT) {
-      // a segment's last, partial unit (one per segment): background, then scatter after the stores
-      for (uint32_t i = lane; i < len; i += 64) out[i] = HASBASE ? bs[i] + 0.0f : 0.0f;
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      for (uint32_t e = lo[r] + lane; e < hi[r]; e += 64) {
-        const uint64_t o = U[r].out_off + e;
-        const uint32_t p2 = (uint32_t)P.cidx[o] - U[r].start;
-        const float v2 = code_value<RAW>(load_code<RAW>(P, o), mn[r], sc[r]);
-        if (p2 < len) out[p2] = HASBASE ? bs[p2] + v2 : v2;
-      }
-      continue;
-    }
     float4 b[UNIT_IT];
 #pragma unroll
-    for (uint32_t it = 0; it < UNIT_IT; ++it)
-      b[it] = HASBASE ? *reinterpret_cast<const float4*>(bs + (it * 64 + lane) * 4) : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    for (uint32_t it = 0; it < UNIT_IT; ++it) {
+      const uint32_t e = (it * 64 + lane) * 4;
+      if (!HASBASE) {
+        b[it] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+      } else if (full || e + 3 < len) {
+        b[it] = *reinterpret_cast<const float4*>(bs + e);
+      } else {
+        b[it].x = e + 0 < len ? bs[e + 0] : 0.0f;
+        b[it].y = e + 1 < len ? bs[e + 1] : 0.0f;
+        b[it].z = e + 2 < len ? bs[e + 2] : 0.0f;
+        b[it].w = 0.0f;
+      }
+    }
     uint64_t kept = 0;
     const uint32_t cnt = hi[r] - lo[r];
     merge_entries<HASBASE>(b, kept, pos[r], code_value<RAW>(q[r], mn[r], sc[r]), min(cnt, 64u), lane);
@@ -1396,8 +1416,15 @@ __global__ __launch_bounds__(BLOCK) void k_decode(Params P) {
         b[it].z = (m & 4u) ? b[it].z : b[it].z + 0.0f;
         b[it].w = (m & 8u) ? b[it].w : b[it].w + 0.0f;
       }
-      const f4v t = {b[it].x, b[it].y, b[it].z, b[it].w};
-      __builtin_nontemporal_store(t, reinterpret_cast<f4v*>(out + (it * 64 + lane) * 4));
+      const uint32_t e = (it * 64 + lane) * 4;
+      if (full || e + 3 < len) {
+        const f4v t = {b[it].x, b[it].y, b[it].z, b[it].w};
+        __builtin_nontemporal_store(t, reinterpret_cast<f4v*>(out + e));
+      } else if (e < len) {  // the partial unit's last 1-3 elements (entries at pos >= len were never
+        out[e] = b[it].x;    // merged: merge_entries only visits rows of the sorted list in order)
+        if (e + 1 < len) out[e + 1] = b[it].y;
+        if (e + 2 < len) out[e + 2] = b[it].z;
+      }
     }
   }
 }
@@ -1701,39 +1728,98 @@ void fill_meta(Params& P, coalac_plan_t plan) {
   P.levels = plan->bits == 32 ? 0.0f : (float)((1u << plan->bits) - 1u);
 }
 
-void record(void* const* ev, int i, hipStream_t st) {
-  if (ev && ev[i]) (void)hipEventRecord(static_cast<hipEvent_t>(ev[i]), st);
+// Stage boundary i of an encode / decode enqueue: wait for sc->wait[i], then record sc->record[i].
+int boundary(const coalac_sched_t* sc, int i, hipStream_t st) {
+  if (!sc) return COALAC_OK;
+  if (sc->wait[i]) HIP_CHECK(hipStreamWaitEvent(st, static_cast<hipEvent_t>(sc->wait[i]), 0));
+  if (sc->record[i]) HIP_CHECK(hipEventRecord(static_cast<hipEvent_t>(sc->record[i]), st));
+  return COALAC_OK;
 }
 
+#define BOUNDARY(i)                          \
+  do {                                       \
+    const int rc_ = boundary(sc, (i), st);   \
+    if (rc_) return rc_;                     \
+  } while (0)
+
+// the _ev variants: record-only schedule
+coalac_sched_t record_only(void* const* ev, int n) {
+  coalac_sched_t s{};
+  if (ev)
+    for (int i = 0; i < n; ++i) s.record[i] = ev[i];
+  return s;
+}
+
+// Small segments go beside the large ones' pipeline on a side stream once the batch is big enough for
+// the fork / join (~10-20 us) to pay off (>= 16384 large units, ~3 ResNet-50 updates).
+constexpr uint32_t FORK_MIN_LUNITS = 16384;
+
+// Is stage boundary i of a call adjacent to an enqueued stage? (stage k spans boundaries [lo_k, hi_k])
+bool at_boundary(unsigned stages, const int (*span)[2], int nst, int i) {
+  for (int k = 0; k < nst; ++k)
+    if ((stages >> k) & 1u)
+      if (span[k][0] <= i && i <= span[k][1]) return true;
+  return false;
+}
+
+constexpr int ENC_SPAN[4][2] = {{0, 1}, {1, 2}, {2, 4}, {0, 1}};  // SAMPLE, SCAN, SELECT, SMALL
+constexpr int DEC_SPAN[2][2] = {{0, 1}, {1, 2}};                  // BOUNDS, DECODE
+
 template <bool DELTA, bool RAW>
-int launch_encode(const Params& P, coalac_plan_t plan, hipStream_t st, void* const* ev) {
+int launch_encode(const Params& P, coalac_plan_t plan, hipStream_t st, const coalac_sched_t* sc) {
   const uint32_t gu = (plan->n_lunits + WAVES - 1) / WAVES;
-  const bool fork = plan->n_small && plan->side != nullptr;
+  const unsigned all = COALAC_STAGE_SAMPLE | COALAC_STAGE_SCAN | COALAC_STAGE_SELECT | COALAC_STAGE_SMALL;
+  const unsigned stages = (sc && (sc->stages & all)) ? (sc->stages & all) : all;
+  // whole encode: small segments forked beside k_sample / k_scan (big batches) or inside k_scan;
+  // split encode: only in stage SMALL (k_small)
+  const bool split = stages != all;
+  const bool fork = plan->n_small && !split && plan->n_lunits >= FORK_MIN_LUNITS;
   Params Q = P;
-  Q.scan_small = fork ? 0u : plan->n_small;
+  Q.scan_small = (fork || split) ? 0u : plan->n_small;
   std::unique_lock<std::mutex> lk(plan->mu, std::defer_lock);
-  if (fork) lk.lock();
-  record(ev, 0, st);
+  if (fork) {
+    lk.lock();
+    if (plan->side == nullptr) {  // created on first use: pipelined plans never need it
+      if (hipStreamCreateWithFlags(&plan->side, hipStreamNonBlocking) != hipSuccess ||
+          hipEventCreateWithFlags(&plan->fork, hipEventDisableTiming) != hipSuccess ||
+          hipEventCreateWithFlags(&plan->join, hipEventDisableTiming) != hipSuccess)
+        return fail(COALAC_EHIP, "creating the plan's side stream / events failed: %s",
+                    hipGetErrorString(hipGetLastError()));
+    }
+  }
+  auto B = [&](int i) { return at_boundary(stages, ENC_SPAN, 4, i) ? boundary(sc, i, st) : COALAC_OK; };
+#define ENC_BOUNDARY(i)       \
+  do {                        \
+    const int rc_ = B(i);     \
+    if (rc_) return rc_;      \
+  } while (0)
+  ENC_BOUNDARY(0);
   if (fork) {
     HIP_CHECK(hipEventRecord(plan->fork, st));
     HIP_CHECK(hipStreamWaitEvent(plan->side, plan->fork, 0));
     hipLaunchKernelGGL((k_small<DELTA, RAW>), dim3(plan->n_small), dim3(BLOCK), 0, plan->side, P);
     HIP_CHECK(hipEventRecord(plan->join, plan->side));
   }
-  if (plan->n_large) hipLaunchKernelGGL((k_sample<DELTA, RAW>), dim3(plan->n_large), dim3(BLOCK), 0, st, P);
-  record(ev, 1, st);
-  if (gu + Q.scan_small) hipLaunchKernelGGL((k_scan<DELTA, RAW>), dim3(gu + Q.scan_small), dim3(BLOCK), 0, st, Q);
-  record(ev, 2, st);
-  if (plan->n_large) {
+  if ((stages & COALAC_STAGE_SAMPLE) && plan->n_large)
+    hipLaunchKernelGGL((k_sample<DELTA, RAW>), dim3(plan->n_large), dim3(BLOCK), 0, st, P);
+  if (split && (stages & COALAC_STAGE_SMALL) && plan->n_small)
+    hipLaunchKernelGGL((k_small<DELTA, RAW>), dim3(plan->n_small), dim3(BLOCK), 0, st, P);
+  ENC_BOUNDARY(1);
+  if ((stages & COALAC_STAGE_SCAN) && Q.scan_small)
+    hipLaunchKernelGGL((k_scan<DELTA, RAW, true>), dim3(gu + Q.scan_small), dim3(BLOCK), 0, st, Q);
+  else if ((stages & COALAC_STAGE_SCAN) && gu)
+    hipLaunchKernelGGL((k_scan<DELTA, RAW, false>), dim3(gu), dim3(BLOCK), 0, st, Q);
+  ENC_BOUNDARY(2);
+  if ((stages & COALAC_STAGE_SELECT) && plan->n_large) {
     hipLaunchKernelGGL(k_ghist, dim3(plan->n_groups), dim3(BLOCK), 0, st, P);
-    hipLaunchKernelGGL(k_pick, dim3(plan->n_large), dim3(BLOCK), 0, st, P);
     hipLaunchKernelGGL(k_gwin, dim3(plan->n_groups), dim3(BLOCK), 0, st, P);
     hipLaunchKernelGGL((k_select<DELTA, RAW>), dim3(plan->n_large), dim3(SEL_NT), 0, st, P);
   }
-  record(ev, 3, st);
-  if (plan->n_large) hipLaunchKernelGGL((k_emit<RAW>), dim3(gu), dim3(BLOCK), 0, st, P);
+  ENC_BOUNDARY(3);
+  if ((stages & COALAC_STAGE_SELECT) && plan->n_large) hipLaunchKernelGGL((k_emit<RAW>), dim3(gu), dim3(BLOCK), 0, st, P);
   if (fork) HIP_CHECK(hipStreamWaitEvent(st, plan->join, 0));
-  record(ev, 4, st);
+  ENC_BOUNDARY(4);
+#undef ENC_BOUNDARY
   return COALAC_OK;
 }
 
@@ -1868,17 +1954,6 @@ int coalac_plan_create(const coalac_seg_t* h_segs, int nseg, int bits, coalac_pl
   p->large_list = reinterpret_cast<uint32_t*>(m + o_large);
   p->groups = reinterpret_cast<uint4*>(m + o_grp);
   p->bchunks = reinterpret_cast<BChunk*>(m + o_bch);
-  // Small segments overlap the large ones' pipeline on a side stream once the batch is big enough for
-  // the fork / join (~10-20 us) to pay off (>= 16384 large units, ~3 ResNet-50 updates).
-  if (p->n_small && p->n_lunits >= 16384) {
-    if (hipStreamCreateWithFlags(&p->side, hipStreamNonBlocking) != hipSuccess ||
-        hipEventCreateWithFlags(&p->fork, hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&p->join, hipEventDisableTiming) != hipSuccess) {
-      const hipError_t ce = hipGetLastError();
-      coalac_plan_destroy(p);
-      return fail(COALAC_EHIP, "creating the plan's side stream / events failed: %s", hipGetErrorString(ce));
-    }
-  }
   *out = p;
   return COALAC_OK;
 }
@@ -1911,6 +1986,14 @@ int coalac_plan_query(coalac_plan_t plan, uint64_t* ws_bytes, uint64_t* dec_ws_b
 int coalac_encode_ev(coalac_plan_t plan, const float* d_in, const float* d_base, int32_t* d_idx,
                      void* d_vals, float* d_mn, float* d_scale, void* d_ws, uint64_t ws_bytes,
                      unsigned flags, void* stream, void* const* events) {
+  const coalac_sched_t s = record_only(events, 5);
+  return coalac_encode_sched(plan, d_in, d_base, d_idx, d_vals, d_mn, d_scale, d_ws, ws_bytes, flags, stream,
+                             events ? &s : nullptr);
+}
+
+int coalac_encode_sched(coalac_plan_t plan, const float* d_in, const float* d_base, int32_t* d_idx,
+                        void* d_vals, float* d_mn, float* d_scale, void* d_ws, uint64_t ws_bytes,
+                        unsigned flags, void* stream, const coalac_sched_t* sched) {
   if (!plan) return fail(COALAC_EINVAL, "coalac_encode: plan is NULL");
   if (plan->nseg == 0) return COALAC_OK;
   if (!d_mn || !d_scale) return fail(COALAC_EINVAL, "coalac_encode: mn/scale pointers are NULL");
@@ -1956,13 +2039,13 @@ int coalac_encode_ev(coalac_plan_t plan, const float* d_in, const float* d_base,
   hipStream_t st = static_cast<hipStream_t>(stream);
   const bool delta = d_base != nullptr, raw = plan->bits == 32;
   if (delta && raw)
-    rc = launch_encode<true, true>(P, plan, st, events);
+    rc = launch_encode<true, true>(P, plan, st, sched);
   else if (delta)
-    rc = launch_encode<true, false>(P, plan, st, events);
+    rc = launch_encode<true, false>(P, plan, st, sched);
   else if (raw)
-    rc = launch_encode<false, true>(P, plan, st, events);
+    rc = launch_encode<false, true>(P, plan, st, sched);
   else
-    rc = launch_encode<false, false>(P, plan, st, events);
+    rc = launch_encode<false, false>(P, plan, st, sched);
   if (rc) return rc;
   HIP_CHECK(hipGetLastError());
   return COALAC_OK;
@@ -1977,6 +2060,16 @@ int coalac_encode(coalac_plan_t plan, const float* d_in, const float* d_base, in
 int coalac_decode_ev(coalac_plan_t plan, const int32_t* d_idx, const void* d_vals, const float* d_mn,
                      const float* d_scale, const float* d_base, float* d_out, void* d_ws, uint64_t ws_bytes,
                      void* stream, void* const* events) {
+  const coalac_sched_t s = record_only(events, 3);
+  return coalac_decode_sched(plan, d_idx, d_vals, d_mn, d_scale, d_base, d_out, d_ws, ws_bytes, stream,
+                             events ? &s : nullptr);
+}
+
+int coalac_decode_sched(coalac_plan_t plan, const int32_t* d_idx, const void* d_vals, const float* d_mn,
+                        const float* d_scale, const float* d_base, float* d_out, void* d_ws, uint64_t ws_bytes,
+                        void* stream, const coalac_sched_t* sched) {
+  const unsigned all = COALAC_STAGE_BOUNDS | COALAC_STAGE_DECODE;
+  const unsigned stages = (sched && (sched->stages & all)) ? (sched->stages & all) : all;
   if (!plan) return fail(COALAC_EINVAL, "coalac_decode: plan is NULL");
   if (plan->n_units == 0) return COALAC_OK;
   if (!d_out) return fail(COALAC_EINVAL, "coalac_decode: output pointer is NULL");
@@ -2002,12 +2095,21 @@ int coalac_decode_ev(coalac_plan_t plan, const int32_t* d_idx, const void* d_val
   const bool raw = plan->bits == 32, hb = d_base != nullptr;
   const uint32_t upb = WAVES * (hb ? decode_dpw<true>() : decode_dpw<false>());  // units per block
   const uint32_t g = (plan->n_units + upb - 1) / upb;
-  record(events, 0, st);
-  if (plan->n_bchunks)
+  const coalac_sched_t* sc = sched;
+  auto B = [&](int i) { return at_boundary(stages, DEC_SPAN, 2, i) ? boundary(sc, i, st) : COALAC_OK; };
+#define DEC_BOUNDARY(i)       \
+  do {                        \
+    const int rc_ = B(i);     \
+    if (rc_) return rc_;      \
+  } while (0)
+  DEC_BOUNDARY(0);
+  if ((stages & COALAC_STAGE_BOUNDS) && plan->n_bchunks)
     hipLaunchKernelGGL(k_bounds, dim3(plan->n_bchunks), dim3(BLOCK), 0, st, P, plan->bchunks,
                        static_cast<uint32_t*>(d_ws));
-  record(events, 1, st);
-  if (raw && hb)
+  DEC_BOUNDARY(1);
+  if (!(stages & COALAC_STAGE_DECODE))
+    ;
+  else if (raw && hb)
     hipLaunchKernelGGL((k_decode<true, true>), dim3(g), dim3(BLOCK), 0, st, P);
   else if (raw)
     hipLaunchKernelGGL((k_decode<true, false>), dim3(g), dim3(BLOCK), 0, st, P);
@@ -2015,7 +2117,8 @@ int coalac_decode_ev(coalac_plan_t plan, const int32_t* d_idx, const void* d_val
     hipLaunchKernelGGL((k_decode<false, true>), dim3(g), dim3(BLOCK), 0, st, P);
   else
     hipLaunchKernelGGL((k_decode<false, false>), dim3(g), dim3(BLOCK), 0, st, P);
-  record(events, 2, st);
+  DEC_BOUNDARY(2);
+#undef DEC_BOUNDARY
   HIP_CHECK(hipGetLastError());
   return COALAC_OK;
 }
@@ -2077,11 +2180,13 @@ int coalac_aggregate_ev(coalac_plan_t plan, int clients, const int32_t* d_idx, c
   A.total = total;
   A.inv_total = 1.0f / total;
   hipStream_t st = static_cast<hipStream_t>(stream);
-  record(events, 0, st);
+  const coalac_sched_t s = record_only(events, 3);
+  const coalac_sched_t* sc = events ? &s : nullptr;
+  BOUNDARY(0);
   if (plan->n_bchunks)
     hipLaunchKernelGGL(k_bounds, dim3(plan->n_bchunks), dim3(BLOCK), 0, st, P, plan->bchunks,
                        static_cast<uint32_t*>(d_ws));
-  record(events, 1, st);
+  BOUNDARY(1);
   const uint32_t g = (U0 + WAVES - 1) / WAVES;
   const bool raw = plan->bits == 32, hb = d_base != nullptr, rc1 = mode == COALAC_AGG_RECIP;
 #define AGG(R, H, M) hipLaunchKernelGGL((k_aggregate<R, H, M>), dim3(g), dim3(BLOCK), 0, st, P, A)
@@ -2093,7 +2198,7 @@ int coalac_aggregate_ev(coalac_plan_t plan, int clients, const int32_t* d_idx, c
     else { if (rc1) AGG(false, false, 1); else AGG(false, false, 0); }
   }
 #undef AGG
-  record(events, 2, st);
+  BOUNDARY(2);
   HIP_CHECK(hipGetLastError());
   return COALAC_OK;
 }

@@ -107,6 +107,43 @@ int coalac_decode_ev(coalac_plan_t plan, const int32_t* d_idx, const void* d_val
                      const float* d_scale, const float* d_base, float* d_out, void* d_ws,
                      uint64_t ws_bytes, void* stream, void* const* events);
 
+/* Scheduled variants: identical work, split into stages that may be enqueued by separate calls on
+ * separate streams. Stages (sched->stages bit mask; 0 = all):
+ *   encode  COALAC_STAGE_SAMPLE  k_sample (large segments: sampled bracket)    boundaries 0 .. 1
+ *           COALAC_STAGE_SMALL   k_small  (segments of <= 4096 elements, whole) 0 .. 1
+ *           COALAC_STAGE_SCAN    k_scan   (the one HBM read of the large segments) 1 .. 2
+ *           COALAC_STAGE_SELECT  k_ghist k_gwin k_select k_emit                  2 .. 4
+ *   decode  COALAC_STAGE_BOUNDS  k_bounds                                  boundaries 0 .. 1
+ *           COALAC_STAGE_DECODE  k_decode                                  1 .. 2
+ * SAMPLE, SCAN, SELECT of one encode (and BOUNDS, DECODE of one decode) must run in this order on the
+ * same workspace; SMALL is independent of them. The caller orders them, e.g. with the events below.
+ * (A whole encode places the small segments itself: beside k_scan on the plan's side stream for big
+ * batches, inside k_scan otherwise.) At every boundary an enqueued stage starts or ends at, the call first makes
+ * `stream` wait for wait[i] (hipStreamWaitEvent; an event another stream recorded) and then records
+ * record[i] (hipEventRecord). Boundaries are those of the _ev variants (encode 0..4, decode 0..2).
+ * This lets a host pipeline independent batches over two streams: the HBM-streaming kernels (k_scan,
+ * k_decode) back to back on one, the latency-bound ones beside them on the other
+ * (coala_amd/compression/pipeline.py). NULL entries are skipped; sched == NULL is the plain call. */
+enum {
+  COALAC_STAGE_SAMPLE = 1,
+  COALAC_STAGE_SCAN = 2,
+  COALAC_STAGE_SELECT = 4,
+  COALAC_STAGE_SMALL = 8,
+  COALAC_STAGE_BOUNDS = 1,
+  COALAC_STAGE_DECODE = 2
+};
+typedef struct coalac_sched {
+  void* wait[5];
+  void* record[5];
+  unsigned stages;
+} coalac_sched_t;
+int coalac_encode_sched(coalac_plan_t plan, const float* d_in, const float* d_base, int32_t* d_idx,
+                        void* d_vals, float* d_mn, float* d_scale, void* d_ws, uint64_t ws_bytes,
+                        unsigned flags, void* stream, const coalac_sched_t* sched);
+int coalac_decode_sched(coalac_plan_t plan, const int32_t* d_idx, const void* d_vals, const float* d_mn,
+                        const float* d_scale, const float* d_base, float* d_out, void* d_ws,
+                        uint64_t ws_bytes, void* stream, const coalac_sched_t* sched);
+
 /* Fused server-side decode + FedAvg of the `clients` updates the plan batches.
  * Replaces, on the server, decompression of every upload (coala/server/base.py:558-560, called :376)
  * followed by strategies.federated_averaging (coala/server/strategies.py:6-29, 57-90) on the decoded

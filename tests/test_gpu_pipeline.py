@@ -1,0 +1,88 @@
+"""GPU parity of the lane pipeline (coala_amd/compression/pipeline.py): L sub-plans over contiguous
+segment ranges, on their own streams, ordered by events through coalac_encode_sched /
+coalac_decode_sched. Bar: bit-identical to the oracle (and so to a single plan), for every lane count,
+including a single client split into lanes and delta mode. Repeated steps check that the event chain
+never lets a lane read a buffer another lane is still writing."""
+import numpy as np
+import pytest
+import torch
+
+from coala_amd.compression import LanePipeline, SegmentTable
+from coala_amd.layouts import fp32_sizes
+from coala_amd.workload import synth_batch
+from oracle import codec_oracle as O
+
+pytestmark = pytest.mark.gpu
+
+
+def oracle_roundtrip(table, flat, bits, base=None):
+    segs = table.segs.astype(np.int64)
+    idx, vals, mn, sc = O.encode(flat, segs, bits, base=base)
+    dec = O.decode(idx, vals, mn, sc, segs, bits, table.span, base=base)
+    return idx, vals, mn, sc, dec
+
+
+def check(table, enc, dec, ref):
+    idx, vals, mn, sc, rdec = ref
+    np.testing.assert_array_equal(enc.idx.cpu().numpy(), idx)
+    np.testing.assert_array_equal(enc.vals.cpu().numpy().view(np.uint8), vals.view(np.uint8))
+    np.testing.assert_array_equal(enc.mn.cpu().numpy().view(np.uint32), mn.view(np.uint32))
+    np.testing.assert_array_equal(enc.scale.cpu().numpy().view(np.uint32), sc.view(np.uint32))
+    d = dec.cpu().numpy()
+    for (off, n, k, oo) in table.segs.astype(np.int64):
+        np.testing.assert_array_equal(d[off:off + n].view(np.uint32), rdec[off:off + n].view(np.uint32))
+
+
+@pytest.mark.parametrize("lanes", [1, 2, 3, 4])
+@pytest.mark.parametrize("delta", [False, True])
+@pytest.mark.parametrize("fused", [False, True])
+def test_pipeline_resnet18_x2(cuda, lanes, delta, fused):
+    t = SegmentTable(fp32_sizes("resnet18"), 0.01, 2)
+    flat = synth_batch(t, cuda, client_ids=[5, 6])
+    base = synth_batch(t, cuda, client_ids=[50, 60]) if delta else None
+    pipe = LanePipeline(t, 8, lanes=lanes, device=cuda)
+    assert pipe.n_lanes == lanes
+    if fused:
+        enc, dec = pipe.roundtrip(flat, base=base)
+    else:
+        enc = pipe.encode(flat, base=base)
+        dec = pipe.decode(enc, base=base)
+    torch.cuda.synchronize()
+    ref = oracle_roundtrip(t, flat.cpu().numpy(), 8, None if base is None else base.cpu().numpy())
+    check(t, enc, dec, ref)
+    assert pipe.fallbacks() == 0
+
+
+@pytest.mark.parametrize("bits", [4, 32])
+def test_pipeline_single_client_split(cuda, bits):
+    """One client's update cut into 3 lanes by segment ranges (idx / vals shared, mn / scale sliced)."""
+    t = SegmentTable(fp32_sizes("vit_b16"), 0.02, 1)
+    flat = synth_batch(t, cuda, client_ids=[9])
+    pipe = LanePipeline(t, bits, lanes=3, device=cuda)
+    enc = pipe.encode(flat)
+    dec = pipe.decode(enc)
+    torch.cuda.synchronize()
+    check(t, enc, dec, oracle_roundtrip(t, flat.cpu().numpy(), bits))
+
+
+def test_pipeline_repeated_steps_stable(cuda):
+    """Five back-to-back encode+decode steps into the same buffers on 4 lanes: every step's result equals
+    the first (a missing cross-lane dependency would let decode read idx/vals mid-write)."""
+    t = SegmentTable(fp32_sizes("resnet50_tv"), 0.01, 4)
+    flat = synth_batch(t, cuda)
+    pipe = LanePipeline(t, 8, lanes=4, device=cuda)
+    enc, out = pipe.empty_encoded(), pipe.empty_flat()
+    pipe.roundtrip(flat, enc=enc, out=out)
+    torch.cuda.synchronize()
+    first = (enc.idx.clone(), enc.vals.clone(), out.clone())
+    for _ in range(5):
+        pipe.roundtrip(flat, enc=enc, out=out)
+    torch.cuda.synchronize()
+    assert torch.equal(first[0], enc.idx) and torch.equal(first[1], enc.vals) and torch.equal(first[2], out)
+    # and against the oracle, client 0 only (seconds on the CPU)
+    t1 = SegmentTable(fp32_sizes("resnet50_tv"), 0.01, 1)
+    S, K = t1.span_per_client, t1.total_k_per_client
+    idx, vals, mn, sc, rdec = oracle_roundtrip(t1, flat[:S].cpu().numpy(), 8)
+    np.testing.assert_array_equal(enc.idx[:K].cpu().numpy(), idx)
+    np.testing.assert_array_equal(enc.vals[:K].cpu().numpy(), vals)
+    np.testing.assert_array_equal(out[:S].cpu().numpy().view(np.uint32), rdec.view(np.uint32))

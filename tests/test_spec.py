@@ -63,3 +63,31 @@ def test_constants_mirror_kernel():
     src = open(__import__("coala_amd._build", fromlist=["SRC"]).SRC).read()
     assert f"constexpr uint32_t SMALL_MAX = {spec.SMALL_MAX};" in src
     assert f"constexpr uint32_t UNIT = {spec.UNIT};" in src
+
+
+@pytest.mark.parametrize("lanes", [1, 2, 3, 4, 8])
+@pytest.mark.parametrize("name,clients", [("resnet50_tv", 16), ("resnet50_tv", 1), ("vit_b16", 2), ("lenet", 1)])
+def test_split_lanes_contiguous_balanced(name, clients, lanes):
+    """Lane ranges tile [0, T) in order, never empty, and (with many segments) each lane holds about
+    1/L of the elements."""
+    from coala_amd.compression import split_lanes
+    t = SegmentTable(fp32_sizes(name), 0.01, clients)
+    sizes = t.segs[:, 1].astype(np.int64)
+    r = split_lanes(sizes.tolist(), lanes)
+    assert r[0][0] == 0 and r[-1][1] == len(sizes)
+    assert all(a < b for a, b in r) and all(r[i][1] == r[i + 1][0] for i in range(len(r) - 1))
+    assert len(r) <= lanes
+    if len(sizes) >= 16 * lanes and max(sizes) * lanes * 4 <= sizes.sum():
+        assert len(r) == lanes
+        share = np.array([sizes[a:b].sum() for a, b in r]) / sizes.sum()
+        assert share.max() <= 1.0 / lanes + max(sizes) / sizes.sum() + 1e-9
+
+
+def test_subtable_extents():
+    from coala_amd.compression import SubTable
+    t = SegmentTable([10, 5000, 70], 0.1, 2)
+    sub = SubTable(t.segs[2:5])
+    assert sub.n_segments == 3
+    assert sub.total_k == int(t.segs[4, 3] + t.segs[4, 2])
+    assert sub.span == int(t.segs[4, 0] + t.segs[4, 1])
+    assert sub.n_elements == int(t.segs[2:5, 1].sum())
