@@ -42,6 +42,7 @@ def parse():
                    help="pipeline lanes per GPU (coala_amd/compression/pipeline.py): the batch's segments "
                         "cut into this many contiguous ranges, one HIP stream each, streaming kernels "
                         "serialised across lanes")
+    p.add_argument("--c-priority", type=int, default=-1, help="stream priority of the latency-stage streams")
     p.add_argument("--flags", type=int, default=0, help="coalac encode flags (test hooks; 0 for the bench)")
     p.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline time budget")
     p.add_argument("--no-cpu-baseline", action="store_true")
@@ -126,7 +127,7 @@ def main():
     ids = range(rank * a.clients, (rank + 1) * a.clients)
     flat = synth_batch(t, dev, client_ids=ids)
     base = synth_batch(t, dev, client_ids=[10_000 + i for i in ids]) if a.mode == "delta" else None
-    pipe = LanePipeline(t, a.bits, lanes=a.lanes, device=dev, flags=a.flags)
+    pipe = LanePipeline(t, a.bits, lanes=a.lanes, device=dev, flags=a.flags, c_priority=a.c_priority)
     enc, out = pipe.empty_encoded(), pipe.empty_flat()
     torch.cuda.synchronize()
 

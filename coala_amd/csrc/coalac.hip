@@ -63,7 +63,8 @@ constexpr uint32_t UNIT_SHIFT = 12;
 constexpr uint32_t UNIT_IT = UNIT / 256;  // float4 loads per lane per unit
 constexpr uint32_t SMALL_MAX = 4096;      // segments up to this size are encoded whole in one block
 constexpr uint32_t SAMPLE_MAX = 8192;     // sampled keys per large segment
-constexpr int SEL_NT = 512;               // threads of a k_select block
+constexpr int SEL_NT = 256;               // threads of a k_select block (4 waves: one per SIMD, so a
+                                          // block finds room beside a streaming kernel's waves)
 constexpr uint32_t STAGE_CAP = 512;       // candidate records staged in LDS per k_scan wave
 constexpr uint32_t GU = 32;               // units per select group (k_ghist / k_gwin block)
 constexpr uint32_t HB2 = 512;             // bins of the per-group band histograms
@@ -824,7 +825,7 @@ DEV void select_generic(const Params& P, uint32_t lb, uint32_t nu, uint32_t tlo,
     for (uint32_t c0 = 0; c0 < nu; c0 += UCAP) {
       const uint32_t cn = min(UCAP, nu - c0);
       const uint32_t total = chunk_prefix<NT>(P.cntC + lb + c0, cn, S.upre, S.sh);
-      unit_sweep<NW, 16>(
+      unit_sweep<NW, 4>(
           P.cand, lb + c0, S.upre, cn, total,
           [&](float x, bool valid, uint32_t) {
             if (valid) f(fkey(x));
@@ -851,7 +852,7 @@ DEV void select_generic(const Params& P, uint32_t lb, uint32_t nu, uint32_t tlo,
     }
     const uint32_t total = chunk_prefix<NT>(P.cntC + lb + c0, cn, S.upre, S.sh);
     uint32_t weq = 0, wfp = NONE, wfn = NONE, ug = 0, ue = 0;  // wave-uniform
-    unit_sweep<NW, 16>(
+    unit_sweep<NW, 4>(
         P.cand, lb + c0, S.upre, cn, total,
         [&](float x, bool valid, uint32_t) {
           const uint32_t key = fkey(x);
@@ -1384,18 +1385,22 @@ __global__ __launch_bounds__(BLOCK) void k_decode(Params P) {
     const float* bs = HASBASE ? P.base + U[r].off : nullptr;
     float* out = P.out + U[r].off;
     float4 b[UNIT_IT];
+    if (!HASBASE || full) {
 #pragma unroll
-    for (uint32_t it = 0; it < UNIT_IT; ++it) {
-      const uint32_t e = (it * 64 + lane) * 4;
-      if (!HASBASE) {
-        b[it] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-      } else if (full || e + 3 < len) {
-        b[it] = *reinterpret_cast<const float4*>(bs + e);
-      } else {
-        b[it].x = e + 0 < len ? bs[e + 0] : 0.0f;
-        b[it].y = e + 1 < len ? bs[e + 1] : 0.0f;
-        b[it].z = e + 2 < len ? bs[e + 2] : 0.0f;
-        b[it].w = 0.0f;
+      for (uint32_t it = 0; it < UNIT_IT; ++it)
+        b[it] = HASBASE ? *reinterpret_cast<const float4*>(bs + (it * 64 + lane) * 4) : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    } else {
+#pragma unroll
+      for (uint32_t it = 0; it < UNIT_IT; ++it) {
+        const uint32_t e = (it * 64 + lane) * 4;
+        if (e + 3 < len) {
+          b[it] = *reinterpret_cast<const float4*>(bs + e);
+        } else {
+          b[it].x = e + 0 < len ? bs[e + 0] : 0.0f;
+          b[it].y = e + 1 < len ? bs[e + 1] : 0.0f;
+          b[it].z = e + 2 < len ? bs[e + 2] : 0.0f;
+          b[it].w = 0.0f;
+        }
       }
     }
     uint64_t kept = 0;
@@ -1407,23 +1412,34 @@ __global__ __launch_bounds__(BLOCK) void k_decode(Params P) {
       const float v2 = code_value<RAW>(load_code<RAW>(P, e), mn[r], sc[r]);
       merge_entries<HASBASE>(b, kept, p2, v2, min(hi[r] - e0, 64u), lane);
     }
+    if (HASBASE) {
 #pragma unroll
-    for (uint32_t it = 0; it < UNIT_IT; ++it) {
-      if (HASBASE) {  // base + 0.0f where nothing was kept (-0 -> +0, as the oracle's base + dense)
-        const uint32_t m = (uint32_t)(kept >> (it * 4)) & 15u;
+      for (uint32_t it = 0; it < UNIT_IT; ++it) {  // base + 0.0f where nothing was kept (-0 -> +0, as the
+        const uint32_t m = (uint32_t)(kept >> (it * 4)) & 15u;  // oracle's base + dense)
         b[it].x = (m & 1u) ? b[it].x : b[it].x + 0.0f;
         b[it].y = (m & 2u) ? b[it].y : b[it].y + 0.0f;
         b[it].z = (m & 4u) ? b[it].z : b[it].z + 0.0f;
         b[it].w = (m & 8u) ? b[it].w : b[it].w + 0.0f;
       }
-      const uint32_t e = (it * 64 + lane) * 4;
-      if (full || e + 3 < len) {
+    }
+    if (full) {  // wave-uniform: a full unit is one straight run of 16 non-temporal float4 stores per lane
+#pragma unroll
+      for (uint32_t it = 0; it < UNIT_IT; ++it) {
         const f4v t = {b[it].x, b[it].y, b[it].z, b[it].w};
-        __builtin_nontemporal_store(t, reinterpret_cast<f4v*>(out + e));
-      } else if (e < len) {  // the partial unit's last 1-3 elements (entries at pos >= len were never
-        out[e] = b[it].x;    // merged: merge_entries only visits rows of the sorted list in order)
-        if (e + 1 < len) out[e + 1] = b[it].y;
-        if (e + 2 < len) out[e + 2] = b[it].z;
+        __builtin_nontemporal_store(t, reinterpret_cast<f4v*>(out + (it * 64 + lane) * 4));
+      }
+    } else {
+#pragma unroll
+      for (uint32_t it = 0; it < UNIT_IT; ++it) {
+        const uint32_t e = (it * 64 + lane) * 4;
+        if (e + 3 < len) {
+          const f4v t = {b[it].x, b[it].y, b[it].z, b[it].w};
+          __builtin_nontemporal_store(t, reinterpret_cast<f4v*>(out + e));
+        } else if (e < len) {  // the partial unit's last 1-3 elements (entries at pos >= len were never
+          out[e] = b[it].x;    // merged: merge_entries only visits rows of the sorted list in order)
+          if (e + 1 < len) out[e + 1] = b[it].y;
+          if (e + 2 < len) out[e + 2] = b[it].z;
+        }
       }
     }
   }
