@@ -25,7 +25,9 @@ sys.path.insert(0, ROOT)
 
 METRIC = "encode+decode GB/s over fp32 weight updates (device-resident), 1/2/4/8 GPU"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md: 8.0 TB/s)
-LANES = 2  # default pipeline lanes per GPU
+LANES = 1  # default pipeline lanes per GPU (2-3 lanes measured equal or slower: the latency-bound stages
+           # of one lane slow the other lane's streaming kernel by as much as they overlap it)
+EVENT_EVERY = 4  # timing events on every 4th timed step (each recorded event adds a ~4 us dispatch gap)
 
 
 def parse():
@@ -43,6 +45,8 @@ def parse():
                         "cut into this many contiguous ranges, one HIP stream each, streaming kernels "
                         "serialised across lanes")
     p.add_argument("--c-priority", type=int, default=-1, help="stream priority of the latency-stage streams")
+    p.add_argument("--event-every", type=int, default=EVENT_EVERY,
+                   help="record the per-kernel timing events on every Nth timed step (1 = every step)")
     p.add_argument("--flags", type=int, default=0, help="coalac encode flags (test hooks; 0 for the bench)")
     p.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline time budget")
     p.add_argument("--no-cpu-baseline", action="store_true")
@@ -86,12 +90,16 @@ def cpu_baseline(layout, ratio, bits, budget_s):
     t = SegmentTable(sizes, ratio, 1)
     segs = t.segs.astype(np.int64)
     N = sum(sizes)
-    done, el = 0, 0.0
-    while el < budget_s and done < 64:
-        rng = np.random.default_rng(1234 + done)
+    flats = []  # 4 distinct synthetic updates, cycled (generating one costs more than coding it)
+    for c in range(4):
+        rng = np.random.default_rng(1234 + c)
         flat = np.zeros(t.span, np.float32)
         for off, n in zip(t.offsets, sizes):
             flat[off:off + n] = rng.standard_normal(n, dtype=np.float32) * np.float32(10 ** rng.uniform(-4, -2))
+        flats.append(flat)
+    done, el = 0, 0.0
+    while el < budget_s and done < 1000:
+        flat = flats[done % len(flats)]
         t0 = time.perf_counter()
         idx, vals, mn, sc = O.encode(flat, segs, bits)
         O.decode(idx, vals, mn, sc, segs, bits, t.span)
@@ -154,8 +162,10 @@ def main():
                 ev[1] = make_events(torch, 1)[0]
             evs.append(ev)
         return evs
-    ev_e = [lane_events(5) for _ in range(a.steps)]
-    ev_d = [lane_events(3) for _ in range(a.steps)]
+    every = max(1, a.event_every)
+    timed_steps = [i for i in range(a.steps) if i % every == 0]
+    ev_e = [lane_events(5) if i % every == 0 else None for i in range(a.steps)]
+    ev_d = [lane_events(3) if i % every == 0 else None for i in range(a.steps)]
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -172,7 +182,8 @@ def main():
         dist.all_reduce(x, op=dist.ReduceOp.MAX)
         el = x.item()
 
-    # Per-kernel mean durations (ms per launch, averaged over lanes and steps) from the HIP events each
+    # Per-kernel mean durations (ms per launch, averaged over lanes and the event-carrying steps of the
+    # timed region, every `--event-every`th one) from the HIP events each
     # lane records on its own stream at the stage boundaries. With several lanes a stage's interval can
     # include co-running latency-bound kernels of other lanes (never another streaming kernel: the
     # pipeline serialises k_scan / k_decode across lanes), i.e. it is the kernel's wall-clock time.
@@ -181,7 +192,7 @@ def main():
     stages = {}
     for name, which in {"k_scan": ev_e, "k_decode": ev_d}.items():
         stages[name] = mean([(lanes[li][1] if li == 0 else lanes[li - 1][2], lanes[li][2])
-                             for lanes in which for li in range(pipe.n_lanes)])
+                             for lanes in (which[i] for i in timed_steps) for li in range(pipe.n_lanes)])
     N, K, T = t.n_elements, t.total_k, t.n_segments
     delta = a.mode == "delta"
     vb = 4 if a.bits == 32 else 1
@@ -217,6 +228,8 @@ def main():
                               "achieved_GBs": round(step_alg / (step_ms * 1e-3) / 1e9, 1),
                               "frac": round(step_alg / (step_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)},
             "stages_ms": {k: round(v, 4) for k, v in stages.items()},
+            "stage_timing": f"HIP events on the pipeline stream around k_scan / k_decode, {len(timed_steps)} of "
+                            f"the {a.steps} timed steps",
             "sample_fallbacks": fallbacks,
         }
         if world == 1 and not a.no_cpu_baseline:
