@@ -106,8 +106,9 @@ class CompressedUpdate:
     def nbytes(self):
         h = self.header
         vb = 4 if h["bits"] == RAW_BITS else 1
+        ib = 0 if h["ratio"] >= 1.0 else 4  # ratio 1: indices implied, not shipped (wire.py "dense")
         raw_b = sum(t.numel() * t.element_size() for t in self.raw.values())
-        return 8 * h["n_segments"] + (4 + vb) * h["total_k"] + raw_b
+        return 8 * h["n_segments"] + (ib + vb) * h["total_k"] + raw_b
 
     def parameters(self):
         """One meta tensor whose numel * 32 bit equals the payload size, so the reference's
@@ -127,6 +128,8 @@ class CompressedUpdate:
                 pos += len(b)
             raw_entries.append(e)
         h["entries"] = raw_entries
+        if h["ratio"] >= 1.0:
+            h["dense"] = True
         enc = self.encoded
         return wire.pack(h, enc.mn.cpu().numpy(), enc.scale.cpu().numpy(), enc.idx.cpu().numpy(),
                          enc.vals.cpu().numpy(), b"".join(chunks))
@@ -221,9 +224,10 @@ class UpdateCodec:
         return p
 
     # -- encode -----------------------------------------------------------------------------------
-    def encode(self, state, base=None):
-        """state_dict -> CompressedUpdate. `base` (delta mode): FlatState of w_global (same layout)."""
-        fs = flatten_state(state)
+    def encode(self, state, base=None, device=None):
+        """state_dict -> CompressedUpdate. `base` (delta mode): FlatState of w_global (same layout).
+        `device`: where to flatten and encode (default: where the state lives)."""
+        fs = flatten_state(state, device=device)
         if self.mode == "delta" and base is None:
             raise ValueError("delta mode needs the global-model snapshot (base)")
         sizes = [e["n"] for e in fs.entries if e["kind"] == "seg"]

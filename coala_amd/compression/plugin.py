@@ -8,6 +8,8 @@ The reference exposes compression only as no-op hooks that users override in sub
     BaseServer.compression(self) -> None            coala/server/base.py:347-349   (called :196)
     BaseServer.decompression(self, model) -> model  coala/server/base.py:558-560   (called :376,
                                                     server/service.py:106,125)
+    plus BaseServer.aggregation() / aggregation_test() (server/base.py:562-571, test path :265-267), which
+    the server mixin wraps to put the real global model back after a compressed download.
 
 Usage (drop-in, nothing else in COALA changes):
 
@@ -30,12 +32,19 @@ Behaviour:
     + decoded delta, fused in the decode kernel); anything else (plain modules, splitFL feature dicts,
     server/service.py:124-131) passes through unchanged. Safe to call from several threads
     (server/service.py:74 spawns one per upload).
+  * download direction (opt-in, `codec_download = True`): server compression()
+    encodes the global model once per round into a CompressedModel (download.py) that stands where the
+    global module stood during distribution; aggregation() restores the real module first. Client
+    decompression() turns a received CompressedModel into a real module (later rounds decode inside
+    set_model's load_state_dict). Delta-mode uploads are decoded against the server's reconstruction of
+    its own download, which is bit-identical to what the clients decoded.
 """
 import threading
 
 from torch import nn
 
 from .codec import CompressedUpdate, UpdateCodec
+from .download import CompressedModel, compress_model
 
 EQUAL_AVERAGE = "equal"                     # coala/server/base.py:37
 AGGREGATION_CONTENT_PARAMS = "parameters"   # coala/server/base.py:40
@@ -63,9 +72,21 @@ class _CodecOwner:
 class CompressionClientMixin(_CodecOwner):
     """Mix in before coala's BaseClient: `class Client(CompressionClientMixin, BaseClient)`."""
 
+    def set_model(self, model):
+        # a compressed download decodes with this client's codec backend (inside the reference's
+        # set_model: load_state_dict(model.state_dict()), client/base.py:197-201)
+        if isinstance(model, CompressedModel):
+            model.bind(self._codec().backend)
+        parent = getattr(super(), "set_model", None)
+        if parent is not None:
+            return parent(model)
+        self.model = model
+
     def decompression(self):
         if getattr(self, "model", None) is None:
             return
+        if isinstance(self.model, CompressedModel):  # compressed download, first round (set_model deepcopy)
+            self.model = self.model.materialize()
         if isinstance(self.model, nn.Module) and self._codec().mode == "delta":
             self._codec_base = self._codec().snapshot(self.model)
 
@@ -99,12 +120,68 @@ class CompressionClientMixin(_CodecOwner):
 class CompressionServerMixin(_CodecOwner):
     """Mix in before coala's BaseServer: `class Server(CompressionServerMixin, BaseServer)`."""
 
+    codec_download = False        # compress the distributed global model (download direction)
+    codec_download_ratio = 1.0    # dense: indices implied (wire.py "dense")
+    codec_download_bits = 8
+
+    def _download_codec(self):
+        c = self.__dict__.get("_download_update_codec")
+        if c is None:
+            c = UpdateCodec(self.codec_download_ratio, self.codec_download_bits, "weights", self.codec_backend)
+            self.__dict__["_download_update_codec"] = c
+        return c
+
+    def _real_global(self):
+        """The global nn.Module, also while a CompressedModel stands in for it during distribution."""
+        g = self.__dict__.get("_codec_global")
+        return g if g is not None else self.model
+
+    @staticmethod
+    def _stamp(module, state):
+        # storage address + version counter (state_dict() returns fresh detached views each call, which
+        # share the parameter's storage and version counter)
+        return (id(module), tuple((t.data_ptr(), t._version) for t in state.values()))
+
+    def _restore_global(self):
+        g = self.__dict__.pop("_codec_global", None)
+        if g is not None:
+            self.model = g
+
+    def compression(self):
+        if not self.codec_download:
+            parent = getattr(super(), "compression", None)
+            return parent() if parent is not None else None
+        self._restore_global()
+        g = self.model
+        carrier = compress_model(g, self._download_codec())
+        # what every client will decode: base of their delta-mode uploads (kept until the global changes)
+        recon = self._codec().snapshot(carrier.decoded_state())
+        self.__dict__["_codec_recon"] = (self._stamp(g, g.state_dict()), recon)
+        self.__dict__["_codec_global"] = g
+        self.model = carrier
+
+    def aggregation(self):
+        self._restore_global()
+        parent = getattr(super(), "aggregation", None)
+        return parent() if parent is not None else None
+
+    def aggregation_test(self):
+        self._restore_global()
+        parent = getattr(super(), "aggregation_test", None)
+        return parent() if parent is not None else None
+
     def _global_snapshot(self):
-        """Flat fp32 copy of the current global model, rebuilt only when its tensors changed."""
+        """Flat fp32 copy of the global model the clients started from: the reconstruction of the
+        compressed download when there was one, else the global model itself (rebuilt only when its
+        tensors changed)."""
         lock = self.__dict__.setdefault("_codec_lock", threading.Lock())
         with lock:
-            state = self.model.state_dict()
-            stamp = (id(self.model), tuple((id(t), t._version) for t in state.values()))
+            g = self._real_global()
+            state = g.state_dict()
+            stamp = self._stamp(g, state)
+            recon = self.__dict__.get("_codec_recon")
+            if recon is not None and recon[0] == stamp:
+                return recon[1]
             snap = self.__dict__.get("_codec_snapshot")
             if snap is None or snap[0] != stamp:
                 snap = (stamp, self._codec().snapshot(state))
@@ -115,7 +192,7 @@ class CompressionServerMixin(_CodecOwner):
 
     def _decode_upload(self, model):
         base = self._global_snapshot() if model.header["mode"] == "delta" else None
-        return self._codec().decode_module(model, self.model, base=base)
+        return self._codec().decode_module(model, self._real_global(), base=base)
 
     def decompression(self, model):
         if isinstance(model, CompressedUpdate):
@@ -143,7 +220,7 @@ class CompressionServerMixin(_CodecOwner):
                 dev = base.flat.device if base is not None and base.flat is not None else \
                     codec.backend.default_device()
                 mode = "div" if dev.type == "cpu" else "recip"  # torch's division semantics on that device
-                return codec.aggregate(models, weights, self.model, base=base, mode=mode)
+                return codec.aggregate(models, weights, self._real_global(), base=base, mode=mode)
         models = [self._decode_upload(m) if isinstance(m, CompressedUpdate) else m for m in models]
         parent = getattr(super(), "aggregate", None)
         if parent is not None:

@@ -14,6 +14,9 @@ Layout (little-endian):
                    | {"name", "dtype", "shape", "kind": "raw", "off", "nbytes"}
     then, each section starting at a 16-byte boundary:
          mn f32[T] | scale f32[T] | idx i32[K] | vals (u8[K], or f32[K] if bits == 32) | raw bytes
+    A header with "dense": true (ratio 1: every segment keeps all n elements, idx = 0..n-1 per segment)
+    carries an empty idx section; unpack regenerates it. This is the download-direction default
+    (dense 8-bit weights, ~4x smaller than fp32 instead of 5 B per element with explicit indices).
 """
 import json
 import struct
@@ -28,8 +31,18 @@ def _pad16(n):
     return (16 - n % 16) % 16
 
 
+def dense_idx(header):
+    """idx of a dense (ratio 1) update: 0..n-1 for every fp32 segment, in segment order."""
+    ns = [int(e["n"]) for e in sorted((e for e in header["entries"] if e["kind"] == "seg"), key=lambda e: e["seg"])]
+    if not ns:
+        return np.zeros(0, dtype=np.int32)
+    return np.concatenate([np.arange(n, dtype=np.int32) for n in ns])
+
+
 def pack(header, mn, scale, idx, vals, raw):
-    """numpy arrays + raw bytes -> blob (bytes)."""
+    """numpy arrays + raw bytes -> blob (bytes). A "dense" header drops idx (it is implied)."""
+    if header.get("dense"):
+        idx = np.zeros(0, dtype=np.int32)
     h = json.dumps(header, separators=(",", ":"), sort_keys=True).encode()
     parts = [MAGIC, struct.pack("<II", VERSION, len(h)), h]
     size = 16 + len(h)
@@ -59,10 +72,15 @@ def unpack(blob):
     vdt = np.dtype("<f4") if int(header["bits"]) == 32 else np.dtype("u1")
     pos = 16 + hl
     out = []
-    for dt, n in ((np.dtype("<f4"), T), (np.dtype("<f4"), T), (np.dtype("<i4"), K), (vdt, K)):
+    dense = bool(header.get("dense"))
+    for dt, n in ((np.dtype("<f4"), T), (np.dtype("<f4"), T), (np.dtype("<i4"), 0 if dense else K), (vdt, K)):
         pos += _pad16(pos)
         out.append(np.frombuffer(mv, dtype=dt, count=n, offset=pos))
         pos += n * dt.itemsize
     pos += _pad16(pos)
     raw = bytes(mv[pos:])
+    if dense:
+        out[2] = dense_idx(header)
+        if out[2].size != K:
+            raise ValueError("COALAQ1: dense header with k != n")
     return (header, *out, raw)

@@ -114,11 +114,17 @@ class LoopbackClient:
 
 
 class LoopbackServer:
-    def __init__(self, model, clients):
+    """remote=True distributes the way remote training does: `codec.marshal(self.model)` per client
+    (server/base.py:397) and the client unpickles it (client/service.py), instead of handing the object
+    over as local training does (server/base.py:373)."""
+
+    def __init__(self, model, clients, remote=False):
         self.model = model
         self.clients = clients
+        self.remote = remote
         self.uploaded = {}
         self.weights = {}
+        self.download_sizes = []
 
     def compression(self):
         pass
@@ -126,17 +132,29 @@ class LoopbackServer:
     def decompression(self, model):
         return model
 
-    def round(self, round_id):
+    def round(self, round_id):  # server/base.py:190-201: compression -> distribution -> aggregation
         self.compression()
+        self.distribution_to_train(round_id)
+        self.aggregation()
+        return self.model
+
+    def distribution_to_train(self, round_id):  # server/base.py:363-381 (local) / :383-410 (remote)
         self.uploaded, self.weights = {}, {}
         for c in self.clients:
-            req = c.run_train(self.model, round_id)
+            if self.remote:
+                data = marshal(self.model)
+                self.download_sizes.append(len(data))
+                sent = unmarshal(data)
+            else:
+                sent = self.model
+            req = c.run_train(sent, round_id)
             model = self.decompression(unmarshal(req.content.data))
             self.uploaded[c.cid] = model
             self.weights[c.cid] = req.content.data_size
+
+    def aggregation(self):  # server/base.py:562-571
         agg = self.aggregate(list(self.uploaded.values()), list(self.weights.values()))
         self.model.load_state_dict(agg.state_dict())  # set_model(load_dict=True), server/base.py:571
-        return self.model
 
     def aggregate(self, models, weights):  # server/base.py:573-601, non-distributed "all" branch
         return federated_averaging(models, weights)

@@ -1,0 +1,153 @@
+"""Download direction on CPU: server compression() -> CompressedModel carrier ->
+client set_model / decompression(), inside the loopback loop that mirrors the reference's
+compression -> distribution -> aggregation order (coala/server/base.py:190-201, 363-410; client
+base.py:138-141,191-205). The CPU oracle is the injected backend (the checker; the product has no CPU
+path). Parity of the decoded global model is against the oracle's own encode/decode of each tensor."""
+import copy
+import pickle
+
+import numpy as np
+import pytest
+import torch
+from torch import nn
+
+from coala_amd.compression import CompressedModel, CompressedUpdate, CompressionClientMixin, \
+    CompressionServerMixin, UpdateCodec, compress_model, skeleton_of
+from coala_amd.fl import LoopbackClient, LoopbackServer, federated_averaging
+from coala_amd.layouts import build_module
+from oracle import codec_oracle as O
+from tests.oracle_backend import OracleBackend
+
+
+def make_classes(ratio, bits, mode, down_ratio=1.0, down_bits=8):
+    class Client(CompressionClientMixin, LoopbackClient):
+        codec_ratio, codec_bits, codec_mode, codec_backend = ratio, bits, mode, OracleBackend()
+
+    class Server(CompressionServerMixin, LoopbackServer):
+        codec_ratio, codec_bits, codec_mode, codec_backend = ratio, bits, mode, OracleBackend()
+        codec_download, codec_download_ratio, codec_download_bits = True, down_ratio, down_bits
+
+    return Client, Server
+
+
+def oracle_weights_roundtrip(state, ratio, bits):
+    """Per fp32 tensor: oracle decode(encode(w)) in weights mode; other dtypes unchanged."""
+    out = {}
+    for name, w in state.items():
+        if w.dtype != torch.float32 or w.numel() == 0:
+            out[name] = w.clone()
+            continue
+        x = w.reshape(-1).numpy()
+        idx, q, mn, sc = O.encode_segment(x, O.k_for(x.size, ratio), bits)
+        out[name] = torch.from_numpy(O.decode_segment(idx, q, mn, sc, x.size, bits)).view(w.shape)
+    return out
+
+
+def _bits_equal(a, b):
+    assert a.dtype == b.dtype and a.shape == b.shape
+    if a.dtype == torch.float32:
+        np.testing.assert_array_equal(a.numpy().view(np.uint32), b.numpy().view(np.uint32))
+    else:
+        assert torch.equal(a, b)
+
+
+def test_dense_wire_drops_indices_and_round_trips():
+    codec = UpdateCodec(1.0, 8, "weights", OracleBackend())
+    m = build_module("lenet", seed=2)
+    up = codec.encode(m.state_dict())
+    blob = up.to_bytes()
+    n = sum(t.numel() for t in m.state_dict().values() if t.dtype == torch.float32)
+    assert len(blob) < 1.01 * n + 4096          # 1 B per element + header, no 4 B indices
+    assert up.nbytes < 1.01 * n + 64
+    back = CompressedUpdate.from_bytes(blob)
+    assert torch.equal(back.encoded.idx, up.encoded.idx.cpu())
+    for a, b in zip(codec.decode_state(back).values(), codec.decode_state(up).values()):
+        _bits_equal(a, b)
+
+
+def test_skeleton_has_no_weights_and_carrier_pickles_small():
+    m = build_module("resnet18_split_cut4", seed=1)
+    sk = skeleton_of(m)
+    assert all(t.device.type == "meta" for t in sk.state_dict().values())
+    assert all(t.device.type == "cpu" for t in m.state_dict().values())  # original untouched
+    cm = compress_model(m, UpdateCodec(1.0, 8, "weights", OracleBackend()))
+    blob = pickle.dumps(cm)
+    fp32 = sum(t.numel() * 4 for t in m.state_dict().values())
+    assert len(blob) < fp32 / 3
+    back = pickle.loads(blob).bind(OracleBackend())
+    for a, b in zip(back.state_dict().values(), cm.state_dict().values()):
+        _bits_equal(a, b)
+    with pytest.raises(RuntimeError):
+        cm(torch.zeros(1))
+
+
+@pytest.mark.parametrize("remote", [False, True])
+def test_compressed_download_round_delta_uploads(remote):
+    """8-bit dense download + delta uploads over two rounds: clients start from exactly the oracle's
+    reconstruction of the global model, the server decodes their uploads against that same base, and
+    the server keeps a real module for aggregation."""
+    Client, Server = make_classes(0.05, 8, "delta")
+    g0 = build_module("lenet", seed=7)
+    clients = [Client(f"c{i}", 5 + i, step_seed=i) for i in range(3)]
+    server = Server(copy.deepcopy(g0), clients, remote=remote)
+    for r in range(2):
+        g_before = {k: v.clone() for k, v in server.model.state_dict().items()}
+        recon = oracle_weights_roundtrip(g_before, 1.0, 8)
+        server.round(r)
+        assert isinstance(server.model, nn.Module) and not isinstance(server.model, CompressedModel)
+        for c in clients:
+            assert c.trace[:2] == ["decompression", "pre_train"]
+            # the client's delta base is the decoded download, bit for bit
+            base = c._codec_base
+            for e in base.entries:
+                if e["kind"] == "seg":
+                    got = base.flat[e["off"]:e["off"] + e["n"]].view(e["shape"])
+                    _bits_equal(got, recon[e["name"]])
+            # the server decoded this client's upload as recon + decode(encode(trained - recon))
+            up = server.uploaded[c.cid]
+            trained = c.model.state_dict()
+            for name, w in up.state_dict().items():
+                if w.dtype != torch.float32:
+                    assert torch.equal(w, trained[name])
+                    continue
+                d = (trained[name] - recon[name]).reshape(-1).numpy()
+                idx, q, mn, sc = O.encode_segment(d, O.k_for(d.size, 0.05), 8)
+                ref = recon[name].reshape(-1).numpy() + O.decode_segment(idx, q, mn, sc, d.size, 8)
+                np.testing.assert_array_equal(w.reshape(-1).numpy().view(np.uint32), ref.view(np.uint32))
+        ref_avg = federated_averaging(list(server.uploaded.values()), list(server.weights.values()))
+        for a, b in zip(ref_avg.state_dict().values(), server.model.state_dict().values()):
+            assert torch.equal(a.to(b.dtype), b)
+    if remote:
+        fp32 = sum(t.numel() * 4 for t in g0.state_dict().values())
+        assert server.download_sizes and max(server.download_sizes) < fp32 / 3
+
+
+def test_lossless_download_matches_uncompressed_run():
+    """ratio 1 / 32 bits in both directions: a compressed-download run is bit-identical to a plain one."""
+    Client, Server = make_classes(1.0, 32, "weights", down_ratio=1.0, down_bits=32)
+    g0 = build_module("resnet18_split_cut2", seed=4)
+    plain = LoopbackServer(copy.deepcopy(g0), [LoopbackClient(f"c{i}", 3 + i, step_seed=i) for i in range(3)])
+    comp = Server(copy.deepcopy(g0), [Client(f"c{i}", 3 + i, step_seed=i) for i in range(3)], remote=True)
+    for r in range(2):
+        plain.round(r)
+        comp.round(r)
+    for (k, a), (k2, b) in zip(plain.model.state_dict().items(), comp.model.state_dict().items()):
+        assert k == k2
+        _bits_equal(a, b)
+
+
+def test_download_off_is_a_no_op_and_aggregation_restores_global():
+    Client, Server = make_classes(0.05, 8, "delta")
+    Server.codec_download = False
+    g0 = build_module("lenet", seed=1)
+    s = Server(copy.deepcopy(g0), [])
+    s.compression()
+    assert not isinstance(s.model, CompressedModel)
+    Server.codec_download = True
+    s.compression()
+    assert isinstance(s.model, CompressedModel)
+    s.compression()  # twice in a row (test_in_client after train): still wraps the real module
+    assert isinstance(s._real_global(), nn.Module) and not isinstance(s._real_global(), CompressedModel)
+    s.uploaded, s.weights = {}, {}
+    s._restore_global()
+    assert not isinstance(s.model, CompressedModel)
