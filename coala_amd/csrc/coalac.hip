@@ -65,6 +65,12 @@ constexpr uint32_t SMALL_MAX = 4096;      // segments up to this size are encode
 constexpr uint32_t SAMPLE_MAX = 8192;     // sampled keys per large segment
 constexpr int SEL_NT = 256;               // threads of a k_select block (4 waves: one per SIMD, so a
                                           // block finds room beside a streaming kernel's waves)
+#ifndef SCAN_WPE
+#define SCAN_WPE 5
+#endif
+#ifndef DECODE_WPE
+#define DECODE_WPE 5
+#endif
 constexpr uint32_t STAGE_CAP = 512;       // candidate records staged in LDS per k_scan wave
 constexpr uint32_t GU = 32;               // units per select group (k_ghist / k_gwin block)
 constexpr uint32_t HB2 = 512;             // bins of the per-group band histograms
@@ -370,6 +376,42 @@ DEV int band_shift(uint32_t tlo, uint32_t thi, int bin_bits = 11) {
   return bl > bin_bits ? bl - bin_bits : 0;
 }
 
+// Buffer resource over n fp32 elements at p (gfx9 word 3; loads at byte offsets >= 4n return 0).
+DEV __amdgpu_buffer_rsrc_t unit_rsrc(const float* p, uint32_t n) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(p), (short)0, (int)(n * 4u), 0x00020000);
+}
+
+// non-temporal 16-byte buffer load (aux bit 1 = nt on gfx94x/gfx950) of x (or x - base) at byte offset
+template <bool DELTA>
+DEV float4 unit_load_x4(__amdgpu_buffer_rsrc_t rin, __amdgpu_buffer_rsrc_t rbase, uint32_t boff) {
+  typedef unsigned int u4v __attribute__((ext_vector_type(4)));
+  const u4v a = __builtin_amdgcn_raw_buffer_load_b128(rin, (int)boff, 0, 2);
+  float4 v = make_float4(__uint_as_float(a.x), __uint_as_float(a.y), __uint_as_float(a.z), __uint_as_float(a.w));
+  if (DELTA) {
+    const u4v b = __builtin_amdgcn_raw_buffer_load_b128(rbase, (int)boff, 0, 2);
+    v.x = v.x - __uint_as_float(b.x);
+    v.y = v.y - __uint_as_float(b.y);
+    v.z = v.z - __uint_as_float(b.z);
+    v.w = v.w - __uint_as_float(b.w);
+  }
+  return v;
+}
+
+// non-temporal 16-byte buffer store (dropped when it lies past the resource's range)
+DEV void unit_store_x4(__amdgpu_buffer_rsrc_t r, uint32_t boff, float4 v) {
+  typedef unsigned int u4v __attribute__((ext_vector_type(4)));
+  const u4v a = {__float_as_uint(v.x), __float_as_uint(v.y), __float_as_uint(v.z), __float_as_uint(v.w)};
+  __builtin_amdgcn_raw_buffer_store_b128(a, r, (int)boff, 0, 2);
+}
+
+// the same 16 bytes as four dword stores: the range check drops exactly the dwords past the end
+DEV void unit_store_x1x4(__amdgpu_buffer_rsrc_t r, uint32_t boff, float4 v) {
+  __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v.x), r, (int)boff, 0, 2);
+  __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v.y), r, (int)boff + 4, 0, 2);
+  __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v.z), r, (int)boff + 8, 0, 2);
+  __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v.w), r, (int)boff + 12, 0, 2);
+}
+
 // non-temporal (read-once) 16-byte load of x (or x - base)
 template <bool DELTA>
 DEV float4 load_x4_nt(const Params& P, uint64_t off) {
@@ -418,26 +460,15 @@ DEV void scan_unit(const Params& P, uint32_t lu, const UnitDev& L, uint32_t tlo,
   const uint64_t off = L.off;
   uint2* R = P.cand + (uint64_t)lu * UNIT;
   uint32_t cC = 0, cA = 0;
+  // buffer resources over exactly this unit: one shared lane offset for all loads (constant offsets
+  // fold into the instruction), and loads past len return 0 — no separate partial-unit path
+  const __amdgpu_buffer_rsrc_t rin = unit_rsrc(P.in + off, len);
+  const __amdgpu_buffer_rsrc_t rbase = unit_rsrc(DELTA ? P.base + off : P.in + off, len);
 
   for (uint32_t nb = 0; nb < (uint32_t)NB; ++nb) {
     float4 v[IT];
-    if (len == UNIT) {
 #pragma unroll
-      for (uint32_t i = 0; i < IT; ++i) v[i] = load_x4_nt<DELTA>(P, off + ((nb * IT + i) * 64 + lane) * 4);
-    } else {
-#pragma unroll
-      for (uint32_t i = 0; i < IT; ++i) {
-        const uint32_t e = ((nb * IT + i) * 64 + lane) * 4;
-        if (e + 3 < len) {
-          v[i] = load_x4<DELTA>(P, off + e);
-        } else {
-          v[i].x = e + 0 < len ? load_x1<DELTA>(P, off + e + 0) : 0.0f;
-          v[i].y = e + 1 < len ? load_x1<DELTA>(P, off + e + 1) : 0.0f;
-          v[i].z = e + 2 < len ? load_x1<DELTA>(P, off + e + 2) : 0.0f;
-          v[i].w = e + 3 < len ? load_x1<DELTA>(P, off + e + 3) : 0.0f;
-        }
-      }
-    }
+    for (uint32_t i = 0; i < IT; ++i) v[i] = unit_load_x4<DELTA>(rin, rbase, ((nb * IT + i) * 64 + lane) * 16);
 #pragma unroll
     for (uint32_t i = 0; i < IT; ++i) {
       const uint32_t e0 = ((nb * IT + i) * 64 + lane) * 4;
@@ -706,7 +737,7 @@ __global__ __launch_bounds__(BLOCK) void k_sample(Params P) {
 // k_scan: streams the large units, one wave each. Blocks [0, scan_small) first encode the small
 // segments when they are not forked to the side stream (small plans: the fork costs more than it hides).
 template <bool DELTA, bool RAW, bool WITH_SMALL>
-__global__ __launch_bounds__(BLOCK) void k_scan(Params P) {
+__global__ __launch_bounds__(BLOCK, SCAN_WPE) void k_scan(Params P) {
   // one LDS arena: candidate staging (WAVES x STAGE_CAP records) or a small segment's values + histogram
   // (WITH_SMALL only: without it the block needs 16 KB of LDS instead of 24.8 KB)
   constexpr size_t SMALL_BYTES = WITH_SMALL ? (SMALL_MAX + HIST_BINS + 64) * 4 : 0;
@@ -1350,7 +1381,7 @@ template <bool HASBASE>
 constexpr uint32_t decode_dpw() { return HASBASE ? 1u : 2u; }
 
 template <bool RAW, bool HASBASE>
-__global__ __launch_bounds__(BLOCK) void k_decode(Params P) {
+__global__ __launch_bounds__(BLOCK, DECODE_WPE) void k_decode(Params P) {
   constexpr uint32_t DPW = decode_dpw<HASBASE>();
   const uint32_t lane = lane_id(), wv = threadIdx.x >> 6;
   const uint32_t u0 = (blockIdx.x * WAVES + wv) * DPW;
@@ -1381,27 +1412,17 @@ __global__ __launch_bounds__(BLOCK) void k_decode(Params P) {
   for (uint32_t r = 0; r < DPW; ++r) {
     if (u0 + r >= P.n_units) break;
     const uint32_t len = U[r].len;
-    const bool full = len == UNIT;  // else a segment's last, partial unit: same path, masked
-    const float* bs = HASBASE ? P.base + U[r].off : nullptr;
-    float* out = P.out + U[r].off;
+    // buffer resources over exactly this unit: base loads past len return 0, stores past len are
+    // dropped, so partial units take the same straight-line path
+    const __amdgpu_buffer_rsrc_t rout = unit_rsrc(P.out + U[r].off, len);
     float4 b[UNIT_IT];
-    if (!HASBASE || full) {
+    if (HASBASE) {
+      const __amdgpu_buffer_rsrc_t rb = unit_rsrc(P.base + U[r].off, len);
 #pragma unroll
-      for (uint32_t it = 0; it < UNIT_IT; ++it)
-        b[it] = HASBASE ? *reinterpret_cast<const float4*>(bs + (it * 64 + lane) * 4) : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+      for (uint32_t it = 0; it < UNIT_IT; ++it) b[it] = unit_load_x4<false>(rb, rb, (it * 64 + lane) * 16);
     } else {
 #pragma unroll
-      for (uint32_t it = 0; it < UNIT_IT; ++it) {
-        const uint32_t e = (it * 64 + lane) * 4;
-        if (e + 3 < len) {
-          b[it] = *reinterpret_cast<const float4*>(bs + e);
-        } else {
-          b[it].x = e + 0 < len ? bs[e + 0] : 0.0f;
-          b[it].y = e + 1 < len ? bs[e + 1] : 0.0f;
-          b[it].z = e + 2 < len ? bs[e + 2] : 0.0f;
-          b[it].w = 0.0f;
-        }
-      }
+      for (uint32_t it = 0; it < UNIT_IT; ++it) b[it] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
     }
     uint64_t kept = 0;
     const uint32_t cnt = hi[r] - lo[r];
@@ -1422,25 +1443,12 @@ __global__ __launch_bounds__(BLOCK) void k_decode(Params P) {
         b[it].w = (m & 8u) ? b[it].w : b[it].w + 0.0f;
       }
     }
-    if (full) {  // wave-uniform: a full unit is one straight run of 16 non-temporal float4 stores per lane
+    if ((len & 3u) == 0) {  // wave-uniform: one non-temporal float4 buffer store per slot
 #pragma unroll
-      for (uint32_t it = 0; it < UNIT_IT; ++it) {
-        const f4v t = {b[it].x, b[it].y, b[it].z, b[it].w};
-        __builtin_nontemporal_store(t, reinterpret_cast<f4v*>(out + (it * 64 + lane) * 4));
-      }
-    } else {
+      for (uint32_t it = 0; it < UNIT_IT; ++it) unit_store_x4(rout, (it * 64 + lane) * 16, b[it]);
+    } else {  // a segment's last unit with n % 4 != 0: dword stores (range-checked per dword)
 #pragma unroll
-      for (uint32_t it = 0; it < UNIT_IT; ++it) {
-        const uint32_t e = (it * 64 + lane) * 4;
-        if (e + 3 < len) {
-          const f4v t = {b[it].x, b[it].y, b[it].z, b[it].w};
-          __builtin_nontemporal_store(t, reinterpret_cast<f4v*>(out + e));
-        } else if (e < len) {  // the partial unit's last 1-3 elements (entries at pos >= len were never
-          out[e] = b[it].x;    // merged: merge_entries only visits rows of the sorted list in order)
-          if (e + 1 < len) out[e + 1] = b[it].y;
-          if (e + 2 < len) out[e + 2] = b[it].z;
-        }
-      }
+      for (uint32_t it = 0; it < UNIT_IT; ++it) unit_store_x1x4(rout, (it * 64 + lane) * 16, b[it]);
     }
   }
 }
