@@ -27,6 +27,8 @@ METRIC = "encode+decode GB/s over fp32 weight updates (device-resident), 1/2/4/8
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md: 8.0 TB/s)
 LANES = 1  # default pipeline lanes per GPU (2-3 lanes measured equal or slower: the latency-bound stages
            # of one lane slow the other lane's streaming kernel by as much as they overlap it)
+SPLIT = 2  # sub-batches per step: two independent 8-client pipelines side by side fill the CUs the other
+           # leaves idle in its latency-bound stages and launch tails (+11 % over one 16-client pipeline)
 EVENT_EVERY = 4  # timing events on every 4th timed step (each recorded event adds a ~4 us dispatch gap)
 
 
@@ -44,6 +46,12 @@ def parse():
                    help="pipeline lanes per GPU (coala_amd/compression/pipeline.py): the batch's segments "
                         "cut into this many contiguous ranges, one HIP stream each, streaming kernels "
                         "serialised across lanes")
+    p.add_argument("--split", type=int, default=SPLIT,
+                   help="the step's clients are cut into this many equal sub-batches, each an independent "
+                        "pipeline (own plan, buffers, HIP stream) launched side by side")
+    p.add_argument("--inflight", type=int, default=1,
+                   help="independent pipelines (own plan, buffers and stream) taking the steps round-robin, so "
+                        "consecutive batches overlap (each step still encodes + decodes its whole batch)")
     p.add_argument("--c-priority", type=int, default=-1, help="stream priority of the latency-stage streams")
     p.add_argument("--event-every", type=int, default=EVENT_EVERY,
                    help="record the per-kernel timing events on every Nth timed step (1 = every step)")
@@ -66,7 +74,8 @@ def pmc_traffic(kernel, a):
     doubled (gfx950 reports half the bytes of wide coalesced streaming reads, MI355X_MICROARCH.md §HBM)
     + WRITE_SIZE. Only reported for the default configuration the summary was collected on."""
     import glob
-    default = (a.layout, a.clients, a.ratio, a.bits, a.mode, a.lanes) == ("resnet50_tv", 16, 0.01, 8, "weights", LANES)
+    default = (a.layout, a.clients, a.ratio, a.bits, a.mode, a.lanes, a.inflight, a.split) == \
+        ("resnet50_tv", 16, 0.01, 8, "weights", LANES, 1, SPLIT)
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_summary.json")))
     if not default or not files:
         return None, None
@@ -135,19 +144,34 @@ def main():
     ids = range(rank * a.clients, (rank + 1) * a.clients)
     flat = synth_batch(t, dev, client_ids=ids)
     base = synth_batch(t, dev, client_ids=[10_000 + i for i in ids]) if a.mode == "delta" else None
-    pipe = LanePipeline(t, a.bits, lanes=a.lanes, device=dev, flags=a.flags, c_priority=a.c_priority)
-    enc, out = pipe.empty_encoded(), pipe.empty_flat()
+    split = max(1, a.split)
+    if a.clients % split:
+        raise SystemExit(f"--clients {a.clients} is not a multiple of --split {split}")
+    tg = SegmentTable(sizes, a.ratio, a.clients // split)  # one sub-batch: clients / split updates
+    sl = lambda x, g: None if x is None else x[g * tg.span:(g + 1) * tg.span]  # noqa: E731
+    # slots[j]: the split sub-batch pipelines of in-flight copy j, each (pipeline, input, base, enc, out)
+    slots = []
+    for _ in range(max(1, a.inflight)):
+        slot = []
+        for g in range(split):
+            p = LanePipeline(tg, a.bits, lanes=a.lanes, device=dev, flags=a.flags, c_priority=a.c_priority)
+            slot.append((p, sl(flat, g), sl(base, g), p.empty_encoded(), p.empty_flat()))
+        slots.append(slot)
+    pipes = [e[0] for slot in slots for e in slot]
+    pipe = pipes[0]
     torch.cuda.synchronize()
 
-    def step(i=None):
-        # the pipeline's streaming stream as the current stream: back-to-back steps need no join hops
-        with torch.cuda.stream(pipe.stream):
-            pipe.roundtrip(flat, base=base, enc=enc, out=out, enc_events=None if i is None else ev_e[i],
-                           dec_events=None if i is None else ev_d[i])
+    def step(i=None, j=0):
+        for g, (p, x, b, enc, out) in enumerate(slots[j % len(slots)]):
+            # the pipeline's streaming stream as the current stream: back-to-back steps need no join hops
+            with torch.cuda.stream(p.stream):
+                timed = i is not None and ev_e[i] is not None
+                p.roundtrip(x, base=b, enc=enc, out=out, enc_events=ev_e[i][g] if timed else None,
+                            dec_events=ev_d[i][g] if timed else None)
 
-    for _ in range(a.warmup):
-        step()
-    fallbacks = pipe.fallbacks()
+    for w in range(max(a.warmup, len(slots))):
+        step(j=w)
+    fallbacks = sum(p.fallbacks() for p in pipes)
     # Timing events only at the streaming kernels' boundaries, and as few as possible: every recorded
     # event costs ~6 us of dispatch gap (rocprofv3 trace, profiles/). The streaming kernels run back to
     # back on one stream, so lane 0 records before and after its kernel and every later lane only
@@ -164,15 +188,18 @@ def main():
         return evs
     every = max(1, a.event_every)
     timed_steps = [i for i in range(a.steps) if i % every == 0]
-    ev_e = [lane_events(5) if i % every == 0 else None for i in range(a.steps)]
-    ev_d = [lane_events(3) if i % every == 0 else None for i in range(a.steps)]
+    if pipe.n_lanes > 1 and split > 1:
+        raise SystemExit("--lanes > 1 needs --split 1")
+    # per event-carrying step: one lane_events list per sub-batch (each on that sub-batch's stream)
+    ev_e = [[lane_events(5) for _ in range(split)] if i % every == 0 else None for i in range(a.steps)]
+    ev_d = [[lane_events(3) for _ in range(split)] if i % every == 0 else None for i in range(a.steps)]
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for i in range(a.steps):
-        step(i)
+        step(i, i)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -182,30 +209,43 @@ def main():
         dist.all_reduce(x, op=dist.ReduceOp.MAX)
         el = x.item()
 
-    # Per-kernel mean durations (ms per launch, averaged over lanes and the event-carrying steps of the
-    # timed region, every `--event-every`th one) from the HIP events each
-    # lane records on its own stream at the stage boundaries. With several lanes a stage's interval can
-    # include co-running latency-bound kernels of other lanes (never another streaming kernel: the
-    # pipeline serialises k_scan / k_decode across lanes), i.e. it is the kernel's wall-clock time.
-    def mean(pairs):
-        return sum(s.elapsed_time(e) for s, e in pairs) / len(pairs)
+    # Per-kernel durations (ms, averaged over the event-carrying steps of the timed region, every
+    # `--event-every`th one) from the HIP events recorded on each sub-batch's stream around its
+    # streaming kernel. With --split S the S sub-batches' launches of a kernel run concurrently, so the
+    # measured quantity is their union interval, first start to last end (events on different streams
+    # of one device share a clock): the HBM phase the launch group occupies, against the bytes of all S
+    # launches. With lanes (split 1) a lane's interval is [previous lane's end, its end] on the one
+    # streaming stream; it can include co-running latency-bound kernels of other lanes.
+    def union(pairs):
+        ref = pairs[0][0]
+        return max(ref.elapsed_time(e) for _, e in pairs) - min(ref.elapsed_time(s) for s, _ in pairs)
     stages = {}
     for name, which in {"k_scan": ev_e, "k_decode": ev_d}.items():
-        stages[name] = mean([(lanes[li][1] if li == 0 else lanes[li - 1][2], lanes[li][2])
-                             for lanes in (which[i] for i in timed_steps) for li in range(pipe.n_lanes)])
+        per_step = []
+        for i in timed_steps:
+            groups = which[i]
+            if pipe.n_lanes == 1:
+                per_step.append(union([(g[0][1], g[0][2]) for g in groups]))
+            else:
+                lanes = groups[0]
+                per_step.extend((lanes[li][1] if li == 0 else lanes[li - 1][2]).elapsed_time(lanes[li][2])
+                                for li in range(pipe.n_lanes))
+        stages[name] = sum(per_step) / len(per_step)
     N, K, T = t.n_elements, t.total_k, t.n_segments
     delta = a.mode == "delta"
     vb = 4 if a.bits == 32 else 1
-    nl = pipe.n_lanes
+    nl = pipe.n_lanes  # timed intervals of each streaming kernel per step (a lane, or the split's union)
     segs = t.segs.astype("int64")
     large_elems = int(segs[segs[:, 1] > SMALL_MAX, 1].sum())
-    alg = {  # algorithmic HBM bytes per launch, averaged over the lanes' launches
+    alg = {  # algorithmic HBM bytes per timed interval
         "k_scan": 4 * large_elems * (2 if delta else 1) / nl,
         "k_decode": (4 * N * (2 if delta else 1) + (4 + vb) * K + 8 * T) / nl,
     }
     dom = max(alg, key=lambda k: stages[k])
     ach = alg[dom] / (stages[dom] * 1e-3) / 1e9
     traffic, traffic_src = pmc_traffic(dom, a)
+    if traffic is not None:
+        traffic *= split  # the summary is per dispatch; the timed interval holds `split` of them
     step_ms = el / a.steps * 1e3
     step_alg = t.algorithmic_bytes(a.bits, delta)
     value = 4.0 * N * world * a.steps / el / 1e9
@@ -216,20 +256,22 @@ def main():
             "warmup": a.warmup, "ms_per_step": round(step_ms, 4), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
             "config": {"workload": f"C3-per-GPU: {a.clients} x {a.layout} fp32 updates per GPU, top-k "
-                                   f"{a.ratio}, {a.bits}-bit codes, {a.mode} mode, encode+decode batched",
+                                   f"{a.ratio}, {a.bits}-bit codes, {a.mode} mode, encode+decode batched "
+                                   f"as {split} concurrent sub-batches",
                        "layout": a.layout, "clients_per_gpu": a.clients, "global_clients": a.clients * world,
                        "elements_per_client": sum(sizes), "segments_per_client": len(sizes),
                        "ratio": a.ratio, "bits": a.bits, "mode": a.mode, "lanes_per_gpu": pipe.n_lanes,
+                       "sub_batches_per_step": split, "inflight_steps": len(slots),
                        "parallelism": f"replicas{world}"},
-            "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,
+            "roofline": {"bound": "hbm", "kernel": dom if split == 1 else f"{dom} x{split} concurrent launches (union interval)", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": traffic,
                          "traffic_source": traffic_src, "alg_bytes_per_launch": int(alg[dom])},
             "step_roofline": {"alg_bytes_per_step": step_alg,
                               "achieved_GBs": round(step_alg / (step_ms * 1e-3) / 1e9, 1),
                               "frac": round(step_alg / (step_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)},
             "stages_ms": {k: round(v, 4) for k, v in stages.items()},
-            "stage_timing": f"HIP events on the pipeline stream around k_scan / k_decode, {len(timed_steps)} of "
-                            f"the {a.steps} timed steps",
+            "stage_timing": f"HIP events on each sub-batch stream around k_scan / k_decode (union over the "
+                            f"{split} sub-batches), {len(timed_steps)} of the {a.steps} timed steps",
             "sample_fallbacks": fallbacks,
         }
         if world == 1 and not a.no_cpu_baseline:

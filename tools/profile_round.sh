@@ -16,6 +16,9 @@ timeout -k 10 240 rocprofv3 --pmc FETCH_SIZE -d "$OUT/fetch" -o run --output-for
 timeout -k 10 240 rocprofv3 --pmc WRITE_SIZE -d "$OUT/write" -o run --output-format csv \
   -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline > "$OUT/bench_write.json" 2> "$OUT/write.err"
 python3 tools/pmc_summary.py "$OUT" > "$OUT/summary.json"
+# bench --split 2 (default): the two sub-batches' launches of a streaming kernel run together; the bench
+# times their union interval, which this reproduces from the trace
+python3 tools/timeline.py "$OUT/trace" --group 2 > "$OUT/timeline_union.json"
 find "$OUT/trace" -name "*kernel_stats.csv" -exec python3 tools/filter_stats.py {} "$OUT/kernel_stats_codec.csv" \;
 # keep the small summaries only (raw per-dispatch CSVs can exceed gpurun's 64 MiB pull limit)
 du -sh "$OUT"/trace "$OUT"/fetch "$OUT"/write || true

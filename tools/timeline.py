@@ -43,6 +43,9 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("dir")
     ap.add_argument("--last-frac", type=float, default=0.5)
+    ap.add_argument("--group", type=int, default=1,
+                    help="streaming kernels launched this many at a time (bench --split): also report the mean "
+                         "union interval (first start to last end) of each group of consecutive launches")
     ap.add_argument("--dump", type=int, default=0, help="also print the last N kernels (start/end us, queue)")
     a = ap.parse_args()
     files = glob.glob(os.path.join(a.dir, "**", "*kernel_trace.csv"), recursive=True)
@@ -57,6 +60,7 @@ def main():
                     rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), k,
                                  r.get("Queue_Id", r.get("Stream_Id", "?"))))
     rows.sort()
+    all_rows = rows
     rows = rows[int(len(rows) * (1.0 - a.last_frac)):]
     t0, t1 = rows[0][0], max(r[1] for r in rows)
     span = t1 - t0
@@ -76,6 +80,17 @@ def main():
         d = [e - s for s, e, kk, _ in rows if kk == k]
         if d:
             out["mean_us"][k] = round(sum(d) / len(d) / 1e3, 2)
+    if a.group > 1:
+        out["group"] = a.group
+        out["group_union_us"] = {}
+        for k in STREAMING:
+            # group over the whole trace (every step launches `group` of them), keep the last groups
+            d = sorted((s, e) for s, e, kk, _ in all_rows if kk == k)
+            spans = [max(e for _, e in d[i:i + a.group]) - d[i][0]
+                     for i in range(0, len(d) - a.group + 1, a.group)]
+            spans = spans[int(len(spans) * (1.0 - a.last_frac)):]
+            if spans:
+                out["group_union_us"][k] = round(sum(spans) / len(spans) / 1e3, 2)
     print(json.dumps(out, indent=1))
     if a.dump:
         tail = rows[-a.dump:]
