@@ -49,6 +49,9 @@ def parse():
     p.add_argument("--split", type=int, default=SPLIT,
                    help="the step's clients are cut into this many equal sub-batches, each an independent "
                         "pipeline (own plan, buffers, HIP stream) launched side by side")
+    p.add_argument("--fork", action="store_true", help="keep the per-plan small-segment side streams with --split > 1")
+    p.add_argument("--joined", action="store_true",
+                   help="join the sub-batch streams with the caller's stream on entry/exit of every step")
     p.add_argument("--inflight", type=int, default=1,
                    help="independent pipelines (own plan, buffers and stream) taking the steps round-robin, so "
                         "consecutive batches overlap (each step still encodes + decodes its whole batch)")
@@ -124,7 +127,7 @@ def main():
     import torch
     import torch.distributed as dist
 
-    from coala_amd.compression import LanePipeline, SegmentTable
+    from coala_amd.compression import LanePipeline, SegmentTable, SplitPipeline
     from coala_amd.compression.spec import SMALL_MAX
     from coala_amd.layouts import fp32_sizes
     from coala_amd.workload import synth_batch
@@ -147,27 +150,33 @@ def main():
     split = max(1, a.split)
     if a.clients % split:
         raise SystemExit(f"--clients {a.clients} is not a multiple of --split {split}")
-    tg = SegmentTable(sizes, a.ratio, a.clients // split)  # one sub-batch: clients / split updates
-    sl = lambda x, g: None if x is None else x[g * tg.span:(g + 1) * tg.span]  # noqa: E731
-    # slots[j]: the split sub-batch pipelines of in-flight copy j, each (pipeline, input, base, enc, out)
+    if a.lanes > 1 and split > 1:
+        raise SystemExit("--lanes > 1 needs --split 1")
+    # slots[j]: in-flight copy j of the step's pipeline with its own encoded / dense buffers
     slots = []
     for _ in range(max(1, a.inflight)):
-        slot = []
-        for g in range(split):
-            p = LanePipeline(tg, a.bits, lanes=a.lanes, device=dev, flags=a.flags, c_priority=a.c_priority)
-            slot.append((p, sl(flat, g), sl(base, g), p.empty_encoded(), p.empty_flat()))
-        slots.append(slot)
-    pipes = [e[0] for slot in slots for e in slot]
+        if a.lanes > 1:
+            p = LanePipeline(t, a.bits, lanes=a.lanes, device=dev, flags=a.flags, c_priority=a.c_priority)
+        else:
+            p = SplitPipeline(t, a.bits, split=split, device=dev, flags=a.flags, fork=a.fork)
+        slots.append((p, p.empty_encoded(), p.empty_flat()))
+    pipes = [s[0] for s in slots]
     pipe = pipes[0]
+    n_timed = pipe.n_lanes if a.lanes > 1 else 1  # timed intervals per streaming kernel and step
     torch.cuda.synchronize()
 
     def step(i=None, j=0):
-        for g, (p, x, b, enc, out) in enumerate(slots[j % len(slots)]):
+        p, enc, out = slots[j % len(slots)]
+        ee = ev_e[i] if i is not None else None
+        de = ev_d[i] if i is not None else None
+        if a.lanes > 1:
             # the pipeline's streaming stream as the current stream: back-to-back steps need no join hops
             with torch.cuda.stream(p.stream):
-                timed = i is not None and ev_e[i] is not None
-                p.roundtrip(x, base=b, enc=enc, out=out, enc_events=ev_e[i][g] if timed else None,
-                            dec_events=ev_d[i][g] if timed else None)
+                p.roundtrip(flat, base=base, enc=enc, out=out, enc_events=ee, dec_events=de)
+        else:
+            # sub-batch streams ordered by themselves step after step (each slot's buffers are used by
+            # its own streams only): no joins with the caller's stream inside the timed loop
+            p.roundtrip(flat, base=base, enc=enc, out=out, enc_events=ee, dec_events=de, joined=a.joined)
 
     for w in range(max(a.warmup, len(slots))):
         step(j=w)
@@ -177,7 +186,7 @@ def main():
     # back on one stream, so lane 0 records before and after its kernel and every later lane only
     # after; a lane's interval is [previous lane's end, its end]. The latency-bound stages are timed
     # by rocprofv3 (profiles/) instead.
-    def lane_events(n):
+    def lane_events(n):  # LanePipeline: per lane, [1] before lane 0's kernel, [2] after every lane's
         evs = []
         for li in range(pipe.n_lanes):
             ev = [None] * n
@@ -186,13 +195,19 @@ def main():
                 ev[1] = make_events(torch, 1)[0]
             evs.append(ev)
         return evs
+
+    def part_events(n):  # SplitPipeline: per sub-batch, [1] / [2] around its kernel
+        evs = []
+        for _ in range(split):
+            ev = [None] * n
+            ev[1], ev[2] = make_events(torch, 2)
+            evs.append(ev)
+        return evs
+    mk = lane_events if a.lanes > 1 else part_events
     every = max(1, a.event_every)
     timed_steps = [i for i in range(a.steps) if i % every == 0]
-    if pipe.n_lanes > 1 and split > 1:
-        raise SystemExit("--lanes > 1 needs --split 1")
-    # per event-carrying step: one lane_events list per sub-batch (each on that sub-batch's stream)
-    ev_e = [[lane_events(5) for _ in range(split)] if i % every == 0 else None for i in range(a.steps)]
-    ev_d = [[lane_events(3) for _ in range(split)] if i % every == 0 else None for i in range(a.steps)]
+    ev_e = [mk(5) if i % every == 0 else None for i in range(a.steps)]
+    ev_d = [mk(3) if i % every == 0 else None for i in range(a.steps)]
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -223,18 +238,17 @@ def main():
     for name, which in {"k_scan": ev_e, "k_decode": ev_d}.items():
         per_step = []
         for i in timed_steps:
-            groups = which[i]
-            if pipe.n_lanes == 1:
-                per_step.append(union([(g[0][1], g[0][2]) for g in groups]))
+            evs = which[i]
+            if a.lanes == 1:
+                per_step.append(union([(e[1], e[2]) for e in evs]))
             else:
-                lanes = groups[0]
-                per_step.extend((lanes[li][1] if li == 0 else lanes[li - 1][2]).elapsed_time(lanes[li][2])
+                per_step.extend((evs[li][1] if li == 0 else evs[li - 1][2]).elapsed_time(evs[li][2])
                                 for li in range(pipe.n_lanes))
         stages[name] = sum(per_step) / len(per_step)
     N, K, T = t.n_elements, t.total_k, t.n_segments
     delta = a.mode == "delta"
     vb = 4 if a.bits == 32 else 1
-    nl = pipe.n_lanes  # timed intervals of each streaming kernel per step (a lane, or the split's union)
+    nl = n_timed  # timed intervals of each streaming kernel per step (a lane, or the split's union)
     segs = t.segs.astype("int64")
     large_elems = int(segs[segs[:, 1] > SMALL_MAX, 1].sum())
     alg = {  # algorithmic HBM bytes per timed interval
@@ -260,7 +274,7 @@ def main():
                                    f"as {split} concurrent sub-batches",
                        "layout": a.layout, "clients_per_gpu": a.clients, "global_clients": a.clients * world,
                        "elements_per_client": sum(sizes), "segments_per_client": len(sizes),
-                       "ratio": a.ratio, "bits": a.bits, "mode": a.mode, "lanes_per_gpu": pipe.n_lanes,
+                       "ratio": a.ratio, "bits": a.bits, "mode": a.mode, "lanes_per_gpu": pipe.n_lanes if a.lanes > 1 else 1,
                        "sub_batches_per_step": split, "inflight_steps": len(slots),
                        "parallelism": f"replicas{world}"},
             "roofline": {"bound": "hbm", "kernel": dom if split == 1 else f"{dom} x{split} concurrent launches (union interval)", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,

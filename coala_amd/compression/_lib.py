@@ -12,6 +12,7 @@ from .. import _build
 COALAC_FLAG_FORCE_EXACT = 1
 COALAC_FLAG_GENERIC_SELECT = 2
 COALAC_FLAG_STAMPS = 4
+COALAC_FLAG_NO_FORK = 8
 # stages of a split encode / decode (coalac_sched_t.stages; 0 = all)
 COALAC_STAGE_SAMPLE, COALAC_STAGE_SCAN, COALAC_STAGE_SELECT, COALAC_STAGE_SMALL = 1, 2, 4, 8
 COALAC_STAGE_BOUNDS, COALAC_STAGE_DECODE = 1, 2

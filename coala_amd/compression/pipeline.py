@@ -227,3 +227,128 @@ class LanePipeline:
         for L in self.lanes:
             L["plan"].close()
         self.lanes = []
+
+
+class SplitPipeline:
+    """A batch of C client updates as S independent sub-batches of C / S clients, each with its own plan,
+    workspaces and HIP stream, launched side by side.
+
+    Why: one batch's launch sequence alternates HBM-bound kernels (k_scan, k_decode) with
+    latency-bound ones (k_sample, the select chain, k_bounds) whose few blocks leave most CUs idle, and
+    every kernel has a launch tail. Two sub-batches on two streams fill each other's idle phases and
+    tails: 16 ResNet-50 updates run 11-14 % faster as 2 x 8 than as 1 x 16 (bench.py --split). Unlike
+    LanePipeline's lanes, nothing is serialised across sub-batches; the hardware interleaves them.
+
+    Sub-batches are contiguous client ranges. Every per-client quantity of a SegmentTable batch is
+    client-major (input / dense output spans, idx / vals of total_k_per_client, mn / scale of the
+    client's segments), so sub-batch g is an ordinary plan over its C_g clients working on views of the
+    whole batch's buffers: results are bit-identical to a single plan's. (A plan over absolute segment
+    rows, as LanePipeline uses, measured 2.5 % slower here.) Calls are asynchronous and ordered after /
+    before the caller's current stream (the sub-batch streams wait for it on entry, it waits for them
+    on exit), unless joined=False.
+    """
+
+    def __init__(self, table: SegmentTable, bits=8, split=2, device=None, flags=0, fork=False):
+        self.table = table
+        self.bits = int(bits)
+        self.flags = int(flags)
+        self.device = torch.device("cuda", torch.cuda.current_device() if device is None
+                                   else torch.device(device).index or 0)
+        C = max(1, int(table.clients))
+        S = max(1, min(int(split), C))
+        cuts = [round(g * C / S) for g in range(S + 1)]
+        # several sub-batches already run side by side: no per-plan side stream for the small segments
+        # (HIP maps streams onto 4 hardware queues; a side stream sharing one with the other sub-batch
+        # would queue its k_small behind that sub-batch's kernels)
+        self.fork_flag = _lib.COALAC_FLAG_NO_FORK if S > 1 and fork is False else 0
+        sp, kp, tp = table.span_per_client, table.total_k_per_client, table.n_segments // C
+        self.parts = []
+        with torch.cuda.device(self.device):
+            for c0, c1 in zip(cuts[:-1], cuts[1:]):
+                plan = CodecPlan(table.sizes, table.ratio, self.bits, clients=c1 - c0, device=self.device)
+                self.parts.append(dict(x=slice(c0 * sp, c1 * sp), k=slice(c0 * kp, c1 * kp), t=slice(c0 * tp, c1 * tp),
+                                       plan=plan, ws=plan.empty_workspace(), dws=plan.empty_decode_workspace(),
+                                       stream=torch.cuda.Stream(self.device)))
+
+    @property
+    def n_parts(self):
+        return len(self.parts)
+
+    @property
+    def streams(self):
+        return [P["stream"] for P in self.parts]
+
+    def empty_flat(self):
+        return torch.empty(self.table.span, dtype=torch.float32, device=self.device)
+
+    def empty_encoded(self):
+        d, vt = self.device, torch.float32 if self.bits == 32 else torch.uint8
+        T, K = self.table.n_segments, self.table.total_k
+        return Encoded(torch.empty(K, dtype=torch.int32, device=d), torch.empty(K, dtype=vt, device=d),
+                       torch.empty(T, dtype=torch.float32, device=d), torch.empty(T, dtype=torch.float32, device=d))
+
+    @staticmethod
+    def _enc(enc, P):
+        return Encoded(enc.idx[P["k"]], enc.vals[P["k"]], enc.mn[P["t"]], enc.scale[P["t"]])
+
+    @staticmethod
+    def _x(t, P):
+        return None if t is None else t[P["x"]]
+
+    def _run(self, fn, joined):
+        cur = torch.cuda.current_stream(self.device)
+        if joined:
+            for P in self.parts:
+                P["stream"].wait_stream(cur)
+        for g, P in enumerate(self.parts):
+            with torch.cuda.stream(P["stream"]):
+                fn(g, P)
+        if joined:
+            for P in self.parts:
+                cur.wait_stream(P["stream"])
+
+    def _encode_part(self, g, P, flat, base, out, events):
+        P["plan"].encode(self._x(flat, P), base=self._x(base, P), out=self._enc(out, P), workspace=P["ws"],
+                         flags=self.flags | self.fork_flag, events=None if events is None else events[g])
+
+    def _decode_part(self, g, P, enc, base, out, events):
+        P["plan"].decode(self._enc(enc, P), base=self._x(base, P), out=self._x(out, P), workspace=P["dws"],
+                         events=None if events is None else events[g])
+
+    def encode(self, flat, base=None, out=None, events=None, joined=True):
+        """Encode the batch -> Encoded. events: optional per-sub-batch lists of 5 timing events
+        (coalac_encode_ev boundaries; [1] / [2] bracket k_scan). joined=False skips the entry/exit joins
+        with the caller's stream (a caller that orders consecutive calls itself, e.g. the bench)."""
+        out = self.empty_encoded() if out is None else out
+        self._run(lambda g, P: self._encode_part(g, P, flat, base, out, events), joined)
+        return out
+
+    def decode(self, enc, base=None, out=None, events=None, joined=True):
+        """Decode into the dense out (+ base, fused). events: per-sub-batch lists of 3 ([1] / [2] bracket
+        k_decode)."""
+        if out is None:
+            out = self.empty_flat() if base is None else torch.empty_like(base)
+        self._run(lambda g, P: self._decode_part(g, P, enc, base, out, events), joined)
+        return out
+
+    def roundtrip(self, flat, base=None, enc=None, out=None, enc_events=None, dec_events=None, joined=True):
+        """encode() then decode() with one join each way: sub-batch g's decode follows its own encode on
+        its stream only."""
+        enc = self.empty_encoded() if enc is None else enc
+        if out is None:
+            out = self.empty_flat() if base is None else torch.empty_like(base)
+
+        def both(g, P):
+            self._encode_part(g, P, flat, base, enc, enc_events)
+            self._decode_part(g, P, enc, base, out, dec_events)
+        self._run(both, joined)
+        return enc, out
+
+    def fallbacks(self):
+        torch.cuda.synchronize(self.device)
+        return sum(P["plan"].fallbacks(P["ws"]) for P in self.parts)
+
+    def close(self):
+        for P in self.parts:
+            P["plan"].close()
+        self.parts = []

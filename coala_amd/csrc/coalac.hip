@@ -1797,7 +1797,7 @@ int launch_encode(const Params& P, coalac_plan_t plan, hipStream_t st, const coa
   // whole encode: small segments forked beside k_sample / k_scan (big batches) or inside k_scan;
   // split encode: only in stage SMALL (k_small)
   const bool split = stages != all;
-  const bool fork = plan->n_small && !split && plan->n_lunits >= FORK_MIN_LUNITS;
+  const bool fork = plan->n_small && !split && plan->n_lunits >= FORK_MIN_LUNITS && !(P.flags & COALAC_FLAG_NO_FORK);
   Params Q = P;
   Q.scan_small = (fork || split) ? 0u : plan->n_small;
   std::unique_lock<std::mutex> lk(plan->mu, std::defer_lock);

@@ -48,7 +48,9 @@ enum {
 enum {
   COALAC_FLAG_FORCE_EXACT = 1,    /* test hook: re-select every large segment exactly (no sampling) */
   COALAC_FLAG_GENERIC_SELECT = 2, /* test hook: resolve the k-th key with the multi-pass select only */
-  COALAC_FLAG_STAMPS = 4          /* diagnostics: record per-block phase timestamps of k_select */
+  COALAC_FLAG_STAMPS = 4,         /* diagnostics: record per-block phase timestamps of k_select */
+  COALAC_FLAG_NO_FORK = 8         /* encode small segments inside k_scan, never on the plan's side stream
+                                     (for callers that run several plans concurrently themselves) */
 };
 
 /* One fp32 segment (= one flattened tensor of the state_dict). Offsets are in ELEMENTS.

@@ -7,7 +7,7 @@ import numpy as np
 import pytest
 import torch
 
-from coala_amd.compression import LanePipeline, SegmentTable
+from coala_amd.compression import CodecPlan, LanePipeline, SegmentTable, SplitPipeline
 from coala_amd.layouts import fp32_sizes
 from coala_amd.workload import synth_batch
 from oracle import codec_oracle as O
@@ -87,3 +87,45 @@ def test_pipeline_repeated_steps_stable(cuda):
     np.testing.assert_array_equal(enc.idx[:K].cpu().numpy(), idx)
     np.testing.assert_array_equal(enc.vals[:K].cpu().numpy(), vals)
     np.testing.assert_array_equal(out[:S].cpu().numpy().view(np.uint32), rdec.view(np.uint32))
+
+
+@pytest.mark.parametrize("split", [1, 2, 3])
+@pytest.mark.parametrize("delta", [False, True])
+@pytest.mark.parametrize("fused", [False, True])
+def test_split_pipeline_resnet18_x3(cuda, split, delta, fused):
+    """SplitPipeline: client sub-batches on independent streams, results in the whole batch's buffers,
+    bit-identical to the oracle (3 clients into 1 / 2 / 3 sub-batches: uneven cuts included)."""
+    t = SegmentTable(fp32_sizes("resnet18"), 0.01, 3)
+    flat = synth_batch(t, cuda, client_ids=[7, 8, 9])
+    base = synth_batch(t, cuda, client_ids=[70, 80, 90]) if delta else None
+    pipe = SplitPipeline(t, 8, split=split, device=cuda)
+    assert pipe.n_parts == split
+    if fused:
+        enc, dec = pipe.roundtrip(flat, base=base)
+    else:
+        enc = pipe.encode(flat, base=base)
+        dec = pipe.decode(enc, base=base)
+    torch.cuda.synchronize()
+    check(t, enc, dec, oracle_roundtrip(t, flat.cpu().numpy(), 8, None if base is None else base.cpu().numpy()))
+    assert pipe.fallbacks() == 0
+
+
+def test_split_pipeline_unjoined_steps_match_single_plan(cuda):
+    """The bench's schedule: 6 back-to-back unjoined roundtrips of 16 ResNet-50 updates as 2 x 8 (plus
+    the batch's small segments forked per sub-plan) equal one plan over the whole batch, bit for bit."""
+    t = SegmentTable(fp32_sizes("resnet50_tv"), 0.01, 16)
+    flat = synth_batch(t, cuda)
+    pipe = SplitPipeline(t, 8, split=2, device=cuda)
+    enc, out = pipe.empty_encoded(), pipe.empty_flat()
+    out.zero_()
+    for _ in range(6):
+        pipe.roundtrip(flat, enc=enc, out=out, joined=False)
+    torch.cuda.synchronize()
+    plan = CodecPlan(fp32_sizes("resnet50_tv"), 0.01, 8, clients=16, device=cuda)
+    e1 = plan.encode(flat)
+    d1 = torch.zeros_like(out)
+    plan.decode(e1, out=d1)
+    torch.cuda.synchronize()
+    assert torch.equal(enc.idx, e1.idx) and torch.equal(enc.vals, e1.vals)
+    assert torch.equal(enc.mn, e1.mn) and torch.equal(enc.scale, e1.scale)
+    assert torch.equal(out, d1)
