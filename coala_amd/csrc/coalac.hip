@@ -32,7 +32,7 @@
 //     k_select  one 512-thread block per large segment: exact k-th key + tie quota from the window
 //               lists (generic multi-pass select / exact re-select on a bracket miss), per-unit output
 //               offsets, min / max -> scale
-//     k_emit    one wave per large unit: kept records -> ascending idx + codes
+//     k_emit    one wave per 8 large units: kept records -> ascending idx + codes
 //   Decode: k_bounds (first kept entry of every unit) and k_decode (two units per wave, hoisted loads,
 //   kept values merged in registers, one non-temporal write per output line).
 //   Aggregate (fused decode + FedAvg, server side): k_bounds + k_aggregate.
@@ -193,6 +193,18 @@ DEV float wave_min(float v) {
 DEV float wave_max(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v = fmax_nan(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+DEV uint32_t wave_min_u32(uint32_t v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = min(v, (uint32_t)__shfl_xor((int)v, o, 64));
+  return v;
+}
+
+DEV uint32_t wave_max_u32(uint32_t v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = max(v, (uint32_t)__shfl_xor((int)v, o, 64));
   return v;
 }
 
@@ -661,7 +673,7 @@ __global__ __launch_bounds__(BLOCK) void k_small(Params P) {
 template <bool DELTA, bool RAW>
 __global__ __launch_bounds__(BLOCK) void k_sample(Params P) {
   constexpr int NT = BLOCK;
-  __shared__ __attribute__((aligned(16))) uint32_t keys[SAMPLE_MAX];
+  constexpr uint32_t MAXIT = SAMPLE_MAX / 16 / 64;  // run batches per block (64 runs of 16 per batch)
   __shared__ uint32_t hist[HIST_BINS];
   __shared__ uint32_t sh[64];
   const uint32_t t = threadIdx.x;
@@ -673,19 +685,23 @@ __global__ __launch_bounds__(BLOCK) void k_sample(Params P) {
   R = R < 64 ? 64 : (R > SAMPLE_MAX / 16 ? SAMPLE_MAX / 16 : R);
   R &= ~63u;
   const uint32_t m = R * 16;
+  const uint32_t nit = R / 64;
   const uint32_t stride = n / R;  // >= 16 because n > SMALL_MAX >= 1024
   const uint32_t room = stride - 16;
-  for (uint32_t it = 0; it < R / 64; ++it) {
-    const uint32_t run = it * 64 + (t >> 2), q = t & 3;
+  // The sampled keys stay in registers (4 per batch per thread): all loads in flight at once, and with
+  // 8 KB of LDS per block (histogram only) twice as many sample blocks fit a CU as with an LDS key copy.
+  uint32_t kk[MAXIT][4];
+#pragma unroll
+  for (uint32_t it = 0; it < MAXIT; ++it) {
+    const uint32_t run = min(it, nit - 1) * 64 + (t >> 2), q = t & 3;
     uint32_t start = run * stride + hash32(run * 0x9E3779B9u ^ (s + 1u) * 0x85EBCA6Bu) % (room + 1u);
     start &= ~3u;
     const float4 v = load_x4<DELTA>(P, sd.in_off + start + q * 4);
-    keys[run * 16 + q * 4 + 0] = fkey(v.x);
-    keys[run * 16 + q * 4 + 1] = fkey(v.y);
-    keys[run * 16 + q * 4 + 2] = fkey(v.z);
-    keys[run * 16 + q * 4 + 3] = fkey(v.w);
+    kk[it][0] = fkey(v.x);
+    kk[it][1] = fkey(v.y);
+    kk[it][2] = fkey(v.z);
+    kk[it][3] = fkey(v.w);
   }
-  __syncthreads();
   // Expected sample rank of the k-th key, widened by a margin that assumes partially correlated runs.
   const double p = (double)k / (double)n;
   const double se = p * (double)m;
@@ -700,16 +716,32 @@ __global__ __launch_bounds__(BLOCK) void k_sample(Params P) {
   for (uint32_t i = t; i < HIST_BINS; i += NT) hist[i] = 0;
   __syncthreads();
   uint32_t kmn = KEY_MAX, kmx = 0;
-  for (uint32_t i = t; i < m; i += NT) {
-    kmn = min(kmn, keys[i]);
-    kmx = max(kmx, keys[i]);
+#pragma unroll
+  for (uint32_t it = 0; it < MAXIT; ++it) {
+    if (it < nit) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        kmn = min(kmn, kk[it][j]);
+        kmx = max(kmx, kk[it][j]);
+      }
+    }
   }
-  atomicMin(&sh[44], kmn);
-  atomicMax(&sh[45], kmx);
+  kmn = wave_min_u32(kmn);
+  kmx = wave_max_u32(kmx);
+  if (lane_id() == 0) {
+    atomicMin(&sh[44], kmn);
+    atomicMax(&sh[45], kmx);
+  }
   __syncthreads();
   const uint32_t kmin = sh[44], kmax = sh[45];
   const int shift = band_shift(kmin, kmax);
-  for (uint32_t i = t; i < m; i += NT) atomicAdd(&hist[(keys[i] - kmin) >> shift], 1u);
+#pragma unroll
+  for (uint32_t it = 0; it < MAXIT; ++it) {
+    if (it < nit) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) atomicAdd(&hist[(kk[it][j] - kmin) >> shift], 1u);
+    }
+  }
   __syncthreads();
   uint32_t tlo = 0u, thi = KEY_MAX;
   if (rlo < (double)m) {
@@ -754,7 +786,8 @@ __global__ __launch_bounds__(BLOCK, SCAN_WPE) void k_scan(Params P) {
   const uint32_t lu = (blockIdx.x - P.scan_small) * WAVES + wv;
   if (lu >= P.n_lunits) return;
   const UnitDev L = P.lunits[lu];
-  scan_unit<DELTA, 1>(P, lu, L, P.tlo[lu], P.thi[lu], stage + wv * STAGE_CAP);
+  // delta: 4 load batches (32 float4 in flight spill)
+  scan_unit<DELTA, DELTA ? 4 : 1>(P, lu, L, P.tlo[lu], P.thi[lu], stage + wv * STAGE_CAP);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -1302,42 +1335,70 @@ __global__ __launch_bounds__(SEL_NT) void k_select(Params P) {
 }
 
 // ------------------------------------------------------------------------------------------------
-// k_emit: per large unit (one wave) — the candidate list is already in index order: keep key > T and
-// the ties whose segment-wide tie rank is < rt, compact with ballots, write idx + code. No LDS.
+// k_emit: EMIT_UPW consecutive large units per wave — each unit's candidate list is already in index
+// order: keep key > T and the ties whose segment-wide tie rank is < rt, compact with ballots, write idx +
+// code. No LDS. A unit holds ~1.5 % of its 4096 elements as candidates (about one record per lane), so
+// one unit per wave was a chain of dependent loads (count -> unit/segment metadata -> records) per 64
+// records: here lane g loads unit g's metadata (two dependent rounds for all units at once) and every
+// unit's first 64 records are in flight before the first one is classified.
 // ------------------------------------------------------------------------------------------------
+constexpr uint32_t EMIT_UPW = 8;
+
+DEV uint32_t rl(uint32_t v, uint32_t l) { return (uint32_t)__builtin_amdgcn_readlane((int)v, (int)l); }
+
 template <bool RAW>
 __global__ __launch_bounds__(BLOCK) void k_emit(Params P) {
   const uint32_t lane = lane_id(), wv = threadIdx.x >> 6;
-  const uint32_t lu = blockIdx.x * WAVES + wv;
-  if (lu >= P.n_lunits) return;
-  const uint32_t nC = P.cntC[lu];
-  if (nC == 0) return;
-  const UnitDev L = P.lunits[lu];
-  const uint32_t eqp = P.eqpre[lu], oo = P.outoff[lu];
-  const uint32_t T = P.tstar[L.seg], rt = P.rtie[L.seg];
-  const float mn = RAW ? 0.0f : P.mn[L.seg];
-  const float scale = RAW ? 0.0f : P.scale[L.seg];
-  const uint2* R = P.cand + (uint64_t)lu * UNIT;
-  const uint64_t obase = L.out_off + oo;
-  uint32_t eqc = 0, outc = 0;
-  for (uint32_t i0 = 0; i0 < nC; i0 += 64) {
-    const uint32_t i = i0 + lane;
-    const bool valid = i < nC;
-    const uint2 rec = R[min(i, nC - 1)];  // unconditional load (clamped index)
-    const float x = __uint_as_float(rec.y);
-    const uint32_t key = fkey(x);
-    const bool e = valid && key == T;
-    const uint64_t eb = __ballot(e);
-    const uint32_t rank = eqp + eqc + mbcnt(eb);
-    eqc += (uint32_t)__popcll(eb);
-    const bool sel = valid && (key > T || (e && rank < rt));
-    const uint64_t sb = __ballot(sel);
-    if (sel) {
-      const uint64_t o = obase + outc + mbcnt(sb);
-      P.idx[o] = (int32_t)(rec.x & ~A_FLAG);
-      store_val<RAW>(P, o, x, mn, scale);
+  const uint32_t lu0 = (blockIdx.x * WAVES + wv) * EMIT_UPW;
+  if (lu0 >= P.n_lunits) return;
+  // round 1 / 2: lane g < EMIT_UPW holds unit lu0 + g's count, offsets and its segment's T*, tie budget,
+  // mn, scale (lanes past EMIT_UPW or past the last unit repeat a valid unit; never used)
+  const uint32_t lug = min(lu0 + min(lane, EMIT_UPW - 1), P.n_lunits - 1);
+  const uint32_t nCg = P.cntC[lug];
+  const uint32_t segg = P.lunits[lug].seg;
+  const uint64_t sog = P.lunits[lug].out_off;
+  const uint32_t eqpg = P.eqpre[lug], oog = P.outoff[lug];
+  const uint32_t Tg = P.tstar[segg], rtg = P.rtie[segg];
+  const float mng = RAW ? 0.0f : P.mn[segg];
+  const float scg = RAW ? 0.0f : P.scale[segg];
+  uint2 rec0[EMIT_UPW];
+#pragma unroll
+  for (uint32_t g = 0; g < EMIT_UPW; ++g) {
+    const uint32_t lu = min(lu0 + g, P.n_lunits - 1), nC = rl(nCg, g);
+    rec0[g] = P.cand[(uint64_t)lu * UNIT + min(lane, nC ? nC - 1 : 0u)];  // unconditional (clamped) load
+  }
+#pragma unroll
+  for (uint32_t g = 0; g < EMIT_UPW; ++g) {
+    const uint32_t nC = rl(nCg, g);
+    if (lu0 + g < P.n_lunits && nC != 0) {
+      const uint32_t lu = lu0 + g;
+      const uint32_t T = rl(Tg, g), rt = rl(rtg, g), eqp = rl(eqpg, g);
+      const float mn = __uint_as_float(rl(__float_as_uint(mng), g));
+      const float scale = __uint_as_float(rl(__float_as_uint(scg), g));
+      const uint64_t so = ((uint64_t)rl((uint32_t)(sog >> 32), g) << 32) | rl((uint32_t)sog, g);
+      const uint64_t obase = so + rl(oog, g);
+      const uint2* R = P.cand + (uint64_t)lu * UNIT;
+      uint32_t eqc = 0, outc = 0;
+      for (uint32_t i0 = 0; i0 < nC; i0 += 64) {
+        const uint32_t i = i0 + lane;
+        const bool valid = i < nC;
+        const uint2 rec = i0 == 0 ? rec0[g] : R[min(i, nC - 1)];
+        const float x = __uint_as_float(rec.y);
+        const uint32_t key = fkey(x);
+        const bool e = valid && key == T;
+        const uint64_t eb = __ballot(e);
+        const uint32_t rank = eqp + eqc + mbcnt(eb);
+        eqc += (uint32_t)__popcll(eb);
+        const bool sel = valid && (key > T || (e && rank < rt));
+        const uint64_t sb = __ballot(sel);
+        if (sel) {
+          const uint64_t o = obase + outc + mbcnt(sb);
+          P.idx[o] = (int32_t)(rec.x & ~A_FLAG);
+          store_val<RAW>(P, o, x, mn, scale);
+        }
+        outc += (uint32_t)__popcll(sb);
+      }
     }
-    outc += (uint32_t)__popcll(sb);
   }
 }
 
@@ -1840,7 +1901,7 @@ int launch_encode(const Params& P, coalac_plan_t plan, hipStream_t st, const coa
     hipLaunchKernelGGL((k_select<DELTA, RAW>), dim3(plan->n_large), dim3(SEL_NT), 0, st, P);
   }
   ENC_BOUNDARY(3);
-  if ((stages & COALAC_STAGE_SELECT) && plan->n_large) hipLaunchKernelGGL((k_emit<RAW>), dim3(gu), dim3(BLOCK), 0, st, P);
+  if ((stages & COALAC_STAGE_SELECT) && plan->n_large) hipLaunchKernelGGL((k_emit<RAW>), dim3((plan->n_lunits + WAVES * EMIT_UPW - 1) / (WAVES * EMIT_UPW)), dim3(BLOCK), 0, st, P);
   if (fork) HIP_CHECK(hipStreamWaitEvent(st, plan->join, 0));
   ENC_BOUNDARY(4);
 #undef ENC_BOUNDARY
