@@ -494,7 +494,27 @@ DEV void scan_unit(const Params& P, uint32_t lu, const UnitDev& L, uint32_t tlo,
         fa[j] = fc[j] && key > thi;
         any = any || fc[j];
       }
-      if (!__any(any)) continue;
+      const uint32_t c = (uint32_t)fc[0] + (uint32_t)fc[1] + (uint32_t)fc[2] + (uint32_t)fc[3];
+      const uint64_t b1 = __ballot(any);
+      if (b1 == 0) continue;
+      if (__ballot(c >= 2) == 0) {
+        // common case (~1.5 % candidates: ~4 per 256-element row): at most one candidate per lane, so its
+        // position is one mbcnt instead of four, and each lane writes at most one record
+        cA += (uint32_t)__popcll(__ballot(fa[0] || fa[1] || fa[2] || fa[3]));
+        if (any) {
+          const uint32_t pc = cC + mbcnt(b1);
+          const uint32_t j = fc[0] ? 0u : fc[1] ? 1u : fc[2] ? 2u : 3u;
+          const float xj = j == 0 ? xs[0] : j == 1 ? xs[1] : j == 2 ? xs[2] : xs[3];
+          const bool aj = fa[0] || fa[1] || fa[2] || fa[3];
+          const uint2 rec = make_uint2((L.start + e0 + j) | (aj ? A_FLAG : 0u), __float_as_uint(xj));
+          if (stage != nullptr && pc < STAGE_CAP)
+            stage[pc] = rec;
+          else
+            R[pc] = rec;
+        }
+        cC += (uint32_t)__popcll(b1);
+        continue;
+      }
       uint64_t bc[4];
       uint32_t pc = cC;
 #pragma unroll

@@ -9,6 +9,7 @@ mkdir -p $O
 export TMPDIR=/tmp
 timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_pipeline.py -x -q -m gpu \
   --timeout 120 --timeout-method thread > $O/pytest.log 2>&1
+timeout -k 10 120 python tools/stage_probe.py > $O/stage_probe.json 2>&1
 for i in 1 2; do
   timeout -k 10 120 python bench.py --no-cpu-baseline > $O/bench$i.json 2> $O/bench$i.err
 done
