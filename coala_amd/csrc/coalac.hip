@@ -1496,32 +1496,31 @@ __global__ __launch_bounds__(BLOCK, DECODE_WPE) void k_decode(Params P) {
     // buffer resources over exactly this unit: base loads past len return 0, stores past len are
     // dropped, so partial units take the same straight-line path
     const __amdgpu_buffer_rsrc_t rout = unit_rsrc(P.out + U[r].off, len);
+    // kept values are merged into zeros first; with a base, the base is read afterwards and added one
+    // float4 at a time (out = base + v where kept, base + 0.0f elsewhere: -0 -> +0, as the oracle's
+    // base + dense). Loading the base before the merge held 2 x 64 VGPRs live and spilled to scratch.
     float4 b[UNIT_IT];
-    if (HASBASE) {
-      const __amdgpu_buffer_rsrc_t rb = unit_rsrc(P.base + U[r].off, len);
 #pragma unroll
-      for (uint32_t it = 0; it < UNIT_IT; ++it) b[it] = unit_load_x4<false>(rb, rb, (it * 64 + lane) * 16);
-    } else {
-#pragma unroll
-      for (uint32_t it = 0; it < UNIT_IT; ++it) b[it] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-    }
+    for (uint32_t it = 0; it < UNIT_IT; ++it) b[it] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
     uint64_t kept = 0;
     const uint32_t cnt = hi[r] - lo[r];
-    merge_entries<HASBASE>(b, kept, pos[r], code_value<RAW>(q[r], mn[r], sc[r]), min(cnt, 64u), lane);
+    merge_entries<false>(b, kept, pos[r], code_value<RAW>(q[r], mn[r], sc[r]), min(cnt, 64u), lane);
     for (uint32_t e0 = lo[r] + 64; e0 < hi[r]; e0 += 64) {  // more than 64 kept entries in the unit
       const uint64_t e = U[r].out_off + min(e0 + lane, hi[r] - 1);
       const uint32_t p2 = (uint32_t)P.cidx[e] - U[r].start;
       const float v2 = code_value<RAW>(load_code<RAW>(P, e), mn[r], sc[r]);
-      merge_entries<HASBASE>(b, kept, p2, v2, min(hi[r] - e0, 64u), lane);
+      merge_entries<false>(b, kept, p2, v2, min(hi[r] - e0, 64u), lane);
     }
     if (HASBASE) {
+      const __amdgpu_buffer_rsrc_t rb = unit_rsrc(P.base + U[r].off, len);
 #pragma unroll
-      for (uint32_t it = 0; it < UNIT_IT; ++it) {  // base + 0.0f where nothing was kept (-0 -> +0, as the
-        const uint32_t m = (uint32_t)(kept >> (it * 4)) & 15u;  // oracle's base + dense)
-        b[it].x = (m & 1u) ? b[it].x : b[it].x + 0.0f;
-        b[it].y = (m & 2u) ? b[it].y : b[it].y + 0.0f;
-        b[it].z = (m & 4u) ? b[it].z : b[it].z + 0.0f;
-        b[it].w = (m & 8u) ? b[it].w : b[it].w + 0.0f;
+      for (uint32_t it = 0; it < UNIT_IT; ++it) {
+        const float4 a = unit_load_x4<false>(rb, rb, (it * 64 + lane) * 16);
+        const uint32_t m = (uint32_t)(kept >> (it * 4)) & 15u;
+        b[it].x = a.x + ((m & 1u) ? b[it].x : 0.0f);
+        b[it].y = a.y + ((m & 2u) ? b[it].y : 0.0f);
+        b[it].z = a.z + ((m & 4u) ? b[it].z : 0.0f);
+        b[it].w = a.w + ((m & 8u) ? b[it].w : 0.0f);
       }
     }
     if ((len & 3u) == 0) {  // wave-uniform: one non-temporal float4 buffer store per slot
