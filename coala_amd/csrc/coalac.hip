@@ -71,6 +71,9 @@ constexpr int SEL_NT = 256;               // threads of a k_select block (4 wave
 #ifndef DECODE_WPE
 #define DECODE_WPE 5
 #endif
+#ifndef SCAN_NB
+#define SCAN_NB 1  // load batches per k_scan unit (weights mode): 1 = all 16 float4 per lane in flight
+#endif
 constexpr uint32_t STAGE_CAP = 512;       // candidate records staged in LDS per k_scan wave
 constexpr uint32_t GU = 32;               // units per select group (k_ghist / k_gwin block)
 constexpr uint32_t HB2 = 512;             // bins of the per-group band histograms
@@ -807,7 +810,7 @@ __global__ __launch_bounds__(BLOCK, SCAN_WPE) void k_scan(Params P) {
   if (lu >= P.n_lunits) return;
   const UnitDev L = P.lunits[lu];
   // delta: 4 load batches (32 float4 in flight spill)
-  scan_unit<DELTA, DELTA ? 4 : 1>(P, lu, L, P.tlo[lu], P.thi[lu], stage + wv * STAGE_CAP);
+  scan_unit<DELTA, DELTA ? 4 : SCAN_NB>(P, lu, L, P.tlo[lu], P.thi[lu], stage + wv * STAGE_CAP);
 }
 
 // ------------------------------------------------------------------------------------------------
