@@ -1365,7 +1365,9 @@ __global__ __launch_bounds__(SEL_NT) void k_select(Params P) {
 // records: here lane g loads unit g's metadata (two dependent rounds for all units at once) and every
 // unit's first 64 records are in flight before the first one is classified.
 // ------------------------------------------------------------------------------------------------
-constexpr uint32_t EMIT_UPW = 8;
+#ifndef EMIT_UPW
+#define EMIT_UPW 8u  // large units per k_emit wave
+#endif
 
 DEV uint32_t rl(uint32_t v, uint32_t l) { return (uint32_t)__builtin_amdgcn_readlane((int)v, (int)l); }
 
