@@ -18,6 +18,7 @@ COALAC_STAGE_SAMPLE, COALAC_STAGE_SCAN, COALAC_STAGE_SELECT, COALAC_STAGE_SMALL 
 COALAC_STAGE_BOUNDS, COALAC_STAGE_DECODE = 1, 2
 COALAC_AGG_DIV = 0     # acc / total            (torch CPU division by a scalar)
 COALAC_AGG_RECIP = 1   # acc * (1.0f / total)   (torch GPU division by a host scalar)
+COALAC_AGG_SUM = 2     # acc                    (weighted_sum: the multi-GPU per-rank sum)
 
 ERRORS = {
     -1: "COALAC_EINVAL",

@@ -24,7 +24,7 @@ from torch import nn
 
 from . import wire
 from .plan import CodecPlan, Encoded
-from .spec import ALIGN, RAW_BITS, VALID_BITS, align_up, k_for
+from .spec import ALIGN, RAW_BITS, VALID_BITS, SegmentTable, align_up, k_for
 
 MODES = ("delta", "weights")
 
@@ -36,6 +36,9 @@ class HipBackend:
 
     def default_device(self):
         return torch.device("cuda", torch.cuda.current_device())
+
+    def runs_on(self, device):
+        return torch.device(device).type == "cuda"
 
     def make_plan(self, sizes, ratio, bits, device, clients=1):
         if device.type != "cuda":
@@ -51,6 +54,19 @@ class FlatState:
         self.entries = entries  # list of dicts: name, dtype, shape, kind, (seg, off, n) | ()
         self.flat = flat        # fp32 [span] on device (None if no fp32 entry)
         self.raw = raw          # OrderedDict name -> tensor
+        self._on = {}           # device -> flat copy (a snapshot taken on one device, used on another)
+
+    def flat_on(self, device):
+        """The flat buffer on `device` (copied once per device and cached: the w_global snapshot of a
+        round is immutable)."""
+        if self.flat is None or self.flat.device == torch.device(device):
+            return self.flat
+        key = str(device)
+        t = self._on.get(key)
+        if t is None:
+            t = self.flat.to(device)
+            self._on[key] = t
+        return t
 
 
 def layout_of(state):
@@ -96,10 +112,24 @@ class CompressedUpdate:
     raw passthrough entries. Pickles to the COALAQ1 blob (wire.py).
     """
 
-    def __init__(self, header, encoded, raw):
+    def __init__(self, header, encoded, raw, blob=None):
         self.header = header
         self.encoded = encoded
         self.raw = raw
+        # the packed COALAQ1 bytes, built on first pickle and shared by every deep copy: the reference
+        # pickles copy.deepcopy(self.model) (client/base.py:363), so the payload is packed once
+        self._blob = [blob]
+
+    def __deepcopy__(self, memo):
+        # The encoded payload is immutable after encode: a deep copy shares it (and the packed blob)
+        # instead of a D2H + pack + unpack round trip through __getstate__/__setstate__.
+        other = CompressedUpdate.__new__(CompressedUpdate)
+        other.header = copy.deepcopy(self.header, memo)
+        other.encoded = self.encoded
+        other.raw = self.raw
+        other._blob = self._blob
+        memo[id(self)] = other
+        return other
 
     # -- size accounting (client/base.py:155, 474-487) -------------------------------------------
     @property
@@ -117,6 +147,11 @@ class CompressedUpdate:
 
     # -- wire -------------------------------------------------------------------------------------
     def to_bytes(self):
+        if self._blob[0] is None:
+            self._blob[0] = self._pack()
+        return self._blob[0]
+
+    def _pack(self):
         h = dict(self.header)
         raw_entries, chunks, pos = [], [], 0
         for e in h["entries"]:
@@ -147,7 +182,7 @@ class CompressedUpdate:
                 raw[e["name"]] = t.reshape(e["shape"]).clone()
         enc = Encoded(torch.from_numpy(idx.copy()), torch.from_numpy(vals.copy()),
                       torch.from_numpy(mn.copy()), torch.from_numpy(scale.copy()))
-        return cls(h, enc, raw)
+        return cls(h, enc, raw, blob=bytes(blob))
 
     def __getstate__(self):
         return {"blob": self.to_bytes()}
@@ -155,6 +190,14 @@ class CompressedUpdate:
     def __setstate__(self, state):
         other = CompressedUpdate.from_bytes(state["blob"])
         self.__dict__.update(other.__dict__)
+
+    @property
+    def compression_ratio(self):
+        """Dense fp32 (+ raw) bytes of the update / its payload bytes."""
+        h = self.header
+        dense = 4 * sum(e["n"] for e in h["entries"] if e["kind"] == "seg")
+        dense += sum(t.numel() * t.element_size() for t in self.raw.values())
+        return dense / max(1, self.nbytes)
 
     def __repr__(self):
         h = self.header
@@ -171,6 +214,13 @@ def validate(header, idx):
     segs = [e for e in header["entries"] if e["kind"] == "seg"]
     if len(segs) != int(header["n_segments"]):
         raise ValueError("COALAQ1: segment count mismatch")
+    # the decoder slices its output with the offsets it derives itself (SegmentTable of the sizes); a
+    # header whose own offsets / sizes disagree with that, or with the tensor shapes, is corrupt
+    table = SegmentTable([e["n"] for e in segs], header["ratio"], 1) if segs else None
+    for i, e in enumerate(segs):
+        if int(e["seg"]) != i or int(e["n"]) != int(np.prod(e["shape"], dtype=np.int64)) or \
+                int(e["off"]) != table.offsets[i]:
+            raise ValueError(f"COALAQ1: segment entry {e.get('name')!r} has inconsistent seg/n/off/shape")
     ks = np.array([k_for(e["n"], header["ratio"]) for e in segs], dtype=np.int64)
     if int(ks.sum()) != int(header["total_k"]) or idx.size != int(header["total_k"]):
         raise ValueError("COALAQ1: kept-entry count mismatch")
@@ -226,7 +276,10 @@ class UpdateCodec:
     # -- encode -----------------------------------------------------------------------------------
     def encode(self, state, base=None, device=None):
         """state_dict -> CompressedUpdate. `base` (delta mode): FlatState of w_global (same layout).
-        `device`: where to flatten and encode (default: where the state lives)."""
+        `device`: where to flatten and encode (default: where the state lives if the backend runs there,
+        else the backend's default device — a model trained on the CPU is encoded on the GPU)."""
+        if device is None:
+            device = self._device_for(state)
         fs = flatten_state(state, device=device)
         if self.mode == "delta" and base is None:
             raise ValueError("delta mode needs the global-model snapshot (base)")
@@ -240,16 +293,27 @@ class UpdateCodec:
         base_flat = None
         if self.mode == "delta":
             _check_same_layout(fs.entries, base.entries)
-            base_flat = base.flat
+            # the snapshot may have been taken where the global model arrived (the reference client's
+            # set_model runs before pretrain moves the model to its device, client/base.py:138 vs :245)
+            base_flat = base.flat_on(fs.flat.device)
         plan = self.plan_for(sizes, fs.flat.device)
         enc = plan.encode(fs.flat, base=base_flat)
         header["total_k"] = int(plan.table.total_k)
         return CompressedUpdate(header, enc, fs.raw)
 
-    def snapshot(self, module_or_state):
-        """FlatState of a model (the w_global snapshot for delta mode)."""
+    def _device_for(self, state):
+        for t in state.values():
+            if t.dtype == torch.float32 and t.numel() > 0:
+                runs = getattr(self.backend, "runs_on", None)
+                return t.device if runs is None or runs(t.device) else self.backend.default_device()
+        return None
+
+    def snapshot(self, module_or_state, device=None):
+        """FlatState of a model (the w_global snapshot for delta mode), flattened on `device` (default:
+        where the codec will run: the state's own device if the backend runs there, else the backend's
+        default device)."""
         state = module_or_state.state_dict() if isinstance(module_or_state, nn.Module) else module_or_state
-        return flatten_state(state)
+        return flatten_state(state, device=device if device is not None else self._device_for(state))
 
     # -- decode -----------------------------------------------------------------------------------
     def decode_state(self, update, base=None, device=None):
@@ -258,20 +322,24 @@ class UpdateCodec:
         sizes = [e["n"] for e in h["entries"] if e["kind"] == "seg"]
         state = OrderedDict()
         flat = None
+        offs = None
         if sizes:
+            if device is None:
+                device = self.backend.default_device()
+            base_flat = None
             if h["mode"] == "delta":
                 if base is None:
                     raise ValueError("delta-mode update needs the global model (base) to decode")
                 _check_same_layout(h["entries"], base.entries)
-                device = base.flat.device
-            elif device is None:
-                device = self.backend.default_device()
+                base_flat = base.flat_on(device)
             plan = self.plan_for(sizes, device, ratio=h["ratio"], bits=h["bits"])
             enc = update.encoded.to(device, non_blocking=True)
-            flat = plan.decode(enc, base=base.flat if h["mode"] == "delta" else None)
+            flat = plan.decode(enc, base=base_flat)
+            offs = plan.table.offsets  # the decoder's own offsets, never the (untrusted) header's
         for e in h["entries"]:
             if e["kind"] == "seg":
-                state[e["name"]] = flat[e["off"]:e["off"] + e["n"]].view(e["shape"])
+                o = offs[e["seg"]]
+                state[e["name"]] = flat[o:o + e["n"]].view(e["shape"])
             else:
                 t = update.raw[e["name"]]
                 state[e["name"]] = t.to(device) if device is not None else t
@@ -288,16 +356,18 @@ class UpdateCodec:
 
 
     # -- fused server-side aggregation ------------------------------------------------------------
-    def aggregate(self, updates, weights, template, base=None, mode="recip"):
+    def aggregate(self, updates, weights, template, base=None, mode="recip", device=None):
         """Fused decode + FedAvg of several CompressedUpdates of one layout -> new nn.Module.
 
         Equivalent to decode_module() of every update followed by the reference's
         strategies.federated_averaging(models, weights) (coala/server/strategies.py:6-29, 57-90), with
         the fp32 entries decoded and averaged in ONE kernel (coalac_aggregate) instead of C dense
         modules. mode "recip": torch-on-GPU division semantics (the decoded modules live on the GPU);
-        "div": torch-on-CPU. Non-fp32 entries (int64 BatchNorm counters) are averaged with the same
-        torch ops as the reference, on the output device. Weights follow federated_averaging: empty or
-        all-zero weights become 1 per update.
+        "div": torch-on-CPU; "sum": strategies.weighted_sum (:57-90) — no division, the module a
+        multi-GPU server passes to reduce_models (coala/distributed/distributed.py:42-57). Non-fp32
+        entries (int64 BatchNorm counters) are combined with the same torch ops as the reference, on the
+        output device. Weights follow federated_averaging / weighted_sum: empty or all-zero weights
+        become 1 per update.
         """
         if not updates:
             return None
@@ -313,31 +383,33 @@ class UpdateCodec:
             if (h["ratio"], h["bits"], h["mode"], h["entries"]) != (h0["ratio"], h0["bits"], h0["mode"], h0["entries"]):
                 raise ValueError("fused aggregation needs updates of one layout / ratio / bits / mode")
         sizes = [e["n"] for e in h0["entries"] if e["kind"] == "seg"]
+        device = self.backend.default_device() if device is None else torch.device(device)
+        base_flat = None
         if h0["mode"] == "delta":
             if base is None:
                 raise ValueError("delta-mode updates need the global model (base) to aggregate")
             _check_same_layout(h0["entries"], base.entries)
-            device = base.flat.device if base.flat is not None else self.backend.default_device()
-        else:
-            device = self.backend.default_device()
+            base_flat = base.flat_on(device)
         state = OrderedDict()
         flat = None
+        offs = None
         if sizes:
             C = len(updates)
             plan = self.plan_for(sizes, device, ratio=h0["ratio"], bits=h0["bits"], clients=C)
             encs = [u.encoded.to(device, non_blocking=True) for u in updates]
             batched = Encoded(*(torch.cat([getattr(e, f) for e in encs]) for f in ("idx", "vals", "mn", "scale")))
-            flat = plan.aggregate(batched, weights, total=total,
-                                  base=base.flat if h0["mode"] == "delta" else None, mode=mode)
+            flat = plan.aggregate(batched, weights, total=total, base=base_flat, mode=mode)
+            offs = plan.table.offsets
         for e in h0["entries"]:
             if e["kind"] == "seg":
-                state[e["name"]] = flat[e["off"]:e["off"] + e["n"]].view(e["shape"])
-            else:  # restated weighted_sum + torch.div on the raw entries, then the dtype cast load_state_dict does
+                o = offs[e["seg"]]
+                state[e["name"]] = flat[o:o + e["n"]].view(e["shape"])
+            else:  # restated weighted_sum (+ torch.div) on the raw entries
                 acc = updates[0].raw[e["name"]].to(device).clone()
                 acc *= weights[0]
                 for i in range(1, len(updates)):
                     acc += updates[i].raw[e["name"]].to(device) * weights[i]
-                state[e["name"]] = torch.div(acc, total).to(acc.dtype)
+                state[e["name"]] = acc if mode == "sum" else torch.div(acc, total).to(acc.dtype)
         return module_with_state(template, state)
 
 

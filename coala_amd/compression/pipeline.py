@@ -53,6 +53,25 @@ def split_lanes(sizes, lanes):
     return [(a, b) for a, b in zip(cuts[:-1], cuts[1:]) if b > a]
 
 
+def balanced_cuts(costs, parts):
+    """Cut a client list into `parts` contiguous non-empty ranges of about equal total cost (element
+    count): returns the cut points [0, ..., len(costs)]. Equal costs give equal client counts."""
+    C = len(costs)
+    parts = max(1, min(int(parts), C))
+    pre = [0]
+    for c in costs:
+        pre.append(pre[-1] + int(c))
+    total = pre[-1]
+    cuts = [0]
+    for g in range(1, parts):
+        target = total * g / parts
+        # first cut point whose prefix reaches the target, keeping every range non-empty
+        j = max(cuts[-1] + 1, min(range(1, C), key=lambda i: abs(pre[i] - target)))
+        cuts.append(min(j, C - (parts - g)))
+    cuts.append(C)
+    return cuts
+
+
 class LanePipeline:
     """Encode / decode a SegmentTable's batch as L pipelined lanes on one GPU.
 
@@ -256,17 +275,17 @@ class SplitPipeline:
                                    else torch.device(device).index or 0)
         C = max(1, int(table.clients))
         S = max(1, min(int(split), C))
-        cuts = [round(g * C / S) for g in range(S + 1)]
+        cuts = balanced_cuts(table.client_elements(), S)
         # several sub-batches already run side by side: no per-plan side stream for the small segments
         # (HIP maps streams onto 4 hardware queues; a side stream sharing one with the other sub-batch
         # would queue its k_small behind that sub-batch's kernels)
         self.fork_flag = _lib.COALAC_FLAG_NO_FORK if S > 1 and fork is False else 0
-        sp, kp, tp = table.span_per_client, table.total_k_per_client, table.n_segments // C
+        so, ko, to = table.client_span_off, table.client_k_off, table.client_seg_off
         self.parts = []
         with torch.cuda.device(self.device):
             for c0, c1 in zip(cuts[:-1], cuts[1:]):
-                plan = CodecPlan(table.sizes, table.ratio, self.bits, clients=c1 - c0, device=self.device)
-                self.parts.append(dict(x=slice(c0 * sp, c1 * sp), k=slice(c0 * kp, c1 * kp), t=slice(c0 * tp, c1 * tp),
+                plan = CodecPlan(None, table.ratio, self.bits, device=self.device, table=table.sub_table(c0, c1))
+                self.parts.append(dict(x=slice(so[c0], so[c1]), k=slice(ko[c0], ko[c1]), t=slice(to[c0], to[c1]),
                                        plan=plan, ws=plan.empty_workspace(), dws=plan.empty_decode_workspace(),
                                        stream=torch.cuda.Stream(self.device)))
 

@@ -5,6 +5,7 @@ used purely as device memory; streams are torch's current HIP stream unless one 
 argument is checked against what the kernels assume (dtype, device, contiguity, length, 16-B
 alignment) BEFORE a launch.
 """
+import contextlib
 import ctypes
 from dataclasses import dataclass
 
@@ -29,6 +30,12 @@ class Encoded:
 
 def _ptr(t):
     return ctypes.c_void_p(t.data_ptr()) if t is not None else ctypes.c_void_p(0)
+
+
+def _on(stream):
+    """Allocation context for buffers a call creates itself: on the stream the kernels run on, so the
+    caching allocator never hands their memory to other work before those kernels are done."""
+    return torch.cuda.stream(stream) if stream is not None else contextlib.nullcontext()
 
 
 def _stream_handle(stream):
@@ -146,9 +153,10 @@ class CodecPlan:
         record[, stages]) — lists of 5 events (or None) and a COALAC_STAGE_* mask (coalac_encode_sched)."""
         self._check_flat(flat, "input")
         self._check_flat(base, "base")
-        out = self.empty_encoded() if out is None else out
+        with _on(stream):
+            out = self.empty_encoded() if out is None else out
+            ws = self.empty_workspace() if workspace is None else workspace
         self._check_encoded(out)
-        ws = self.empty_workspace() if workspace is None else workspace
         if ws.device != self.device or ws.numel() * ws.element_size() < self.ws_bytes:
             raise ValueError(f"workspace: need {self.ws_bytes} bytes on {self.device}")
         args = (self._h, _ptr(flat), _ptr(base), _ptr(out.idx), _ptr(out.vals), _ptr(out.mn),
@@ -170,10 +178,11 @@ class CodecPlan:
         events / sched: as encode(), 3 boundaries (coalac_decode_ev / coalac_decode_sched)."""
         self._check_encoded(enc)
         self._check_flat(base, "base")
-        if out is None:
-            out = self.empty_flat() if base is None else torch.empty_like(base)
+        with _on(stream):
+            if out is None:
+                out = self.empty_flat() if base is None else torch.empty_like(base)
+            ws = self.empty_decode_workspace() if workspace is None else workspace
         self._check_flat(out, "output")
-        ws = self.empty_decode_workspace() if workspace is None else workspace
         if ws.device != self.device or ws.numel() * ws.element_size() < self.dec_ws_bytes:
             raise ValueError(f"decode workspace: need {self.dec_ws_bytes} bytes on {self.device}")
         args = (self._h, _ptr(enc.idx), _ptr(enc.vals), _ptr(enc.mn), _ptr(enc.scale), _ptr(base), _ptr(out),
@@ -197,26 +206,31 @@ class CodecPlan:
         sum(weights)). Returns out fp32[span_per_client] indexed like client 0's segments:
         base + decoded_i averaged exactly as coala/server/strategies.py:6-29,57-90 would on the decoded
         modules — mode "recip" reproduces torch on the GPU (division by a host scalar becomes a multiply
-        by its fp32 reciprocal), "div" torch on the CPU.
+        by its fp32 reciprocal), "div" torch on the CPU, "sum" stops before the division (weighted_sum,
+        strategies.py:57-90: what a multi-GPU server hands to reduce_models, distributed.py:42-57).
         """
         self._check_encoded(enc)
+        if not getattr(self.table, "uniform", False):
+            raise ValueError("fused aggregation needs a plan over copies of one layout (a SegmentTable)")
         C = self.table.clients
         if len(weights) != C:
             raise ValueError(f"need {C} weights, got {len(weights)}")
-        if mode not in ("recip", "div"):
-            raise ValueError(f"mode must be 'recip' or 'div', got {mode!r}")
+        modes = {"recip": _lib.COALAC_AGG_RECIP, "div": _lib.COALAC_AGG_DIV, "sum": _lib.COALAC_AGG_SUM}
+        if mode not in modes:
+            raise ValueError(f"mode must be one of {sorted(modes)}, got {mode!r}")
         n_out = self.table.span_per_client
         if base is not None:
             self._check_flat(base, "base", n_out)
-        out = torch.empty(n_out, dtype=torch.float32, device=self.device) if out is None else out
+        with _on(stream):
+            out = torch.empty(n_out, dtype=torch.float32, device=self.device) if out is None else out
+            ws = self.empty_decode_workspace() if workspace is None else workspace
+            w = torch.tensor([float(x) for x in weights], dtype=torch.float64).to(torch.float32).to(self.device)
         self._check_flat(out, "output", n_out)
-        ws = self.empty_decode_workspace() if workspace is None else workspace
         if ws.device != self.device or ws.numel() * ws.element_size() < self.dec_ws_bytes:
             raise ValueError(f"aggregate workspace: need {self.dec_ws_bytes} bytes on {self.device}")
-        w = torch.tensor([float(x) for x in weights], dtype=torch.float64).to(torch.float32).to(self.device)
         total = float(sum(weights)) if total is None else float(total)
         args = (self._h, C, _ptr(enc.idx), _ptr(enc.vals), _ptr(enc.mn), _ptr(enc.scale), _ptr(w),
-                ctypes.c_float(total), _lib.COALAC_AGG_RECIP if mode == "recip" else _lib.COALAC_AGG_DIV,
+                ctypes.c_float(total), modes[mode],
                 _ptr(base), _ptr(out), _ptr(ws), ctypes.c_uint64(self.dec_ws_bytes), _stream_handle(stream))
         with torch.cuda.device(self.device):
             if events is None:
@@ -224,8 +238,7 @@ class CodecPlan:
             else:
                 rc = self._lib.coalac_aggregate_ev(*args, _event_array(events, 3))
         _lib.check(rc, "coalac_aggregate")
-        self._keepalive = w  # the weights buffer must outlive the asynchronous launch
-        return out
+        return out  # w was allocated on the launch stream: its memory is reused only after the kernel
 
     def fallbacks(self, workspace, stream=None):
         """Segments of the last encode with this workspace whose sampled bracket missed (synchronises)."""

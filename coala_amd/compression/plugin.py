@@ -47,6 +47,7 @@ from .codec import CompressedUpdate, UpdateCodec
 from .download import CompressedModel, compress_model
 
 EQUAL_AVERAGE = "equal"                     # coala/server/base.py:37
+TRAIN_UPLOAD_COMPRESSION_RATIO = "train_upload_compression_ratio"  # tracked next to metric.TRAIN_UPLOAD_SIZE
 AGGREGATION_CONTENT_PARAMS = "parameters"   # coala/server/base.py:40
 
 
@@ -99,6 +100,11 @@ class CompressionClientMixin(_CodecOwner):
         update = codec.encode(model.state_dict(), base=base)
         self._codec_trained_model = model
         self.model = update
+        # §8(f) 3: the compression ratio next to TRAIN_UPLOAD_SIZE (client/base.py:155); an unknown
+        # metric name lands in the tracker's "extra" dict (coala/tracking/metric.py:64-73)
+        track = getattr(self, "track", None)
+        if track is not None and getattr(getattr(self, "conf", None), "track", True):
+            track(TRAIN_UPLOAD_COMPRESSION_RATIO, update.compression_ratio)
 
     def post_upload(self):
         trained = self.__dict__.pop("_codec_trained_model", None)
@@ -109,12 +115,24 @@ class CompressionClientMixin(_CodecOwner):
             parent()
 
     def calculate_model_size(self, model, param_size=32):
-        if isinstance(model, CompressedUpdate):
+        # real payload sizes for the carriers: the upload (client/base.py:155) and a compressed
+        # download (TRAIN/TEST_DOWNLOAD_SIZE, client/base.py:139, :178)
+        if isinstance(model, (CompressedUpdate, CompressedModel)):
             return _bit_to_megabyte(model.nbytes * 8)
         parent = getattr(super(), "calculate_model_size", None)
         if parent is not None:
             return parent(model, param_size)
         return _bit_to_megabyte(sum(p.numel() for p in model.parameters()) * param_size)
+
+
+def reduce_models():
+    """The reference's reduce_models (coala/distributed/distributed.py:42-57) when COALA is installed,
+    else its restatement (coala_amd/fl/distributed.py)."""
+    try:
+        from coala.distributed.distributed import reduce_models as fn
+    except ImportError:
+        from ..fl.distributed import reduce_models as fn
+    return fn
 
 
 class CompressionServerMixin(_CodecOwner):
@@ -202,11 +220,14 @@ class CompressionServerMixin(_CodecOwner):
         return model
 
     def aggregate(self, models, weights):
+        """server/base.py:573-601 with the fused decode: FedAvg in one kernel (single process), or in a
+        multi-GPU run the per-rank weighted sum in one kernel followed by the reference's reduce_models
+        (:595-598), exactly the two calls the reference makes on decoded modules."""
         conf = getattr(self, "conf", None)
         server_conf = getattr(conf, "server", None)
         distributed = bool(getattr(conf, "is_distributed", False))
         params_only = getattr(server_conf, "aggregation_content", "all") == AGGREGATION_CONTENT_PARAMS
-        fusable = (self.codec_fused_aggregate and models and not distributed and not params_only
+        fusable = (self.codec_fused_aggregate and models and not params_only
                    and all(isinstance(m, CompressedUpdate) for m in models))
         if fusable:
             if getattr(server_conf, "aggregation_strategy", None) == EQUAL_AVERAGE:
@@ -217,10 +238,17 @@ class CompressionServerMixin(_CodecOwner):
                    for m in models):
                 base = self._global_snapshot() if h0["mode"] == "delta" else None
                 codec = self._codec()
-                dev = base.flat.device if base is not None and base.flat is not None else \
-                    codec.backend.default_device()
+                dev = codec.backend.default_device()
+                if distributed:
+                    import torch
+                    import torch.distributed as dist
+                    dist.barrier()
+                    sample_sum = sum(weights)  # weighted_sum returns the caller's sum (0 stays 0)
+                    model = codec.aggregate(models, weights, self._real_global(), base=base, mode="sum", device=dev)
+                    reduce_models()(model, torch.tensor(sample_sum).to(getattr(conf, "device", dev)))
+                    return model
                 mode = "div" if dev.type == "cpu" else "recip"  # torch's division semantics on that device
-                return codec.aggregate(models, weights, self._real_global(), base=base, mode=mode)
+                return codec.aggregate(models, weights, self._real_global(), base=base, mode=mode, device=dev)
         models = [self._decode_upload(m) if isinstance(m, CompressedUpdate) else m for m in models]
         parent = getattr(super(), "aggregate", None)
         if parent is not None:

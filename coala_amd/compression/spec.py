@@ -68,6 +68,8 @@ class SegmentTable:
                                    c * self.total_k_per_client + oofs[t])
         self.segs = segs
 
+    uniform = True  # clients are copies of one layout (fused aggregation needs this)
+
     @property
     def n_segments(self):
         return len(self.segs)
@@ -84,18 +86,108 @@ class SegmentTable:
     def n_elements(self):
         return self.clients * sum(self.sizes)
 
-    def algorithmic_bytes(self, bits=8, delta=False):
-        """HBM bytes an ideal encode+decode moves: 8N + 10K + 32T for 8-bit codes.
+    # per-client extents (client-major), as cumulative offsets of length clients + 1
+    @property
+    def client_span_off(self):
+        return [c * self.span_per_client for c in range(self.clients + 1)]
 
-        Encode reads 4N, writes idx (4K) + codes (1K, or 4K raw) + mn/scale/k/off (16T); decode reads
-        those and writes 4N. Delta mode adds a 4N base read on each side.
-        """
-        N, K, T = self.n_elements, self.total_k, self.n_segments
-        vb = 4 if bits == RAW_BITS else 1
-        b = 8 * N + 2 * (4 + vb) * K + 32 * T
-        if delta:
-            b += 8 * N
-        return b
+    @property
+    def client_k_off(self):
+        return [c * self.total_k_per_client for c in range(self.clients + 1)]
+
+    @property
+    def client_seg_off(self):
+        T = len(self.sizes)
+        return [c * T for c in range(self.clients + 1)]
+
+    def client_sizes(self, c):
+        return self.sizes
+
+    def client_elements(self):
+        return [sum(self.sizes)] * self.clients
+
+    def sub_table(self, c0, c1):
+        """Table of clients [c0, c1) with offsets relative to client c0's start."""
+        return SegmentTable(self.sizes, self.ratio, c1 - c0)
+
+    def algorithmic_bytes(self, bits=8, delta=False):
+        return algorithmic_bytes(self.n_elements, self.total_k, self.n_segments, bits, delta)
+
+
+def algorithmic_bytes(N, K, T, bits=8, delta=False):
+    """HBM bytes an ideal encode+decode moves: 8N + 10K + 32T for 8-bit codes.
+
+    Encode reads 4N, writes idx (4K) + codes (1K, or 4K raw) + mn/scale/k/off (16T); decode reads
+    those and writes 4N. Delta mode adds a 4N base read on each side.
+    """
+    vb = 4 if bits == RAW_BITS else 1
+    b = 8 * N + 2 * (4 + vb) * K + 32 * T
+    if delta:
+        b += 8 * N
+    return b
+
+
+class MixedTable:
+    """Segment table of clients with DIFFERENT layouts (splitFL client-side models of
+    several architectures and cut layers next to feature tensors), laid out client-major in one flat
+    buffer exactly like SegmentTable: every segment start ALIGN-aligned, each client's span a multiple
+    of ALIGN, each client's kept entries contiguous.
+
+    layouts: one list of fp32 segment sizes per client.
+    """
+
+    uniform = False
+
+    def __init__(self, layouts, ratio, align=ALIGN):
+        self.layouts = [[int(s) for s in sizes] for sizes in layouts]
+        self.ratio = float(ratio)
+        self.clients = len(self.layouts)
+        if self.clients < 1:
+            raise ValueError("a MixedTable needs at least one client")
+        rows = []
+        span_off, k_off, seg_off = [0], [0], [0]
+        off = oo = 0
+        for sizes in self.layouts:
+            c0 = off
+            for n in sizes:
+                k = k_for(n, ratio)
+                rows.append((off, n, k, oo))
+                off = align_up(off + n, align)
+                oo += k
+            off = max(off, c0 + align)  # a client with no fp32 element still owns one aligned slot
+            span_off.append(off)
+            k_off.append(oo)
+            seg_off.append(len(rows))
+        self.segs = np.array(rows, dtype=np.uint64).reshape(-1, 4)
+        self.client_span_off, self.client_k_off, self.client_seg_off = span_off, k_off, seg_off
+
+    @property
+    def n_segments(self):
+        return len(self.segs)
+
+    @property
+    def span(self):
+        return self.client_span_off[-1]
+
+    @property
+    def total_k(self):
+        return self.client_k_off[-1]
+
+    @property
+    def n_elements(self):
+        return int(self.segs[:, 1].sum()) if len(self.segs) else 0
+
+    def client_sizes(self, c):
+        return self.layouts[c]
+
+    def client_elements(self):
+        return [sum(s) for s in self.layouts]
+
+    def sub_table(self, c0, c1):
+        return MixedTable(self.layouts[c0:c1], self.ratio)
+
+    def algorithmic_bytes(self, bits=8, delta=False):
+        return algorithmic_bytes(self.n_elements, self.total_k, self.n_segments, bits, delta)
 
 
 class SubTable:
@@ -104,6 +196,7 @@ class SubTable:
     the rows need (max out_off + k, max in_off + n), not their sums."""
 
     clients = None  # not a copies-of-one-layout table: no fused aggregation over it
+    uniform = False
 
     def __init__(self, segs):
         self.segs = np.ascontiguousarray(np.asarray(segs, dtype=np.uint64).reshape(-1, 4))

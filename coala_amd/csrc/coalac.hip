@@ -1592,6 +1592,8 @@ struct AggArgs {
 //   acc = x_0 * w_0, then acc = acc + (x_i * w_i)        (torch: params *= w0; params += s_i * w_i)
 //   out = acc / total (mode DIV, torch CPU division) or acc * (1.0f / total) (mode RECIP, torch GPU
 //   division by a host scalar)                       — coala/server/strategies.py:6-29, 57-90
+//   or out = acc (mode SUM: weighted_sum, strategies.py:57-90, whose result the distributed server hands
+//   to reduce_models, coala/distributed/distributed.py:42-57)
 // d_i goes through a per-wave LDS tile: the client's kept values are scattered into the zeroed tile,
 // every lane reads its 64 elements back with ds_read_b128, then the same positions are re-zeroed.
 // Latency: every client's range / mn / scale / weight is fetched lane-parallel in one round (lane j =
@@ -1705,8 +1707,10 @@ __global__ __launch_bounds__(BLOCK) void k_aggregate(Params P, AggArgs A) {
 #pragma unroll
   for (uint32_t it = 0; it < UNIT_IT; ++it) {
     float4 o;
-    if (MODE == 0) {
+    if (MODE == COALAC_AGG_DIV) {
       o = make_float4(acc[it].x / A.total, acc[it].y / A.total, acc[it].z / A.total, acc[it].w / A.total);
+    } else if (MODE == COALAC_AGG_SUM) {
+      o = acc[it];
     } else {
       o = make_float4(acc[it].x * A.inv_total, acc[it].y * A.inv_total, acc[it].z * A.inv_total,
                       acc[it].w * A.inv_total);
@@ -2245,7 +2249,8 @@ int coalac_aggregate_ev(coalac_plan_t plan, int clients, const int32_t* d_idx, c
   if (!plan) return fail(COALAC_EINVAL, "coalac_aggregate: plan is NULL");
   if (clients < 1 || plan->nseg % clients) return fail(COALAC_EINVAL, "coalac_aggregate: %d segments are not %d copies "
                                                        "of one layout", plan->nseg, clients);
-  if (mode != COALAC_AGG_DIV && mode != COALAC_AGG_RECIP) return fail(COALAC_EINVAL, "coalac_aggregate: bad mode %d", mode);
+  if (mode != COALAC_AGG_DIV && mode != COALAC_AGG_RECIP && mode != COALAC_AGG_SUM)
+    return fail(COALAC_EINVAL, "coalac_aggregate: bad mode %d", mode);
   if (plan->n_units == 0) return COALAC_OK;
   if (!d_out || !d_weights) return fail(COALAC_EINVAL, "coalac_aggregate: output/weights pointer is NULL");
   if (plan->total_k && (!d_idx || !d_vals)) return fail(COALAC_EINVAL, "coalac_aggregate: idx/vals pointers are NULL");
@@ -2297,15 +2302,23 @@ int coalac_aggregate_ev(coalac_plan_t plan, int clients, const int32_t* d_idx, c
                        static_cast<uint32_t*>(d_ws));
   BOUNDARY(1);
   const uint32_t g = (U0 + WAVES - 1) / WAVES;
-  const bool raw = plan->bits == 32, hb = d_base != nullptr, rc1 = mode == COALAC_AGG_RECIP;
+  const bool raw = plan->bits == 32, hb = d_base != nullptr;
 #define AGG(R, H, M) hipLaunchKernelGGL((k_aggregate<R, H, M>), dim3(g), dim3(BLOCK), 0, st, P, A)
+#define AGG_MODES(R, H)                     \
+  do {                                      \
+    if (mode == COALAC_AGG_RECIP)           \
+      AGG(R, H, COALAC_AGG_RECIP);          \
+    else if (mode == COALAC_AGG_SUM)        \
+      AGG(R, H, COALAC_AGG_SUM);            \
+    else                                    \
+      AGG(R, H, COALAC_AGG_DIV);            \
+  } while (0)
   if (raw) {
-    if (hb) { if (rc1) AGG(true, true, 1); else AGG(true, true, 0); }
-    else { if (rc1) AGG(true, false, 1); else AGG(true, false, 0); }
+    if (hb) AGG_MODES(true, true); else AGG_MODES(true, false);
   } else {
-    if (hb) { if (rc1) AGG(false, true, 1); else AGG(false, true, 0); }
-    else { if (rc1) AGG(false, false, 1); else AGG(false, false, 0); }
+    if (hb) AGG_MODES(false, true); else AGG_MODES(false, false);
   }
+#undef AGG_MODES
 #undef AGG
   BOUNDARY(2);
   HIP_CHECK(hipGetLastError());

@@ -1,9 +1,10 @@
 """Loopback client/server with the reference's hook order and upload framing.
 
 LoopbackClient.run_train mirrors /root/reference/coala/client/base.py:123-159 (set_model :191-201,
-decompression :141, pre_train/train/post_train :143-145, compression :153, upload size :155,
-encryption :157, upload :159 -> construct_upload_request :353-383 with codec.marshal(deepcopy(model))
-and DATA_TYPE_PARAMS = 0). LoopbackServer.round mirrors distribution_to_train_locally
+download size :139, decompression :141, pre_train/train/post_train :143-145, compression :153, upload
+size :155, encryption :157, upload :159 -> construct_upload_request :353-383 with
+codec.marshal(deepcopy(model)) and DATA_TYPE_PARAMS = 0). track() records into `metrics` the way the
+reference's ClientMetric does (known names as keys, the rest under "extra": tracking/metric.py:64-73). LoopbackServer.round mirrors distribution_to_train_locally
 (/root/reference/coala/server/base.py:363-381: decompression(codec.unmarshal(data)) per client) and
 aggregation (:562-571 -> strategies.federated_averaging). The hook order is checked against
 tests/golden/hooks.json, captured from the reference itself.
@@ -55,6 +56,8 @@ class LoopbackClient:
         self.step_scale = step_scale
         self.trace = []
         self.upload_sizes = []
+        self.download_sizes = []
+        self.metrics = {"extra": {}}
 
     # hook points (no-ops, as in the reference)
     def decompression(self):
@@ -95,17 +98,28 @@ class LoopbackClient:
     def calculate_model_size(self, model, param_size=32):
         return sum(p.numel() for p in model.parameters()) * param_size / (8 * 1024 * 1024)
 
+    KNOWN_METRICS = ("train_download_size", "train_upload_size", "train_time", "train_metric")
+
+    def track(self, metric_name, value):  # client/base.py:447-457 -> ClientMetric.add (metric.py:64-73)
+        if metric_name in self.KNOWN_METRICS:
+            self.metrics[metric_name] = value
+        else:
+            self.metrics["extra"][metric_name] = value
+
     def _t(self, name):
         self.trace.append(name)
 
     def run_train(self, model, round_id, task_id="task"):
         self.set_model(model)
+        self.download_sizes.append(self.calculate_model_size(model))
+        self.track("train_download_size", self.download_sizes[-1])
         self._t("decompression"); self.decompression()
         self._t("pre_train"); self.pre_train()
         self._t("train"); self.train(round_id)
         self._t("post_train"); self.post_train()
         self._t("compression"); self.compression()
         self.upload_sizes.append(self.calculate_model_size(self.model))
+        self.track("train_upload_size", self.upload_sizes[-1])
         self._t("encryption"); self.encryption()
         data = marshal(copy.deepcopy(self.model))
         req = UploadRequest(task_id, round_id, self.cid, UploadContent(data, DATA_TYPE_PARAMS, self._datasize))

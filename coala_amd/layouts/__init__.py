@@ -11,12 +11,27 @@ _DIR = os.path.dirname(os.path.abspath(__file__))
 
 SPLITFL = [f"{m}_cut{c}" for m in ("resnet18_split", "resnet50_split", "simple_cnn_split") for c in (1, 2, 4)]
 
+# splitFL feature uploads: the client-side activations a splitFL client sends every
+# step as {"content": [feature, label], "name": [...]} (application/splitFL/client/base_sfl.py:249-257),
+# batch 32; one fp32 tensor each (the int64 label rides raw)
+FEATURES = {"sfl_feature_64x32x32": [32, 64, 32, 32],
+            "sfl_feature_256x32x32": [32, 256, 32, 32],
+            "sfl_feature_128x16x16": [32, 128, 16, 16]}
+
 
 def names():
-    return sorted(f[:-5] for f in os.listdir(_DIR) if f.endswith(".json"))
+    return sorted(f[:-5] for f in os.listdir(_DIR) if f.endswith(".json")) + sorted(FEATURES)
 
 
 def load(name):
+    if name in FEATURES:
+        shape = FEATURES[name]
+        n = 1
+        for d in shape:
+            n *= d
+        return {"model": name, "source": "application/splitFL/client/base_sfl.py:249-257 feature upload",
+                "n_entries": 1, "n_float32_entries": 1, "n_float32_elements": n,
+                "entries": [{"name": "feature", "shape": list(shape), "dtype": "float32"}]}
     with open(os.path.join(_DIR, name + ".json")) as f:
         return json.load(f)
 

@@ -37,14 +37,48 @@ def fill_client(flat, table, client_id, seed_base=1234, zero_frac=0.005, tie_fra
 
 
 def synth_batch(table, device, client_ids=None, seed_base=1234):
-    """Flat fp32 buffer [table.span] holding table.clients synthetic updates back to back."""
+    """Flat fp32 buffer [table.span] holding table.clients synthetic updates back to back (a SegmentTable
+    of copies of one layout, or a MixedTable of per-client layouts)."""
     ids = list(range(table.clients)) if client_ids is None else list(client_ids)
     flat = torch.zeros(table.span, dtype=torch.float32, device=device)
-    S = table.span_per_client
-    single = SegmentTable(table.sizes, table.ratio, 1)
+    so = table.client_span_off
     for c, cid in enumerate(ids):
-        fill_client(flat[c * S:(c + 1) * S], single, cid, seed_base)
+        single = SegmentTable(table.client_sizes(c), table.ratio, 1)
+        fill_client(flat[so[c]:so[c + 1]], single, cid, seed_base)
     return flat
+
+
+# C5 (SURVEY.md §8(d)): 256 splitFL clients on 8 GPUs; each client draws (seeded) one of the client-side
+# models at cut 1/2/4 or one of the three feature-tensor uploads
+C5_CHOICES = [f"{m}_cut{c}" for m in ("resnet18_split", "resnet50_split", "simple_cnn_split") for c in (1, 2, 4)] + \
+    ["sfl_feature_64x32x32", "sfl_feature_256x32x32", "sfl_feature_128x16x16"]
+C5_CLIENTS, C5_GPUS, C5_SEED = 256, 8, 2024
+
+
+def c5_draw(n_clients=C5_CLIENTS, seed=C5_SEED):
+    """Layout name of every client of the C5 round (seeded, uniform over C5_CHOICES)."""
+    import numpy as np
+    rng = np.random.default_rng(seed)
+    return [C5_CHOICES[i] for i in rng.integers(0, len(C5_CHOICES), n_clients)]
+
+
+def c5_groups(names, world=C5_GPUS):
+    """Clients -> GPUs by the reference's greedy grouping (LPT on the update size; coala_amd/sharding.py,
+    restating coala/distributed/distributed.py:192-217)."""
+    from .sharding import greedy_groups
+    return greedy_groups([sum(fp32_sizes(n)) for n in names], world)
+
+
+def c5_share(rank, n_clients=C5_CLIENTS, gpus=C5_GPUS, seed=C5_SEED):
+    """(client ids, layout names) of GPU `rank % gpus`'s share of the C5 round, in client-id order."""
+    names = c5_draw(n_clients, seed)
+    ids = sorted(c5_groups(names, gpus)[rank % gpus])
+    return ids, [names[i] for i in ids]
+
+
+def mixed_table(names, ratio):
+    from .compression.spec import MixedTable
+    return MixedTable([fp32_sizes(n) for n in names], ratio)
 
 
 def layout_table(name, ratio, clients=1):

@@ -156,10 +156,13 @@ int coalac_decode_sched(coalac_plan_t plan, const int32_t* d_idx, const void* d_
  *   acc = x_0 * w_0;  acc = acc + (x_i * w_i) for i = 1.. in client order (fp32, no FMA)
  *   d_out = acc / total               (mode COALAC_AGG_DIV: torch's CPU division by a scalar)
  *         = acc * (1.0f / total)      (mode COALAC_AGG_RECIP: torch's GPU division by a host scalar)
+ *         = acc                       (mode COALAC_AGG_SUM: strategies.weighted_sum, :57-90 — the
+ *                                      multi-GPU server's per-rank sum before reduce_models'
+ *                                      all_reduce + division, coala/server/base.py:595-598)
  * d_weights: DEVICE fp32[clients] = float(w_i); total: float(sum of the weights). d_out / d_base are
  * indexed like client 0's segments. Workspace: dec_ws_bytes of coalac_plan_query. Events (the _ev
  * variant): [0] before the unit-bounds pass, [1] before k_aggregate, [2] after. */
-enum { COALAC_AGG_DIV = 0, COALAC_AGG_RECIP = 1 };
+enum { COALAC_AGG_DIV = 0, COALAC_AGG_RECIP = 1, COALAC_AGG_SUM = 2 };
 int coalac_aggregate(coalac_plan_t plan, int clients, const int32_t* d_idx, const void* d_vals,
                      const float* d_mn, const float* d_scale, const float* d_weights, float total, int mode,
                      const float* d_base, float* d_out, void* d_ws, uint64_t ws_bytes, void* stream);

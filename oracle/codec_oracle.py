@@ -167,7 +167,7 @@ def decode(idx, vals, mn, scale, segs, bits, span, base=None, out=None):
     return out
 
 
-AGG_DIV, AGG_RECIP = 0, 1
+AGG_DIV, AGG_RECIP, AGG_SUM = 0, 1, 2
 
 
 def aggregate(idx, vals, mn, scale, segs, bits, clients, weights, total, mode, base=None, out_span=None):
@@ -179,7 +179,8 @@ def aggregate(idx, vals, mn, scale, segs, bits, clients, weights, total, mode, b
 
     torch evaluates the division as params / total on the CPU (mode AGG_DIV) and as
     params * (1.0f / total) on a GPU, where a host scalar divisor becomes a reciprocal multiply (mode
-    AGG_RECIP). weights / total are taken as fp32 (torch converts the Python scalars to the tensor's
+    AGG_RECIP); AGG_SUM stops before the division (weighted_sum, strategies.py:57-90, the per-rank
+    sum a multi-GPU server hands to reduce_models, distributed.py:42-57). weights / total are taken as fp32 (torch converts the Python scalars to the tensor's
     fp32 compute type). segs: [clients * T, 4] client-major copies of one layout; the output is
     indexed like client 0's segments (positions outside them: 0).
     """
@@ -201,5 +202,8 @@ def aggregate(idx, vals, mn, scale, segs, bits, clients, weights, total, mode, b
                 acc = term if acc is None else acc + term
             if acc is None:
                 continue
-            out[off0:off0 + n] = acc / tot if mode == AGG_DIV else acc * (F32(1.0) / tot)
+            if mode == AGG_SUM:
+                out[off0:off0 + n] = acc
+            else:
+                out[off0:off0 + n] = acc / tot if mode == AGG_DIV else acc * (F32(1.0) / tot)
     return out

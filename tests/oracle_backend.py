@@ -34,7 +34,7 @@ class OraclePlan:
         b = None if base is None else base.detach().cpu().numpy()
         out = O.aggregate(enc.idx.numpy(), enc.vals.numpy(), enc.mn.numpy(), enc.scale.numpy(),
                           self.table.segs.astype(np.int64), self.bits, self.table.clients, weights, total,
-                          O.AGG_DIV if mode == "div" else O.AGG_RECIP, base=b,
+                          {"div": O.AGG_DIV, "recip": O.AGG_RECIP, "sum": O.AGG_SUM}[mode], base=b,
                           out_span=self.table.span_per_client)
         return torch.from_numpy(out)
 
@@ -44,6 +44,9 @@ class OracleBackend:
 
     def default_device(self):
         return torch.device("cpu")
+
+    def runs_on(self, device):
+        return torch.device(device).type == "cpu"
 
     def make_plan(self, sizes, ratio, bits, device, clients=1):
         return OraclePlan(sizes, ratio, bits, clients)

@@ -1,0 +1,127 @@
+"""Size accounting, carrier copy semantics and blob validation, on CPU (oracle backend).
+
+Reference behaviour pinned here:
+  * run_train tracks calculate_model_size(model) of the DOWNLOADED model (coala/client/base.py:139) and
+    of the upload (:155); the reference counts params x 32 bit (:474-487), the mixin reports the payload;
+  * unknown metric names go to the tracker's "extra" dict (coala/tracking/metric.py:64-73);
+  * the upload is codec.marshal(copy.deepcopy(self.model)) (client/base.py:363).
+"""
+import copy
+import pickle
+
+import numpy as np
+import pytest
+import torch
+
+from coala_amd.compression import CompressedModel, CompressedUpdate, CompressionClientMixin, \
+    CompressionServerMixin, UpdateCodec, wire
+from coala_amd.compression.codec import validate
+from coala_amd.compression.plugin import TRAIN_UPLOAD_COMPRESSION_RATIO
+from coala_amd.fl import LoopbackClient, LoopbackServer
+from coala_amd.layouts import build_module
+from tests.oracle_backend import OracleBackend
+
+
+def classes(download=False):
+    class Client(CompressionClientMixin, LoopbackClient):
+        codec_ratio, codec_bits, codec_mode, codec_backend = 0.01, 8, "delta", OracleBackend()
+
+    class Server(CompressionServerMixin, LoopbackServer):
+        codec_ratio, codec_bits, codec_mode, codec_backend = 0.01, 8, "delta", OracleBackend()
+        codec_download = download
+
+    return Client, Server
+
+
+@pytest.mark.parametrize("download", [False, True])
+def test_download_and_upload_sizes_and_ratio_are_tracked(download):
+    Client, Server = classes(download)
+    g0 = build_module("lenet", seed=1)
+    clients = [Client(f"c{i}", 5 + i, step_seed=i) for i in range(2)]
+    server = Server(copy.deepcopy(g0), clients)
+    server.round(0)
+    nominal = sum(p.numel() for p in g0.parameters()) * 32 / 8 / 2 ** 20
+    for c in clients:
+        # download: the compressed carrier's payload (dense 8-bit: ~1/4 of fp32), never 0 MB
+        d = c.download_sizes[-1]
+        if download:
+            assert 0 < d < nominal / 3.5
+        else:
+            assert d == pytest.approx(nominal)
+        assert c.metrics["train_download_size"] == d
+        up = c.upload_sizes[-1]
+        assert 0 < up < nominal / 15
+        assert c.metrics["train_upload_size"] == up
+        r = c.metrics["extra"][TRAIN_UPLOAD_COMPRESSION_RATIO]
+        assert r > 15
+
+
+def test_compressed_model_size_is_payload():
+    Client, _ = classes()
+    codec = UpdateCodec(1.0, 8, "weights", OracleBackend())
+    from coala_amd.compression import compress_model
+    m = build_module("resnet18_split_cut2", seed=3)
+    cm = compress_model(m, codec)
+    assert isinstance(cm, CompressedModel)
+    c = Client("c", 1)
+    assert c.calculate_model_size(cm) == cm.nbytes * 8 / (8 * 1024 * 1024) > 0
+
+
+def test_deepcopy_shares_payload_and_packs_once():
+    codec = UpdateCodec(0.05, 8, "weights", OracleBackend())
+    up = codec.encode(build_module("simple_cnn_split_cut4", seed=4).state_dict())
+    dup = copy.deepcopy(up)
+    assert dup is not up and dup.encoded is up.encoded and dup.raw is up.raw
+    b1 = pickle.dumps(dup)
+    assert up._blob[0] is not None            # the copy's pack is the original's too
+    b2 = pickle.dumps(up)
+    assert b1 == b2
+    back = pickle.loads(b1)
+    assert back.to_bytes() == up.to_bytes()
+    for f in ("idx", "vals", "mn", "scale"):
+        assert torch.equal(getattr(back.encoded, f), getattr(up.encoded, f))
+
+
+def _blob_with(header_edit):
+    codec = UpdateCodec(0.05, 8, "weights", OracleBackend())
+    up = codec.encode(build_module("lenet", seed=6).state_dict())
+    h, mn, sc, idx, vals, raw = wire.unpack(up.to_bytes())
+    h = copy.deepcopy(h)
+    header_edit(h)
+    return wire.pack(h, mn, sc, idx, vals, raw)
+
+
+@pytest.mark.parametrize("edit", ["off", "n", "seg"])
+def test_validate_rejects_inconsistent_segment_entries(edit):
+    def change(h):
+        segs = [e for e in h["entries"] if e["kind"] == "seg"]
+        if edit == "off":
+            segs[1]["off"] += 32
+        elif edit == "n":
+            segs[0]["shape"] = [segs[0]["n"] + 1]
+        else:
+            segs[0]["seg"], segs[1]["seg"] = 1, 0
+    with pytest.raises(ValueError):
+        CompressedUpdate.from_bytes(_blob_with(change))
+
+
+def test_validate_accepts_encoder_output():
+    codec = UpdateCodec(0.05, 8, "weights", OracleBackend())
+    up = codec.encode(build_module("resnet18_split_cut4", seed=8).state_dict())
+    h, mn, sc, idx, vals, raw = wire.unpack(up.to_bytes())
+    validate(h, idx)
+
+
+def test_snapshot_follows_codec_device_and_moves_once():
+    """the delta base is put where the codec runs. With the oracle backend that is
+    the CPU; flat_on() caches one copy per device."""
+    codec = UpdateCodec(0.05, 8, "delta", OracleBackend())
+    g = build_module("lenet", seed=2)
+    snap = codec.snapshot(g)
+    assert snap.flat.device.type == "cpu"
+    assert snap.flat_on("cpu") is snap.flat
+    w = build_module("lenet", seed=3)
+    up = codec.encode(w.state_dict(), base=snap)
+    st = codec.decode_state(up, base=snap)
+    assert all(t.device.type == "cpu" for t in st.values())
+    assert np.isfinite(np.concatenate([t.reshape(-1).float().numpy() for t in st.values()])).all()

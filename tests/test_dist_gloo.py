@@ -87,3 +87,68 @@ def test_two_rank_gloo_sharded_equals_serial():
     assert all(p.exitcode == 0 for p in procs)
     serial = sorted(client_digest(c) for c in range(n_clients))
     assert got == serial
+
+
+def _fused_sum_worker(rank, world, port, q):
+    """Each rank aggregates its own uploads; the fused path (one coalac_aggregate in "sum" mode, then
+    reduce_models) must equal the reference's distributed branch on decoded modules (server/base.py:
+    594-598: weighted_sum, then reduce_models = all_reduce + div, distributed.py:42-57)."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from coala_amd.compression import CompressionServerMixin, UpdateCodec
+    from coala_amd.fl import LoopbackServer, weighted_sum
+    from coala_amd.fl.distributed import reduce_models
+    from coala_amd.layouts import build_module
+    from tests.oracle_backend import OracleBackend
+
+    class Conf:
+        class server:
+            aggregation_strategy = "FedAvg"
+            aggregation_content = "all"
+        is_distributed = True
+        device = "cpu"
+
+    class Fused(CompressionServerMixin, LoopbackServer):
+        codec_ratio, codec_bits, codec_mode, codec_backend = 0.05, 8, "delta", OracleBackend()
+        codec_fused_aggregate = True
+
+    name = "resnet18_split_cut4"
+    g = build_module(name, seed=1)
+    codec = UpdateCodec(0.05, 8, "delta", backend=OracleBackend())
+    base = codec.snapshot(g)
+    ups, weights = [], []
+    for i in range(3):
+        cid = rank * 3 + i
+        w = build_module(name, seed=50 + cid)
+        for b in w.buffers():
+            if b.dtype == torch.int64:
+                b.fill_(cid + 2)
+        ups.append(codec.encode(w.state_dict(), base=base))
+        weights.append([4, 0, 9, 1, 6, 2][cid])
+    s = Fused(g, [])
+    s.conf = Conf
+    fused = s.aggregate(list(ups), list(weights))
+    dec = [codec.decode_module(u, g, base=base) for u in ups]
+    ref, tot = weighted_sum(dec, list(weights))
+    reduce_models(ref, torch.tensor(tot))
+    same = all(a.dtype == b.dtype and torch.equal(a, b)
+               for a, b in zip(ref.state_dict().values(), fused.state_dict().values()))
+    res = [None] * world
+    dist.all_gather_object(res, same)
+    if rank == 0:
+        q.put(res)
+    dist.destroy_process_group()
+
+
+@pytest.mark.timeout(300)
+def test_two_rank_gloo_fused_weighted_sum_equals_reference_reduce():
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_fused_sum_worker, args=(r, world, port, q)) for r in range(world)]
+    [p.start() for p in procs]
+    got = q.get(timeout=240)
+    [p.join(timeout=60) for p in procs]
+    assert all(p.exitcode == 0 for p in procs)
+    assert got == [True, True]

@@ -260,3 +260,36 @@ def test_decode_untrusted_idx_stays_in_bounds(cuda, kind):
         seg = o[off:off + n]
         assert np.all((seg == 0.0) | ((seg >= 1.0) & (seg <= 1.0 + 255 * 0.5)))
     assert np.all(o[~inside] == sentinel)
+
+
+GOLD_NPZ = __import__("os").path.join(__import__("os").path.dirname(__file__), "golden", "codec_vectors.npz")
+
+
+@pytest.mark.parametrize("bits", [1, 4, 8, 32])
+@pytest.mark.parametrize("ratio", [0.001, 0.01, 0.3, 1.0])
+def test_golden_vectors_bit_exact(cuda, ratio, bits):
+    """Every committed golden case (tests/golden/codec_vectors.npz: ties, signed zeros, denormals, NaN / inf
+    keys, constant segments, half-to-even rounding, n = 1, k = 1, k = n) × this ratio × bits, encoded as
+    the segments of one batched plan: idx, codes, mn, scale and the dense decode equal the committed
+    vectors bit for bit."""
+    gold = np.load(GOLD_NPZ)
+    names = sorted({k.split("/")[0] for k in gold.files})
+    xs = [gold[f"{n}/x"] for n in names]
+    plan = CodecPlan([x.size for x in xs], ratio, bits)
+    t = plan.table
+    flat = np.zeros(t.span, np.float32)
+    for off, x in zip(t.offsets, xs):
+        flat[off:off + x.size] = x
+    enc = plan.encode(torch.from_numpy(flat).cuda())
+    dec = plan.decode(enc).cpu().numpy()
+    idx, vals = enc.idx.cpu().numpy(), enc.vals.cpu().numpy()
+    mn, sc = enc.mn.cpu().numpy(), enc.scale.cpu().numpy()
+    for s, (n, (off, _, k, oo)) in enumerate(zip(names, t.segs.astype(np.int64))):
+        tag = f"{n}/r{ratio}/b{bits}"
+        assert int(gold[f"{tag}/k"][0]) == k, tag
+        np.testing.assert_array_equal(idx[oo:oo + k], gold[f"{tag}/idx"], err_msg=tag)
+        np.testing.assert_array_equal(vals[oo:oo + k].view(np.uint8), gold[f"{tag}/vals"].view(np.uint8), err_msg=tag)
+        np.testing.assert_array_equal(np.array([mn[s], sc[s]], np.float32).view(np.uint32),
+                                      gold[f"{tag}/mn_scale"].view(np.uint32), err_msg=tag)
+        np.testing.assert_array_equal(dec[off:off + xs[s].size].view(np.uint32), gold[f"{tag}/dec"].view(np.uint32),
+                                      err_msg=tag)

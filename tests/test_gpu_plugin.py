@@ -1,0 +1,79 @@
+"""The plugin mixins on the GPU with the reference's device placement:
+
+  * the server's global model stays on the CPU (coala/server/base.py keeps self.model there until
+    test_in_server, :280; set_model(load_dict=True) loads into it, :571);
+  * the client snapshots w_global in decompression() right after set_model (client/base.py:138-141),
+    BEFORE pretrain moves the model to the training device (:245), so the snapshot starts on the CPU;
+  * compression() then encodes the trained GPU state (client/base.py:144-153).
+
+The HIP codec must run on the GPU in all three places, and every decoded upload must equal the oracle
+backend's (w_global + decode(encode(delta))) bit for bit.
+"""
+import copy
+
+import numpy as np
+import pytest
+import torch
+
+from coala_amd.compression import CompressedUpdate, CompressionClientMixin, CompressionServerMixin
+from coala_amd.fl import LoopbackClient, LoopbackServer
+from coala_amd.layouts import build_module
+from tests.oracle_backend import OracleBackend
+
+pytestmark = pytest.mark.gpu
+
+
+def classes(backend, device):
+    class Client(CompressionClientMixin, LoopbackClient):
+        codec_ratio, codec_bits, codec_mode, codec_backend = 0.01, 8, "delta", backend
+
+        def __init__(self, *a, **k):
+            super().__init__(*a, device=device, **k)
+
+    class Server(CompressionServerMixin, LoopbackServer):
+        codec_ratio, codec_bits, codec_mode, codec_backend = 0.01, 8, "delta", backend
+
+    return Client, Server
+
+
+@pytest.mark.parametrize("layout", ["lenet", "resnet18"])
+def test_cpu_global_gpu_training_delta_mode(cuda, layout):
+    g0 = build_module(layout, seed=4)  # on the CPU, like the reference server's global model
+    Cg, Sg = classes(None, "cuda")      # default backend: the HIP codec
+    Co, So = classes(OracleBackend(), "cpu")
+    hip = Sg(copy.deepcopy(g0), [Cg(f"c{i}", 10 + i, step_seed=i) for i in range(3)])
+    ora = So(copy.deepcopy(g0), [Co(f"c{i}", 10 + i, step_seed=i) for i in range(3)])
+    for r in range(2):
+        hip.distribution_to_train(r)
+        ora.distribution_to_train(r)
+        for cid in hip.uploaded:
+            a, b = hip.uploaded[cid].state_dict(), ora.uploaded[cid].state_dict()
+            for (k, x), (k2, y) in zip(a.items(), b.items()):
+                assert k == k2 and x.dtype == y.dtype
+                assert x.device.type == "cuda"
+                xc = x.cpu()
+                if x.dtype == torch.float32:
+                    np.testing.assert_array_equal(xc.numpy().view(np.uint32), y.numpy().view(np.uint32), err_msg=k)
+                else:
+                    assert torch.equal(xc, y), k
+        hip.aggregation()
+        ora.aggregation()
+        assert all(t.device.type == "cpu" for t in hip.model.state_dict().values())
+        # the two global models differ only by torch's GPU-vs-CPU scalar division inside FedAvg
+        for x, y in zip(hip.model.state_dict().values(), ora.model.state_dict().values()):
+            if x.dtype == torch.float32:
+                assert torch.allclose(x, y, rtol=1e-6, atol=1e-9)
+        ora.model.load_state_dict(hip.model.state_dict())  # next round starts from the same global
+
+
+def test_carrier_deepcopy_then_marshal_on_gpu(cuda):
+    """construct_upload_request's codec.marshal(copy.deepcopy(self.model)) (client/base.py:363) on a
+    GPU carrier: the deep copy shares the device payload; the pickle is one pack."""
+    import pickle
+    Cg, _ = classes(None, "cuda")
+    c = Cg("c0", 3)
+    g = build_module("resnet18_split_cut4", seed=1)
+    req = c.run_train(g, 0)
+    up = pickle.loads(req.content.data)
+    assert isinstance(up, CompressedUpdate) and up.encoded.idx.device.type == "cpu"
+    assert len(req.content.data) < up.nbytes + 16384
