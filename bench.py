@@ -32,6 +32,7 @@ sys.path.insert(0, ROOT)
 
 METRIC = "encode+decode GB/s over fp32 weight updates (device-resident), 1/2/4/8 GPU"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md: 8.0 TB/s)
+MULTI_LAUNCH = 16  # COALAC_FLAG_MULTI_LAUNCH: the k_sample .. k_emit kernel sequence instead of k_fused
 SPLIT = 2  # sub-batches per step: two independent pipelines side by side fill the CUs the other leaves
            # idle in its latency-bound stages and launch tails (+11 % over one 16-client pipeline)
 EVENT_EVERY = 4  # timing events on every 4th timed step (each recorded event adds a ~4 us dispatch gap)
@@ -238,6 +239,7 @@ def run_workload(cfg, a, dev, world, rank, headline):
     for w in range(max(a.warmup, len(slots))):
         step(j=w)
     fallbacks = sum(p.fallbacks() for p in pipes)
+    timeouts = sum(p.timeouts() for p in pipes)
 
     # Timing events only around the streaming kernels (every recorded event costs a dispatch gap):
     # per sub-batch, [1] / [2] around its k_scan / k_decode.
@@ -276,8 +278,11 @@ def run_workload(cfg, a, dev, world, rank, headline):
     def union(pairs):
         ref = pairs[0][0]
         return max(ref.elapsed_time(e) for _, e in pairs) - min(ref.elapsed_time(s) for s, _ in pairs)
+    # one-launch encode (default): events [1] / [2] bracket k_fused; multi-launch: k_scan
+    multi = bool(a.flags & MULTI_LAUNCH)
+    enc_kernel = "k_scan" if multi else "k_fused"
     stages = {}
-    for name, which in {"k_scan": ev_e, "k_decode": ev_d}.items():
+    for name, which in {enc_kernel: ev_e, "k_decode": ev_d}.items():
         per = [union([(e[1], e[2]) for e in which[i]]) for i in timed_steps]
         stages[name] = sum(per) / len(per)
     N, K, T = t.n_elements, t.total_k, t.n_segments
@@ -286,7 +291,7 @@ def run_workload(cfg, a, dev, world, rank, headline):
     segs = t.segs.astype("int64")
     large_elems = int(segs[segs[:, 1] > SMALL_MAX, 1].sum())
     alg = {  # algorithmic HBM bytes per timed interval
-        "k_scan": 4 * large_elems * (2 if delta else 1),
+        enc_kernel: (4 * large_elems if multi else 4 * N + (4 + vb) * K + 8 * T) + (4 * N if delta else 0),
         "k_decode": 4 * N * (2 if delta else 1) + (4 + vb) * K + 8 * T,
     }
     dom = max(alg, key=lambda k: stages[k])
@@ -304,13 +309,14 @@ def run_workload(cfg, a, dev, world, rank, headline):
                           "frac": round(step_alg / (step_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)},
         "stages_ms": {k: round(v, 4) for k, v in stages.items()},
         "sample_fallbacks": fallbacks,
+        "wait_timeouts": timeouts,
     }
     if headline:
         traffic, src = pmc_traffic(dom, cfg, a, split)
         res["roofline"]["traffic"] = traffic * split if traffic is not None else None
         res["roofline"]["traffic_source"] = src
-        res["stage_timing"] = (f"HIP events on each sub-batch stream around k_scan / k_decode (union over the "
-                               f"{split} sub-batches), {len(timed_steps)} of the {a.steps} timed steps")
+        res["stage_timing"] = (f"HIP events on each sub-batch stream around {enc_kernel} / k_decode (union over "
+                               f"the {split} sub-batches), {len(timed_steps)} of the {a.steps} timed steps")
     for p in pipes:
         p.close()
     del slots, pipes, flat, base
@@ -356,6 +362,7 @@ def main():
                        "parallelism": f"replicas{world}"},
             "roofline": head["roofline"], "step_roofline": head["step_roofline"], "stages_ms": head["stages_ms"],
             "stage_timing": head["stage_timing"], "sample_fallbacks": head["sample_fallbacks"],
+            "wait_timeouts": head["wait_timeouts"],
             "configs": {k: {f: v[f] for f in ("value", "ms_per_step", "step_roofline", "roofline", "stages_ms", "desc",
                                               "elements_per_gpu", "segments_per_gpu", "split", "sample_fallbacks")}
                         for k, v in extras.items()},

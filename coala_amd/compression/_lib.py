@@ -13,6 +13,7 @@ COALAC_FLAG_FORCE_EXACT = 1
 COALAC_FLAG_GENERIC_SELECT = 2
 COALAC_FLAG_STAMPS = 4
 COALAC_FLAG_NO_FORK = 8
+COALAC_FLAG_MULTI_LAUNCH = 16  # encode as the k_sample .. k_emit kernel sequence instead of one k_fused launch
 # stages of a split encode / decode (coalac_sched_t.stages; 0 = all)
 COALAC_STAGE_SAMPLE, COALAC_STAGE_SCAN, COALAC_STAGE_SELECT, COALAC_STAGE_SMALL = 1, 2, 4, 8
 COALAC_STAGE_BOUNDS, COALAC_STAGE_DECODE = 1, 2
@@ -50,9 +51,10 @@ SIGNATURES = [
     ("coalac_aggregate_ev", _I, [_P, _I, _P, _P, _P, _P, _P, ctypes.c_float, _I, _P, _P, _P, _U64, _P, _P]),
     ("coalac_workspace_fallbacks", _I, [_P, _P, _P, ctypes.POINTER(_I)]),
     ("coalac_debug_stamps", _I, [_P, _P, _P, ctypes.POINTER(ctypes.c_uint64), _I]),
+    ("coalac_workspace_timeouts", _I, [_P, _P, _P, ctypes.POINTER(_I)]),
 ]
 
-ABI_VERSION = 1
+ABI_VERSION = 2
 
 
 class CodecError(RuntimeError):

@@ -367,6 +367,10 @@ class SplitPipeline:
         torch.cuda.synchronize(self.device)
         return sum(P["plan"].fallbacks(P["ws"]) for P in self.parts)
 
+    def timeouts(self):
+        torch.cuda.synchronize(self.device)
+        return sum(P["plan"].timeouts(P["ws"]) for P in self.parts)
+
     def close(self):
         for P in self.parts:
             P["plan"].close()

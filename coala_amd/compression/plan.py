@@ -240,6 +240,15 @@ class CodecPlan:
         _lib.check(rc, "coalac_aggregate")
         return out  # w was allocated on the launch stream: its memory is reused only after the kernel
 
+    def timeouts(self, workspace, stream=None):
+        """1 if a bounded in-launch wait of the last one-launch encode with this workspace gave up (its
+        results are then invalid; never expected), else 0 (synchronises)."""
+        c = ctypes.c_int()
+        with torch.cuda.device(self.device):
+            _lib.check(self._lib.coalac_workspace_timeouts(self._h, _ptr(workspace), _stream_handle(stream),
+                                                           ctypes.byref(c)), "coalac_workspace_timeouts")
+        return c.value
+
     def fallbacks(self, workspace, stream=None):
         """Segments of the last encode with this workspace whose sampled bracket missed (synchronises)."""
         c = ctypes.c_int()

@@ -47,8 +47,10 @@
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
+#include <queue>
 #include <string>
 #include <vector>
 
@@ -143,8 +145,22 @@ struct Params {
   uint4* sstate;           // [n_large] {wlo, whi, rank inside the window, path: 0 fast / 1 generic}
   uint32_t* shhi;          // [n_large] histogram upper bound: min(T_hi, largest sampled key)
 
+  // one-launch encode (k_fused): per-block work items, the scan order, and the hand-off words (the
+  // workspace's control block, zeroed before every launch)
+  const uint32_t* items;   // [grid] role << 28 | index
+  const uint32_t* fsched;  // large units in scan order (segments by descending size)
+  const uint32_t* lgroup;  // [n_lunits] select group of each large unit
+  const uint4* eblocks;    // emit blocks {first large unit, units (<= 32), segment, 0}
+  uint32_t* hf_sampled;    // [nseg] sampler done
+  uint32_t* hf_garr;       // [n_groups] units of the group scanned
+  uint32_t* hf_ghist;      // [nseg] group histograms done
+  uint32_t* hf_gwin;       // [nseg] group windows done
+  uint32_t* hf_sel;        // [nseg] segment selected
+  uint32_t* hf_err;        // [4] [0]: a bounded wait gave up
+  uint32_t wt;             // 1 in k_fused: data another block of the launch reads is stored write-through
+
   // decode workspace
-  const uint32_t* ustart;  // [n_units + 1] first kept entry of every unit (k_bounds)
+  const uint32_t* ustart;  // [n_units + 1] first kept entry of every unit (k_bounds; aggregate only)
   // diagnostics: per-block phase timestamps (COALAC_FLAG_STAMPS), NSTAMP per block, 100 MHz ticks
   uint64_t* stamps;
 };
@@ -216,6 +232,74 @@ DEV void wave_fence() {
   __builtin_amdgcn_wave_barrier();
 }
 
+// ---- in-launch hand-offs (k_fused), the agent-scope forms of cdna_hip_programming.md §6 Guideline 16:
+// a producer's payload is either stored write-through (sc1: relaxed agent-scope atomic stores, global
+// address space) and drained, or plain-stored and published by ONE agent-scope release (L2 write-back)
+// after every storing wave has drained and met the block barrier; the signal is an agent-scope atomic. A
+// consumer polls ONE word relaxed (bounded, with s_sleep), then either reads the payload with sc1 loads
+// only, or runs ONE agent-scope acquire (L1 invalidate) before a barrier and plain loads.
+typedef __attribute__((address_space(1))) uint32_t gu32;
+typedef __attribute__((address_space(1))) uint64_t gu64;
+constexpr uint32_t SPIN_MAX = 1u << 18;  // >= 0.1 s of polling: a wait that long means a broken schedule
+
+DEV uint32_t ld_sc1(const uint32_t* p) {
+  return __hip_atomic_load((gu32*)(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+DEV void st_sc1(uint32_t* p, uint32_t v) { __hip_atomic_store((gu32*)(p), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
+DEV void st_sc1(uint2* p, uint2 v) {
+  __hip_atomic_store((gu64*)(p), ((uint64_t)v.y << 32) | v.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+DEV void add_sc1(uint32_t* p, uint32_t v) {
+  (void)__hip_atomic_fetch_add((gu32*)(p), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// a store another block of the same launch will read (k_fused: write-through, so no release is needed)
+DEV void pst(const Params& P, uint32_t* p, uint32_t v) {
+  if (P.wt)
+    st_sc1(p, v);
+  else
+    *p = v;
+}
+DEV void pst(const Params& P, float* p, float v) { pst(P, reinterpret_cast<uint32_t*>(p), __float_as_uint(v)); }
+DEV void pst(const Params& P, uint2* p, uint2 v) {
+  if (P.wt)
+    st_sc1(p, v);
+  else
+    *p = v;
+}
+DEV void drain() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+DEV void acquire_agent() { __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent"); }
+
+// one lane waits until *p >= target (relaxed agent-scope polls); false (and hf_err[0] set) on timeout
+DEV bool wait_ge(const uint32_t* p, uint32_t target, uint32_t* err) {
+  for (uint32_t it = 0;; ++it) {
+    if (ld_sc1(p) >= target) return true;
+    if (it >= SPIN_MAX) {
+      st_sc1(err, 1u);
+      return false;
+    }
+    __builtin_amdgcn_s_sleep(2);
+  }
+}
+
+// block-level consume: thread 0 polls, ONE acquire, every wave then reads after the barrier
+DEV void block_wait(const uint32_t* p, uint32_t target, uint32_t* err) {
+  if (threadIdx.x == 0) {
+    wait_ge(p, target, err);
+    acquire_agent();
+  }
+  drain();
+  __syncthreads();
+}
+
+// block-level publish of write-through (sc1) stores: every storing wave drains, barrier, then ONE lane
+// signals (no release: nothing the consumer reads sits dirty in an L2; a release would write back the
+// whole XCD L2, including other kernels' dirty output, once per block)
+DEV void block_publish_add(uint32_t* counter, uint32_t v) {
+  drain();
+  __syncthreads();
+  if (threadIdx.x == 0) add_sc1(counter, v);
+}
+
 // Block-wide exclusive scan over NT threads. sh needs >= NT/64 words. Returns the exclusive prefix and
 // the block total. Contains barriers: call from all threads.
 template <int NT>
@@ -272,16 +356,18 @@ DEV void block_minmax(float& mn, float& mx, float* shf) {
 // count(key in (T, hi]) < r <= count(key in [T, hi]) and leaves in r the number of keys == T to take
 // (r - count(key in (T, hi])). Radix narrowing with 2048-bin LDS histograms: at most 3 passes over the
 // keys for a full 31-bit range. sh needs >= 64 words (broadcast slots sh[40], sh[41]).
-template <int NT, class ForEach>
+template <int NT, int NB = HIST_BINS, class ForEach>
 DEV uint32_t block_select(ForEach&& for_each, uint32_t lo, uint32_t hi, uint32_t& r, uint32_t* hist,
                           uint32_t* sh) {
-  constexpr int BPT = HIST_BINS / NT;  // bins per thread
+  constexpr int BPT = NB / NT;  // bins per thread
+  constexpr int BITS = NB == 2048 ? 11 : NB == 1024 ? 10 : NB == 512 ? 9 : 8;
+  static_assert((1 << BITS) == NB, "power-of-two bins");
   const uint32_t t = threadIdx.x;
   while (lo < hi) {
     const uint32_t w = hi - lo;
     const int bl = 32 - __clz(w);
-    const int shift = bl > 11 ? bl - 11 : 0;
-    for (uint32_t i = t; i < HIST_BINS; i += NT) hist[i] = 0;
+    const int shift = bl > BITS ? bl - BITS : 0;
+    for (uint32_t i = t; i < NB; i += NT) hist[i] = 0;
     __syncthreads();
     const uint32_t l0 = lo, h0 = hi;
     for_each([&](uint32_t key) {
@@ -467,23 +553,39 @@ DEV uint32_t hash32(uint32_t x) {
 // The unit is loaded in NB batches of UNIT_IT/NB float4 per lane: NB = 1 for the streaming pass (all
 // loads in flight at once), more for the register-lean fallback inside k_select.
 // ------------------------------------------------------------------------------------------------
-template <bool DELTA, int NB>
-DEV void scan_unit(const Params& P, uint32_t lu, const UnitDev& L, uint32_t tlo, uint32_t thi, uint2* stage) {
+// SC1 (k_fused): records and counts are stored write-through for the in-launch hand-off to the select
+// phases. get_t() returns {T_lo, T_hi}; it is called once the first batch of loads is in flight (k_fused
+// waits there for the sampler).
+template <bool DELTA, int NB, bool SC1 = false, class GetT>
+DEV void scan_unit_t(const Params& P, uint32_t lu, const UnitDev& L, GetT&& get_t, uint2* stage) {
   constexpr uint32_t IT = UNIT_IT / NB;
   const uint32_t lane = lane_id();
   const uint32_t len = L.len;
   const uint64_t off = L.off;
   uint2* R = P.cand + (uint64_t)lu * UNIT;
   uint32_t cC = 0, cA = 0;
+  uint32_t tlo = 0, thi = 0;
   // buffer resources over exactly this unit: one shared lane offset for all loads (constant offsets
   // fold into the instruction), and loads past len return 0 — no separate partial-unit path
   const __amdgpu_buffer_rsrc_t rin = unit_rsrc(P.in + off, len);
   const __amdgpu_buffer_rsrc_t rbase = unit_rsrc(DELTA ? P.base + off : P.in + off, len);
+  auto put = [&](uint32_t i, uint2 rec) {
+    if (SC1)
+      st_sc1(R + i, rec);
+    else
+      R[i] = rec;
+  };
 
   for (uint32_t nb = 0; nb < (uint32_t)NB; ++nb) {
     float4 v[IT];
 #pragma unroll
     for (uint32_t i = 0; i < IT; ++i) v[i] = unit_load_x4<DELTA>(rin, rbase, ((nb * IT + i) * 64 + lane) * 16);
+    if (nb == 0) {
+      asm volatile("" ::: "memory");  // the loads above stay ahead of a wait inside get_t
+      const uint2 tt = get_t();
+      tlo = tt.x;
+      thi = tt.y;
+    }
 #pragma unroll
     for (uint32_t i = 0; i < IT; ++i) {
       const uint32_t e0 = ((nb * IT + i) * 64 + lane) * 4;
@@ -513,7 +615,7 @@ DEV void scan_unit(const Params& P, uint32_t lu, const UnitDev& L, uint32_t tlo,
           if (stage != nullptr && pc < STAGE_CAP)
             stage[pc] = rec;
           else
-            R[pc] = rec;
+            put(pc, rec);
         }
         cC += (uint32_t)__popcll(b1);
         continue;
@@ -533,7 +635,7 @@ DEV void scan_unit(const Params& P, uint32_t lu, const UnitDev& L, uint32_t tlo,
           if (stage != nullptr && pc < STAGE_CAP)
             stage[pc] = rec;
           else
-            R[pc] = rec;
+            put(pc, rec);
           ++pc;
         }
         cC += (uint32_t)__popcll(bc[j]);
@@ -542,12 +644,22 @@ DEV void scan_unit(const Params& P, uint32_t lu, const UnitDev& L, uint32_t tlo,
   }
   if (stage != nullptr) {
     wave_fence();
-    for (uint32_t i = lane; i < cC && i < STAGE_CAP; i += 64) R[i] = stage[i];
+    for (uint32_t i = lane; i < cC && i < STAGE_CAP; i += 64) put(i, stage[i]);
   }
   if (lane == 0) {
-    P.cntA[lu] = cA;
-    P.cntC[lu] = cC;
+    if (SC1) {
+      st_sc1(P.cntA + lu, cA);
+      st_sc1(P.cntC + lu, cC);
+    } else {
+      P.cntA[lu] = cA;
+      P.cntC[lu] = cC;
+    }
   }
+}
+
+template <bool DELTA, int NB>
+DEV void scan_unit(const Params& P, uint32_t lu, const UnitDev& L, uint32_t tlo, uint32_t thi, uint2* stage) {
+  scan_unit_t<DELTA, NB, false>(P, lu, L, [&]() { return make_uint2(tlo, thi); }, stage);
 }
 
 
@@ -693,14 +805,12 @@ __global__ __launch_bounds__(BLOCK) void k_small(Params P) {
 // ------------------------------------------------------------------------------------------------
 // k_sample: per large segment, sampled thresholds [T_lo, T_hi] for every unit of the segment
 // ------------------------------------------------------------------------------------------------
-template <bool DELTA, bool RAW>
-__global__ __launch_bounds__(BLOCK) void k_sample(Params P) {
+template <bool DELTA, bool SC1>
+DEV void sample_segment(const Params& P, uint32_t li, uint32_t* hist, uint32_t* sh) {
   constexpr int NT = BLOCK;
   constexpr uint32_t MAXIT = SAMPLE_MAX / 16 / 64;  // run batches per block (64 runs of 16 per batch)
-  __shared__ uint32_t hist[HIST_BINS];
-  __shared__ uint32_t sh[64];
   const uint32_t t = threadIdx.x;
-  const uint32_t s = P.large_list[blockIdx.x];
+  const uint32_t s = P.large_list[li];
   const SegDev sd = P.segs[s];
   const uint32_t n = sd.n, k = sd.k;
   // R runs of 16 contiguous elements, one per stratum of n / R elements, jittered inside it.
@@ -780,13 +890,31 @@ __global__ __launch_bounds__(BLOCK) void k_sample(Params P) {
   }
   const uint32_t nu = sd.unit_end - sd.unit_begin;
   for (uint32_t i = t; i < nu; i += NT) {
-    P.tlo[sd.lu_begin + i] = tlo;
-    P.thi[sd.lu_begin + i] = thi;
+    if (SC1) {
+      st_sc1(P.tlo + sd.lu_begin + i, tlo);
+      st_sc1(P.thi + sd.lu_begin + i, thi);
+    } else {
+      P.tlo[sd.lu_begin + i] = tlo;
+      P.thi[sd.lu_begin + i] = thi;
+    }
   }
   // The band histograms of the parallel select span [T_lo, min(T_hi, max sampled key)] (keys above go
   // to the last bin): with T_hi = KEY_MAX a full-range histogram would be too coarse.
-  if (t == 0) P.shhi[blockIdx.x] = max(tlo, min(thi, kmax));
-  if (t == 0) P.status[s] = 0;
+  if (t == 0) {
+    if (SC1) {
+      st_sc1(P.shhi + li, max(tlo, min(thi, kmax)));
+    } else {
+      P.shhi[li] = max(tlo, min(thi, kmax));
+      P.status[s] = 0;  // (k_fused: the control block, status included, is zeroed before the launch)
+    }
+  }
+}
+
+template <bool DELTA, bool RAW>
+__global__ __launch_bounds__(BLOCK) void k_sample(Params P) {
+  __shared__ uint32_t hist[HIST_BINS];
+  __shared__ uint32_t sh[64];
+  sample_segment<DELTA, false>(P, blockIdx.x, hist, sh);
 }
 
 // k_scan: streams the large units, one wave each. Blocks [0, scan_small) first encode the small
@@ -885,19 +1013,20 @@ DEV void unit_sweep(const uint2* cand, uint32_t lu0, const uint32_t* upre, uint3
   }
 }
 
-// LDS scratch of k_select
-constexpr uint32_t WLIST = 2048;               // in-window entries the fast path can hold
+// LDS scratch of the segment select (k_select, and the SELECT role of the one-launch encode, whose LDS
+// must stay <= 32 KB so five streaming blocks still fit a CU): 28.3 KB
+constexpr uint32_t WLIST = 1024;  // in-window entries the fast path can hold
+constexpr int SEL_HB = 1024;      // bins of the select's radix histograms
 struct SelSmem {
-  uint32_t hist[HIST_BINS];
+  uint32_t hist[SEL_HB];
   uint32_t upre[UCAP + 1];
-  uint32_t ugt[UCAP];
-  uint32_t ueq[UCAP];
-  uint32_t lst_val[WLIST];    // in-window entries, all waves concatenated = index order
-  uint32_t lst_unit[WLIST];
+  uint32_t ge[UCAP];   // per unit of the chunk: count above T* (bits 0-15) | count equal T* (bits 16-31)
+  uint2 lst[WLIST];    // in-window entries {value bits, unit}, all waves concatenated = index order
   uint32_t wcnt[SEL_NT / 64];
   uint32_t sh[64];
   float shf[2 * (SEL_NT / 64)];
 };
+static_assert(sizeof(SelSmem) <= 29 * 1024, "select LDS budget");
 
 // Generic path: radix select over all candidates (1-3 coalesced sweeps) + a counts sweep; handles any
 // number of ties and segments of any size (units in chunks of UCAP).
@@ -921,7 +1050,7 @@ DEV void select_generic(const Params& P, uint32_t lb, uint32_t nu, uint32_t tlo,
       __syncthreads();
     }
   };
-  const uint32_t T = rt == 0 ? thi : block_select<NT>(forC, tlo, thi, rt, S.hist, S.sh);
+  const uint32_t T = rt == 0 ? thi : block_select<NT, SEL_HB>(forC, tlo, thi, rt, S.hist, S.sh);
 
   // counts sweep: per-unit gt/eq, segment-wide tie rank of the first positive / negative tie, min/max
   // of the values with key > T (all of them are kept).
@@ -933,10 +1062,7 @@ DEV void select_generic(const Params& P, uint32_t lb, uint32_t nu, uint32_t tlo,
   }
   for (uint32_t c0 = 0; c0 < nu; c0 += UCAP) {
     const uint32_t cn = min(UCAP, nu - c0);
-    for (uint32_t i = t; i < cn; i += NT) {
-      S.ugt[i] = 0;
-      S.ueq[i] = 0;
-    }
+    for (uint32_t i = t; i < cn; i += NT) S.ge[i] = 0;
     const uint32_t total = chunk_prefix<NT>(P.cntC + lb + c0, cn, S.upre, S.sh);
     uint32_t weq = 0, wfp = NONE, wfn = NONE, ug = 0, ue = 0;  // wave-uniform
     unit_sweep<NW, 4>(
@@ -960,10 +1086,7 @@ DEV void select_generic(const Params& P, uint32_t lb, uint32_t nu, uint32_t tlo,
           }
         },
         [&](uint32_t u) {
-          if (lane == 0) {
-            S.ugt[u] = ug;
-            S.ueq[u] = ue;
-          }
+          if (lane == 0) S.ge[u] = ug | (ue << 16);
           ug = ue = 0;
         });
     if (lane == 0) S.wcnt[wv] = weq;
@@ -980,8 +1103,8 @@ DEV void select_generic(const Params& P, uint32_t lb, uint32_t nu, uint32_t tlo,
     carry_eq += tot;
     __syncthreads();
     for (uint32_t i = t; i < cn; i += NT) {
-      P.gtC[lb + c0 + i] = S.ugt[i];
-      P.eqC[lb + c0 + i] = S.ueq[i];
+      P.gtC[lb + c0 + i] = S.ge[i] & 0xFFFFu;
+      P.eqC[lb + c0 + i] = S.ge[i] >> 16;
     }
     __syncthreads();
   }
@@ -1014,11 +1137,8 @@ struct Band {
 // k_ghist: the group's HB2-bin histogram of the band keys [tlo, thi] -> ghist[group]. (A fused variant in
 // which the segment's last-arriving group block ran segment_pick needed an agent-scope release fence in
 // every block — an L2 writeback on gfx950 — and was ~100x slower; kernel boundaries are cheaper.)
-__global__ __launch_bounds__(BLOCK) void k_ghist(Params P) {
-  __shared__ uint32_t hist[HB2];
-  __shared__ uint32_t upre[GU + 1];
-  __shared__ uint32_t sh[64];
-  const uint4 G = P.groups[blockIdx.x];  // x: large-segment index, y: first large unit, z: units, w: segment
+DEV void group_hist(const Params& P, uint32_t gi, uint32_t* hist, uint32_t* upre, uint32_t* sh) {
+  const uint4 G = P.groups[gi];  // x: large-segment index, y: first large unit, z: units, w: segment
   const uint32_t t = threadIdx.x;
   const uint32_t tlo = P.tlo[G.y], thi = P.thi[G.y];
   const Band band(tlo, thi, P.shhi[G.x]);
@@ -1032,7 +1152,14 @@ __global__ __launch_bounds__(BLOCK) void k_ghist(Params P) {
       },
       [&](uint32_t) {});
   __syncthreads();
-  for (uint32_t i = t; i < HB2; i += BLOCK) P.ghist[(uint64_t)blockIdx.x * HB2 + i] = hist[i];
+  for (uint32_t i = t; i < HB2; i += BLOCK) pst(P, P.ghist + (uint64_t)gi * HB2 + i, hist[i]);
+}
+
+__global__ __launch_bounds__(BLOCK) void k_ghist(Params P) {
+  __shared__ uint32_t hist[HB2];
+  __shared__ uint32_t upre[GU + 1];
+  __shared__ uint32_t sh[64];
+  group_hist(P, blockIdx.x, hist, upre, sh);
 }
 
 // segment_pick: per large segment — validate the sampled bracket, sum the group histograms, pick the bin of
@@ -1094,7 +1221,7 @@ struct GwinSmem {
 template <int NT, bool DELTA, bool RAW>
 DEV void segment_select(const Params& P, uint32_t li, SelSmem& S);
 
-DEV void group_window(const Params& P, const uint4 G, const uint4 st, GwinSmem& W_, uint32_t* sh) {
+DEV void group_window(const Params& P, uint32_t gi, const uint4 G, const uint4 st, GwinSmem& W_, uint32_t* sh) {
   uint32_t* upre = W_.upre;
   auto& slots = W_.slots;
   uint32_t* wcnt = W_.wcnt;
@@ -1124,8 +1251,8 @@ DEV void group_window(const Params& P, const uint4 G, const uint4 st, GwinSmem& 
       },
       [&](uint32_t u) {
         if (lane == 0) {
-          P.gtC[G.y + u] = ug;
-          P.eqC[G.y + u] = 0;
+          pst(P, P.gtC + G.y + u, ug);
+          pst(P, P.eqC + G.y + u, 0u);
         }
         ug = 0;
       });
@@ -1139,23 +1266,31 @@ DEV void group_window(const Params& P, const uint4 G, const uint4 st, GwinSmem& 
     W += c;
   }
   for (uint32_t q = lane; q < wc && q < GCAP; q += 64)
-    if (wpre + q < GCAP) P.glist[(uint64_t)blockIdx.x * GCAP + wpre + q] = slots[wv][q];
+    if (wpre + q < GCAP) pst(P, P.glist + (uint64_t)gi * GCAP + wpre + q, slots[wv][q]);
   block_minmax<BLOCK>(lmn, lmx, shf);
   if (t == 0) {
-    P.gcnt[blockIdx.x] = W;
-    P.gmm[2 * blockIdx.x] = lmn;
-    P.gmm[2 * blockIdx.x + 1] = lmx;
+    pst(P, P.gcnt + gi, W);
+    pst(P, P.gmm + 2 * gi, lmn);
+    pst(P, P.gmm + 2 * gi + 1, lmx);
   }
+}
+
+DEV void group_pick_window(const Params& P, uint32_t gi, GwinSmem& W, uint32_t* hist, uint32_t* sh) {
+  const uint4 G = P.groups[gi];
+  const uint4 st = segment_pick(P, G.x, hist, sh);
+  if (threadIdx.x == 0 && G.y == P.segs[G.w].lu_begin) {  // the segment's first group
+    uint2* ss = reinterpret_cast<uint2*>(P.sstate + G.x);
+    pst(P, ss, make_uint2(st.x, st.y));
+    pst(P, ss + 1, make_uint2(st.z, st.w));
+  }
+  if (st.w == 0) group_window(P, gi, G, st, W, sh);
 }
 
 __global__ __launch_bounds__(BLOCK) void k_gwin(Params P) {
   __shared__ GwinSmem W;
   __shared__ uint32_t hist[HB2];
   __shared__ uint32_t sh[64];
-  const uint4 G = P.groups[blockIdx.x];
-  const uint4 st = segment_pick(P, G.x, hist, sh);
-  if (threadIdx.x == 0 && G.y == P.segs[G.w].lu_begin) P.sstate[G.x] = st;  // the segment's first group
-  if (st.w == 0) group_window(P, G, st, W, sh);
+  group_pick_window(P, blockIdx.x, W, hist, sh);
 }
 
 // Fast-path resolution in k_select: gather the groups' in-window lists (group order = index order),
@@ -1194,21 +1329,15 @@ DEV bool select_from_groups(const Params& P, const SegDev& sd, uint32_t lb, uint
 #pragma unroll
     for (uint32_t j = 0; j < EPT; ++j) {
       const uint32_t e = t + j * NT;
-      if (e < W) {
-        S.lst_val[e] = v[j].x;
-        S.lst_unit[e] = v[j].y;
-      }
+      if (e < W) S.lst[e] = v[j];
     }
   }
-  for (uint32_t i = t; i < nu; i += NT) {
-    S.ugt[i] = P.gtC[lb + i];
-    S.ueq[i] = 0;
-  }
+  for (uint32_t i = t; i < nu; i += NT) S.ge[i] = P.gtC[lb + i];
   __syncthreads();
   uint32_t rt = st.z;
-  const uint32_t T = block_select<NT>(
+  const uint32_t T = block_select<NT, SEL_HB>(
       [&](auto&& f) {
-        for (uint32_t i = t; i < W; i += NT) f(S.lst_val[i] & KEY_MAX);
+        for (uint32_t i = t; i < W; i += NT) f(S.lst[i].x & KEY_MAX);
       },
       st.x, st.y, rt, S.hist, S.sh);
   constexpr uint32_t EPT = WLIST / NT;
@@ -1216,14 +1345,14 @@ DEV bool select_from_groups(const Params& P, const SegDev& sd, uint32_t lb, uint
   float lmn = qnan(), lmx = qnan();
   uint32_t leq = 0, lfp = NONE, lfn = NONE;
   for (uint32_t q = q0; q < q1; ++q) {
-    const uint32_t vb = S.lst_val[q];
+    const uint32_t vb = S.lst[q].x;
     const uint32_t key = vb & KEY_MAX;
     if (key > T) {
-      atomicAdd(&S.ugt[S.lst_unit[q]], 1u);
+      atomicAdd(&S.ge[S.lst[q].y], 1u);
       lmn = fmin_nan(lmn, __uint_as_float(vb));
       lmx = fmax_nan(lmx, __uint_as_float(vb));
     } else if (key == T) {
-      atomicAdd(&S.ueq[S.lst_unit[q]], 1u);
+      atomicAdd(&S.ge[S.lst[q].y], 1u << 16);
       const bool neg = (vb >> 31) != 0;
       lfp = min(lfp, neg ? NONE : leq);
       lfn = min(lfn, neg ? leq : NONE);
@@ -1244,7 +1373,7 @@ DEV bool select_from_groups(const Params& P, const SegDev& sd, uint32_t lb, uint
   if (lfp != NONE) atomicMin(&S.sh[42], ex + lfp);
   if (lfn != NONE) atomicMin(&S.sh[43], ex + lfn);
   __syncthreads();
-  T_out = T;  // per-unit counts stay in S.ugt / S.ueq for the caller's in-order scan
+  T_out = T;  // per-unit counts stay in S.ge for the caller's in-order scan
   rt_out = rt;
   fp = S.sh[42];
   fn = S.sh[43];
@@ -1283,12 +1412,23 @@ DEV void segment_select(const Params& P, uint32_t li, SelSmem& S) {
     // candidate lists with tlo = thi = T*.
     const uint32_t n = sd.n;
     uint32_t rk = k;
-    const uint32_t T = block_select<NT>(
+    const uint32_t T = block_select<NT, SEL_HB>(
         [&](auto&& f) {
           for (uint32_t i = t; i < n; i += NT) f(fkey(load_x1<DELTA>(P, sd.in_off + i)));
         },
         0u, KEY_MAX, rk, S.hist, S.sh);
-    for (uint32_t i = wv; i < nu; i += NW) scan_unit<DELTA, 4>(P, lb + i, P.lunits[lb + i], T, T, nullptr);
+    for (uint32_t i = wv; i < nu; i += NW) {
+      if (P.wt)  // k_fused: the emit blocks of other CUs read these records
+        scan_unit_t<DELTA, 4, true>(P, lb + i, P.lunits[lb + i], [&]() { return make_uint2(T, T); }, nullptr);
+      else
+        scan_unit<DELTA, 4>(P, lb + i, P.lunits[lb + i], T, T, nullptr);
+    }
+    if (P.wt) {  // the counts / records this CU read before the rewrite may sit stale in its L1
+      drain();
+      __syncthreads();
+      if (t == 0) acquire_agent();
+      drain();
+    }
     __syncthreads();
     sa = 0;
     for (uint32_t i = t; i < nu; i += NT) sa += P.cntA[lb + i];
@@ -1310,18 +1450,18 @@ DEV void segment_select(const Params& P, uint32_t li, SelSmem& S) {
   for (uint32_t c0 = 0; c0 < nu; c0 += NT) {
     const uint32_t i = c0 + t;
     const bool valid = i < nu;
-    const uint32_t e = valid ? (done ? S.ueq[i] : P.eqC[lb + i]) : 0u;  // fast path: counts in LDS
+    const uint32_t e = valid ? (done ? S.ge[i] >> 16 : P.eqC[lb + i]) : 0u;  // fast path: counts in LDS
     uint32_t tot;
     const uint32_t ex = block_excl_scan<NT>(e, S.sh, tot) + carry_e;
     carry_e += tot;
     const uint32_t quota = !valid ? 0u : (ex >= rt ? 0u : min(e, rt - ex));
-    const uint32_t sel = valid ? (done ? S.ugt[i] : P.gtC[lb + i]) + quota : 0u;
+    const uint32_t sel = valid ? (done ? S.ge[i] & 0xFFFFu : P.gtC[lb + i]) + quota : 0u;
     uint32_t tot2;
     const uint32_t so = block_excl_scan<NT>(sel, S.sh, tot2) + carry_sel;
     carry_sel += tot2;
     if (valid) {
-      P.eqpre[lb + i] = ex;
-      P.outoff[lb + i] = so;
+      pst(P, P.eqpre + lb + i, ex);
+      pst(P, P.outoff + lb + i, so);
     }
   }
   STAMP(P, li, 11);
@@ -1343,10 +1483,10 @@ DEV void segment_select(const Params& P, uint32_t li, SelSmem& S) {
     scale = (gmx == gmn) ? 0.0f : (gmx - gmn) / P.levels;
   }
   if (t == 0) {
-    P.tstar[s] = T;
-    P.rtie[s] = rt;
-    P.mn[s] = mn;
-    P.scale[s] = scale;
+    pst(P, P.tstar + s, T);
+    pst(P, P.rtie + s, rt);
+    pst(P, P.mn + s, mn);
+    pst(P, P.scale + s, scale);
   }
   STAMP(P, li, 12);
 }
@@ -1371,14 +1511,13 @@ __global__ __launch_bounds__(SEL_NT) void k_select(Params P) {
 
 DEV uint32_t rl(uint32_t v, uint32_t l) { return (uint32_t)__builtin_amdgcn_readlane((int)v, (int)l); }
 
+// one wave emits the large units [lu0, lu1) (lu1 - lu0 <= EMIT_UPW)
 template <bool RAW>
-__global__ __launch_bounds__(BLOCK) void k_emit(Params P) {
-  const uint32_t lane = lane_id(), wv = threadIdx.x >> 6;
-  const uint32_t lu0 = (blockIdx.x * WAVES + wv) * EMIT_UPW;
-  if (lu0 >= P.n_lunits) return;
+DEV void emit_units(const Params& P, uint32_t lu0, uint32_t lu1) {
+  const uint32_t lane = lane_id();
   // round 1 / 2: lane g < EMIT_UPW holds unit lu0 + g's count, offsets and its segment's T*, tie budget,
   // mn, scale (lanes past EMIT_UPW or past the last unit repeat a valid unit; never used)
-  const uint32_t lug = min(lu0 + min(lane, EMIT_UPW - 1), P.n_lunits - 1);
+  const uint32_t lug = min(lu0 + min(lane, EMIT_UPW - 1), lu1 - 1);
   const uint32_t nCg = P.cntC[lug];
   const uint32_t segg = P.lunits[lug].seg;
   const uint64_t sog = P.lunits[lug].out_off;
@@ -1389,13 +1528,13 @@ __global__ __launch_bounds__(BLOCK) void k_emit(Params P) {
   uint2 rec0[EMIT_UPW];
 #pragma unroll
   for (uint32_t g = 0; g < EMIT_UPW; ++g) {
-    const uint32_t lu = min(lu0 + g, P.n_lunits - 1), nC = rl(nCg, g);
+    const uint32_t lu = min(lu0 + g, lu1 - 1), nC = rl(nCg, g);
     rec0[g] = P.cand[(uint64_t)lu * UNIT + min(lane, nC ? nC - 1 : 0u)];  // unconditional (clamped) load
   }
 #pragma unroll
   for (uint32_t g = 0; g < EMIT_UPW; ++g) {
     const uint32_t nC = rl(nCg, g);
-    if (lu0 + g < P.n_lunits && nC != 0) {
+    if (lu0 + g < lu1 && nC != 0) {
       const uint32_t lu = lu0 + g;
       const uint32_t T = rl(Tg, g), rt = rl(rtg, g), eqp = rl(eqpg, g);
       const float mn = __uint_as_float(rl(__float_as_uint(mng), g));
@@ -1424,6 +1563,120 @@ __global__ __launch_bounds__(BLOCK) void k_emit(Params P) {
         outc += (uint32_t)__popcll(sb);
       }
     }
+  }
+}
+
+template <bool RAW>
+__global__ __launch_bounds__(BLOCK) void k_emit(Params P) {
+  const uint32_t wv = threadIdx.x >> 6;
+  const uint32_t lu0 = (blockIdx.x * WAVES + wv) * EMIT_UPW;
+  if (lu0 >= P.n_lunits) return;
+  emit_units<RAW>(P, lu0, min(lu0 + EMIT_UPW, P.n_lunits));
+}
+
+// ------------------------------------------------------------------------------------------------
+// k_fused: the whole encode as ONE launch (no kernel boundaries; the select phases of a segment run while
+// later segments still stream). Every block runs one work item, named by P.items[blockIdx.x]:
+//   SAMPLE(li)  the sampler of large segment li                                    k_sample
+//   SMALL(i)    small segment i, whole, in LDS                                     k_small
+//   SCAN(j)     4 large units of the scan order, one wave each; the loads go out before the wave waits
+//               for its segment's sampler                                           k_scan
+//   GHIST(g)    band histogram of group g, once its units are scanned              k_ghist
+//   GWIN(g)     window + per-unit counts of group g, once the segment's histograms are in   k_gwin
+//   SELECT(li)  exact k-th key, offsets, min/max of segment li, once its windows are in     k_select
+//   EMIT(e)     up to 32 units of one segment (8 per wave), once it is selected   k_emit
+// The host orders the items so that every item comes after everything it waits for (plan_create:
+// fused_schedule); workgroups are dispatched in order, so a waiting block only ever waits for blocks
+// that were dispatched before it. Every wait is bounded (hf_err[0] records a give-up).
+// Hand-offs: sampler -> scan: T_lo/T_hi stored write-through, flag, read by the scan wave with sc1 loads.
+// scan -> GHIST: records and counts stored write-through, drained, one atomic add per wave; the group
+// blocks acquire. GHIST -> GWIN -> SELECT -> EMIT: write-through stores (Params::wt), drained, barrier,
+// one atomic per block; one acquire per consuming block.
+// ------------------------------------------------------------------------------------------------
+enum : uint32_t { R_SAMPLE = 0, R_SMALL = 1, R_SCAN = 2, R_GHIST = 3, R_GWIN = 4, R_SELECT = 5, R_EMIT = 6 };
+constexpr uint32_t EMIT_BLOCK_UNITS = WAVES * EMIT_UPW;
+
+struct GhistSmem {
+  uint32_t hist[HB2];
+  uint32_t upre[GU + 1];
+  uint32_t sh[64];
+};
+struct GwinAll {
+  GwinSmem w;
+  uint32_t hist[HB2];
+  uint32_t sh[64];
+};
+struct SmallSmem {
+  float vals[SMALL_MAX];
+  uint32_t hist[HIST_BINS];
+  uint32_t sh[64];
+};
+constexpr size_t cmax(size_t a, size_t b) { return a > b ? a : b; }
+constexpr size_t FUSED_LDS =
+    cmax(cmax(sizeof(SelSmem), sizeof(SmallSmem)), cmax(cmax(sizeof(GwinAll), sizeof(GhistSmem)), WAVES * STAGE_CAP * sizeof(uint2)));
+static_assert(FUSED_LDS <= 32 * 1024, "k_fused keeps five blocks per CU (160 KB of LDS)");
+
+template <bool DELTA, bool RAW>
+__global__ __launch_bounds__(BLOCK, SCAN_WPE) void k_fused(Params P) {
+  __shared__ __attribute__((aligned(16))) uint8_t arena[FUSED_LDS];
+  const uint32_t item = P.items[blockIdx.x];
+  const uint32_t role = item >> 28, idx = item & 0x0FFFFFFFu;
+  const uint32_t t = threadIdx.x, lane = lane_id(), wv = t >> 6;
+  if (role == R_SCAN) {
+    const uint32_t q = idx * WAVES + wv;
+    if (q >= P.n_lunits) return;
+    const uint32_t lu = P.fsched[q];
+    const UnitDev L = P.lunits[lu];
+    uint2* stage = reinterpret_cast<uint2*>(arena) + wv * STAGE_CAP;
+    auto get_t = [&]() {
+      uint32_t lo = 0, hi = 0;
+      if (lane == 0) {
+        wait_ge(P.hf_sampled + L.seg, 1u, P.hf_err);
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // compiler order only: sc1 loads follow
+        lo = ld_sc1(P.tlo + lu);
+        hi = ld_sc1(P.thi + lu);
+      }
+      return make_uint2(__builtin_amdgcn_readfirstlane(lo), __builtin_amdgcn_readfirstlane(hi));
+    };
+    scan_unit_t<DELTA, DELTA ? 4 : SCAN_NB, true>(P, lu, L, get_t, stage);
+    drain();  // every lane's write-through stores have landed
+    if (lane == 0) add_sc1(P.hf_garr + P.lgroup[lu], 1u);
+  } else if (role == R_SAMPLE) {
+    uint32_t* hist = reinterpret_cast<uint32_t*>(arena);
+    sample_segment<DELTA, true>(P, idx, hist, hist + HIST_BINS);
+    drain();
+    __syncthreads();
+    if (t == 0) st_sc1(P.hf_sampled + P.large_list[idx], 1u);
+  } else if (role == R_SMALL) {
+    SmallSmem& S = *reinterpret_cast<SmallSmem*>(arena);
+    small_encode<DELTA, RAW>(P, P.small_list[idx], S.vals, S.hist, S.sh);
+  } else if (role == R_GHIST) {
+    GhistSmem& S = *reinterpret_cast<GhistSmem*>(arena);
+    const uint4 G = P.groups[idx];
+    block_wait(P.hf_garr + idx, G.z, P.hf_err);
+    group_hist(P, idx, S.hist, S.upre, S.sh);
+    block_publish_add(P.hf_ghist + G.w, 1u);
+  } else if (role == R_GWIN) {
+    GwinAll& S = *reinterpret_cast<GwinAll*>(arena);
+    const uint4 G = P.groups[idx];
+    const SegDev sd = P.segs[G.w];
+    const uint32_t ng = (sd.unit_end - sd.unit_begin + GU - 1) / GU;
+    block_wait(P.hf_ghist + G.w, ng, P.hf_err);
+    group_pick_window(P, idx, S.w, S.hist, S.sh);
+    block_publish_add(P.hf_gwin + G.w, 1u);
+  } else if (role == R_SELECT) {
+    SelSmem& S = *reinterpret_cast<SelSmem*>(arena);
+    const uint32_t s = P.large_list[idx];
+    const SegDev sd = P.segs[s];
+    const uint32_t ng = (sd.unit_end - sd.unit_begin + GU - 1) / GU;
+    block_wait(P.hf_gwin + s, ng, P.hf_err);
+    segment_select<BLOCK, DELTA, RAW>(P, idx, S);
+    block_publish_add(P.hf_sel + s, 1u);
+  } else if (role == R_EMIT) {
+    const uint4 E = P.eblocks[idx];  // {first large unit, units, segment, 0}
+    block_wait(P.hf_sel + E.z, 1u, P.hf_err);
+    const uint32_t u0 = E.x + wv * EMIT_UPW, u1 = min(u0 + EMIT_UPW, E.x + E.y);
+    if (u0 < u1) emit_units<RAW>(P, u0, u1);
   }
 }
 
@@ -1462,11 +1715,60 @@ DEV void merge_entries(float4 (&b)[UNIT_IT], uint64_t& kept, uint32_t pos0, floa
   }
 }
 
+// First entry e of each list L_m[0, k_m) with (uint32)L_m[e] >= target_m (k_m if none), for M lists at once,
+// by one wave: each round probes 64 evenly spaced entries of every remaining interval (all M probe loads
+// in flight together) and keeps the 1/64 of it the answer lies in; ceil(log64 k) rounds (3 for k <= 262k).
+// The lists are segment idx lists (ascending); a corrupt (unsorted) list still gives a result in [0, k]
+// after at most 6 rounds, so decode stays in bounds.
+template <int M>
+DEV void wave_lower_bound(const int32_t* const (&L)[M], const uint32_t (&k)[M], const uint32_t (&target)[M],
+                          uint32_t (&res)[M]) {
+  const uint32_t lane = lane_id();
+  uint32_t a[M], b[M];
+#pragma unroll
+  for (int m = 0; m < M; ++m) {
+    a[m] = 0;
+    b[m] = k[m];
+  }
+  for (int round = 0; round < 6; ++round) {
+    bool more = false;
+#pragma unroll
+    for (int m = 0; m < M; ++m) more = more || a[m] < b[m];
+    if (!more) break;
+    uint32_t v[M], p[M], step[M];
+#pragma unroll
+    for (int m = 0; m < M; ++m) {  // issue every probe load before any is used
+      const uint32_t len = b[m] - a[m];
+      step[m] = len > 64 ? (len + 63) / 64 : 1u;
+      p[m] = a[m] + lane * step[m];
+      v[m] = (uint32_t)L[m][min(p[m], k[m] ? k[m] - 1 : 0u)];
+    }
+#pragma unroll
+    for (int m = 0; m < M; ++m) {
+      if (a[m] >= b[m]) continue;
+      const uint32_t c = (uint32_t)__popcll(__ballot(p[m] < b[m] && v[m] < target[m]));
+      if (c == 0) {
+        b[m] = a[m];
+      } else {
+        const uint32_t lo = a[m] + (c - 1) * step[m] + 1;
+        b[m] = min(b[m], a[m] + c * step[m]);
+        a[m] = min(lo, b[m]);
+        if (step[m] == 1) a[m] = b[m];
+      }
+    }
+  }
+#pragma unroll
+  for (int m = 0; m < M; ++m) res[m] = a[m];
+}
+
 // units per wave of k_decode: 1 with a base (its 16 float4 of base per unit would double the registers)
 template <bool HASBASE>
 constexpr uint32_t decode_dpw() { return HASBASE ? 1u : 2u; }
 
-template <bool RAW, bool HASBASE>
+// SEARCH: the units' entry ranges are found in-kernel (wave_lower_bound) instead of read from k_bounds'
+// ustart: one launch less, three more dependent load rounds per wave — worth it when the plan is small
+// and latency-bound (one update), not for a batch (the rounds then cost write-stream slots).
+template <bool RAW, bool HASBASE, bool SEARCH>
 __global__ __launch_bounds__(BLOCK, DECODE_WPE) void k_decode(Params P) {
   constexpr uint32_t DPW = decode_dpw<HASBASE>();
   const uint32_t lane = lane_id(), wv = threadIdx.x >> 6;
@@ -1475,11 +1777,33 @@ __global__ __launch_bounds__(BLOCK, DECODE_WPE) void k_decode(Params P) {
   UnitDev U[DPW];
   uint32_t lo[DPW], hi[DPW];
 #pragma unroll
-  for (uint32_t r = 0; r < DPW; ++r) {
-    const uint32_t uu = min(u0 + r, P.n_units - 1);
-    U[r] = P.units[uu];
-    lo[r] = P.ustart[uu];
-    hi[r] = P.ustart[uu + 1];  // ustart has n_units + 1 entries
+  for (uint32_t r = 0; r < DPW; ++r) U[r] = P.units[min(u0 + r, P.n_units - 1)];
+  if (!SEARCH) {
+#pragma unroll
+    for (uint32_t r = 0; r < DPW; ++r) {
+      const uint32_t uu = min(u0 + r, P.n_units - 1);
+      lo[r] = P.ustart[uu];
+      hi[r] = P.ustart[uu + 1];  // ustart has n_units + 1 entries
+    }
+  } else {
+    // the unit's kept entries [lo, hi) in its segment's sorted idx list, found in-kernel (no k_bounds
+    // launch): lower bounds of the unit's first and one-past-last element index
+    const int32_t* L[2 * DPW];
+    uint32_t kk[2 * DPW], tg[2 * DPW], res[2 * DPW];
+#pragma unroll
+    for (uint32_t r = 0; r < DPW; ++r) {
+      L[2 * r] = L[2 * r + 1] = P.cidx + U[r].out_off;
+      kk[2 * r] = U[r].k;
+      kk[2 * r + 1] = U[r].last ? 0u : U[r].k;  // a segment's last unit ends at k: no search
+      tg[2 * r] = U[r].start;
+      tg[2 * r + 1] = U[r].last ? 0xFFFFFFFFu : U[r].start + U[r].len;
+    }
+    wave_lower_bound<2 * DPW>(L, kk, tg, res);
+#pragma unroll
+    for (uint32_t r = 0; r < DPW; ++r) {
+      lo[r] = res[2 * r];
+      hi[r] = res[2 * r + 1];
+    }
   }
   uint32_t pos[DPW], q[DPW];
   float mn[DPW], sc[DPW];
@@ -1751,7 +2075,9 @@ int fail(int code, const char* fmt, ...) {
 size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 
 struct WsLayout {
-  size_t tstar, rtie, status;
+  size_t ctl_bytes;  // the control block at offset 0: status and the k_fused hand-off words
+  size_t status, hf_sampled, hf_ghist, hf_gwin, hf_sel, hf_err, hf_garr;
+  size_t tstar, rtie;
   size_t tlo, thi, cntA, cntC, gtC, eqC, eqpre, outoff;
   size_t cand, stamps, ghist, gcnt, glist, gmm, sstate, shhi;
   size_t total;
@@ -1759,7 +2085,18 @@ struct WsLayout {
 
 WsLayout ws_layout(size_t S, size_t LU, size_t NG, size_t NL) {
   WsLayout L{};
-  size_t o = 0;
+  // control block: words k_fused polls, zeroed by one memset before every launch (a block of its own at
+  // the workspace start, a multiple of 16 bytes: Guideline 16 "Re-initialise every call")
+  size_t c = 0;
+  L.status = c; c += 4 * S;
+  L.hf_sampled = c; c += 4 * S;
+  L.hf_ghist = c; c += 4 * S;
+  L.hf_gwin = c; c += 4 * S;
+  L.hf_sel = c; c += 4 * S;
+  L.hf_err = c; c += 16;
+  L.hf_garr = c; c += 4 * NG;
+  L.ctl_bytes = align_up(c, 16);
+  size_t o = align_up(L.ctl_bytes, 256);
   auto take = [&](size_t bytes) {
     size_t r = o;
     o = align_up(o + bytes, 256);
@@ -1767,7 +2104,6 @@ WsLayout ws_layout(size_t S, size_t LU, size_t NG, size_t NL) {
   };
   L.tstar = take(4 * S);
   L.rtie = take(4 * S);
-  L.status = take(4 * S);
   L.tlo = take(4 * LU);
   L.thi = take(4 * LU);
   L.cntA = take(4 * LU);
@@ -1788,6 +2124,85 @@ WsLayout ws_layout(size_t S, size_t LU, size_t NG, size_t NL) {
   return L;
 }
 
+// k_fused work items in launch order (see k_fused). Scan order: large segments by descending size, so the
+// long select chains of the big segments start while the small ones still stream. Each waiting item is
+// placed `delay` items after the last item it waits for (a block dispatched much earlier would hold a CU
+// slot while it spins); dependencies always precede their dependents, so in-order dispatch cannot
+// deadlock.
+struct FusedSchedule {
+  std::vector<uint32_t> items, fsched, lgroup;
+  std::vector<uint4> eblocks;
+};
+
+FusedSchedule fused_schedule(const std::vector<SegDev>& segs, const std::vector<uint32_t>& large_list,
+                             uint32_t n_small, uint32_t n_lunits, const std::vector<uint4>& groups, uint32_t delay) {
+  FusedSchedule F;
+  const uint32_t NL = (uint32_t)large_list.size();
+  std::vector<uint32_t> order(NL);
+  for (uint32_t i = 0; i < NL; ++i) order[i] = i;
+  std::stable_sort(order.begin(), order.end(),
+                   [&](uint32_t a, uint32_t b) { return segs[large_list[a]].n > segs[large_list[b]].n; });
+  F.lgroup.assign(n_lunits, 0);
+  std::vector<uint32_t> ng(NL), eb_first(NL), eb_count(NL);
+  std::vector<std::vector<uint32_t>> done_at;
+  for (uint32_t li : order) {
+    const SegDev& d = segs[large_list[li]];
+    const uint32_t nu = d.unit_end - d.unit_begin;
+    ng[li] = (nu + GU - 1) / GU;
+    for (uint32_t u = 0; u < nu; ++u) {
+      F.lgroup[d.lu_begin + u] = d.g_begin + u / GU;
+      F.fsched.push_back(d.lu_begin + u);
+      if ((u + 1) % GU == 0 || u + 1 == nu) {  // the group's last unit: its block completes the group
+        const uint32_t blk = (uint32_t)(F.fsched.size() - 1) / WAVES;
+        if (done_at.size() <= blk) done_at.resize(blk + 1);
+        done_at[blk].push_back(d.g_begin + u / GU);
+      }
+    }
+    eb_first[li] = (uint32_t)F.eblocks.size();
+    for (uint32_t u0 = 0; u0 < nu; u0 += EMIT_BLOCK_UNITS)
+      F.eblocks.push_back(make_uint4(d.lu_begin + u0, std::min(EMIT_BLOCK_UNITS, nu - u0), large_list[li], 0u));
+    eb_count[li] = (uint32_t)F.eblocks.size() - eb_first[li];
+  }
+  const uint32_t nscan = (n_lunits + WAVES - 1) / WAVES;
+  auto mk = [](uint32_t role, uint32_t idx) { return (role << 28) | idx; };
+  for (uint32_t li : order) F.items.push_back(mk(R_SAMPLE, li));
+  for (uint32_t i = 0; i < n_small; ++i) F.items.push_back(mk(R_SMALL, i));
+  // pending items: (ready position, sequence, item)
+  typedef std::pair<std::pair<uint64_t, uint64_t>, uint32_t> Pending;
+  std::priority_queue<Pending, std::vector<Pending>, std::greater<Pending>> q;
+  uint64_t seq = 0;
+  std::vector<uint32_t> gh_done(NL, 0), gw_done(NL, 0);
+  auto push = [&](uint32_t item) { q.push(Pending({(uint64_t)F.items.size() + delay, seq++}, item)); };
+  auto place = [&](uint32_t item) {
+    F.items.push_back(item);
+    const uint32_t role = item >> 28, idx = item & 0x0FFFFFFFu;
+    if (role == R_SCAN) {
+      if (idx < done_at.size())
+        for (uint32_t g : done_at[idx]) push(mk(R_GHIST, g));
+    } else if (role == R_GHIST) {
+      const uint32_t li = groups[idx].x;
+      if (++gh_done[li] == ng[li])
+        for (uint32_t g = 0; g < ng[li]; ++g) push(mk(R_GWIN, segs[large_list[li]].g_begin + g));
+    } else if (role == R_GWIN) {
+      const uint32_t li = groups[idx].x;
+      if (++gw_done[li] == ng[li]) push(mk(R_SELECT, li));
+    } else if (role == R_SELECT) {
+      for (uint32_t e = 0; e < eb_count[idx]; ++e) push(mk(R_EMIT, eb_first[idx] + e));
+    }
+  };
+  uint32_t j = 0;
+  while (j < nscan || !q.empty()) {
+    if (!q.empty() && (q.top().first.first <= F.items.size() || j == nscan)) {
+      const uint32_t item = q.top().second;
+      q.pop();
+      place(item);
+    } else {
+      place(mk(R_SCAN, j++));
+    }
+  }
+  return F;
+}
+
 }  // namespace
 
 struct coalac_plan {
@@ -1806,6 +2221,12 @@ struct coalac_plan {
   uint32_t n_groups = 0;
   BChunk* bchunks = nullptr;  // aggregate: k_bounds work list
   uint32_t n_bchunks = 0;
+  // one-launch encode (k_fused): block work items, scan order, unit -> group, emit blocks
+  uint32_t* items = nullptr;
+  uint32_t n_items = 0;
+  uint32_t* fsched = nullptr;
+  uint32_t* lgroup = nullptr;
+  uint4* eblocks = nullptr;
   std::vector<SegDev> hsegs;  // host copy (aggregate validates the client-copy structure)
   // encode fork/join: k_small runs on `side`, concurrently with k_sample / k_scan on the caller's stream
   hipStream_t side = nullptr;
@@ -1833,6 +2254,10 @@ void fill_meta(Params& P, coalac_plan_t plan) {
   P.large_list = plan->large_list;
   P.groups = plan->groups;
   P.n_groups = plan->n_groups;
+  P.items = plan->items;
+  P.fsched = plan->fsched;
+  P.lgroup = plan->lgroup;
+  P.eblocks = plan->eblocks;
   P.nseg = (uint32_t)plan->nseg;
   P.n_small = plan->n_small;
   P.n_large = plan->n_large;
@@ -1874,6 +2299,10 @@ bool at_boundary(unsigned stages, const int (*span)[2], int nst, int i) {
       if (span[k][0] <= i && i <= span[k][1]) return true;
   return false;
 }
+
+// decode plans of up to this many 4096-element units (~1.3 ResNet-50 updates) search their entry ranges
+// in k_decode; bigger ones run k_bounds first
+constexpr uint32_t DECODE_SEARCH_MAX_UNITS = 8192;
 
 constexpr int ENC_SPAN[4][2] = {{0, 1}, {1, 2}, {2, 4}, {0, 1}};  // SAMPLE, SCAN, SELECT, SMALL
 constexpr int DEC_SPAN[2][2] = {{0, 1}, {1, 2}};                  // BOUNDS, DECODE
@@ -1933,6 +2362,22 @@ int launch_encode(const Params& P, coalac_plan_t plan, hipStream_t st, const coa
   if (fork) HIP_CHECK(hipStreamWaitEvent(st, plan->join, 0));
   ENC_BOUNDARY(4);
 #undef ENC_BOUNDARY
+  return COALAC_OK;
+}
+
+// The one-launch encode: zero the control block, then k_fused. Events (the _ev / _sched boundaries):
+// [0] before the memset, [1] before k_fused, [2] [3] [4] after it.
+template <bool DELTA, bool RAW>
+int launch_fused(const Params& P, coalac_plan_t plan, hipStream_t st, const coalac_sched_t* sc, void* ws) {
+  BOUNDARY(0);
+  HIP_CHECK(hipMemsetAsync(ws, 0, plan->ws.ctl_bytes, st));
+  BOUNDARY(1);
+  Params Q = P;
+  Q.wt = 1;
+  hipLaunchKernelGGL((k_fused<DELTA, RAW>), dim3(plan->n_items), dim3(BLOCK), 0, st, Q);
+  BOUNDARY(2);
+  BOUNDARY(3);
+  BOUNDARY(4);
   return COALAC_OK;
 }
 
@@ -2031,6 +2476,11 @@ int coalac_plan_create(const coalac_seg_t* h_segs, int nseg, int bits, coalac_pl
   p->n_bchunks = (uint32_t)bchunks.size();
   p->hsegs = segs;
   p->dec_ws = align_up(4 * (units.size() + 1), 256);  // decode / aggregate: per-unit bounds
+  uint32_t delay = 1024;  // k_fused: items between a waiting item and what it waits for (~ the blocks
+                          // resident at once: a waiting block is dispatched as its inputs complete)
+  if (const char* e = getenv("COALAC_FUSED_DELAY")) delay = (uint32_t)atoi(e);
+  const FusedSchedule F = fused_schedule(segs, large_list, p->n_small, p->n_lunits, groups, delay);
+  p->n_items = (uint32_t)F.items.size();
 
   const size_t o_segs = 0;
   const size_t o_units = align_up(o_segs + sizeof(SegDev) * segs.size(), 256);
@@ -2039,7 +2489,11 @@ int coalac_plan_create(const coalac_seg_t* h_segs, int nseg, int bits, coalac_pl
   const size_t o_large = align_up(o_small + 4 * small_list.size(), 256);
   const size_t o_grp = align_up(o_large + 4 * large_list.size(), 256);
   const size_t o_bch = align_up(o_grp + sizeof(uint4) * groups.size(), 256);
-  const size_t bytes = align_up(o_bch + sizeof(BChunk) * bchunks.size(), 256) + 256;
+  const size_t o_items = align_up(o_bch + sizeof(BChunk) * bchunks.size(), 256);
+  const size_t o_fsched = align_up(o_items + 4 * F.items.size(), 256);
+  const size_t o_lgroup = align_up(o_fsched + 4 * F.fsched.size(), 256);
+  const size_t o_eblk = align_up(o_lgroup + 4 * F.lgroup.size(), 256);
+  const size_t bytes = align_up(o_eblk + sizeof(uint4) * F.eblocks.size(), 256) + 256;
   std::vector<uint8_t> host(bytes, 0);
   if (!segs.empty()) memcpy(host.data() + o_segs, segs.data(), sizeof(SegDev) * segs.size());
   if (!units.empty()) memcpy(host.data() + o_units, units.data(), sizeof(UnitDev) * units.size());
@@ -2048,6 +2502,10 @@ int coalac_plan_create(const coalac_seg_t* h_segs, int nseg, int bits, coalac_pl
   if (!large_list.empty()) memcpy(host.data() + o_large, large_list.data(), 4 * large_list.size());
   if (!groups.empty()) memcpy(host.data() + o_grp, groups.data(), sizeof(uint4) * groups.size());
   if (!bchunks.empty()) memcpy(host.data() + o_bch, bchunks.data(), sizeof(BChunk) * bchunks.size());
+  if (!F.items.empty()) memcpy(host.data() + o_items, F.items.data(), 4 * F.items.size());
+  if (!F.fsched.empty()) memcpy(host.data() + o_fsched, F.fsched.data(), 4 * F.fsched.size());
+  if (!F.lgroup.empty()) memcpy(host.data() + o_lgroup, F.lgroup.data(), 4 * F.lgroup.size());
+  if (!F.eblocks.empty()) memcpy(host.data() + o_eblk, F.eblocks.data(), sizeof(uint4) * F.eblocks.size());
   hipError_t e = hipMalloc(&p->meta, bytes);
   if (e != hipSuccess) {
     delete p;
@@ -2067,6 +2525,10 @@ int coalac_plan_create(const coalac_seg_t* h_segs, int nseg, int bits, coalac_pl
   p->large_list = reinterpret_cast<uint32_t*>(m + o_large);
   p->groups = reinterpret_cast<uint4*>(m + o_grp);
   p->bchunks = reinterpret_cast<BChunk*>(m + o_bch);
+  p->items = reinterpret_cast<uint32_t*>(m + o_items);
+  p->fsched = reinterpret_cast<uint32_t*>(m + o_fsched);
+  p->lgroup = reinterpret_cast<uint32_t*>(m + o_lgroup);
+  p->eblocks = reinterpret_cast<uint4*>(m + o_eblk);
   *out = p;
   return COALAC_OK;
 }
@@ -2130,6 +2592,12 @@ int coalac_encode_sched(coalac_plan_t plan, const float* d_in, const float* d_ba
   P.flags = flags;
   uint8_t* w = static_cast<uint8_t*>(d_ws);
   const WsLayout& L = plan->ws;
+  P.hf_sampled = reinterpret_cast<uint32_t*>(w + L.hf_sampled);
+  P.hf_ghist = reinterpret_cast<uint32_t*>(w + L.hf_ghist);
+  P.hf_gwin = reinterpret_cast<uint32_t*>(w + L.hf_gwin);
+  P.hf_sel = reinterpret_cast<uint32_t*>(w + L.hf_sel);
+  P.hf_err = reinterpret_cast<uint32_t*>(w + L.hf_err);
+  P.hf_garr = reinterpret_cast<uint32_t*>(w + L.hf_garr);
   P.tstar = reinterpret_cast<uint32_t*>(w + L.tstar);
   P.rtie = reinterpret_cast<uint32_t*>(w + L.rtie);
   P.status = reinterpret_cast<uint32_t*>(w + L.status);
@@ -2151,7 +2619,19 @@ int coalac_encode_sched(coalac_plan_t plan, const float* d_in, const float* d_ba
   P.shhi = reinterpret_cast<uint32_t*>(w + L.shhi);
   hipStream_t st = static_cast<hipStream_t>(stream);
   const bool delta = d_base != nullptr, raw = plan->bits == 32;
-  if (delta && raw)
+  const unsigned all = COALAC_STAGE_SAMPLE | COALAC_STAGE_SCAN | COALAC_STAGE_SELECT | COALAC_STAGE_SMALL;
+  const bool whole = !(sched && (sched->stages & all) && (sched->stages & all) != all);
+  const bool fused = whole && !(flags & (COALAC_FLAG_MULTI_LAUNCH | COALAC_FLAG_STAMPS)) && plan->n_items > 0;
+  if (fused) {
+    if (delta && raw)
+      rc = launch_fused<true, true>(P, plan, st, sched, d_ws);
+    else if (delta)
+      rc = launch_fused<true, false>(P, plan, st, sched, d_ws);
+    else if (raw)
+      rc = launch_fused<false, true>(P, plan, st, sched, d_ws);
+    else
+      rc = launch_fused<false, false>(P, plan, st, sched, d_ws);
+  } else if (delta && raw)
     rc = launch_encode<true, true>(P, plan, st, sched);
   else if (delta)
     rc = launch_encode<true, false>(P, plan, st, sched);
@@ -2215,21 +2695,31 @@ int coalac_decode_sched(coalac_plan_t plan, const int32_t* d_idx, const void* d_
     const int rc_ = B(i);     \
     if (rc_) return rc_;      \
   } while (0)
+  // small plans: k_decode finds its units' entry ranges itself (one launch); batches: k_bounds first
+  const bool search = plan->n_units <= DECODE_SEARCH_MAX_UNITS;
   DEC_BOUNDARY(0);
-  if ((stages & COALAC_STAGE_BOUNDS) && plan->n_bchunks)
+  if ((stages & COALAC_STAGE_BOUNDS) && plan->n_bchunks && !search)
     hipLaunchKernelGGL(k_bounds, dim3(plan->n_bchunks), dim3(BLOCK), 0, st, P, plan->bchunks,
                        static_cast<uint32_t*>(d_ws));
   DEC_BOUNDARY(1);
+#define DEC(R, H)                                                                          \
+  do {                                                                                     \
+    if (search)                                                                            \
+      hipLaunchKernelGGL((k_decode<R, H, true>), dim3(g), dim3(BLOCK), 0, st, P);          \
+    else                                                                                   \
+      hipLaunchKernelGGL((k_decode<R, H, false>), dim3(g), dim3(BLOCK), 0, st, P);         \
+  } while (0)
   if (!(stages & COALAC_STAGE_DECODE))
     ;
   else if (raw && hb)
-    hipLaunchKernelGGL((k_decode<true, true>), dim3(g), dim3(BLOCK), 0, st, P);
+    DEC(true, true);
   else if (raw)
-    hipLaunchKernelGGL((k_decode<true, false>), dim3(g), dim3(BLOCK), 0, st, P);
+    DEC(true, false);
   else if (hb)
-    hipLaunchKernelGGL((k_decode<false, true>), dim3(g), dim3(BLOCK), 0, st, P);
+    DEC(false, true);
   else
-    hipLaunchKernelGGL((k_decode<false, false>), dim3(g), dim3(BLOCK), 0, st, P);
+    DEC(false, false);
+#undef DEC
   DEC_BOUNDARY(2);
 #undef DEC_BOUNDARY
   HIP_CHECK(hipGetLastError());
@@ -2347,6 +2837,16 @@ int coalac_workspace_fallbacks(coalac_plan_t plan, const void* d_ws, void* strea
   int c = 0;
   for (uint32_t s2 : large) c += st[s2] == 1;
   *out = c;
+  return COALAC_OK;
+}
+
+int coalac_workspace_timeouts(coalac_plan_t plan, const void* d_ws, void* stream, int* out) {
+  if (!plan || !d_ws || !out) return fail(COALAC_EINVAL, "coalac_workspace_timeouts: NULL argument");
+  uint32_t e[4] = {0, 0, 0, 0};
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  HIP_CHECK(hipMemcpyAsync(e, static_cast<const uint8_t*>(d_ws) + plan->ws.hf_err, sizeof(e), hipMemcpyDeviceToHost, s));
+  HIP_CHECK(hipStreamSynchronize(s));
+  *out = (int)e[0];
   return COALAC_OK;
 }
 

@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define COALAC_ABI_VERSION 1
+#define COALAC_ABI_VERSION 2
 
 enum {
   COALAC_OK = 0,
@@ -49,8 +49,10 @@ enum {
   COALAC_FLAG_FORCE_EXACT = 1,    /* test hook: re-select every large segment exactly (no sampling) */
   COALAC_FLAG_GENERIC_SELECT = 2, /* test hook: resolve the k-th key with the multi-pass select only */
   COALAC_FLAG_STAMPS = 4,         /* diagnostics: record per-block phase timestamps of k_select */
-  COALAC_FLAG_NO_FORK = 8         /* encode small segments inside k_scan, never on the plan's side stream
+  COALAC_FLAG_NO_FORK = 8,        /* encode small segments inside k_scan, never on the plan's side stream
                                      (for callers that run several plans concurrently themselves) */
+  COALAC_FLAG_MULTI_LAUNCH = 16   /* encode as the kernel sequence k_sample .. k_emit instead of the
+                                     one-launch k_fused (a whole encode is one launch by default) */
 };
 
 /* One fp32 segment (= one flattened tensor of the state_dict). Offsets are in ELEMENTS.
@@ -98,10 +100,13 @@ int coalac_decode(coalac_plan_t plan, const int32_t* d_idx, const void* d_vals, 
                   void* stream);
 
 /* Profiling variants: identical work, plus hipEventRecord(events[i], stream) between kernels.
- * encode: events[0] before k_sample, [1] after k_sample, [2] after k_scan, [3] after the select
- *         kernels (k_ghist, k_pick, k_gwin, k_select), [4] after k_emit (recorded even if the plan has
- *         no large segment); decode: [0] before k_bounds, [1] after k_bounds, [2] after k_decode.
- *         NULL array or NULL entries are skipped. */
+ * encode (one launch, the default): events[0] before the control-block memset, [1] before k_fused,
+ *         [2] [3] [4] after it;
+ * encode (COALAC_FLAG_MULTI_LAUNCH): [0] before k_sample, [1] after k_sample, [2] after k_scan, [3]
+ *         after the select kernels (k_ghist, k_gwin, k_select), [4] after k_emit (recorded even if the
+ *         plan has no large segment);
+ * decode: [0] before k_bounds (plans of > 8192 units only), [1] before k_decode, [2] after it. NULL
+ *         array or NULL entries are skipped. */
 int coalac_encode_ev(coalac_plan_t plan, const float* d_in, const float* d_base, int32_t* d_idx,
                      void* d_vals, float* d_mn, float* d_scale, void* d_ws, uint64_t ws_bytes,
                      unsigned flags, void* stream, void* const* events);
@@ -115,7 +120,8 @@ int coalac_decode_ev(coalac_plan_t plan, const int32_t* d_idx, const void* d_val
  *           COALAC_STAGE_SMALL   k_small  (segments of <= 4096 elements, whole) 0 .. 1
  *           COALAC_STAGE_SCAN    k_scan   (the one HBM read of the large segments) 1 .. 2
  *           COALAC_STAGE_SELECT  k_ghist k_gwin k_select k_emit                  2 .. 4
- *   decode  COALAC_STAGE_BOUNDS  k_bounds                                  boundaries 0 .. 1
+ *   decode  COALAC_STAGE_BOUNDS  k_bounds (plans of > 8192 units; smaller    boundaries 0 .. 1
+ *                                 plans: k_decode finds its units' entry ranges itself)
  *           COALAC_STAGE_DECODE  k_decode                                  1 .. 2
  * SAMPLE, SCAN, SELECT of one encode (and BOUNDS, DECODE of one decode) must run in this order on the
  * same workspace; SMALL is independent of them. The caller orders them, e.g. with the events below.
@@ -174,6 +180,10 @@ int coalac_aggregate_ev(coalac_plan_t plan, int clients, const int32_t* d_idx, c
 /* Diagnostics: number of segments whose sampled thresholds were rejected and re-selected exactly in
  * the last encode that used workspace d_ws (synchronises `stream`). */
 int coalac_workspace_fallbacks(coalac_plan_t plan, const void* d_ws, void* stream, int* out);
+
+/* Diagnostics: 1 if a bounded in-launch wait of the last one-launch encode with d_ws gave up (its results
+ * are then not valid; never expected), else 0 (synchronises `stream`). */
+int coalac_workspace_timeouts(coalac_plan_t plan, const void* d_ws, void* stream, int* out);
 
 /* Diagnostics: copy up to n phase timestamps (16 per k_select block = per large segment, 100 MHz
  * ticks; 0 = phase not reached) of the last COALAC_FLAG_STAMPS encode with d_ws to host (synchronises
