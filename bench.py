@@ -32,7 +32,8 @@ sys.path.insert(0, ROOT)
 
 METRIC = "encode+decode GB/s over fp32 weight updates (device-resident), 1/2/4/8 GPU"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md: 8.0 TB/s)
-MULTI_LAUNCH = 16  # COALAC_FLAG_MULTI_LAUNCH: the k_sample .. k_emit kernel sequence instead of k_fused
+ONE_LAUNCH = 64     # COALAC_FLAG_ONE_LAUNCH: the whole encode as one k_fused launch
+FRONT_LAUNCH = 128  # COALAC_FLAG_FRONT_LAUNCH: samplers + scan + small segments as one launch
 SPLIT = 2  # sub-batches per step: two independent pipelines side by side fill the CUs the other leaves
            # idle in its latency-bound stages and launch tails (+11 % over one 16-client pipeline)
 EVENT_EVERY = 4  # timing events on every 4th timed step (each recorded event adds a ~4 us dispatch gap)
@@ -41,8 +42,9 @@ CONFIGS = {  # name -> (layout | "c5", clients per GPU, split)
     "C3": ("resnet50_tv", 16, SPLIT),
     "C4": ("vit_b16", 16, SPLIT),
     "C5": ("c5", None, SPLIT),
-    "single": ("resnet50_tv", 1, 1),
+    "single": ("resnet50_tv", 1, "single"),
 }
+SINGLE_SPLIT = 1  # segment ranges of the single update run as this many concurrent sub-plans
 DEFAULT_EXTRAS = "C2,C4,C5,single"
 
 
@@ -70,6 +72,9 @@ def parse():
     p.add_argument("--event-every", type=int, default=EVENT_EVERY,
                    help="record the per-kernel timing events on every Nth timed step (1 = every step)")
     p.add_argument("--flags", type=int, default=0, help="coalac encode flags (test hooks; 0 for the bench)")
+    p.add_argument("--single-split", type=int, default=SINGLE_SPLIT,
+                   help="config 'single': the update's segments cut into this many ranges, each a sub-plan on its "
+                        "own stream (their latency-bound phases overlap)")
     p.add_argument("--cpu-seconds", type=float, default=8.0, help="CPU baseline time budget per leg")
     p.add_argument("--no-cpu-baseline", action="store_true")
     return p.parse_args()
@@ -193,6 +198,8 @@ def build_table(cfg, a, rank, headline):
     from coala_amd.layouts import fp32_sizes
     from coala_amd.workload import c5_share, mixed_table
     layout, clients, split = CONFIGS[cfg]
+    if split == "single":
+        split = a.single_split
     if headline:
         layout = a.layout or layout
         clients = a.clients or clients
@@ -278,9 +285,11 @@ def run_workload(cfg, a, dev, world, rank, headline):
     def union(pairs):
         ref = pairs[0][0]
         return max(ref.elapsed_time(e) for _, e in pairs) - min(ref.elapsed_time(s) for s, _ in pairs)
-    # one-launch encode (default): events [1] / [2] bracket k_fused; multi-launch: k_scan
-    multi = bool(a.flags & MULTI_LAUNCH)
-    enc_kernel = "k_scan" if multi else "k_fused"
+    # events [1] / [2] bracket the encode's streaming launch: k_scan (the default kernel sequence), the front
+    # launch (samplers + scan + small segments) or the whole k_fused (one launch)
+    one = bool(a.flags & ONE_LAUNCH)
+    multi = not one and not (a.flags & FRONT_LAUNCH)
+    enc_kernel = "k_scan" if multi else "k_fused" if one else "k_front"
     stages = {}
     for name, which in {enc_kernel: ev_e, "k_decode": ev_d}.items():
         per = [union([(e[1], e[2]) for e in which[i]]) for i in timed_steps]
@@ -291,7 +300,7 @@ def run_workload(cfg, a, dev, world, rank, headline):
     segs = t.segs.astype("int64")
     large_elems = int(segs[segs[:, 1] > SMALL_MAX, 1].sum())
     alg = {  # algorithmic HBM bytes per timed interval
-        enc_kernel: (4 * large_elems if multi else 4 * N + (4 + vb) * K + 8 * T) + (4 * N if delta else 0),
+        enc_kernel: (4 * large_elems if multi else 4 * N + (4 + vb) * K + 8 * T if one else 4 * N) + (4 * N if delta else 0),
         "k_decode": 4 * N * (2 if delta else 1) + (4 + vb) * K + 8 * T,
     }
     dom = max(alg, key=lambda k: stages[k])

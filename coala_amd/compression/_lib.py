@@ -13,7 +13,9 @@ COALAC_FLAG_FORCE_EXACT = 1
 COALAC_FLAG_GENERIC_SELECT = 2
 COALAC_FLAG_STAMPS = 4
 COALAC_FLAG_NO_FORK = 8
-COALAC_FLAG_MULTI_LAUNCH = 16  # encode as the k_sample .. k_emit kernel sequence instead of one k_fused launch
+COALAC_FLAG_ITEM_STAMPS = 32   # diagnostics: per-work-item timestamps of k_fused
+COALAC_FLAG_ONE_LAUNCH = 64    # the whole encode as one k_fused launch (select phases as in-launch work items)
+COALAC_FLAG_FRONT_LAUNCH = 128 # samplers + scan + small segments as one launch, then the select kernels
 # stages of a split encode / decode (coalac_sched_t.stages; 0 = all)
 COALAC_STAGE_SAMPLE, COALAC_STAGE_SCAN, COALAC_STAGE_SELECT, COALAC_STAGE_SMALL = 1, 2, 4, 8
 COALAC_STAGE_BOUNDS, COALAC_STAGE_DECODE = 1, 2
@@ -52,6 +54,7 @@ SIGNATURES = [
     ("coalac_workspace_fallbacks", _I, [_P, _P, _P, ctypes.POINTER(_I)]),
     ("coalac_debug_stamps", _I, [_P, _P, _P, ctypes.POINTER(ctypes.c_uint64), _I]),
     ("coalac_workspace_timeouts", _I, [_P, _P, _P, ctypes.POINTER(_I)]),
+    ("coalac_debug_item_stamps", _I, [_P, _P, _P, ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_uint64), _I]),
 ]
 
 ABI_VERSION = 2

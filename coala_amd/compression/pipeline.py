@@ -274,20 +274,30 @@ class SplitPipeline:
         self.device = torch.device("cuda", torch.cuda.current_device() if device is None
                                    else torch.device(device).index or 0)
         C = max(1, int(table.clients))
-        S = max(1, min(int(split), C))
-        cuts = balanced_cuts(table.client_elements(), S)
+        S = max(1, int(split))
         # several sub-batches already run side by side: no per-plan side stream for the small segments
         # (HIP maps streams onto 4 hardware queues; a side stream sharing one with the other sub-batch
         # would queue its k_small behind that sub-batch's kernels)
         self.fork_flag = _lib.COALAC_FLAG_NO_FORK if S > 1 and fork is False else 0
-        so, ko, to = table.client_span_off, table.client_k_off, table.client_seg_off
         self.parts = []
         with torch.cuda.device(self.device):
-            for c0, c1 in zip(cuts[:-1], cuts[1:]):
-                plan = CodecPlan(None, table.ratio, self.bits, device=self.device, table=table.sub_table(c0, c1))
-                self.parts.append(dict(x=slice(so[c0], so[c1]), k=slice(ko[c0], ko[c1]), t=slice(to[c0], to[c1]),
-                                       plan=plan, ws=plan.empty_workspace(), dws=plan.empty_decode_workspace(),
-                                       stream=torch.cuda.Stream(self.device)))
+            if S <= C:  # client ranges: ordinary plans over views of the batch buffers
+                cuts = balanced_cuts(table.client_elements(), S)
+                so, ko, to = table.client_span_off, table.client_k_off, table.client_seg_off
+                for c0, c1 in zip(cuts[:-1], cuts[1:]):
+                    plan = CodecPlan(None, table.ratio, self.bits, device=self.device, table=table.sub_table(c0, c1))
+                    self.parts.append(dict(x=slice(so[c0], so[c1]), k=slice(ko[c0], ko[c1]), t=slice(to[c0], to[c1]),
+                                           plan=plan, ws=plan.empty_workspace(), dws=plan.empty_decode_workspace(),
+                                           stream=torch.cuda.Stream(self.device)))
+            else:
+                # fewer clients than sub-batches (e.g. ONE update): contiguous SEGMENT ranges balanced by
+                # element count, each a plan over absolute segment rows that reads / writes the whole
+                # buffers in place (its own segments only) — the ranges' latency-bound phases overlap
+                for s0, s1 in split_lanes(table.segs[:, 1].tolist(), S):
+                    plan = CodecPlan.from_segments(table.segs[s0:s1], self.bits, device=self.device)
+                    self.parts.append(dict(x=slice(None), k=slice(None), t=slice(s0, s1), plan=plan,
+                                           ws=plan.empty_workspace(), dws=plan.empty_decode_workspace(),
+                                           stream=torch.cuda.Stream(self.device)))
 
     @property
     def n_parts(self):
@@ -309,6 +319,7 @@ class SplitPipeline:
     @staticmethod
     def _enc(enc, P):
         return Encoded(enc.idx[P["k"]], enc.vals[P["k"]], enc.mn[P["t"]], enc.scale[P["t"]])
+
 
     @staticmethod
     def _x(t, P):

@@ -158,6 +158,7 @@ struct Params {
   uint32_t* hf_sel;        // [nseg] segment selected
   uint32_t* hf_err;        // [4] [0]: a bounded wait gave up
   uint32_t wt;             // 1 in k_fused: data another block of the launch reads is stored write-through
+  uint64_t* istamps;       // diagnostics (COALAC_FLAG_ITEM_STAMPS): per item {start, inputs ready, end}
 
   // decode workspace
   const uint32_t* ustart;  // [n_units + 1] first kept entry of every unit (k_bounds; aggregate only)
@@ -1617,11 +1618,29 @@ constexpr size_t FUSED_LDS =
 static_assert(FUSED_LDS <= 32 * 1024, "k_fused keeps five blocks per CU (160 KB of LDS)");
 
 template <bool DELTA, bool RAW>
+DEV void k_fused_item(const Params& P, uint32_t role, uint32_t idx, uint8_t* arena, uint64_t* stamp);
+
+template <bool DELTA, bool RAW>
 __global__ __launch_bounds__(BLOCK, SCAN_WPE) void k_fused(Params P) {
   __shared__ __attribute__((aligned(16))) uint8_t arena[FUSED_LDS];
   const uint32_t item = P.items[blockIdx.x];
   const uint32_t role = item >> 28, idx = item & 0x0FFFFFFFu;
   const uint32_t t = threadIdx.x, lane = lane_id(), wv = t >> 6;
+  uint64_t* const stamp = P.istamps != nullptr ? P.istamps + 3 * (uint64_t)blockIdx.x : nullptr;
+  if (stamp != nullptr && t == 0) stamp[0] = __builtin_amdgcn_s_memrealtime();
+  k_fused_item<DELTA, RAW>(P, role, idx, arena, stamp);
+  if (stamp != nullptr) {
+    __syncthreads();
+    if (t == 0) stamp[2] = __builtin_amdgcn_s_memrealtime();
+  }
+}
+
+template <bool DELTA, bool RAW>
+DEV void k_fused_item(const Params& P, uint32_t role, uint32_t idx, uint8_t* arena, uint64_t* stamp) {
+  const uint32_t t = threadIdx.x, lane = lane_id(), wv = t >> 6;
+  auto ready = [&]() {  // inputs available (after the wait)
+    if (stamp != nullptr && t == 0) stamp[1] = __builtin_amdgcn_s_memrealtime();
+  };
   if (role == R_SCAN) {
     const uint32_t q = idx * WAVES + wv;
     if (q >= P.n_lunits) return;
@@ -1635,25 +1654,33 @@ __global__ __launch_bounds__(BLOCK, SCAN_WPE) void k_fused(Params P) {
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // compiler order only: sc1 loads follow
         lo = ld_sc1(P.tlo + lu);
         hi = ld_sc1(P.thi + lu);
+        if (stamp != nullptr && wv == 0) stamp[1] = __builtin_amdgcn_s_memrealtime();
       }
       return make_uint2(__builtin_amdgcn_readfirstlane(lo), __builtin_amdgcn_readfirstlane(hi));
     };
-    scan_unit_t<DELTA, DELTA ? 4 : SCAN_NB, true>(P, lu, L, get_t, stage);
-    drain();  // every lane's write-through stores have landed
-    if (lane == 0) add_sc1(P.hf_garr + P.lgroup[lu], 1u);
+    if (P.wt) {  // one launch: the group blocks of this launch read the records
+      scan_unit_t<DELTA, DELTA ? 4 : SCAN_NB, true>(P, lu, L, get_t, stage);
+      drain();  // every lane's write-through stores have landed
+      if (lane == 0) add_sc1(P.hf_garr + P.lgroup[lu], 1u);
+    } else {  // front launch: the select kernels after this launch read them
+      scan_unit_t<DELTA, DELTA ? 4 : SCAN_NB, false>(P, lu, L, get_t, stage);
+    }
   } else if (role == R_SAMPLE) {
     uint32_t* hist = reinterpret_cast<uint32_t*>(arena);
+    ready();
     sample_segment<DELTA, true>(P, idx, hist, hist + HIST_BINS);
     drain();
     __syncthreads();
     if (t == 0) st_sc1(P.hf_sampled + P.large_list[idx], 1u);
   } else if (role == R_SMALL) {
     SmallSmem& S = *reinterpret_cast<SmallSmem*>(arena);
+    ready();
     small_encode<DELTA, RAW>(P, P.small_list[idx], S.vals, S.hist, S.sh);
   } else if (role == R_GHIST) {
     GhistSmem& S = *reinterpret_cast<GhistSmem*>(arena);
     const uint4 G = P.groups[idx];
     block_wait(P.hf_garr + idx, G.z, P.hf_err);
+    ready();
     group_hist(P, idx, S.hist, S.upre, S.sh);
     block_publish_add(P.hf_ghist + G.w, 1u);
   } else if (role == R_GWIN) {
@@ -1662,6 +1689,7 @@ __global__ __launch_bounds__(BLOCK, SCAN_WPE) void k_fused(Params P) {
     const SegDev sd = P.segs[G.w];
     const uint32_t ng = (sd.unit_end - sd.unit_begin + GU - 1) / GU;
     block_wait(P.hf_ghist + G.w, ng, P.hf_err);
+    ready();
     group_pick_window(P, idx, S.w, S.hist, S.sh);
     block_publish_add(P.hf_gwin + G.w, 1u);
   } else if (role == R_SELECT) {
@@ -1670,11 +1698,13 @@ __global__ __launch_bounds__(BLOCK, SCAN_WPE) void k_fused(Params P) {
     const SegDev sd = P.segs[s];
     const uint32_t ng = (sd.unit_end - sd.unit_begin + GU - 1) / GU;
     block_wait(P.hf_gwin + s, ng, P.hf_err);
+    ready();
     segment_select<BLOCK, DELTA, RAW>(P, idx, S);
     block_publish_add(P.hf_sel + s, 1u);
   } else if (role == R_EMIT) {
     const uint4 E = P.eblocks[idx];  // {first large unit, units, segment, 0}
     block_wait(P.hf_sel + E.z, 1u, P.hf_err);
+    ready();
     const uint32_t u0 = E.x + wv * EMIT_UPW, u1 = min(u0 + EMIT_UPW, E.x + E.y);
     if (u0 < u1) emit_units<RAW>(P, u0, u1);
   }
@@ -2079,11 +2109,11 @@ struct WsLayout {
   size_t status, hf_sampled, hf_ghist, hf_gwin, hf_sel, hf_err, hf_garr;
   size_t tstar, rtie;
   size_t tlo, thi, cntA, cntC, gtC, eqC, eqpre, outoff;
-  size_t cand, stamps, ghist, gcnt, glist, gmm, sstate, shhi;
+  size_t cand, stamps, ghist, gcnt, glist, gmm, sstate, shhi, istamps;
   size_t total;
 };
 
-WsLayout ws_layout(size_t S, size_t LU, size_t NG, size_t NL) {
+WsLayout ws_layout(size_t S, size_t LU, size_t NG, size_t NL, size_t NI) {
   WsLayout L{};
   // control block: words k_fused polls, zeroed by one memset before every launch (a block of its own at
   // the workspace start, a multiple of 16 bytes: Guideline 16 "Re-initialise every call")
@@ -2120,6 +2150,7 @@ WsLayout ws_layout(size_t S, size_t LU, size_t NG, size_t NL) {
   L.gmm = take(8 * NG);
   L.sstate = take(sizeof(uint4) * NL);
   L.shhi = take(4 * NL);
+  L.istamps = take(24 * NI);
   L.total = std::max<size_t>(o, 256);
   return L;
 }
@@ -2130,7 +2161,7 @@ WsLayout ws_layout(size_t S, size_t LU, size_t NG, size_t NL) {
 // slot while it spins); dependencies always precede their dependents, so in-order dispatch cannot
 // deadlock.
 struct FusedSchedule {
-  std::vector<uint32_t> items, fsched, lgroup;
+  std::vector<uint32_t> items, fsched, lgroup, front;  // front: SAMPLE + SCAN + SMALL only
   std::vector<uint4> eblocks;
 };
 
@@ -2166,11 +2197,14 @@ FusedSchedule fused_schedule(const std::vector<SegDev>& segs, const std::vector<
   const uint32_t nscan = (n_lunits + WAVES - 1) / WAVES;
   auto mk = [](uint32_t role, uint32_t idx) { return (role << 28) | idx; };
   for (uint32_t li : order) F.items.push_back(mk(R_SAMPLE, li));
-  for (uint32_t i = 0; i < n_small; ++i) F.items.push_back(mk(R_SMALL, i));
   // pending items: (ready position, sequence, item)
   typedef std::pair<std::pair<uint64_t, uint64_t>, uint32_t> Pending;
   std::priority_queue<Pending, std::vector<Pending>, std::greater<Pending>> q;
   uint64_t seq = 0;
+  // small segments (independent, latency-bound) spread evenly over the scan blocks: ahead of them they
+  // would hold the CUs before the first byte streams
+  for (uint32_t i = 0; i < n_small; ++i)
+    q.push(Pending({(uint64_t)F.items.size() + (uint64_t)(i + 1) * nscan / (n_small + 1), seq++}, mk(R_SMALL, i)));
   std::vector<uint32_t> gh_done(NL, 0), gw_done(NL, 0);
   auto push = [&](uint32_t item) { q.push(Pending({(uint64_t)F.items.size() + delay, seq++}, item)); };
   auto place = [&](uint32_t item) {
@@ -2190,6 +2224,14 @@ FusedSchedule fused_schedule(const std::vector<SegDev>& segs, const std::vector<
       for (uint32_t e = 0; e < eb_count[idx]; ++e) push(mk(R_EMIT, eb_first[idx] + e));
     }
   };
+  // the front launch: samplers, then the scan blocks with the small segments spread among them
+  for (uint32_t li : order) F.front.push_back(mk(R_SAMPLE, li));
+  for (uint32_t j = 0, i = 0; j < nscan || i < n_small; ) {
+    if (i < n_small && (j == nscan || (uint64_t)(i + 1) * nscan / (n_small + 1) <= j))
+      F.front.push_back(mk(R_SMALL, i++));
+    else
+      F.front.push_back(mk(R_SCAN, j++));
+  }
   uint32_t j = 0;
   while (j < nscan || !q.empty()) {
     if (!q.empty() && (q.top().first.first <= F.items.size() || j == nscan)) {
@@ -2224,6 +2266,8 @@ struct coalac_plan {
   // one-launch encode (k_fused): block work items, scan order, unit -> group, emit blocks
   uint32_t* items = nullptr;
   uint32_t n_items = 0;
+  uint32_t* front = nullptr;  // the front launch (samplers + scan + small segments)
+  uint32_t n_front = 0;
   uint32_t* fsched = nullptr;
   uint32_t* lgroup = nullptr;
   uint4* eblocks = nullptr;
@@ -2381,6 +2425,34 @@ int launch_fused(const Params& P, coalac_plan_t plan, hipStream_t st, const coal
   return COALAC_OK;
 }
 
+// COALAC_FLAG_FRONT_LAUNCH: ONE front launch (samplers, the scan, the small segments; the scan waves issue
+// their loads before they wait for their segment's sampler), then the select kernels k_ghist, k_gwin,
+// k_select, k_emit. Measured no faster than the kernel sequence: the waves holding loaded
+// data while they wait keep the next waves from streaming. Events: [0] before the control-block memset,
+// [1] before the front launch, [2] after it, [3] after k_select, [4] after k_emit.
+template <bool DELTA, bool RAW>
+int launch_front(const Params& P, coalac_plan_t plan, hipStream_t st, const coalac_sched_t* sc, void* ws) {
+  BOUNDARY(0);
+  HIP_CHECK(hipMemsetAsync(ws, 0, plan->ws.ctl_bytes, st));
+  BOUNDARY(1);
+  Params Q = P;
+  Q.wt = 0;
+  Q.items = plan->front;
+  hipLaunchKernelGGL((k_fused<DELTA, RAW>), dim3(plan->n_front), dim3(BLOCK), 0, st, Q);
+  BOUNDARY(2);
+  if (plan->n_large) {
+    hipLaunchKernelGGL(k_ghist, dim3(plan->n_groups), dim3(BLOCK), 0, st, P);
+    hipLaunchKernelGGL(k_gwin, dim3(plan->n_groups), dim3(BLOCK), 0, st, P);
+    hipLaunchKernelGGL((k_select<DELTA, RAW>), dim3(plan->n_large), dim3(SEL_NT), 0, st, P);
+  }
+  BOUNDARY(3);
+  if (plan->n_large)
+    hipLaunchKernelGGL((k_emit<RAW>), dim3((plan->n_lunits + WAVES * EMIT_UPW - 1) / (WAVES * EMIT_UPW)), dim3(BLOCK), 0,
+                       st, P);
+  BOUNDARY(4);
+  return COALAC_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -2472,7 +2544,6 @@ int coalac_plan_create(const coalac_seg_t* h_segs, int nseg, int bits, coalac_pl
   p->n_groups = (uint32_t)groups.size();
   p->span = span;
   p->total_k = total_k;
-  p->ws = ws_layout((size_t)nseg, lunits.size(), groups.size(), large_list.size());
   p->n_bchunks = (uint32_t)bchunks.size();
   p->hsegs = segs;
   p->dec_ws = align_up(4 * (units.size() + 1), 256);  // decode / aggregate: per-unit bounds
@@ -2481,6 +2552,8 @@ int coalac_plan_create(const coalac_seg_t* h_segs, int nseg, int bits, coalac_pl
   if (const char* e = getenv("COALAC_FUSED_DELAY")) delay = (uint32_t)atoi(e);
   const FusedSchedule F = fused_schedule(segs, large_list, p->n_small, p->n_lunits, groups, delay);
   p->n_items = (uint32_t)F.items.size();
+  p->n_front = (uint32_t)F.front.size();
+  p->ws = ws_layout((size_t)nseg, lunits.size(), groups.size(), large_list.size(), F.items.size());
 
   const size_t o_segs = 0;
   const size_t o_units = align_up(o_segs + sizeof(SegDev) * segs.size(), 256);
@@ -2493,7 +2566,8 @@ int coalac_plan_create(const coalac_seg_t* h_segs, int nseg, int bits, coalac_pl
   const size_t o_fsched = align_up(o_items + 4 * F.items.size(), 256);
   const size_t o_lgroup = align_up(o_fsched + 4 * F.fsched.size(), 256);
   const size_t o_eblk = align_up(o_lgroup + 4 * F.lgroup.size(), 256);
-  const size_t bytes = align_up(o_eblk + sizeof(uint4) * F.eblocks.size(), 256) + 256;
+  const size_t o_front = align_up(o_eblk + sizeof(uint4) * F.eblocks.size(), 256);
+  const size_t bytes = align_up(o_front + 4 * F.front.size(), 256) + 256;
   std::vector<uint8_t> host(bytes, 0);
   if (!segs.empty()) memcpy(host.data() + o_segs, segs.data(), sizeof(SegDev) * segs.size());
   if (!units.empty()) memcpy(host.data() + o_units, units.data(), sizeof(UnitDev) * units.size());
@@ -2506,6 +2580,7 @@ int coalac_plan_create(const coalac_seg_t* h_segs, int nseg, int bits, coalac_pl
   if (!F.fsched.empty()) memcpy(host.data() + o_fsched, F.fsched.data(), 4 * F.fsched.size());
   if (!F.lgroup.empty()) memcpy(host.data() + o_lgroup, F.lgroup.data(), 4 * F.lgroup.size());
   if (!F.eblocks.empty()) memcpy(host.data() + o_eblk, F.eblocks.data(), sizeof(uint4) * F.eblocks.size());
+  if (!F.front.empty()) memcpy(host.data() + o_front, F.front.data(), 4 * F.front.size());
   hipError_t e = hipMalloc(&p->meta, bytes);
   if (e != hipSuccess) {
     delete p;
@@ -2529,6 +2604,7 @@ int coalac_plan_create(const coalac_seg_t* h_segs, int nseg, int bits, coalac_pl
   p->fsched = reinterpret_cast<uint32_t*>(m + o_fsched);
   p->lgroup = reinterpret_cast<uint32_t*>(m + o_lgroup);
   p->eblocks = reinterpret_cast<uint4*>(m + o_eblk);
+  p->front = reinterpret_cast<uint32_t*>(m + o_front);
   *out = p;
   return COALAC_OK;
 }
@@ -2598,6 +2674,7 @@ int coalac_encode_sched(coalac_plan_t plan, const float* d_in, const float* d_ba
   P.hf_sel = reinterpret_cast<uint32_t*>(w + L.hf_sel);
   P.hf_err = reinterpret_cast<uint32_t*>(w + L.hf_err);
   P.hf_garr = reinterpret_cast<uint32_t*>(w + L.hf_garr);
+  P.istamps = (flags & COALAC_FLAG_ITEM_STAMPS) ? reinterpret_cast<uint64_t*>(w + L.istamps) : nullptr;
   P.tstar = reinterpret_cast<uint32_t*>(w + L.tstar);
   P.rtie = reinterpret_cast<uint32_t*>(w + L.rtie);
   P.status = reinterpret_cast<uint32_t*>(w + L.status);
@@ -2621,8 +2698,19 @@ int coalac_encode_sched(coalac_plan_t plan, const float* d_in, const float* d_ba
   const bool delta = d_base != nullptr, raw = plan->bits == 32;
   const unsigned all = COALAC_STAGE_SAMPLE | COALAC_STAGE_SCAN | COALAC_STAGE_SELECT | COALAC_STAGE_SMALL;
   const bool whole = !(sched && (sched->stages & all) && (sched->stages & all) != all);
-  const bool fused = whole && !(flags & (COALAC_FLAG_MULTI_LAUNCH | COALAC_FLAG_STAMPS)) && plan->n_items > 0;
-  if (fused) {
+  const bool one = whole && (flags & COALAC_FLAG_ONE_LAUNCH) && !(flags & COALAC_FLAG_STAMPS) && plan->n_items > 0;
+  const bool front = whole && !one && (flags & COALAC_FLAG_FRONT_LAUNCH) && !(flags & COALAC_FLAG_STAMPS) &&
+                     plan->n_front > 0;
+  if (front) {
+    if (delta && raw)
+      rc = launch_front<true, true>(P, plan, st, sched, d_ws);
+    else if (delta)
+      rc = launch_front<true, false>(P, plan, st, sched, d_ws);
+    else if (raw)
+      rc = launch_front<false, true>(P, plan, st, sched, d_ws);
+    else
+      rc = launch_front<false, false>(P, plan, st, sched, d_ws);
+  } else if (one) {
     if (delta && raw)
       rc = launch_fused<true, true>(P, plan, st, sched, d_ws);
     else if (delta)
@@ -2838,6 +2926,19 @@ int coalac_workspace_fallbacks(coalac_plan_t plan, const void* d_ws, void* strea
   for (uint32_t s2 : large) c += st[s2] == 1;
   *out = c;
   return COALAC_OK;
+}
+
+int coalac_debug_item_stamps(coalac_plan_t plan, const void* d_ws, void* stream, uint32_t* items,
+                             uint64_t* stamps, int n) {
+  if (!plan || !d_ws || n < 0) return fail(COALAC_EINVAL, "coalac_debug_item_stamps: bad argument");
+  const int cnt = std::min<int>(n, (int)plan->n_items);
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  if (items) HIP_CHECK(hipMemcpyAsync(items, plan->items, 4 * (size_t)cnt, hipMemcpyDeviceToHost, s));
+  if (stamps)
+    HIP_CHECK(hipMemcpyAsync(stamps, static_cast<const uint8_t*>(d_ws) + plan->ws.istamps, 24 * (size_t)cnt,
+                             hipMemcpyDeviceToHost, s));
+  HIP_CHECK(hipStreamSynchronize(s));
+  return cnt;
 }
 
 int coalac_workspace_timeouts(coalac_plan_t plan, const void* d_ws, void* stream, int* out) {

@@ -51,8 +51,13 @@ enum {
   COALAC_FLAG_STAMPS = 4,         /* diagnostics: record per-block phase timestamps of k_select */
   COALAC_FLAG_NO_FORK = 8,        /* encode small segments inside k_scan, never on the plan's side stream
                                      (for callers that run several plans concurrently themselves) */
-  COALAC_FLAG_MULTI_LAUNCH = 16   /* encode as the kernel sequence k_sample .. k_emit instead of the
-                                     one-launch k_fused (a whole encode is one launch by default) */
+  COALAC_FLAG_ITEM_STAMPS = 32,   /* diagnostics: k_fused records per work item {start, inputs ready, end}
+                                     (100 MHz ticks; coalac_debug_item_stamps) */
+  COALAC_FLAG_ONE_LAUNCH = 64,    /* encode as ONE launch: k_fused, every phase an in-launch work item
+                                     behind per-segment hand-offs (default: the kernel sequence k_sample,
+                                     k_scan, k_ghist, k_gwin, k_select, k_emit) */
+  COALAC_FLAG_FRONT_LAUNCH = 128  /* samplers + scan + small segments as one launch, then the select
+                                     kernels */
 };
 
 /* One fp32 segment (= one flattened tensor of the state_dict). Offsets are in ELEMENTS.
@@ -100,11 +105,12 @@ int coalac_decode(coalac_plan_t plan, const int32_t* d_idx, const void* d_vals, 
                   void* stream);
 
 /* Profiling variants: identical work, plus hipEventRecord(events[i], stream) between kernels.
- * encode (one launch, the default): events[0] before the control-block memset, [1] before k_fused,
- *         [2] [3] [4] after it;
- * encode (COALAC_FLAG_MULTI_LAUNCH): [0] before k_sample, [1] after k_sample, [2] after k_scan, [3]
- *         after the select kernels (k_ghist, k_gwin, k_select), [4] after k_emit (recorded even if the
- *         plan has no large segment);
+ * encode (default): [0] before k_sample, [1] after k_sample, [2] after k_scan, [3] after the select
+ *         kernels (k_ghist, k_gwin, k_select), [4] after k_emit (recorded even if the plan has no large
+ *         segment);
+ * encode (COALAC_FLAG_FRONT_LAUNCH): events[0] before the control-block memset, [1] before the front
+ *         launch (samplers + scan + small segments), [2] after it, [3] after k_select, [4] after k_emit;
+ * encode (COALAC_FLAG_ONE_LAUNCH): [0] before the memset, [1] before k_fused, [2] [3] [4] after it;
  * decode: [0] before k_bounds (plans of > 8192 units only), [1] before k_decode, [2] after it. NULL
  *         array or NULL entries are skipped. */
 int coalac_encode_ev(coalac_plan_t plan, const float* d_in, const float* d_base, int32_t* d_idx,
@@ -184,6 +190,12 @@ int coalac_workspace_fallbacks(coalac_plan_t plan, const void* d_ws, void* strea
 /* Diagnostics: 1 if a bounded in-launch wait of the last one-launch encode with d_ws gave up (its results
  * are then not valid; never expected), else 0 (synchronises `stream`). */
 int coalac_workspace_timeouts(coalac_plan_t plan, const void* d_ws, void* stream, int* out);
+
+/* Diagnostics: the k_fused work items (role << 28 | index, launch order) and, after a
+ * COALAC_FLAG_ITEM_STAMPS encode with d_ws, their {start, inputs ready, end} timestamps (3 per item);
+ * either pointer may be NULL. Copies up to n items (synchronises `stream`); returns the count copied. */
+int coalac_debug_item_stamps(coalac_plan_t plan, const void* d_ws, void* stream, uint32_t* items,
+                             uint64_t* stamps, int n);
 
 /* Diagnostics: copy up to n phase timestamps (16 per k_select block = per large segment, 100 MHz
  * ticks; 0 = phase not reached) of the last COALAC_FLAG_STAMPS encode with d_ws to host (synchronises

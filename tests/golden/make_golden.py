@@ -21,6 +21,13 @@ What it pins, and from where (SURVEY.md §8(c) "What reference imports pin"):
 3. Hook order + upload framing of `BaseClient.run_train` (/root/reference/coala/client/base.py:123-159,
    353-383): a recording subclass drives the real method -> hooks.json.
 4. Identity round trip of `codec.marshal/unmarshal` (/root/reference/coala/protocol/codec.py:4-9).
+5. The plugin inside the REAL reference client (plugin_run_train.npz): CompressionClientMixin mixed into
+   the reference's BaseClient (/root/reference/coala/client/base.py:123-159), driven by its own run_train
+   for 3 clients of the reference simple_cnn (/root/reference/coala/models/simple_cnn.py, channels=16),
+   with the CPU oracle as the codec backend: the UploadContent.data bytes the reference produces (the
+   pickled carrier: codec.marshal(copy.deepcopy(self.model)), base.py:363), data_size / type, the
+   tracked upload size, and the reference's strategies.federated_averaging (server/strategies.py:6-29)
+   of the decoded uploads. tests/test_reference_fixture.py reproduces all of it with the HIP backend.
 
 The reference is imported read-only with a namespace stub for `coala` (its __init__ needs omegaconf,
 which is not installed). No reference source is copied; only data is written.
@@ -210,6 +217,75 @@ def make_hooks():
     assert all(torch.equal(a, b) for a, b in zip(m.state_dict().values(), back.state_dict().values()))
 
 
+PLUGIN_SIZES = [13, 7, 21]   # client sample counts (FedAvg weights)
+PLUGIN_SEED, PLUGIN_NOISE_SEED, PLUGIN_NOISE = 7, 1000, 1e-3
+PLUGIN_RATIO, PLUGIN_BITS = 0.05, 8
+
+
+def plugin_train_step(model, cid_index):
+    """The deterministic local 'training' of the fixture (also restated by tests/test_reference_fixture.py):
+    every parameter += N(0, 1) * 1e-3 drawn from a CPU generator seeded 1000 + client index."""
+    g = torch.Generator().manual_seed(PLUGIN_NOISE_SEED + cid_index)
+    with torch.no_grad():
+        for p in model.parameters():
+            p.add_((torch.randn(p.shape, generator=g) * PLUGIN_NOISE).to(p.device))
+
+
+def make_plugin_fixture():
+    import hashlib
+
+    sys.path.insert(0, REPO)
+    from coala.client.base import BaseClient
+    from coala.models import simple_cnn
+    from coala.protocol import codec
+    from coala.server import strategies
+
+    from coala_amd.compression import CompressionClientMixin, UpdateCodec
+    from tests.oracle_backend import OracleBackend
+
+    class _Data:
+        def size(self, cid):
+            return PLUGIN_SIZES[int(cid[1:])]
+
+    class Client(CompressionClientMixin, BaseClient):
+        codec_ratio, codec_bits, codec_mode, codec_backend = PLUGIN_RATIO, PLUGIN_BITS, "delta", OracleBackend()
+
+        def train(self, conf, device="cpu"):
+            plugin_train_step(self.model, int(self.cid[1:]))
+
+    torch.manual_seed(PLUGIN_SEED)
+    g0 = simple_cnn.Model(channels=16, num_classes=10)
+    conf = SimpleNamespace(track=False, local_test=False, task_id="task0", round_id=0)
+    arrays = {f"global/{k}": v.numpy() for k, v in g0.state_dict().items()}
+    ups, weights = [], []
+    for i in range(len(PLUGIN_SIZES)):
+        c = Client(f"c{i}", conf, _Data(), None, "cpu")
+        req = c.run_train(g0, conf)
+        data = req.content.data
+        arrays[f"upload_bytes/{i}"] = np.frombuffer(data, dtype=np.uint8).copy()
+        arrays[f"data_size/{i}"] = np.array([req.content.data_size], np.int64)
+        arrays[f"content_type/{i}"] = np.array([int(req.content.type)], np.int64)
+        arrays[f"upload_size_mb/{i}"] = np.array([c.calculate_model_size(codec.unmarshal(data))], np.float64)
+        ups.append(codec.unmarshal(data))
+        weights.append(req.content.data_size)
+    # server side: w_global + decode(delta) per upload (oracle), then the reference FedAvg on the CPU
+    oc = UpdateCodec(PLUGIN_RATIO, PLUGIN_BITS, "delta", OracleBackend())
+    base = oc.snapshot(g0)
+    dec = [oc.decode_module(u, g0, base=base) for u in ups]
+    for i, m in enumerate(dec):
+        h = hashlib.sha256()
+        for t in m.state_dict().values():
+            h.update(t.contiguous().reshape(-1).view(torch.uint8).numpy().tobytes())
+        arrays[f"decoded_sha256/{i}"] = np.frombuffer(h.digest(), dtype=np.uint8).copy()
+    avg = strategies.federated_averaging([copy.deepcopy(m) for m in dec], list(weights))
+    for k, v in avg.state_dict().items():
+        arrays[f"avg/{k}"] = v.numpy()
+    arrays["weights"] = np.array(weights, np.int64)
+    np.savez_compressed(os.path.join(HERE, "plugin_run_train.npz"), **arrays)
+    print("plugin_run_train.npz:", len(arrays), "arrays; upload bytes",
+          [int(arrays[f"upload_bytes/{i}"].size) for i in range(len(PLUGIN_SIZES))])
+
+
 if __name__ == "__main__":
     if not os.environ.get("PYTHONDONTWRITEBYTECODE"):
         sys.exit("run with PYTHONDONTWRITEBYTECODE=1 so nothing is written into /root/reference")
@@ -218,3 +294,4 @@ if __name__ == "__main__":
     make_layouts()
     make_fedavg()
     make_hooks()
+    make_plugin_fixture()

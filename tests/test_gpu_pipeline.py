@@ -129,3 +129,20 @@ def test_split_pipeline_unjoined_steps_match_single_plan(cuda):
     assert torch.equal(enc.idx, e1.idx) and torch.equal(enc.vals, e1.vals)
     assert torch.equal(enc.mn, e1.mn) and torch.equal(enc.scale, e1.scale)
     assert torch.equal(out, d1)
+
+
+@pytest.mark.parametrize("split", [2, 3, 4])
+@pytest.mark.parametrize("delta", [False, True])
+def test_split_pipeline_single_update_segment_ranges(cuda, split, delta):
+    """One update into `split` segment ranges (SplitPipeline with fewer clients than sub-batches): each
+    range a plan over absolute segment rows on its own stream, writing the shared buffers in place; the
+    result is the oracle's, bit for bit, and equal to one plan over the whole update."""
+    t = SegmentTable(fp32_sizes("resnet50_tv"), 0.01, 1)
+    flat = synth_batch(t, cuda, client_ids=[3])
+    base = synth_batch(t, cuda, client_ids=[30]) if delta else None
+    pipe = SplitPipeline(t, 8, split=split, device=cuda)
+    assert pipe.n_parts == split
+    enc, dec = pipe.roundtrip(flat, base=base)
+    torch.cuda.synchronize()
+    check(t, enc, dec, oracle_roundtrip(t, flat.cpu().numpy(), 8, None if base is None else base.cpu().numpy()))
+    assert pipe.fallbacks() == 0

@@ -9,7 +9,7 @@ shift 2 || true
 O=gpurun_out/sweep_${TAG}
 mkdir -p $O
 export TMPDIR=/tmp
-timeout -k 10 300 python -u -m pytest tests/test_gpu_fused.py tests/test_gpu_parity.py -x -q --timeout 120 \
+timeout -k 10 300 python -u -m pytest tests/test_gpu_fused.py tests/test_gpu_parity.py tests/test_reference_fixture.py -x -q --timeout 120 \
   --timeout-method thread > $O/pytest.log 2>&1 || { tail -30 $O/pytest.log; exit 1; }
 tail -2 $O/pytest.log
 for d in $DELAYS; do
