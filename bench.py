@@ -13,6 +13,8 @@ collective on the data path — torch.distributed only for the barrier and the m
           client-side models at cut 1/2/4 + feature tensors up to 8,388,608 elements), MixedTable
   single  ONE ResNet-50 update per step, steps serialised (north_star's "a 25.6 M-param fp32 update at
           1 GPU"; latency-bound)
+  plugin  the hooks' own path per ResNet-50 client, delta mode: client compression() encoding the trained
+          module's parameters in place + server decompression(model) into a new module on w_global
 value = 4 * N * clients * steps / elapsed (GB/s of fp32 update processed, whole job).
 roofline: the dominant kernel's algorithmic bytes per launch / its mean HIP-event duration, vs 8 TB/s.
 cpu_baseline: the numpy oracle (oracle/codec_oracle.py) on a bounded sample of the same workload, on the
@@ -45,7 +47,7 @@ CONFIGS = {  # name -> (layout | "c5", clients per GPU, split)
     "single": ("resnet50_tv", 1, "single"),
 }
 SINGLE_SPLIT = 1  # segment ranges of the single update run as this many concurrent sub-plans
-DEFAULT_EXTRAS = "C2,C4,C5,single"
+DEFAULT_EXTRAS = "C2,C4,C5,single,plugin"
 
 
 def parse():
@@ -333,6 +335,57 @@ def run_workload(cfg, a, dev, world, rank, headline):
     return res
 
 
+def run_plugin(a, dev, steps):
+    """Client compression() + server decompression(model) of one ResNet-50 client through the codec
+    (UpdateCodec, as the mixins call it), on device-resident modules, delta mode. HBM bytes per client:
+    encode reads the parameters and the w_global snapshot (8N) and writes 5K + 8T; decode reads those and
+    the snapshot (4N) and writes the new module (4N): 16N + 10K + 16T."""
+    import torch
+
+    from coala_amd.compression import UpdateCodec
+    from coala_amd.compression.codec import flatten_state
+    from coala_amd.layouts import build_module
+    m = build_module("resnet50_tv", seed=1, device=dev)
+    g = build_module("resnet50_tv", seed=2, device=dev)
+    codec = UpdateCodec(a.ratio, a.bits, "delta")
+    base = codec.snapshot(g)
+    state = m.state_dict()
+    res = {}
+    for name, fn in (("in_place", lambda: codec.encode(state, base=base)),
+                     ("flattened", lambda: codec.plan_for(
+                         [e["n"] for e in base.entries if e["kind"] == "seg"], dev).encode(
+                         flatten_state(state).flat, base=base.flat))):
+        for _ in range(3):
+            up = fn()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            up = fn()
+        torch.cuda.synchronize()
+        res[f"compression_{name}_ms"] = round((time.perf_counter() - t0) / steps * 1e3, 4)
+    up = codec.encode(state, base=base)
+    for _ in range(3):
+        codec.decode_module(up, g, base=base)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        mod = codec.decode_module(up, g, base=base)
+    torch.cuda.synchronize()
+    dec_ms = (time.perf_counter() - t0) / steps * 1e3
+    N = sum(e["n"] for e in base.entries if e["kind"] == "seg")
+    K, T = up.header["total_k"], up.header["n_segments"]
+    alg = 16 * N + 10 * K + 16 * T
+    ms = res["compression_in_place_ms"] + dec_ms
+    del mod
+    return {"value": round(4.0 * N / (ms * 1e-3) / 1e9, 2), "ms_per_client": round(ms, 4),
+            **res, "decompression_ms": round(dec_ms, 4), "alg_bytes_per_client": alg,
+            "step_roofline": {"achieved_GBs": round(alg / (ms * 1e-3) / 1e9, 1),
+                              "frac": round(alg / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)},
+            "desc": "UpdateCodec.encode(state_dict, base) + decode_module(update, template, base): what "
+                    "CompressionClientMixin.compression() / CompressionServerMixin.decompression() run, "
+                    "host-side Python included; flattened = the round-1 path (torch.cat copy first)"}
+
+
 def main():
     a = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -354,8 +407,12 @@ def main():
 
     head = run_workload(a.config, a, dev, world, rank, headline=True)
     extras = {}
+    plugin = None
     for cfg in ([] if a.extras == "none" else [c for c in a.extras.split(",") if c and c != a.config]):
-        extras[cfg] = run_workload(cfg, a, dev, world, rank, headline=False)
+        if cfg == "plugin":
+            plugin = run_plugin(a, dev, a.steps)
+        else:
+            extras[cfg] = run_workload(cfg, a, dev, world, rank, headline=False)
 
     if rank == 0:
         d = head["desc"]
@@ -376,6 +433,8 @@ def main():
                                               "elements_per_gpu", "segments_per_gpu", "split", "sample_fallbacks")}
                         for k, v in extras.items()},
         }
+        if plugin is not None:
+            res["configs"]["plugin"] = plugin
         if cpu is not None:
             res["cpu_baseline"] = cpu
         print(json.dumps(res), flush=True)

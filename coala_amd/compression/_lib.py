@@ -44,6 +44,7 @@ SIGNATURES = [
     ("coalac_plan_query", _I, [_P, ctypes.POINTER(_U64), ctypes.POINTER(_U64), ctypes.POINTER(_U64),
                                ctypes.POINTER(_U64), ctypes.POINTER(_U64)]),
     ("coalac_encode", _I, [_P, _P, _P, _P, _P, _P, _P, _P, _U64, ctypes.c_uint, _P]),
+    ("coalac_encode_segptr", _I, [_P, _P, _P, _P, _P, _P, _P, _P, _U64, ctypes.c_uint, _P]),
     ("coalac_decode", _I, [_P, _P, _P, _P, _P, _P, _P, _P, _U64, _P]),
     ("coalac_encode_ev", _I, [_P, _P, _P, _P, _P, _P, _P, _P, _U64, ctypes.c_uint, _P, _P]),
     ("coalac_decode_ev", _I, [_P, _P, _P, _P, _P, _P, _P, _P, _U64, _P, _P]),

@@ -172,6 +172,47 @@ class CodecPlan:
         _lib.check(rc, "coalac_encode")
         return out
 
+    def segment_pointers(self, tensors):
+        """Device array of the tensors' data pointers (one per segment), for encode_segments; cached per
+        pointer tuple (a model's parameter storage does not move between rounds)."""
+        segs = self.table.segs
+        if len(tensors) != len(segs):
+            raise ValueError(f"need {len(segs)} segment tensors, got {len(tensors)}")
+        for i, t in enumerate(tensors):
+            if t.device != self.device or t.dtype != torch.float32 or not t.is_contiguous():
+                raise ValueError(f"segment {i}: need a contiguous float32 tensor on {self.device}")
+            if t.numel() != int(segs[i, 1]):
+                raise ValueError(f"segment {i}: {t.numel()} elements, the plan says {int(segs[i, 1])}")
+            if t.data_ptr() % 16:
+                raise ValueError(f"segment {i}: storage must be 16-byte aligned")
+        key = tuple(t.data_ptr() for t in tensors)
+        cache = self.__dict__.setdefault("_segptr_cache", {})
+        d = cache.get(key)
+        if d is None:
+            if len(cache) > 8:
+                cache.clear()
+            d = torch.tensor(key, dtype=torch.int64).to(self.device)
+            cache[key] = d
+        return d
+
+    def encode_segments(self, tensors, base=None, out=None, workspace=None, flags=0, stream=None):
+        """Encode with segment i read from tensors[i] itself (coalac_encode_segptr): e.g. a model's
+        parameters, no flattening copy. base: flat fp32[span] (delta mode), as encode()."""
+        ptrs = self.segment_pointers(tensors)
+        self._check_flat(base, "base")
+        with _on(stream):
+            out = self.empty_encoded() if out is None else out
+            ws = self.empty_workspace() if workspace is None else workspace
+        self._check_encoded(out)
+        if ws.device != self.device or ws.numel() * ws.element_size() < self.ws_bytes:
+            raise ValueError(f"workspace: need {self.ws_bytes} bytes on {self.device}")
+        with torch.cuda.device(self.device):
+            rc = self._lib.coalac_encode_segptr(self._h, _ptr(ptrs), _ptr(base), _ptr(out.idx), _ptr(out.vals),
+                                                _ptr(out.mn), _ptr(out.scale), _ptr(ws), ctypes.c_uint64(self.ws_bytes),
+                                                ctypes.c_uint(flags), _stream_handle(stream))
+        _lib.check(rc, "coalac_encode_segptr")
+        return out
+
     def decode(self, enc, base=None, out=None, workspace=None, stream=None, events=None, sched=None):
         """Decode Encoded -> dense flat fp32[span] (+ base, fused). Asynchronous on `stream`.
 

@@ -110,6 +110,7 @@ static_assert(sizeof(UnitDev) == 32, "UnitDev layout");
 struct Params {
   // encode / decode operands
   const float* in;
+  const float* const* inptr;  // encode from per-segment pointers (coalac_encode_segptr), else null
   const float* base;
   int32_t* idx;
   void* vals;
@@ -536,6 +537,32 @@ DEV float load_x1(const Params& P, uint64_t off) {
   return v;
 }
 
+// Input of segment s: its own pointer (coalac_encode_segptr: the model's parameter storage, no flattening
+// copy) or the flat buffer at in_off. The delta base is always the flat buffer.
+DEV const float* seg_in(const Params& P, uint32_t s, uint64_t in_off) {
+  return P.inptr != nullptr ? P.inptr[s] : P.in + in_off;
+}
+
+template <bool DELTA>
+DEV float4 load_x4p(const float* x, const float* b) {
+  float4 v = *reinterpret_cast<const float4*>(x);
+  if (DELTA) {
+    const float4 c = *reinterpret_cast<const float4*>(b);
+    v.x = v.x - c.x;
+    v.y = v.y - c.y;
+    v.z = v.z - c.z;
+    v.w = v.w - c.w;
+  }
+  return v;
+}
+
+template <bool DELTA>
+DEV float load_x1p(const float* x, const float* b) {
+  float v = *x;
+  if (DELTA) v = v - *b;
+  return v;
+}
+
 DEV uint32_t hash32(uint32_t x) {
   x ^= x >> 16;
   x *= 0x7feb352dU;
@@ -568,8 +595,9 @@ DEV void scan_unit_t(const Params& P, uint32_t lu, const UnitDev& L, GetT&& get_
   uint32_t tlo = 0, thi = 0;
   // buffer resources over exactly this unit: one shared lane offset for all loads (constant offsets
   // fold into the instruction), and loads past len return 0 — no separate partial-unit path
-  const __amdgpu_buffer_rsrc_t rin = unit_rsrc(P.in + off, len);
-  const __amdgpu_buffer_rsrc_t rbase = unit_rsrc(DELTA ? P.base + off : P.in + off, len);
+  const float* xin = P.inptr != nullptr ? P.inptr[L.seg] + L.start : P.in + off;
+  const __amdgpu_buffer_rsrc_t rin = unit_rsrc(xin, len);
+  const __amdgpu_buffer_rsrc_t rbase = unit_rsrc(DELTA ? P.base + off : xin, len);
   auto put = [&](uint32_t i, uint2 rec) {
     if (SC1)
       st_sc1(R + i, rec);
@@ -716,6 +744,8 @@ DEV void small_encode(const Params& P, uint32_t s, float* vals, uint32_t* hist, 
   constexpr int NT = BLOCK;
   const uint32_t t = threadIdx.x;
   const SegDev sd = P.segs[s];
+  const float* xs = seg_in(P, s, sd.in_off);
+  const float* bs = DELTA ? P.base + sd.in_off : xs;
   const uint32_t n = sd.n, k = sd.k;
   if (n == 0) {
     if (t == 0) {
@@ -726,13 +756,13 @@ DEV void small_encode(const Params& P, uint32_t s, float* vals, uint32_t* hist, 
   }
   for (uint32_t i = t * 4; i < n; i += NT * 4) {
     if (i + 3 < n) {
-      const float4 v = load_x4<DELTA>(P, sd.in_off + i);
+      const float4 v = load_x4p<DELTA>(xs + i, bs + i);
       vals[i + 0] = v.x;
       vals[i + 1] = v.y;
       vals[i + 2] = v.z;
       vals[i + 3] = v.w;
     } else {
-      for (uint32_t j = i; j < n; ++j) vals[j] = load_x1<DELTA>(P, sd.in_off + j);
+      for (uint32_t j = i; j < n; ++j) vals[j] = load_x1p<DELTA>(xs + j, bs + j);
     }
   }
   __syncthreads();
@@ -813,6 +843,8 @@ DEV void sample_segment(const Params& P, uint32_t li, uint32_t* hist, uint32_t* 
   const uint32_t t = threadIdx.x;
   const uint32_t s = P.large_list[li];
   const SegDev sd = P.segs[s];
+  const float* xs = seg_in(P, s, sd.in_off);
+  const float* bs = DELTA ? P.base + sd.in_off : xs;
   const uint32_t n = sd.n, k = sd.k;
   // R runs of 16 contiguous elements, one per stratum of n / R elements, jittered inside it.
   uint32_t R = n / 512;
@@ -830,7 +862,7 @@ DEV void sample_segment(const Params& P, uint32_t li, uint32_t* hist, uint32_t* 
     const uint32_t run = min(it, nit - 1) * 64 + (t >> 2), q = t & 3;
     uint32_t start = run * stride + hash32(run * 0x9E3779B9u ^ (s + 1u) * 0x85EBCA6Bu) % (room + 1u);
     start &= ~3u;
-    const float4 v = load_x4<DELTA>(P, sd.in_off + start + q * 4);
+    const float4 v = load_x4p<DELTA>(xs + start + q * 4, bs + start + q * 4);
     kk[it][0] = fkey(v.x);
     kk[it][1] = fkey(v.y);
     kk[it][2] = fkey(v.z);
@@ -1390,6 +1422,8 @@ DEV void segment_select(const Params& P, uint32_t li, SelSmem& S) {
   const uint32_t t = threadIdx.x, wv = t >> 6;
   const uint32_t s = P.large_list[li];
   const SegDev sd = P.segs[s];
+  const float* xs = seg_in(P, s, sd.in_off);
+  const float* bs = DELTA ? P.base + sd.in_off : xs;
   const uint32_t lb = sd.lu_begin, nu = sd.unit_end - sd.unit_begin, k = sd.k;
   STAMP(P, li, 0);
   uint32_t T, rt, fp_rank, fn_rank;
@@ -1415,7 +1449,7 @@ DEV void segment_select(const Params& P, uint32_t li, SelSmem& S) {
     uint32_t rk = k;
     const uint32_t T = block_select<NT, SEL_HB>(
         [&](auto&& f) {
-          for (uint32_t i = t; i < n; i += NT) f(fkey(load_x1<DELTA>(P, sd.in_off + i)));
+          for (uint32_t i = t; i < n; i += NT) f(fkey(load_x1p<DELTA>(xs + i, bs + i)));
         },
         0u, KEY_MAX, rk, S.hist, S.sh);
     for (uint32_t i = wv; i < nu; i += NW) {
@@ -2642,13 +2676,16 @@ int coalac_encode_ev(coalac_plan_t plan, const float* d_in, const float* d_base,
                              events ? &s : nullptr);
 }
 
-int coalac_encode_sched(coalac_plan_t plan, const float* d_in, const float* d_base, int32_t* d_idx,
-                        void* d_vals, float* d_mn, float* d_scale, void* d_ws, uint64_t ws_bytes,
-                        unsigned flags, void* stream, const coalac_sched_t* sched) {
+}  // extern "C"
+
+namespace {
+int encode_impl(coalac_plan_t plan, const float* d_in, const float* const* d_inptr, const float* d_base,
+                int32_t* d_idx, void* d_vals, float* d_mn, float* d_scale, void* d_ws, uint64_t ws_bytes,
+                unsigned flags, void* stream, const coalac_sched_t* sched) {
   if (!plan) return fail(COALAC_EINVAL, "coalac_encode: plan is NULL");
   if (plan->nseg == 0) return COALAC_OK;
   if (!d_mn || !d_scale) return fail(COALAC_EINVAL, "coalac_encode: mn/scale pointers are NULL");
-  if (plan->span && !d_in) return fail(COALAC_EINVAL, "coalac_encode: input pointer is NULL");
+  if (plan->span && !d_in && !d_inptr) return fail(COALAC_EINVAL, "coalac_encode: input pointer is NULL");
   if (plan->total_k && (!d_idx || !d_vals)) return fail(COALAC_EINVAL, "coalac_encode: idx/vals pointers are NULL");
   if ((reinterpret_cast<uintptr_t>(d_in) | reinterpret_cast<uintptr_t>(d_base)) & 15)
     return fail(COALAC_EINVAL, "coalac_encode: input/base must be 16-byte aligned");
@@ -2660,6 +2697,7 @@ int coalac_encode_sched(coalac_plan_t plan, const float* d_in, const float* d_ba
   Params P{};
   fill_meta(P, plan);
   P.in = d_in;
+  P.inptr = d_inptr;
   P.base = d_base;
   P.idx = d_idx;
   P.vals = d_vals;
@@ -2730,6 +2768,23 @@ int coalac_encode_sched(coalac_plan_t plan, const float* d_in, const float* d_ba
   if (rc) return rc;
   HIP_CHECK(hipGetLastError());
   return COALAC_OK;
+}
+}  // namespace
+
+extern "C" {
+
+int coalac_encode_sched(coalac_plan_t plan, const float* d_in, const float* d_base, int32_t* d_idx,
+                        void* d_vals, float* d_mn, float* d_scale, void* d_ws, uint64_t ws_bytes,
+                        unsigned flags, void* stream, const coalac_sched_t* sched) {
+  return encode_impl(plan, d_in, nullptr, d_base, d_idx, d_vals, d_mn, d_scale, d_ws, ws_bytes, flags, stream, sched);
+}
+
+int coalac_encode_segptr(coalac_plan_t plan, const float* const* d_seg_in, const float* d_base, int32_t* d_idx,
+                         void* d_vals, float* d_mn, float* d_scale, void* d_ws, uint64_t ws_bytes, unsigned flags,
+                         void* stream) {
+  if (plan && plan->nseg && !d_seg_in) return fail(COALAC_EINVAL, "coalac_encode_segptr: d_seg_in is NULL");
+  return encode_impl(plan, nullptr, d_seg_in, d_base, d_idx, d_vals, d_mn, d_scale, d_ws, ws_bytes, flags, stream,
+                     nullptr);
 }
 
 int coalac_encode(coalac_plan_t plan, const float* d_in, const float* d_base, int32_t* d_idx, void* d_vals,

@@ -96,6 +96,15 @@ int coalac_encode(coalac_plan_t plan, const float* d_in, const float* d_base, in
                   void* d_vals, float* d_mn, float* d_scale, void* d_ws, uint64_t ws_bytes,
                   unsigned flags, void* stream);
 
+/* Encode with every segment read from its OWN device pointer: d_seg_in is a DEVICE array of nseg
+ * pointers, d_seg_in[s] -> fp32[n_s], 16-byte aligned (e.g. the data pointers of a model's parameters:
+ * the plugin encodes the trained state in place, with no flattening copy — client compression(),
+ * coala/client/base.py:330-332). d_base (delta mode) stays a flat buffer indexed by in_off. Outputs,
+ * workspace, flags and stream as coalac_encode. */
+int coalac_encode_segptr(coalac_plan_t plan, const float* const* d_seg_in, const float* d_base, int32_t* d_idx,
+                         void* d_vals, float* d_mn, float* d_scale, void* d_ws, uint64_t ws_bytes, unsigned flags,
+                         void* stream);
+
 /* Decode into the dense d_out (fp32[span]); only positions inside segments are written.
  * d_base != NULL: d_out = d_base + decoded (fused; d_out may alias d_base). The encoded arrays may come
  * from an untrusted blob: out-of-range or unsorted indices can mis-decode but never write outside the

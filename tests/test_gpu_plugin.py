@@ -77,3 +77,34 @@ def test_carrier_deepcopy_then_marshal_on_gpu(cuda):
     up = pickle.loads(req.content.data)
     assert isinstance(up, CompressedUpdate) and up.encoded.idx.device.type == "cpu"
     assert len(req.content.data) < up.nbytes + 16384
+
+
+@pytest.mark.parametrize("mode", ["delta", "weights"])
+def test_encode_in_place_from_parameters_equals_flat_encode(cuda, mode):
+    """compression() reads the parameters in place (coalac_encode_segptr: one device pointer per tensor,
+    no flattening copy); the result equals the flat-buffer encode bit for bit, and a state with a
+    misaligned tensor (a view at an odd offset) falls back to the flattened path with the same bytes."""
+    from coala_amd.compression import UpdateCodec, flatten_state
+    m = build_module("resnet18", seed=3, device="cuda")
+    g = build_module("resnet18", seed=4, device="cuda")
+    codec = UpdateCodec(0.01, 8, mode)
+    base = codec.snapshot(g) if mode == "delta" else None
+    up = codec.encode(m.state_dict(), base=base)
+    fs = flatten_state(m.state_dict())
+    plan = codec.plan_for([e["n"] for e in fs.entries if e["kind"] == "seg"], fs.flat.device)
+    ref = plan.encode(fs.flat, base=None if base is None else base.flat)
+    torch.cuda.synchronize()
+    for f in ("idx", "vals", "mn", "scale"):
+        assert torch.equal(getattr(up.encoded, f), getattr(ref, f)), f
+    # misaligned tensor: a 4-byte-offset view
+    st = dict(m.state_dict())
+    name = next(k for k, v in st.items() if v.dtype == torch.float32 and v.numel() > 5000)
+    buf = torch.empty(st[name].numel() + 1, device="cuda")
+    view = buf[1:].view(st[name].shape)
+    view.copy_(st[name])
+    assert view.data_ptr() % 16 != 0
+    st[name] = view
+    up2 = codec.encode(st, base=base)
+    torch.cuda.synchronize()
+    for f in ("idx", "vals", "mn", "scale"):
+        assert torch.equal(getattr(up2.encoded, f), getattr(ref, f)), f
