@@ -210,6 +210,31 @@ class CompressedUpdate:
         return wire.pack(h, enc.mn.cpu().numpy(), enc.scale.cpu().numpy(), enc.idx.cpu().numpy(),
                          enc.vals.cpu().numpy(), b"".join(chunks))
 
+    def encoded_to(self, device, staging=None):
+        """The encoded buffers on `device`. An unpickled update (the server side of a remote upload,
+        coala/server/service.py:81-111) is moved with ONE host-to-device copy of the blob's mn / scale /
+        idx / vals region through `staging` (a pinned host buffer: staging(nbytes) -> uint8 tensor), so
+        the copy is asynchronous on the caller's stream; device tensors are typed views into it."""
+        device = torch.device(device)
+        blob = self._blob[0]
+        if (staging is None or device.type != "cuda" or blob is None or self.header.get("dense")
+                or self.encoded.idx.device == device):
+            return self.encoded.to(device, non_blocking=True)
+        _, sec = wire.sections(blob)
+        lo = sec["mn"][0]
+        hi = sec["vals"][0] + sec["vals"][1]
+        stage = staging(hi - lo)
+        stage[:hi - lo].numpy()[:] = np.frombuffer(blob, dtype=np.uint8, count=hi - lo, offset=lo)
+        dev = torch.empty(hi - lo, dtype=torch.uint8, device=device)
+        dev.copy_(stage[:hi - lo], non_blocking=True)
+        vdt = torch.float32 if self.header["bits"] == RAW_BITS else torch.uint8
+
+        def view(name, dt):
+            o, n = sec[name]
+            return dev[o - lo:o - lo + n].view(dt)
+        return Encoded(view("idx", torch.int32), view("vals", vdt), view("mn", torch.float32),
+                       view("scale", torch.float32))
+
     @classmethod
     def from_bytes(cls, blob):
         h, mn, scale, idx, vals, rawb = wire.unpack(blob)
@@ -303,6 +328,7 @@ class UpdateCodec:
         self._plans = {}
         self._ws = {}
         self._lock = threading.Lock()
+        self._tls = threading.local()
 
     def plan_for(self, sizes, device, ratio=None, bits=None, clients=1):
         ratio = self.ratio if ratio is None else float(ratio)
@@ -351,6 +377,28 @@ class UpdateCodec:
         header["total_k"] = int(plan.table.total_k)
         return CompressedUpdate(header, enc, raw)
 
+    def _thread_stream(self, device):
+        """One HIP stream per (thread, device): concurrent decodes from several threads overlap on the GPU
+        instead of queueing on one stream."""
+        streams = getattr(self._tls, "streams", None)
+        if streams is None:
+            streams = self._tls.streams = {}
+        key = str(device)
+        s = streams.get(key)
+        if s is None:
+            s = streams[key] = torch.cuda.Stream(device)
+        return s
+
+    def _staging(self, nbytes):
+        """This thread's pinned host staging buffer of at least nbytes (grown by doubling; reused once the
+        thread's stream has finished with it, which decode_state waits for)."""
+        buf = getattr(self._tls, "staging", None)
+        if buf is None or buf.numel() < nbytes:
+            buf = torch.empty(max(nbytes, 2 * (buf.numel() if buf is not None else 0), 1 << 20),
+                              dtype=torch.uint8, pin_memory=True)
+            self._tls.staging = buf
+        return buf
+
     def _workspace(self, plan):
         """The encode workspace of `plan` for the calling thread and its current stream, reused across
         calls (kernels on one stream run in order, so consecutive encodes can share it)."""
@@ -397,9 +445,20 @@ class UpdateCodec:
                 _check_same_layout(h["entries"], base.entries)
                 base_flat = base.flat_on(device)
             plan = self.plan_for(sizes, device, ratio=h["ratio"], bits=h["bits"])
-            enc = update.encoded.to(device, non_blocking=True)
-            flat = plan.decode(enc, base=base_flat)
             offs = plan.table.offsets  # the decoder's own offsets, never the (untrusted) header's
+            if device.type == "cuda":
+                # this thread's own stream (the remote server decodes from one thread per upload,
+                # coala/server/service.py:74): pinned H2D of the payload + decode, then wait for it
+                side = self._thread_stream(device)
+                side.wait_stream(torch.cuda.current_stream(device))
+                out = torch.empty(plan.span, dtype=torch.float32, device=device)
+                with torch.cuda.stream(side):
+                    enc = update.encoded_to(device, staging=self._staging)
+                    flat = plan.decode(enc, base=base_flat, out=out, stream=side)
+                side.synchronize()
+            else:
+                enc = update.encoded.to(device, non_blocking=True)
+                flat = plan.decode(enc, base=base_flat)
         for e in h["entries"]:
             if e["kind"] == "seg":
                 o = offs[e["seg"]]

@@ -59,6 +59,25 @@ def pack(header, mn, scale, idx, vals, raw):
     return b"".join(parts)
 
 
+def sections(blob):
+    """(header, {name: (byte offset, byte count)}) of the mn / scale / idx / vals sections in `blob`, which
+    lie back to back (each 16-byte aligned) — one host-to-device copy moves all of them."""
+    mv = memoryview(blob)
+    if bytes(mv[:8]) != MAGIC:
+        raise ValueError("not a COALAQ1 blob (bad magic)")
+    ver, hl = struct.unpack_from("<II", mv, 8)
+    header = json.loads(bytes(mv[16:16 + hl]).decode())
+    T, K = int(header["n_segments"]), int(header["total_k"])
+    vsz = 4 if int(header["bits"]) == 32 else 1
+    pos = 16 + hl
+    out = {}
+    for name, n in (("mn", 4 * T), ("scale", 4 * T), ("idx", 0 if header.get("dense") else 4 * K), ("vals", vsz * K)):
+        pos += _pad16(pos)
+        out[name] = (pos, n)
+        pos += n
+    return header, out
+
+
 def unpack(blob):
     """blob -> (header dict, mn, scale, idx, vals, raw bytes). Arrays are read-only views of blob."""
     mv = memoryview(blob)

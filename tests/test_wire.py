@@ -72,3 +72,19 @@ def test_validate_rejects_corrupt_indices():
     blob2 = wire.pack(h, mn, sc, bad, vals, raw)
     with pytest.raises(ValueError):
         CompressedUpdate.from_bytes(blob2)
+
+
+def test_sections_locate_the_unpacked_arrays():
+    """wire.sections gives the byte ranges unpack reads: mn / scale / idx / vals back to back, each
+    16-byte aligned (the one-copy host-to-device transfer of a received upload relies on it)."""
+    import numpy as np
+    from coala_amd.compression import wire
+    h = {"ratio": 0.1, "bits": 8, "mode": "weights", "n_segments": 3, "total_k": 7, "entries": []}
+    mn, sc = np.arange(3, dtype=np.float32), np.arange(3, dtype=np.float32) + 10
+    idx, vals = np.arange(7, dtype=np.int32), np.arange(7, dtype=np.uint8)
+    blob = wire.pack(h, mn, sc, idx, vals, b"xyz")
+    hh, sec = wire.sections(blob)
+    for name, arr in (("mn", mn), ("scale", sc), ("idx", idx), ("vals", vals)):
+        o, n = sec[name]
+        assert o % 16 == 0 and n == arr.nbytes
+        assert blob[o:o + n] == arr.tobytes()
