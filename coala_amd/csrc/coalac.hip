@@ -135,7 +135,9 @@ struct Params {
   uint32_t *tstar, *rtie, *status;
   // per large unit
   uint32_t *tlo, *thi, *cntA, *cntC, *gtC, *eqC, *eqpre, *outoff;
-  uint2* cand;  // candidate records {index | A_FLAG, value bits}, UNIT slots per large unit
+  uint2* cand;  // candidate records {index | A_FLAG, value bits}, ccap slots per large unit
+  uint32_t ccap;  // record slots per large unit (< UNIT: a unit that finds more candidates overflows and its
+                  // segment is selected and emitted from the raw data instead)
   // parallel select (groups of GU units of one large segment)
   const uint4* groups;     // {large-segment index, first large unit, units, segment}
   uint32_t n_groups;
@@ -590,7 +592,8 @@ DEV void scan_unit_t(const Params& P, uint32_t lu, const UnitDev& L, GetT&& get_
   const uint32_t lane = lane_id();
   const uint32_t len = L.len;
   const uint64_t off = L.off;
-  uint2* R = P.cand + (uint64_t)lu * UNIT;
+  uint2* R = P.cand + (uint64_t)lu * P.ccap;
+  const uint32_t cap = P.ccap;
   uint32_t cC = 0, cA = 0;
   uint32_t tlo = 0, thi = 0;
   // buffer resources over exactly this unit: one shared lane offset for all loads (constant offsets
@@ -599,6 +602,7 @@ DEV void scan_unit_t(const Params& P, uint32_t lu, const UnitDev& L, GetT&& get_
   const __amdgpu_buffer_rsrc_t rin = unit_rsrc(xin, len);
   const __amdgpu_buffer_rsrc_t rbase = unit_rsrc(DELTA ? P.base + off : xin, len);
   auto put = [&](uint32_t i, uint2 rec) {
+    if (i >= cap) return;  // overflow: counted, not stored (the segment goes to the raw-data path)
     if (SC1)
       st_sc1(R + i, rec);
     else
@@ -979,12 +983,12 @@ __global__ __launch_bounds__(BLOCK, SCAN_WPE) void k_scan(Params P) {
 // ------------------------------------------------------------------------------------------------
 // Exclusive prefix of cnt[0..cn) into upre[0..cn] (upre[cn] = total). Barriers inside.
 template <int NT>
-DEV uint32_t chunk_prefix(const uint32_t* cnt, uint32_t cn, uint32_t* upre, uint32_t* sh) {
+DEV uint32_t chunk_prefix(const uint32_t* cnt, uint32_t cn, uint32_t cap, uint32_t* upre, uint32_t* sh) {
   const uint32_t t = threadIdx.x;
   uint32_t carry = 0;
   for (uint32_t c0 = 0; c0 < cn; c0 += NT) {
     const uint32_t i = c0 + t;
-    const uint32_t v = i < cn ? cnt[i] : 0u;
+    const uint32_t v = i < cn ? min(cnt[i], cap) : 0u;  // stored records only
     uint32_t tot;
     const uint32_t ex = block_excl_scan<NT>(v, sh, tot);
     if (i < cn) upre[i] = carry + ex;
@@ -1001,8 +1005,8 @@ DEV uint32_t chunk_prefix(const uint32_t* cnt, uint32_t cn, uint32_t* upre, uint
 // wave-uniform so per-unit counts are ballot popcounts), G units per batch with 2 records per lane per
 // unit in flight. f(x, valid, u) is called by ALL lanes (ballots allowed); fend(u) after each unit.
 template <int NW, int G, class F, class FE>
-DEV void unit_sweep(const uint2* cand, uint32_t lu0, const uint32_t* upre, uint32_t cn, uint32_t total, F&& f,
-                    FE&& fend) {
+DEV void unit_sweep(const uint2* cand, uint32_t stride, uint32_t lu0, const uint32_t* upre, uint32_t cn,
+                    uint32_t total, F&& f, FE&& fend) {
   const uint32_t lane = lane_id(), w = threadIdx.x >> 6;
   const uint32_t J0 = (uint32_t)((uint64_t)total * w / NW), J1 = (uint32_t)((uint64_t)total * (w + 1) / NW);
   auto lower = [&](uint32_t key) {  // first u in [0, cn] with upre[u] >= key
@@ -1025,7 +1029,7 @@ DEV void unit_sweep(const uint2* cand, uint32_t lu0, const uint32_t* upre, uint3
       const uint32_t uu = min(u + g, U1 - 1);
       const uint32_t n = upre[uu + 1] - upre[uu];
       const uint32_t last = n ? n - 1 : 0u;  // region slot 0 always exists; read it when n == 0
-      const uint2* R = cand + (uint64_t)(lu0 + uu) * UNIT;
+      const uint2* R = cand + (uint64_t)(lu0 + uu) * stride;
       nn[g] = n;
       x0[g] = R[min(lane, last)].y;
       x1[g] = R[min(lane + 64, last)].y;
@@ -1037,7 +1041,7 @@ DEV void unit_sweep(const uint2* cand, uint32_t lu0, const uint32_t* upre, uint3
         f(__uint_as_float(x0[g]), lane < n, uu);
         if (n > 64) f(__uint_as_float(x1[g]), lane + 64 < n, uu);
         if (n > 128) {
-          const uint2* R = cand + (uint64_t)(lu0 + uu) * UNIT;
+          const uint2* R = cand + (uint64_t)(lu0 + uu) * stride;
           for (uint32_t i0 = 128; i0 < n; i0 += 64) f(__uint_as_float(R[min(i0 + lane, n - 1)].y), i0 + lane < n, uu);
         }
         fend(uu);
@@ -1073,9 +1077,9 @@ DEV void select_generic(const Params& P, uint32_t lb, uint32_t nu, uint32_t tlo,
   auto forC = [&](auto&& f) {
     for (uint32_t c0 = 0; c0 < nu; c0 += UCAP) {
       const uint32_t cn = min(UCAP, nu - c0);
-      const uint32_t total = chunk_prefix<NT>(P.cntC + lb + c0, cn, S.upre, S.sh);
+      const uint32_t total = chunk_prefix<NT>(P.cntC + lb + c0, cn, P.ccap, S.upre, S.sh);
       unit_sweep<NW, 4>(
-          P.cand, lb + c0, S.upre, cn, total,
+          P.cand, P.ccap, lb + c0, S.upre, cn, total,
           [&](float x, bool valid, uint32_t) {
             if (valid) f(fkey(x));
           },
@@ -1096,10 +1100,10 @@ DEV void select_generic(const Params& P, uint32_t lb, uint32_t nu, uint32_t tlo,
   for (uint32_t c0 = 0; c0 < nu; c0 += UCAP) {
     const uint32_t cn = min(UCAP, nu - c0);
     for (uint32_t i = t; i < cn; i += NT) S.ge[i] = 0;
-    const uint32_t total = chunk_prefix<NT>(P.cntC + lb + c0, cn, S.upre, S.sh);
+    const uint32_t total = chunk_prefix<NT>(P.cntC + lb + c0, cn, P.ccap, S.upre, S.sh);
     uint32_t weq = 0, wfp = NONE, wfn = NONE, ug = 0, ue = 0;  // wave-uniform
     unit_sweep<NW, 4>(
-        P.cand, lb + c0, S.upre, cn, total,
+        P.cand, P.ccap, lb + c0, S.upre, cn, total,
         [&](float x, bool valid, uint32_t) {
           const uint32_t key = fkey(x);
           const bool g = valid && key > T;
@@ -1176,9 +1180,9 @@ DEV void group_hist(const Params& P, uint32_t gi, uint32_t* hist, uint32_t* upre
   const uint32_t tlo = P.tlo[G.y], thi = P.thi[G.y];
   const Band band(tlo, thi, P.shhi[G.x]);
   for (uint32_t i = t; i < HB2; i += BLOCK) hist[i] = 0;
-  const uint32_t total = chunk_prefix<BLOCK>(P.cntC + G.y, G.z, upre, sh);  // barrier inside
+  const uint32_t total = chunk_prefix<BLOCK>(P.cntC + G.y, G.z, P.ccap, upre, sh);  // barrier inside
   unit_sweep<WAVES, 4>(
-      P.cand, G.y, upre, G.z, total,
+      P.cand, P.ccap, G.y, upre, G.z, total,
       [&](float x, bool valid, uint32_t) {
         const uint32_t key = fkey(x);
         if (valid && key >= tlo && key <= thi) atomicAdd(&hist[band.bin(key)], 1u);
@@ -1222,17 +1226,21 @@ DEV uint4 segment_pick(const Params& P, uint32_t li, uint32_t* hist, uint32_t* s
       h1 += g + j < ng ? v1[j] : 0u;
     }
   }
-  uint32_t sa = 0, sc = 0;
+  uint32_t sa = 0, sc = 0, ov = 0;
   for (uint32_t i = t; i < nu; i += BLOCK) {
+    const uint32_t c = P.cntC[lb + i];
     sa += P.cntA[lb + i];
-    sc += P.cntC[lb + i];
+    sc += c;
+    ov += c > P.ccap ? 1u : 0u;
   }
   hist[t] = h0;
   hist[BLOCK + t] = h1;
   sa = block_sum<BLOCK>(sa, sh);  // barriers inside (also publish hist)
   sc = block_sum<BLOCK>(sc, sh);
+  ov = block_sum<BLOCK>(ov, sh);
+  // (a unit that overflowed its record slots sends the segment to the raw-data path in segment_select)
   const bool generic = (P.flags & (COALAC_FLAG_FORCE_EXACT | COALAC_FLAG_GENERIC_SELECT)) || !(sa < k && k <= sc) ||
-                       nu > UCAP;
+                       nu > UCAP || ov != 0;
   if (generic) return make_uint4(0u, 0u, 0u, 1u);
   __syncthreads();
   uint32_t r = k - sa;
@@ -1262,11 +1270,11 @@ DEV void group_window(const Params& P, uint32_t gi, const uint4 G, const uint4 s
   const uint32_t t = threadIdx.x, lane = lane_id(), wv = t >> 6;
   const uint32_t wlo = st.x, whi = st.y;
   const uint32_t useg0 = G.y - P.segs[G.w].lu_begin;  // unit index (within the segment) of the group's first unit
-  const uint32_t total = chunk_prefix<BLOCK>(P.cntC + G.y, G.z, upre, sh);
+  const uint32_t total = chunk_prefix<BLOCK>(P.cntC + G.y, G.z, P.ccap, upre, sh);
   uint32_t wc = 0, ug = 0;
   float lmn = qnan(), lmx = qnan();
   unit_sweep<WAVES, 4>(
-      P.cand, G.y, upre, G.z, total,
+      P.cand, P.ccap, G.y, upre, G.z, total,
       [&](float x, bool valid, uint32_t u) {
         const uint32_t key = fkey(x);
         const bool g = valid && key > whi;
@@ -1324,6 +1332,104 @@ __global__ __launch_bounds__(BLOCK) void k_gwin(Params P) {
   __shared__ uint32_t hist[HB2];
   __shared__ uint32_t sh[64];
   group_pick_window(P, blockIdx.x, W, hist, sh);
+}
+
+// ------------------------------------------------------------------------------------------------
+// raw-data path of a segment (bracket miss, COALAC_FLAG_FORCE_EXACT, or a unit with more candidates than
+// its ccap record slots): T* from the raw keys (segment_select), per-unit counts from the raw data here,
+// and the emit re-reads the raw data (emit_raw_unit). No candidate record is used.
+// ------------------------------------------------------------------------------------------------
+// One wave's pass over a unit's raw data (row by row, index order): per element whether key > T and
+// whether key == T, handed to f(row, j, x, gt, tie) for every lane (ballots allowed inside f).
+template <bool DELTA, class F>
+DEV void raw_unit_rows(const Params& P, const UnitDev& L, F&& f) {
+  const uint32_t lane = lane_id();
+  const float* xin = P.inptr != nullptr ? P.inptr[L.seg] + L.start : P.in + L.off;
+  const __amdgpu_buffer_rsrc_t rin = unit_rsrc(xin, L.len);
+  const __amdgpu_buffer_rsrc_t rbase = unit_rsrc(DELTA ? P.base + L.off : xin, L.len);
+  for (uint32_t nb = 0; nb < 4; ++nb) {  // 4 float4 per lane in flight (register-lean)
+    float4 v[4];
+#pragma unroll
+    for (uint32_t i = 0; i < 4; ++i) v[i] = unit_load_x4<DELTA>(rin, rbase, ((nb * 4 + i) * 64 + lane) * 16);
+#pragma unroll
+    for (uint32_t i = 0; i < 4; ++i) f(nb * 4 + i, v[i]);
+  }
+}
+
+// Per-unit counts above / equal to T of the raw segment -> gtC / eqC; min / max of the values above T; the
+// segment-wide tie rank of the first positive and first negative tie (index order). Waves own contiguous
+// unit ranges in order. Block-level: call from all threads.
+template <int NT, bool DELTA>
+DEV void raw_counts(const Params& P, uint32_t lb, uint32_t nu, uint32_t T, uint32_t* sh, uint32_t* wcnt,
+                    uint32_t& fp, uint32_t& fn, float& gmn, float& gmx) {
+  constexpr int NW = NT / 64;
+  const uint32_t lane = lane_id(), wv = threadIdx.x >> 6;
+  const uint32_t u0 = (uint32_t)((uint64_t)nu * wv / NW), u1 = (uint32_t)((uint64_t)nu * (wv + 1) / NW);
+  uint32_t weq = 0, wfp = NONE, wfn = NONE;
+  float lmn = qnan(), lmx = qnan();
+  for (uint32_t u = u0; u < u1; ++u) {
+    const UnitDev L = P.lunits[lb + u];
+    uint32_t ug = 0, ue = 0;
+    raw_unit_rows<DELTA>(P, L, [&](uint32_t row, float4 v) {
+      const float xs[4] = {v.x, v.y, v.z, v.w};
+      const uint32_t e0 = (row * 64 + lane) * 4;
+      uint32_t pre = 0, mine = 0;
+      uint64_t tb[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const uint32_t key = fkey(xs[j]);
+        const bool ok = e0 + j < L.len;
+        const bool g = ok && key > T, e = ok && key == T;
+        ug += (uint32_t)__popcll(__ballot(g));
+        tb[j] = __ballot(e);
+        pre += mbcnt(tb[j]);
+        const float xg = g ? xs[j] : qnan();
+        lmn = fmin_nan(lmn, xg);
+        lmx = fmax_nan(lmx, xg);
+      }
+      // index order inside a row is (lane, j): a tie's rank = ties of lower lanes + earlier ties of its lane
+      uint32_t rp = NONE, rn = NONE;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const bool e = ((tb[j] >> lane) & 1ull) != 0;
+        if (e) {
+          const bool neg = (__float_as_uint(xs[j]) >> 31) != 0;
+          const uint32_t rank = weq + pre + mine;
+          if (neg)
+            rn = min(rn, rank);
+          else
+            rp = min(rp, rank);
+          ++mine;
+        }
+      }
+      wfp = min(wfp, wave_min_u32(rp));
+      wfn = min(wfn, wave_min_u32(rn));
+      const uint32_t rowt = (uint32_t)(__popcll(tb[0]) + __popcll(tb[1]) + __popcll(tb[2]) + __popcll(tb[3]));
+      weq += rowt;
+      ue += rowt;
+    });
+    if (lane == 0) {
+      pst(P, P.gtC + lb + u, ug);
+      pst(P, P.eqC + lb + u, ue);
+    }
+  }
+  // wave prefixes of the tie counts -> segment-wide ranks of the first positive / negative tie
+  if (lane == 0) wcnt[wv] = weq;
+  if (threadIdx.x == 0) {
+    sh[42] = NONE;
+    sh[43] = NONE;
+  }
+  __syncthreads();
+  uint32_t wpre = 0;
+  for (int i = 0; i < (int)wv; ++i) wpre += wcnt[i];
+  if (lane == 0 && wfp != NONE) atomicMin(&sh[42], wpre + wfp);
+  if (lane == 0 && wfn != NONE) atomicMin(&sh[43], wpre + wfn);
+  __syncthreads();
+  fp = sh[42];
+  fn = sh[43];
+  gmn = lmn;
+  gmx = lmx;
+  __syncthreads();
 }
 
 // Fast-path resolution in k_select: gather the groups' in-window lists (group order = index order),
@@ -1439,44 +1545,32 @@ DEV void segment_select(const Params& P, uint32_t li, SelSmem& S) {
   }
   sa = block_sum<NT>(sa, S.sh);
   sc = block_sum<NT>(sc, S.sh);
-  uint32_t tlo = P.tlo[lb], thi = P.thi[lb];
-  bool exact = false;
+  uint32_t mc = 0;  // most candidates any unit found (> ccap: records were dropped)
+  for (uint32_t i = t; i < nu; i += NT) mc = max(mc, P.cntC[lb + i]);
+  mc = wave_max_u32(mc);
+  if (lane_id() == 0) S.wcnt[wv] = mc;
+  __syncthreads();
+  for (int i = 0; i < NW; ++i) mc = max(mc, S.wcnt[i]);
+  __syncthreads();
+  const uint32_t tlo = P.tlo[lb], thi = P.thi[lb];
 
-  if ((P.flags & COALAC_FLAG_FORCE_EXACT) || !(sa <= k && k <= sc)) {
-    // Exact re-selection over the raw segment (rare path): T* of the whole segment, then rewrite the
-    // candidate lists with tlo = thi = T*.
+  if ((P.flags & COALAC_FLAG_FORCE_EXACT) || !(sa <= k && k <= sc) || mc > P.ccap) {
+    // raw-data path (rare): the exact k-th key of the whole segment, per-unit counts from the raw data;
+    // k_emit re-reads the raw data for this segment (status 1)
     const uint32_t n = sd.n;
     uint32_t rk = k;
-    const uint32_t T = block_select<NT, SEL_HB>(
+    T = block_select<NT, SEL_HB>(
         [&](auto&& f) {
           for (uint32_t i = t; i < n; i += NT) f(fkey(load_x1p<DELTA>(xs + i, bs + i)));
         },
         0u, KEY_MAX, rk, S.hist, S.sh);
-    for (uint32_t i = wv; i < nu; i += NW) {
-      if (P.wt)  // k_fused: the emit blocks of other CUs read these records
-        scan_unit_t<DELTA, 4, true>(P, lb + i, P.lunits[lb + i], [&]() { return make_uint2(T, T); }, nullptr);
-      else
-        scan_unit<DELTA, 4>(P, lb + i, P.lunits[lb + i], T, T, nullptr);
-    }
-    if (P.wt) {  // the counts / records this CU read before the rewrite may sit stale in its L1
-      drain();
-      __syncthreads();
-      if (t == 0) acquire_agent();
-      drain();
-    }
-    __syncthreads();
-    sa = 0;
-    for (uint32_t i = t; i < nu; i += NT) sa += P.cntA[lb + i];
-    sa = block_sum<NT>(sa, S.sh);
-    tlo = thi = T;
-    exact = true;
-    if (t == 0) P.status[s] = 1;
+    rt = rk;
+    raw_counts<NT, DELTA>(P, lb, nu, T, S.sh, S.wcnt, fp_rank, fn_rank, gmn, gmx);
+    if (t == 0) pst(P, P.status + s, 1u);
+  } else {
+    // rank of the k-th key among candidates with key <= thi (0: none of them)
+    select_generic<NT>(P, lb, nu, tlo, thi, k - sa, S, T, rt, fp_rank, fn_rank, gmn, gmx);
   }
-
-  // rank of the k-th key among candidates with key <= thi (0: none of them)
-  const uint32_t r = k - sa;
-  (void)exact;
-  select_generic<NT>(P, lb, nu, tlo, thi, r, S, T, rt, fp_rank, fn_rank, gmn, gmx);
   }
   STAMP(P, li, 10);
 
@@ -1546,15 +1640,67 @@ __global__ __launch_bounds__(SEL_NT) void k_select(Params P) {
 
 DEV uint32_t rl(uint32_t v, uint32_t l) { return (uint32_t)__builtin_amdgcn_readlane((int)v, (int)l); }
 
+// the raw-data emit of one large unit (its segment took the raw-data path): re-read the unit, keep key > T
+// and the ties whose segment-wide rank (eqp + ties before them) is < rt, in index order
+template <bool DELTA, bool RAW>
+DEV void emit_raw_unit(const Params& P, const UnitDev& L, uint32_t T, uint32_t rt, uint32_t eqp, uint64_t obase,
+                       float mn, float scale) {
+  const uint32_t lane = lane_id();
+  uint32_t eqc = 0, outc = 0;
+  raw_unit_rows<DELTA>(P, L, [&](uint32_t row, float4 v) {
+    const float xs[4] = {v.x, v.y, v.z, v.w};
+    const uint32_t e0 = (row * 64 + lane) * 4;
+    bool gt[4], tie[4], sel[4];
+    uint32_t tpre = 0, spre = 0, ntie = 0, nsel = 0;
+    uint64_t tb[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const uint32_t key = fkey(xs[j]);
+      const bool ok = e0 + j < L.len;
+      gt[j] = ok && key > T;
+      tie[j] = ok && key == T;
+      tb[j] = __ballot(tie[j]);
+      tpre += mbcnt(tb[j]);
+      ntie += (uint32_t)__popcll(tb[j]);
+    }
+    uint32_t mine = 0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {  // rank of a tie: ties of lower lanes, then earlier ties of this lane
+      sel[j] = gt[j] || (tie[j] && eqp + eqc + tpre + mine < rt);
+      mine += tie[j] ? 1u : 0u;
+    }
+    uint64_t sb[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      sb[j] = __ballot(sel[j]);
+      spre += mbcnt(sb[j]);
+      nsel += (uint32_t)__popcll(sb[j]);
+    }
+    uint32_t k = 0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      if (sel[j]) {
+        const uint64_t o = obase + outc + spre + k;
+        P.idx[o] = (int32_t)(L.start + e0 + j);
+        store_val<RAW>(P, o, xs[j], mn, scale);
+        ++k;
+      }
+    }
+    eqc += ntie;
+    outc += nsel;
+  });
+}
+
 // one wave emits the large units [lu0, lu1) (lu1 - lu0 <= EMIT_UPW)
-template <bool RAW>
+template <bool DELTA, bool RAW>
 DEV void emit_units(const Params& P, uint32_t lu0, uint32_t lu1) {
   const uint32_t lane = lane_id();
   // round 1 / 2: lane g < EMIT_UPW holds unit lu0 + g's count, offsets and its segment's T*, tie budget,
   // mn, scale (lanes past EMIT_UPW or past the last unit repeat a valid unit; never used)
   const uint32_t lug = min(lu0 + min(lane, EMIT_UPW - 1), lu1 - 1);
-  const uint32_t nCg = P.cntC[lug];
+  const uint32_t nCg = min(P.cntC[lug], P.ccap);  // stored records (a raw-path unit may have dropped some)
   const uint32_t segg = P.lunits[lug].seg;
+  const uint32_t stg = P.status[segg];             // != 0: the segment took the raw-data path
   const uint64_t sog = P.lunits[lug].out_off;
   const uint32_t eqpg = P.eqpre[lug], oog = P.outoff[lug];
   const uint32_t Tg = P.tstar[segg], rtg = P.rtie[segg];
@@ -1564,19 +1710,23 @@ DEV void emit_units(const Params& P, uint32_t lu0, uint32_t lu1) {
 #pragma unroll
   for (uint32_t g = 0; g < EMIT_UPW; ++g) {
     const uint32_t lu = min(lu0 + g, lu1 - 1), nC = rl(nCg, g);
-    rec0[g] = P.cand[(uint64_t)lu * UNIT + min(lane, nC ? nC - 1 : 0u)];  // unconditional (clamped) load
+    rec0[g] = P.cand[(uint64_t)lu * P.ccap + min(lane, nC ? nC - 1 : 0u)];  // unconditional (clamped) load
   }
 #pragma unroll
   for (uint32_t g = 0; g < EMIT_UPW; ++g) {
     const uint32_t nC = rl(nCg, g);
-    if (lu0 + g < lu1 && nC != 0) {
+    if (lu0 + g < lu1 && rl(stg, g) != 0) {
+      const uint64_t so = ((uint64_t)rl((uint32_t)(sog >> 32), g) << 32) | rl((uint32_t)sog, g);
+      emit_raw_unit<DELTA, RAW>(P, P.lunits[lu0 + g], rl(Tg, g), rl(rtg, g), rl(eqpg, g), so + rl(oog, g),
+                                __uint_as_float(rl(__float_as_uint(mng), g)), __uint_as_float(rl(__float_as_uint(scg), g)));
+    } else if (lu0 + g < lu1 && nC != 0) {
       const uint32_t lu = lu0 + g;
       const uint32_t T = rl(Tg, g), rt = rl(rtg, g), eqp = rl(eqpg, g);
       const float mn = __uint_as_float(rl(__float_as_uint(mng), g));
       const float scale = __uint_as_float(rl(__float_as_uint(scg), g));
       const uint64_t so = ((uint64_t)rl((uint32_t)(sog >> 32), g) << 32) | rl((uint32_t)sog, g);
       const uint64_t obase = so + rl(oog, g);
-      const uint2* R = P.cand + (uint64_t)lu * UNIT;
+      const uint2* R = P.cand + (uint64_t)lu * P.ccap;
       uint32_t eqc = 0, outc = 0;
       for (uint32_t i0 = 0; i0 < nC; i0 += 64) {
         const uint32_t i = i0 + lane;
@@ -1601,12 +1751,12 @@ DEV void emit_units(const Params& P, uint32_t lu0, uint32_t lu1) {
   }
 }
 
-template <bool RAW>
+template <bool DELTA, bool RAW>
 __global__ __launch_bounds__(BLOCK) void k_emit(Params P) {
   const uint32_t wv = threadIdx.x >> 6;
   const uint32_t lu0 = (blockIdx.x * WAVES + wv) * EMIT_UPW;
   if (lu0 >= P.n_lunits) return;
-  emit_units<RAW>(P, lu0, min(lu0 + EMIT_UPW, P.n_lunits));
+  emit_units<DELTA, RAW>(P, lu0, min(lu0 + EMIT_UPW, P.n_lunits));
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -1740,7 +1890,7 @@ DEV void k_fused_item(const Params& P, uint32_t role, uint32_t idx, uint8_t* are
     block_wait(P.hf_sel + E.z, 1u, P.hf_err);
     ready();
     const uint32_t u0 = E.x + wv * EMIT_UPW, u1 = min(u0 + EMIT_UPW, E.x + E.y);
-    if (u0 < u1) emit_units<RAW>(P, u0, u1);
+    if (u0 < u1) emit_units<DELTA, RAW>(P, u0, u1);
   }
 }
 
@@ -2147,7 +2297,7 @@ struct WsLayout {
   size_t total;
 };
 
-WsLayout ws_layout(size_t S, size_t LU, size_t NG, size_t NL, size_t NI) {
+WsLayout ws_layout(size_t S, size_t LU, size_t NG, size_t NL, size_t NI, uint32_t CC) {
   WsLayout L{};
   // control block: words k_fused polls, zeroed by one memset before every launch (a block of its own at
   // the workspace start, a multiple of 16 bytes: Guideline 16 "Re-initialise every call")
@@ -2176,7 +2326,7 @@ WsLayout ws_layout(size_t S, size_t LU, size_t NG, size_t NL, size_t NI) {
   L.eqC = take(4 * LU);
   L.eqpre = take(4 * LU);
   L.outoff = take(4 * LU);
-  L.cand = take(sizeof(uint2) * UNIT * LU);
+  L.cand = take(sizeof(uint2) * (size_t)CC * LU);
   L.stamps = take(8 * NSTAMP * std::max<size_t>(S, 1));
   L.ghist = take(4 * HB2 * NG);
   L.gcnt = take(4 * NG);
@@ -2286,6 +2436,7 @@ struct coalac_plan {
   int bits = 8;
   int nseg = 0;
   uint32_t n_small = 0, n_large = 0, n_units = 0, n_lunits = 0;
+  uint32_t ccap = UNIT;  // candidate record slots per large unit
   uint64_t span = 0, total_k = 0;
   void* meta = nullptr;
   SegDev* segs = nullptr;
@@ -2342,6 +2493,7 @@ void fill_meta(Params& P, coalac_plan_t plan) {
   P.n_units = plan->n_units;
   P.n_lunits = plan->n_lunits;
   P.levels = plan->bits == 32 ? 0.0f : (float)((1u << plan->bits) - 1u);
+  P.ccap = plan->ccap;
 }
 
 // Stage boundary i of an encode / decode enqueue: wait for sc->wait[i], then record sc->record[i].
@@ -2436,7 +2588,7 @@ int launch_encode(const Params& P, coalac_plan_t plan, hipStream_t st, const coa
     hipLaunchKernelGGL((k_select<DELTA, RAW>), dim3(plan->n_large), dim3(SEL_NT), 0, st, P);
   }
   ENC_BOUNDARY(3);
-  if ((stages & COALAC_STAGE_SELECT) && plan->n_large) hipLaunchKernelGGL((k_emit<RAW>), dim3((plan->n_lunits + WAVES * EMIT_UPW - 1) / (WAVES * EMIT_UPW)), dim3(BLOCK), 0, st, P);
+  if ((stages & COALAC_STAGE_SELECT) && plan->n_large) hipLaunchKernelGGL((k_emit<DELTA, RAW>), dim3((plan->n_lunits + WAVES * EMIT_UPW - 1) / (WAVES * EMIT_UPW)), dim3(BLOCK), 0, st, P);
   if (fork) HIP_CHECK(hipStreamWaitEvent(st, plan->join, 0));
   ENC_BOUNDARY(4);
 #undef ENC_BOUNDARY
@@ -2481,7 +2633,7 @@ int launch_front(const Params& P, coalac_plan_t plan, hipStream_t st, const coal
   }
   BOUNDARY(3);
   if (plan->n_large)
-    hipLaunchKernelGGL((k_emit<RAW>), dim3((plan->n_lunits + WAVES * EMIT_UPW - 1) / (WAVES * EMIT_UPW)), dim3(BLOCK), 0,
+    hipLaunchKernelGGL((k_emit<DELTA, RAW>), dim3((plan->n_lunits + WAVES * EMIT_UPW - 1) / (WAVES * EMIT_UPW)), dim3(BLOCK), 0,
                        st, P);
   BOUNDARY(4);
   return COALAC_OK;
@@ -2587,7 +2739,15 @@ int coalac_plan_create(const coalac_seg_t* h_segs, int nseg, int bits, coalac_pl
   const FusedSchedule F = fused_schedule(segs, large_list, p->n_small, p->n_lunits, groups, delay);
   p->n_items = (uint32_t)F.items.size();
   p->n_front = (uint32_t)F.front.size();
-  p->ws = ws_layout((size_t)nseg, lunits.size(), groups.size(), large_list.size(), F.items.size());
+  // record slots per large unit: the candidates a unit can expect at the plan's largest ratio (kept
+  // share + the sampled band + margin), so the workspace is ~1 B/element at ratio 0.01 instead of 8
+  double rmax = 0.0;
+  for (uint32_t s2 : large_list) rmax = std::max(rmax, (double)segs[s2].k / (double)segs[s2].n);
+  uint32_t ccap = (uint32_t)align_up((size_t)(UNIT * std::min(1.0, 2.0 * rmax + 0.05) + 256.0), 64);
+  if (const char* e = getenv("COALAC_CCAP")) ccap = (uint32_t)atoi(e);  // tests: force overflow
+  ccap = std::max<uint32_t>(STAGE_CAP, std::min<uint32_t>(UNIT, ccap));
+  p->ccap = ccap;
+  p->ws = ws_layout((size_t)nseg, lunits.size(), groups.size(), large_list.size(), F.items.size(), ccap);
 
   const size_t o_segs = 0;
   const size_t o_units = align_up(o_segs + sizeof(SegDev) * segs.size(), 256);

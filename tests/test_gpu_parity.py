@@ -293,3 +293,27 @@ def test_golden_vectors_bit_exact(cuda, ratio, bits):
                                       gold[f"{tag}/mn_scale"].view(np.uint32), err_msg=tag)
         np.testing.assert_array_equal(dec[off:off + xs[s].size].view(np.uint32), gold[f"{tag}/dec"].view(np.uint32),
                                       err_msg=tag)
+
+
+@pytest.mark.parametrize("mode", [0, 64, 128])  # kernel sequence, ONE_LAUNCH, FRONT_LAUNCH
+@pytest.mark.parametrize("delta", [False, True])
+def test_record_slot_overflow_takes_raw_path(cuda, monkeypatch, mode, delta):
+    """The candidate workspace is capped per unit (plan ccap); a unit that finds more candidates than its
+    slots sends its segment to the raw-data path (exact k-th key of the raw segment, per-unit counts and
+    the emit re-read from the raw data). Forced here with COALAC_CCAP=512 at ratio 0.3: bit-exact."""
+    monkeypatch.setenv("COALAC_CCAP", "512")
+    rng = np.random.default_rng(21 + delta)
+    sizes = fp32_sizes("resnet18")
+    xs = [gauss(rng, sizes)]
+    bases = [gauss(rng, sizes, -2, -1)] if delta else None
+    plan, g, r = run_both(sizes, 0.3, 8, xs, bases, flags=mode)
+    assert_same(plan, g, r)
+    assert g["fallbacks"] > 0
+
+
+def test_workspace_is_capped(cuda):
+    """16 ResNet-50 updates at ratio 0.01: the encode workspace is about 1 B per element (round 1: 8)."""
+    sizes = fp32_sizes("resnet50_tv")
+    plan = CodecPlan(sizes, 0.01, 8, clients=16)
+    n = plan.table.n_elements
+    assert plan.ws_bytes < 1.5 * n, plan.ws_bytes / n
