@@ -39,8 +39,8 @@ FRONT_LAUNCH = 128  # COALAC_FLAG_FRONT_LAUNCH: samplers + scan + small segments
 SPLIT = 2  # sub-batches per step: two independent pipelines side by side fill the CUs the other leaves
            # idle in its latency-bound stages and launch tails (+11 % over one 16-client pipeline)
 EVENT_EVERY = 4  # timing events on every 4th timed step (each recorded event adds a ~4 us dispatch gap)
-CONFIGS = {  # name -> (layout | "c5", clients per GPU, split)
-    "C2": ("resnet18", 16, SPLIT),
+CONFIGS = {  # name -> (layout | "c5", clients per GPU, sub-batches: the best of 1..4 on the box)
+    "C2": ("resnet18", 16, 3),
     "C3": ("resnet50_tv", 16, SPLIT),
     "C4": ("vit_b16", 16, SPLIT),
     "C5": ("c5", None, SPLIT),
@@ -74,6 +74,7 @@ def parse():
     p.add_argument("--event-every", type=int, default=EVENT_EVERY,
                    help="record the per-kernel timing events on every Nth timed step (1 = every step)")
     p.add_argument("--flags", type=int, default=0, help="coalac encode flags (test hooks; 0 for the bench)")
+    p.add_argument("--extras-split", type=int, default=None, help="override the sub-batch count of the extras")
     p.add_argument("--single-split", type=int, default=SINGLE_SPLIT,
                    help="config 'single': the update's segments cut into this many ranges, each a sub-plan on its "
                         "own stream (their latency-bound phases overlap)")
@@ -202,6 +203,8 @@ def build_table(cfg, a, rank, headline):
     layout, clients, split = CONFIGS[cfg]
     if split == "single":
         split = a.single_split
+    elif not headline and a.extras_split is not None:
+        split = a.extras_split
     if headline:
         layout = a.layout or layout
         clients = a.clients or clients

@@ -954,8 +954,24 @@ __global__ __launch_bounds__(BLOCK) void k_sample(Params P) {
   sample_segment<DELTA, false>(P, blockIdx.x, hist, sh);
 }
 
-// k_scan: streams the large units, one wave each. Blocks [0, scan_small) first encode the small
-// segments when they are not forked to the side stream (small plans: the fork costs more than it hides).
+// k_presel: the samplers (blocks [0, n_large)) and the small segments (blocks after them) as one launch —
+// both latency-bound, they run side by side ahead of k_scan, which then streams large units only (small
+// segments inside k_scan held its first blocks and a 25 KB LDS arena: C2 as 2 sub-batches streamed at
+// ~2.3 TB/s)
+template <bool DELTA, bool RAW>
+__global__ __launch_bounds__(BLOCK) void k_presel(Params P) {
+  __shared__ __attribute__((aligned(16))) uint8_t arena[(SMALL_MAX + HIST_BINS + 64) * 4];
+  uint32_t* hist = reinterpret_cast<uint32_t*>(arena) + SMALL_MAX;
+  if (blockIdx.x < P.n_large) {
+    sample_segment<DELTA, false>(P, blockIdx.x, hist, hist + HIST_BINS);
+  } else {
+    small_encode<DELTA, RAW>(P, P.small_list[blockIdx.x - P.n_large], reinterpret_cast<float*>(arena), hist,
+                             hist + HIST_BINS);
+  }
+}
+
+// k_scan: streams the large units, one wave each. (WITH_SMALL: blocks [0, scan_small) first encode the
+// small segments — no longer launched: k_presel runs them beside the samplers.)
 template <bool DELTA, bool RAW, bool WITH_SMALL>
 __global__ __launch_bounds__(BLOCK, SCAN_WPE) void k_scan(Params P) {
   // one LDS arena: candidate staging (WAVES x STAGE_CAP records) or a small segment's values + histogram
@@ -2546,8 +2562,10 @@ int launch_encode(const Params& P, coalac_plan_t plan, hipStream_t st, const coa
   // split encode: only in stage SMALL (k_small)
   const bool split = stages != all;
   const bool fork = plan->n_small && !split && plan->n_lunits >= FORK_MIN_LUNITS && !(P.flags & COALAC_FLAG_NO_FORK);
+  // otherwise (whole encode) the small segments run beside the samplers in k_presel
+  const bool presel = !split && !fork && plan->n_small;
   Params Q = P;
-  Q.scan_small = (fork || split) ? 0u : plan->n_small;
+  Q.scan_small = 0u;
   std::unique_lock<std::mutex> lk(plan->mu, std::defer_lock);
   if (fork) {
     lk.lock();
@@ -2572,14 +2590,14 @@ int launch_encode(const Params& P, coalac_plan_t plan, hipStream_t st, const coa
     hipLaunchKernelGGL((k_small<DELTA, RAW>), dim3(plan->n_small), dim3(BLOCK), 0, plan->side, P);
     HIP_CHECK(hipEventRecord(plan->join, plan->side));
   }
-  if ((stages & COALAC_STAGE_SAMPLE) && plan->n_large)
+  if (presel)
+    hipLaunchKernelGGL((k_presel<DELTA, RAW>), dim3(plan->n_large + plan->n_small), dim3(BLOCK), 0, st, P);
+  else if ((stages & COALAC_STAGE_SAMPLE) && plan->n_large)
     hipLaunchKernelGGL((k_sample<DELTA, RAW>), dim3(plan->n_large), dim3(BLOCK), 0, st, P);
   if (split && (stages & COALAC_STAGE_SMALL) && plan->n_small)
     hipLaunchKernelGGL((k_small<DELTA, RAW>), dim3(plan->n_small), dim3(BLOCK), 0, st, P);
   ENC_BOUNDARY(1);
-  if ((stages & COALAC_STAGE_SCAN) && Q.scan_small)
-    hipLaunchKernelGGL((k_scan<DELTA, RAW, true>), dim3(gu + Q.scan_small), dim3(BLOCK), 0, st, Q);
-  else if ((stages & COALAC_STAGE_SCAN) && gu)
+  if ((stages & COALAC_STAGE_SCAN) && gu)
     hipLaunchKernelGGL((k_scan<DELTA, RAW, false>), dim3(gu), dim3(BLOCK), 0, st, Q);
   ENC_BOUNDARY(2);
   if ((stages & COALAC_STAGE_SELECT) && plan->n_large) {
