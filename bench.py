@@ -38,7 +38,7 @@ ONE_LAUNCH = 64     # COALAC_FLAG_ONE_LAUNCH: the whole encode as one k_fused la
 FRONT_LAUNCH = 128  # COALAC_FLAG_FRONT_LAUNCH: samplers + scan + small segments as one launch
 SPLIT = 2  # sub-batches per step: two independent pipelines side by side fill the CUs the other leaves
            # idle in its latency-bound stages and launch tails (+11 % over one 16-client pipeline)
-EVENT_EVERY = 4  # timing events on every 4th timed step (each recorded event adds a ~4 us dispatch gap)
+ROOF_STEPS = 8  # joined steps after the timed region that carry the per-kernel timing events
 CONFIGS = {  # name -> (layout | "c5", clients per GPU, sub-batches: the best of 1..4 on the box)
     "C2": ("resnet18", 16, 3),
     "C3": ("resnet50_tv", 16, SPLIT),
@@ -71,8 +71,9 @@ def parse():
     p.add_argument("--inflight", type=int, default=1,
                    help="independent pipelines (own plan, buffers and stream) taking the steps round-robin, so "
                         "consecutive batches overlap (each step still encodes + decodes its whole batch)")
-    p.add_argument("--event-every", type=int, default=EVENT_EVERY,
-                   help="record the per-kernel timing events on every Nth timed step (1 = every step)")
+    p.add_argument("--roof-steps", type=int, default=ROOF_STEPS,
+                   help="extra steps after the timed region, joined per step and carrying per-kernel HIP events, "
+                        "that measure the streaming kernels' launch durations for the roofline")
     p.add_argument("--flags", type=int, default=0, help="coalac encode flags (test hooks; 0 for the bench)")
     p.add_argument("--extras-split", type=int, default=None, help="override the sub-batch count of the extras")
     p.add_argument("--single-split", type=int, default=SINGLE_SPLIT,
@@ -240,39 +241,29 @@ def run_workload(cfg, a, dev, world, rank, headline):
     pipes = [s[0] for s in slots]
     torch.cuda.synchronize()
 
-    def step(i=None, j=0):
+    def step(i=None, j=0, joined=a.joined):
         p, enc, out = slots[j % len(slots)]
         ee = ev_e[i] if i is not None else None
         de = ev_d[i] if i is not None else None
         # sub-batch streams ordered by themselves step after step (each slot's buffers are used by its own
         # streams only): no joins with the caller's stream inside the timed loop
-        p.roundtrip(flat, base=base, enc=enc, out=out, enc_events=ee, dec_events=de, joined=a.joined)
+        p.roundtrip(flat, base=base, enc=enc, out=out, enc_events=ee, dec_events=de, joined=joined)
 
     for w in range(max(a.warmup, len(slots))):
         step(j=w)
     fallbacks = sum(p.fallbacks() for p in pipes)
     timeouts = sum(p.timeouts() for p in pipes)
 
-    # Timing events only around the streaming kernels (every recorded event costs a dispatch gap):
-    # per sub-batch, [1] / [2] around its k_scan / k_decode.
-    def part_events(n):
-        evs = []
-        for _ in range(split):
-            ev = [None] * n
-            ev[1], ev[2] = make_events(torch, 2)
-            evs.append(ev)
-        return evs
-    every = max(1, a.event_every)
-    timed_steps = [i for i in range(a.steps) if i % every == 0]
-    ev_e = [part_events(5) if i % every == 0 else None for i in range(a.steps)]
-    ev_d = [part_events(3) if i % every == 0 else None for i in range(a.steps)]
+    # The timed region carries no timing event (each recorded event costs a dispatch gap) and its
+    # sub-batch streams are not joined per step, so consecutive steps overlap.
+    ev_e = ev_d = [None] * a.steps
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for i in range(a.steps):
-        step(i, i)
+        step(j=i)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -281,6 +272,25 @@ def run_workload(cfg, a, dev, world, rank, headline):
         x = torch.tensor([el], dtype=torch.float64, device=dev)
         dist.all_reduce(x, op=dist.ReduceOp.MAX)
         el = x.item()
+
+    # Roofline steps (after the timed region, not part of `value`): per sub-batch, HIP events [1] / [2]
+    # recorded on its own stream around its streaming kernels, each step joined with the caller's stream
+    # so the sub-batches' launches of a kernel start together (unjoined, the streams drift apart and a
+    # launch group's interval would hold other kernels).
+    def part_events(n):
+        evs = []
+        for _ in range(split):
+            ev = [None] * n
+            ev[1], ev[2] = make_events(torch, 2)
+            evs.append(ev)
+        return evs
+    timed_steps = list(range(max(1, a.roof_steps)))
+    ev_e = [part_events(5) for _ in timed_steps]
+    ev_d = [part_events(3) for _ in timed_steps]
+    torch.cuda.synchronize()
+    for i in timed_steps:
+        step(i, i, joined=True)
+    torch.cuda.synchronize()
 
     # Per-kernel durations (ms, averaged over the event-carrying steps) from HIP events on each
     # sub-batch's stream around its streaming kernel. With S sub-batches the S launches of a kernel run
@@ -329,8 +339,9 @@ def run_workload(cfg, a, dev, world, rank, headline):
         traffic, src = pmc_traffic(dom, cfg, a, split)
         res["roofline"]["traffic"] = traffic * split if traffic is not None else None
         res["roofline"]["traffic_source"] = src
-        res["stage_timing"] = (f"HIP events on each sub-batch stream around {enc_kernel} / k_decode (union over "
-                               f"the {split} sub-batches), {len(timed_steps)} of the {a.steps} timed steps")
+        res["stage_timing"] = (f"HIP events on each sub-batch stream around {enc_kernel} / k_decode, union over the "
+                               f"{split} concurrent launches, mean of {len(timed_steps)} joined steps run after the "
+                               f"timed region")
     for p in pipes:
         p.close()
     del slots, pipes, flat, base

@@ -14,8 +14,8 @@ import json
 import os
 import sys
 
-CODEC = ("k_sample", "k_scan", "k_small", "k_ghist", "k_pick", "k_gwin", "k_select", "k_emit", "k_bounds",
-         "k_decode", "k_aggregate")
+CODEC = ("k_sample", "k_presel", "k_scan", "k_small", "k_ghist", "k_pick", "k_gwin", "k_select", "k_emit", "k_bounds",
+         "k_decode", "k_aggregate", "k_fused")
 STREAMING = ("k_scan", "k_decode")
 
 
@@ -46,6 +46,8 @@ def main():
     ap.add_argument("--group", type=int, default=1,
                     help="streaming kernels launched this many at a time (bench --split): also report the mean "
                          "union interval (first start to last end) of each group of consecutive launches")
+    ap.add_argument("--last-groups", type=int, default=0,
+                    help="with --group: average only the last N groups (bench.py's joined roofline steps)")
     ap.add_argument("--dump", type=int, default=0, help="also print the last N kernels (start/end us, queue)")
     a = ap.parse_args()
     files = glob.glob(os.path.join(a.dir, "**", "*kernel_trace.csv"), recursive=True)
@@ -88,7 +90,7 @@ def main():
             d = sorted((s, e) for s, e, kk, _ in all_rows if kk == k)
             spans = [max(e for _, e in d[i:i + a.group]) - d[i][0]
                      for i in range(0, len(d) - a.group + 1, a.group)]
-            spans = spans[int(len(spans) * (1.0 - a.last_frac)):]
+            spans = spans[-a.last_groups:] if a.last_groups else spans[int(len(spans) * (1.0 - a.last_frac)):]
             if spans:
                 out["group_union_us"][k] = round(sum(spans) / len(spans) / 1e3, 2)
     print(json.dumps(out, indent=1))
