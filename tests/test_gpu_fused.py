@@ -1,5 +1,5 @@
-"""The front-launch encode (samplers inside the scan launch, the default) and the one-launch encode (k_fused,
-COALAC_FLAG_ONE_LAUNCH) against the kernel-sequence encode (SEQ): bit-identical outputs, no bounded wait ever giving up, control words re-initialised on
+"""The front-launch encode (COALAC_FLAG_FRONT_LAUNCH: samplers inside the scan launch) and the one-launch encode
+(k_fused, COALAC_FLAG_ONE_LAUNCH), both opt-in, against the default kernel-sequence encode (SEQ): bit-identical outputs, no bounded wait ever giving up, control words re-initialised on
 every call (the same workspace reused), and several plans in flight at once on separate streams.
 
 Tolerance: bit-identical (the same bar as test_gpu_parity.py).
@@ -15,7 +15,7 @@ from coala_amd.layouts import fp32_sizes
 from coala_amd.workload import c5_share, mixed_table, synth_batch
 
 pytestmark = pytest.mark.gpu
-SEQ = 0  # the default encode: the kernel sequence k_sample .. k_emit
+SEQ = 0  # the default encode: the kernel sequence k_presel .. k_emit
 
 
 def encode(plan, flat, base=None, flags=0, ws=None):
