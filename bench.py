@@ -65,6 +65,9 @@ def parse():
     p.add_argument("--split", type=int, default=None,
                    help="the step's clients are cut into this many sub-batches (balanced by elements), each an "
                         "independent pipeline (own plan, buffers, HIP stream) launched side by side")
+    p.add_argument("--pipe", choices=["split", "lane"], default="split",
+                   help="split: SplitPipeline sub-batches, free-running side by side; lane: LanePipeline (the "
+                        "streaming kernels of all lanes back to back on one stream, latency stages beside them)")
     p.add_argument("--fork", action="store_true", help="keep the per-plan small-segment side streams with --split > 1")
     p.add_argument("--joined", action="store_true",
                    help="join the sub-batch streams with the caller's stream on entry/exit of every step")
@@ -177,8 +180,8 @@ def pmc_traffic(kernel, cfg, a, split):
     doubled (gfx950 reports half the bytes of wide coalesced streaming reads, MI355X_MICROARCH.md §HBM)
     + WRITE_SIZE. Only reported for the default configuration the summary was collected on."""
     import glob
-    default = (cfg, a.layout, a.clients, a.ratio, a.bits, a.mode, a.inflight, split) == \
-        ("C3", None, None, 0.01, 8, "weights", 1, SPLIT)
+    default = (cfg, a.layout, a.clients, a.ratio, a.bits, a.mode, a.inflight, split, a.pipe) == \
+        ("C3", None, None, 0.01, 8, "weights", 1, SPLIT, "split")
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_summary.json")))
     if not default or not files:
         return None, None
@@ -188,6 +191,17 @@ def pmc_traffic(kernel, cfg, a, split):
         if name.split("<")[0] == kernel and "FETCH_SIZE_x2_bytes" in e and "WRITE_SIZE_bytes" in e:
             return e["FETCH_SIZE_x2_bytes"] + e["WRITE_SIZE_bytes"], os.path.relpath(files[-1], ROOT)
     return None, None
+
+
+def large_elements(pipe):
+    """Elements of the segments the pipeline's plans stream through k_scan (the others are encoded whole
+    in k_presel; each plan's threshold follows its size, spec.small_limit)."""
+    from coala_amd.compression.spec import small_limit
+    tot = 0
+    for q in getattr(pipe, "parts", None) or pipe.lanes:
+        n = q["plan"].table.segs[:, 1].astype("int64")
+        tot += int(n[n > small_limit(n)].sum())
+    return tot
 
 
 def make_events(torch, n):
@@ -224,8 +238,7 @@ def run_workload(cfg, a, dev, world, rank, headline):
     import torch
     import torch.distributed as dist
 
-    from coala_amd.compression import SplitPipeline
-    from coala_amd.compression.spec import SMALL_MAX
+    from coala_amd.compression import LanePipeline, SplitPipeline
     from coala_amd.workload import synth_batch
 
     t, ids, split, desc = build_table(cfg, a, rank, headline)
@@ -235,7 +248,10 @@ def run_workload(cfg, a, dev, world, rank, headline):
     inflight = max(1, a.inflight) if headline else 1
     slots = []
     for _ in range(inflight):
-        p = SplitPipeline(t, a.bits, split=split, device=dev, flags=a.flags, fork=a.fork)
+        if a.pipe == "lane" and headline:
+            p = LanePipeline(t, a.bits, lanes=split, device=dev, flags=a.flags)
+        else:
+            p = SplitPipeline(t, a.bits, split=split, device=dev, flags=a.flags, fork=a.fork)
         slots.append((p, p.empty_encoded(), p.empty_flat()))
     split = slots[0][0].n_parts
     pipes = [s[0] for s in slots]
@@ -313,7 +329,7 @@ def run_workload(cfg, a, dev, world, rank, headline):
     delta = a.mode == "delta"
     vb = 4 if a.bits == 32 else 1
     segs = t.segs.astype("int64")
-    large_elems = int(segs[segs[:, 1] > SMALL_MAX, 1].sum())
+    large_elems = large_elements(pipes[0])
     alg = {  # algorithmic HBM bytes per timed interval
         enc_kernel: (4 * large_elems if multi else 4 * N + (4 + vb) * K + 8 * T if one else 4 * N) + (4 * N if delta else 0),
         "k_decode": 4 * N * (2 if delta else 1) + (4 + vb) * K + 8 * T,
@@ -324,7 +340,7 @@ def run_workload(cfg, a, dev, world, rank, headline):
     step_alg = t.algorithmic_bytes(a.bits, delta)
     res = {
         "value": round(4.0 * N * world * a.steps / el / 1e9, 2), "ms_per_step": round(step_ms, 4),
-        "desc": desc, "split": split, "inflight": len(slots),
+        "desc": desc, "split": split, "inflight": len(slots), "pipe": a.pipe if headline else "split",
         "elements_per_gpu": N, "segments_per_gpu": T, "kept_per_gpu": K,
         "roofline": {"bound": "hbm", "kernel": dom if split == 1 else f"{dom} x{split} concurrent launches (union interval)",
                      "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4),

@@ -30,7 +30,28 @@ import torch
 
 from . import _lib
 from .plan import CodecPlan, Encoded
-from .spec import SMALL_MAX, SegmentTable
+from .spec import SegmentTable, small_limit
+
+_IN_LAUNCH = _lib.COALAC_FLAG_ONE_LAUNCH | _lib.COALAC_FLAG_FRONT_LAUNCH  # encodes with in-launch waits
+
+
+_STREAM_POOL = {}  # device index -> streams shared by every SplitPipeline of the process
+
+
+def pooled_streams(device, n):
+    """The first n streams of a per-device pool created once per process, in order. HIP binds a stream to
+    one of its hardware queues (4 per process by default) when the stream is created, round-robin: two
+    sub-batch streams created far apart can land on one queue and then run one after the other (a C2
+    share as 3 sub-batches measured 1,707 vs 2,279 GB/s depending on which streams the process had made
+    before). Pipelines that take their sub-batch streams from this pool always get the same consecutive,
+    queue-distinct streams, whatever else the process created in between."""
+    d = torch.device(device)
+    key = d.index if d.index is not None else torch.cuda.current_device()
+    pool = _STREAM_POOL.setdefault(key, [])
+    with torch.cuda.device(key):
+        while len(pool) < n:
+            pool.append(torch.cuda.Stream(key))
+    return pool[:n]
 
 
 def split_lanes(sizes, lanes):
@@ -99,10 +120,11 @@ class LanePipeline:
             for i, (s0, s1) in enumerate(self.ranges):
                 plan = CodecPlan.from_segments(table.segs[s0:s1], self.bits, device=self.device)
                 n = table.segs[s0:s1, 1]
+                lim = small_limit(n)
                 L = dict(s0=s0, s1=s1, plan=plan, ws=plan.empty_workspace(), dws=plan.empty_decode_workspace(),
                          c=self.c_streams[i % len(self.c_streams)],
-                         n_small=int((n <= SMALL_MAX).sum()), n_large=int((n > SMALL_MAX).sum()))
-                for name in ("sampled", "scanned", "bounded"):
+                         n_small=int((n <= lim).sum()), n_large=int((n > lim).sum()))
+                for name in ("sampled", "scanned", "bounded", "decoded"):
                     L[name] = torch.cuda.Event()
                     L[name].record(self.s_stream)  # torch creates the HIP event on first record
                 self.lanes.append(L)
@@ -154,19 +176,23 @@ class LanePipeline:
         L["plan"].decode(self._lane_view(enc, L), base=base, out=out, workspace=L["dws"], stream=stream,
                          sched=(wait or [None] * 3, record or [None] * 3, stages))
 
-    def _encode(self, flat, base, out, events, dense=None):
+    def _encode(self, flat, base, out, events, dense=None, free=False):
         S = self.s_stream
-        for i, L in enumerate(self.lanes):  # samples of lanes 1.. and every lane's small segments on C
-            if i and L["n_large"]:
+        for i, L in enumerate(self.lanes):  # samples of lanes 1.. (free: every lane) and the small segments on C
+            if free:
+                L["c"].wait_event(L["decoded"])  # the lane's previous decode read the idx / vals rewritten here
+            if (i or free) and L["n_large"]:
                 self._enc(L, flat, base, out, L["c"], _lib.COALAC_STAGE_SAMPLE,
                           record=[None, L["sampled"], None, None, None])
+            if free and L["n_small"]:
+                self._enc(L, flat, base, out, L["c"], _lib.COALAC_STAGE_SMALL)
         for L in self.lanes:
-            if L["n_small"]:
+            if L["n_small"] and not free:
                 self._enc(L, flat, base, out, L["c"], _lib.COALAC_STAGE_SMALL)
         for i, L in enumerate(self.lanes):  # the read phase: every k_scan back to back on S
             ev = events[i] if events is not None else [None] * 5
-            stages = _lib.COALAC_STAGE_SCAN | (_lib.COALAC_STAGE_SAMPLE if i == 0 else 0)
-            wait = [None, L["sampled"] if i and L["n_large"] else None, None, None, None]
+            stages = _lib.COALAC_STAGE_SCAN | (_lib.COALAC_STAGE_SAMPLE if i == 0 and not free else 0)
+            wait = [None, L["sampled"] if (i or free) and L["n_large"] else None, None, None, None]
             rec = [None, ev[1], ev[2] if ev[2] is not None else L["scanned"], None, None]
             self._enc(L, flat, base, out, S, stages, wait=wait, record=rec)
             L["token"] = rec[2]
@@ -175,7 +201,7 @@ class LanePipeline:
             if dense is not None:  # roundtrip: lane i's decode bounds right after its emit
                 self._dec(L, out, None, dense, L["c"], _lib.COALAC_STAGE_BOUNDS, record=[None, L["bounded"], None])
 
-    def _decode(self, enc, base, out, events, bounds_done=False):
+    def _decode(self, enc, base, out, events, bounds_done=False, free=False):
         S = self.s_stream
         if not bounds_done:
             for L in self.lanes:
@@ -184,6 +210,8 @@ class LanePipeline:
             ev = events[i] if events is not None else [None] * 3
             self._dec(L, enc, base, out, S, _lib.COALAC_STAGE_DECODE, wait=[None, L["bounded"], None],
                       record=[None, ev[1], ev[2]])
+            if free:
+                L["decoded"].record(S)
 
     def encode(self, flat, base=None, out=None, events=None):
         """Encode the whole batch (flat fp32[span]; base: delta mode) -> Encoded. events: optional
@@ -208,19 +236,29 @@ class LanePipeline:
         self._leave()
         return out
 
-    def roundtrip(self, flat, base=None, enc=None, out=None, enc_events=None, dec_events=None):
+    def roundtrip(self, flat, base=None, enc=None, out=None, enc_events=None, dec_events=None, joined=True):
         """encode() then decode() of the same batch with no join in between: lane i's decode depends on
         lane i's encode only (bounds_i follows select_i on C), so the last lanes' select chains run
-        under the first lanes' k_decode. Returns (Encoded, dense out)."""
+        under the first lanes' k_decode. Returns (Encoded, dense out).
+
+        joined=False (back-to-back calls on the same buffers, e.g. the bench): no entry / exit joins with
+        the caller's stream; every lane's sampler and small segments run on C once the lane's previous
+        decode is done (it read what they overwrite), i.e. under the previous call's later decodes, so S
+        runs scan_0 .. scan_{L-1} decode_0 .. decode_{L-1} back to back, call after call. The caller
+        orders its own use of the results (e.g. synchronises, or waits on `self.stream` and the C streams)."""
         enc = self.empty_encoded() if enc is None else enc
         if out is None:
             out = self.empty_flat() if base is None else torch.empty_like(base)
         if self.n_lanes == 1:
             return self._single_encode(flat, base, enc, enc_events), self._single_decode(enc, base, out, dec_events)
-        self._enter()
-        self._encode(flat, base, enc, enc_events, dense=out)
-        self._decode(enc, base, out, dec_events, bounds_done=True)
-        self._leave()
+        if joined:
+            self._enter()
+            self._encode(flat, base, enc, enc_events, dense=out)
+            self._decode(enc, base, out, dec_events, bounds_done=True)
+            self._leave()
+        else:
+            self._encode(flat, base, enc, enc_events, dense=out, free=True)
+            self._decode(enc, base, out, dec_events, bounds_done=True, free=True)
         return enc, out
 
     # one lane: the plain whole-encode / whole-decode calls on the caller's stream (a split would only
@@ -241,6 +279,18 @@ class LanePipeline:
         """Segments of the last encode whose sampled bracket missed (synchronises)."""
         torch.cuda.synchronize(self.device)
         return sum(L["plan"].fallbacks(L["ws"]) for L in self.lanes)
+
+    def timeouts(self):
+        """Bounded in-launch waits that gave up (one-launch / front-launch encodes only; the kernel
+        sequence has none)."""
+        if not self.flags & _IN_LAUNCH:
+            return 0
+        torch.cuda.synchronize(self.device)
+        return sum(L["plan"].timeouts(L["ws"]) for L in self.lanes)
+
+    @property
+    def n_parts(self):
+        return len(self.lanes)
 
     def close(self):
         for L in self.lanes:
@@ -264,7 +314,9 @@ class SplitPipeline:
     whole batch's buffers: results are bit-identical to a single plan's. (A plan over absolute segment
     rows, as LanePipeline uses, measured 2.5 % slower here.) Calls are asynchronous and ordered after /
     before the caller's current stream (the sub-batch streams wait for it on entry, it waits for them
-    on exit), unless joined=False.
+    on exit), unless joined=False. Sub-batch g runs on the process-wide pooled stream g
+    (pooled_streams): pipelines of one process share them, so their calls are ordered with each other
+    per sub-batch index.
     """
 
     def __init__(self, table: SegmentTable, bits=8, split=2, device=None, flags=0, fork=False):
@@ -284,20 +336,22 @@ class SplitPipeline:
             if S <= C:  # client ranges: ordinary plans over views of the batch buffers
                 cuts = balanced_cuts(table.client_elements(), S)
                 so, ko, to = table.client_span_off, table.client_k_off, table.client_seg_off
-                for c0, c1 in zip(cuts[:-1], cuts[1:]):
+                streams = pooled_streams(self.device, len(cuts) - 1)
+                for c0, c1, st in zip(cuts[:-1], cuts[1:], streams):
                     plan = CodecPlan(None, table.ratio, self.bits, device=self.device, table=table.sub_table(c0, c1))
                     self.parts.append(dict(x=slice(so[c0], so[c1]), k=slice(ko[c0], ko[c1]), t=slice(to[c0], to[c1]),
                                            plan=plan, ws=plan.empty_workspace(), dws=plan.empty_decode_workspace(),
-                                           stream=torch.cuda.Stream(self.device)))
+                                           stream=st))
             else:
                 # fewer clients than sub-batches (e.g. ONE update): contiguous SEGMENT ranges balanced by
                 # element count, each a plan over absolute segment rows that reads / writes the whole
                 # buffers in place (its own segments only) — the ranges' latency-bound phases overlap
-                for s0, s1 in split_lanes(table.segs[:, 1].tolist(), S):
+                ranges = split_lanes(table.segs[:, 1].tolist(), S)
+                for (s0, s1), st in zip(ranges, pooled_streams(self.device, len(ranges))):
                     plan = CodecPlan.from_segments(table.segs[s0:s1], self.bits, device=self.device)
                     self.parts.append(dict(x=slice(None), k=slice(None), t=slice(s0, s1), plan=plan,
                                            ws=plan.empty_workspace(), dws=plan.empty_decode_workspace(),
-                                           stream=torch.cuda.Stream(self.device)))
+                                           stream=st))
 
     @property
     def n_parts(self):
@@ -379,6 +433,9 @@ class SplitPipeline:
         return sum(P["plan"].fallbacks(P["ws"]) for P in self.parts)
 
     def timeouts(self):
+        """Bounded in-launch waits that gave up (one-launch / front-launch encodes only)."""
+        if not self.flags & _IN_LAUNCH:
+            return 0
         torch.cuda.synchronize(self.device)
         return sum(P["plan"].timeouts(P["ws"]) for P in self.parts)
 

@@ -282,8 +282,9 @@ class CodecPlan:
         return out  # w was allocated on the launch stream: its memory is reused only after the kernel
 
     def timeouts(self, workspace, stream=None):
-        """1 if a bounded in-launch wait of the last one-launch encode with this workspace gave up (its
-        results are then invalid; never expected), else 0 (synchronises)."""
+        """1 if a bounded in-launch wait of the last one-launch / front-launch encode with this workspace
+        gave up (its results are then invalid; never expected), else 0 (synchronises). Meaningless after a
+        kernel-sequence encode (nothing zeroes or sets the word then)."""
         c = ctypes.c_int()
         with torch.cuda.device(self.device):
             _lib.check(self._lib.coalac_workspace_timeouts(self._h, _ptr(workspace), _stream_handle(stream),

@@ -64,6 +64,11 @@ constexpr uint32_t UNIT = 4096;           // elements per wave work unit
 constexpr uint32_t UNIT_SHIFT = 12;
 constexpr uint32_t UNIT_IT = UNIT / 256;  // float4 loads per lane per unit
 constexpr uint32_t SMALL_MAX = 4096;      // segments up to this size are encoded whole in one block
+constexpr uint32_t SMALL_MAX_LATENCY = 1024;  // ... in latency-bound plans (<= LATENCY_PLAN_UNITS units): a
+                                              // block's radix select grows with n (64: 5 us, 2048: 9 us,
+                                              // 4096: 14 us, alone on a CU) and the slowest small segment set
+                                              // the length of k_presel; bigger segments take the sampled path
+constexpr uint32_t LATENCY_PLAN_UNITS = 8192;  // ~1.3 ResNet-50 updates
 constexpr uint32_t SAMPLE_MAX = 8192;     // sampled keys per large segment
 constexpr int SEL_NT = 256;               // threads of a k_select block (4 waves: one per SIMD, so a
                                           // block finds room beside a streaming kernel's waves)
@@ -751,6 +756,7 @@ DEV void small_encode(const Params& P, uint32_t s, float* vals, uint32_t* hist, 
   const float* xs = seg_in(P, s, sd.in_off);
   const float* bs = DELTA ? P.base + sd.in_off : xs;
   const uint32_t n = sd.n, k = sd.k;
+  STAMP(P, s, 2);  // (slots 2-7: small segments; k_select uses 0, 1, 10-12 of the large segments' rows)
   if (n == 0) {
     if (t == 0) {
       P.mn[s] = 0.0f;
@@ -770,12 +776,14 @@ DEV void small_encode(const Params& P, uint32_t s, float* vals, uint32_t* hist, 
     }
   }
   __syncthreads();
+  STAMP(P, s, 3);
   uint32_t rt = k;
   const uint32_t T = block_select<NT>(
       [&](auto&& f) {
         for (uint32_t i = t; i < n; i += NT) f(fkey(vals[i]));
       },
       0u, KEY_MAX, rt, hist, sh);
+  STAMP(P, s, 4);
 
   // ordered ownership: thread t owns the contiguous range [b0, b1); the first rt ties are kept
   const uint32_t E = (n + NT - 1) / NT;
@@ -791,6 +799,7 @@ DEV void small_encode(const Params& P, uint32_t s, float* vals, uint32_t* hist, 
   const uint32_t quota = eqpre >= rt ? 0u : min(eq, rt - eqpre);
   uint32_t seltot;
   const uint32_t opre = block_excl_scan<NT>(gt + quota, sh, seltot);
+  STAMP(P, s, 5);
 
   float mn = 0.0f, scale = 0.0f;
   if (!RAW) {
@@ -811,6 +820,7 @@ DEV void small_encode(const Params& P, uint32_t s, float* vals, uint32_t* hist, 
     mn = a;
     scale = (b == a) ? 0.0f : (b - a) / P.levels;
   }
+  STAMP(P, s, 6);
   if (t == 0) {
     P.mn[s] = mn;
     P.scale[s] = scale;
@@ -827,6 +837,7 @@ DEV void small_encode(const Params& P, uint32_t s, float* vals, uint32_t* hist, 
       ++o;
     }
   }
+  STAMP(P, s, 7);
 }
 
 template <bool DELTA, bool RAW>
@@ -856,7 +867,7 @@ DEV void sample_segment(const Params& P, uint32_t li, uint32_t* hist, uint32_t* 
   R &= ~63u;
   const uint32_t m = R * 16;
   const uint32_t nit = R / 64;
-  const uint32_t stride = n / R;  // >= 16 because n > SMALL_MAX >= 1024
+  const uint32_t stride = n / R;  // >= 16 because n > small_max >= 1024
   const uint32_t room = stride - 16;
   // The sampled keys stay in registers (4 per batch per thread): all loads in flight at once, and with
   // 8 KB of LDS per block (histogram only) twice as many sample blocks fit a CU as with an LDS key copy.
@@ -1653,6 +1664,9 @@ __global__ __launch_bounds__(SEL_NT) void k_select(Params P) {
 #ifndef EMIT_UPW
 #define EMIT_UPW 8u  // large units per k_emit wave
 #endif
+#ifndef EMIT_ROWS
+#define EMIT_ROWS 1  // 64-record rows of every unit loaded before the first is classified (1 or 2)
+#endif
 
 DEV uint32_t rl(uint32_t v, uint32_t l) { return (uint32_t)__builtin_amdgcn_readlane((int)v, (int)l); }
 
@@ -1722,11 +1736,16 @@ DEV void emit_units(const Params& P, uint32_t lu0, uint32_t lu1) {
   const uint32_t Tg = P.tstar[segg], rtg = P.rtie[segg];
   const float mng = RAW ? 0.0f : P.mn[segg];
   const float scg = RAW ? 0.0f : P.scale[segg];
-  uint2 rec0[EMIT_UPW];
+  // every unit's first 2 x 64 records in flight before the first is classified (at ~1.5 % candidates a
+  // unit holds ~60 records, so about half of the units need the second row: loading it inside the unit
+  // loop made it one dependent round per unit, 8 in a row)
+  uint2 rec0[EMIT_UPW], rec1[EMIT_UPW];
 #pragma unroll
   for (uint32_t g = 0; g < EMIT_UPW; ++g) {
     const uint32_t lu = min(lu0 + g, lu1 - 1), nC = rl(nCg, g);
-    rec0[g] = P.cand[(uint64_t)lu * P.ccap + min(lane, nC ? nC - 1 : 0u)];  // unconditional (clamped) load
+    const uint32_t last = nC ? nC - 1 : 0u;
+    rec0[g] = P.cand[(uint64_t)lu * P.ccap + min(lane, last)];  // unconditional (clamped) loads
+    if (EMIT_ROWS > 1) rec1[g] = P.cand[(uint64_t)lu * P.ccap + min(lane + 64, last)];
   }
 #pragma unroll
   for (uint32_t g = 0; g < EMIT_UPW; ++g) {
@@ -1747,7 +1766,7 @@ DEV void emit_units(const Params& P, uint32_t lu0, uint32_t lu1) {
       for (uint32_t i0 = 0; i0 < nC; i0 += 64) {
         const uint32_t i = i0 + lane;
         const bool valid = i < nC;
-        const uint2 rec = i0 == 0 ? rec0[g] : R[min(i, nC - 1)];
+        const uint2 rec = i0 == 0 ? rec0[g] : (EMIT_ROWS > 1 && i0 == 64) ? rec1[g] : R[min(i, nC - 1)];
         const float x = __uint_as_float(rec.y);
         const uint32_t key = fkey(x);
         const bool e = valid && key == T;
@@ -1772,7 +1791,10 @@ __global__ __launch_bounds__(BLOCK) void k_emit(Params P) {
   const uint32_t wv = threadIdx.x >> 6;
   const uint32_t lu0 = (blockIdx.x * WAVES + wv) * EMIT_UPW;
   if (lu0 >= P.n_lunits) return;
+  const bool st = blockIdx.x < P.nseg;  // diagnostics rows: block index (slots 13-14)
+  if (st) STAMP(P, blockIdx.x, 13);
   emit_units<DELTA, RAW>(P, lu0, min(lu0 + EMIT_UPW, P.n_lunits));
+  if (st) STAMP(P, blockIdx.x, 14);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -2678,6 +2700,10 @@ int coalac_plan_create(const coalac_seg_t* h_segs, int nseg, int bits, coalac_pl
   std::vector<BChunk> bchunks;
   uint64_t span = 0, total_k = 0;
   std::vector<std::pair<uint64_t, uint64_t>> in_r, out_r;
+  uint64_t est_units = 0;
+  for (int s = 0; s < nseg; ++s) est_units += (std::min<uint64_t>(h_segs[s].n, 1ull << 31) + UNIT - 1) / UNIT;
+  uint32_t small_max = est_units <= LATENCY_PLAN_UNITS ? SMALL_MAX_LATENCY : SMALL_MAX;
+  if (const char* e = getenv("COALAC_SMALL_MAX")) small_max = std::min<uint32_t>(std::max(atoi(e), 1024), SMALL_MAX);
   for (int s = 0; s < nseg; ++s) {
     const coalac_seg_t& g = h_segs[s];
     if (g.n >= (1ull << 31)) return fail(COALAC_EINVAL, "segment %d: n=%llu >= 2^31", s, (unsigned long long)g.n);
@@ -2693,7 +2719,7 @@ int coalac_plan_create(const coalac_seg_t* h_segs, int nseg, int bits, coalac_pl
     d.n = (uint32_t)g.n;
     d.k = (uint32_t)g.k;
     d.unit_begin = (uint32_t)units.size();
-    const bool large = g.n > SMALL_MAX;
+    const bool large = g.n > small_max;
     d.lu_begin = large ? (uint32_t)lunits.size() : 0u;
     for (uint64_t st = 0; st < g.n; st += UNIT) {
       UnitDev u{};

@@ -196,8 +196,9 @@ int coalac_aggregate_ev(coalac_plan_t plan, int clients, const int32_t* d_idx, c
  * the last encode that used workspace d_ws (synchronises `stream`). */
 int coalac_workspace_fallbacks(coalac_plan_t plan, const void* d_ws, void* stream, int* out);
 
-/* Diagnostics: 1 if a bounded in-launch wait of the last one-launch encode with d_ws gave up (its results
- * are then not valid; never expected), else 0 (synchronises `stream`). */
+/* Diagnostics: 1 if a bounded in-launch wait of the last one-launch / front-launch encode with d_ws gave up
+ * (its results are then not valid; never expected), else 0 (synchronises `stream`). Only those encodes
+ * zero and set the word: after a kernel-sequence encode it holds whatever the workspace held. */
 int coalac_workspace_timeouts(coalac_plan_t plan, const void* d_ws, void* stream, int* out);
 
 /* Diagnostics: the k_fused work items (role << 28 | index, launch order) and, after a

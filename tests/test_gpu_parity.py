@@ -11,7 +11,7 @@ import torch
 
 from coala_amd.compression import CodecPlan, SegmentTable
 from coala_amd.compression._lib import COALAC_FLAG_FORCE_EXACT, COALAC_FLAG_GENERIC_SELECT
-from coala_amd.compression.spec import SMALL_MAX
+from coala_amd.compression.spec import SMALL_MAX, SMALL_MAX_LATENCY, small_limit
 from coala_amd.layouts import fp32_sizes
 from coala_amd.workload import synth_batch
 from oracle import codec_oracle as O
@@ -75,6 +75,9 @@ def edge_segments(rng):
     segs.append(np.zeros(SMALL_MAX, np.float32))                                # all zero, SMALL_MAX
     x = rng.standard_normal(SMALL_MAX + 1).astype(np.float32)                   # smallest large segment
     segs.append(x)
+    segs.append(rng.standard_normal(SMALL_MAX_LATENCY).astype(np.float32))      # largest small, latency plans
+    x = np.round(rng.standard_normal(SMALL_MAX_LATENCY + 1) * 2).astype(np.float32)  # smallest large there, ties
+    segs.append(x)
     x = np.round(rng.standard_normal(50000) * 4).astype(np.float32) / 4         # heavy ties, large
     segs.append(x)
     segs.append(np.zeros(20000, np.float32))                                    # all-zero large
@@ -84,10 +87,15 @@ def edge_segments(rng):
     return segs
 
 
+@pytest.mark.parametrize("small_max", [None, SMALL_MAX])
 @pytest.mark.parametrize("flags", [0, COALAC_FLAG_GENERIC_SELECT])
 @pytest.mark.parametrize("bits", [8, 4, 1, 32])
 @pytest.mark.parametrize("ratio", [0.001, 0.01, 0.1, 0.5, 1.0])
-def test_edge_cases(cuda, bits, ratio, flags):
+def test_edge_cases(cuda, bits, ratio, flags, small_max, monkeypatch):
+    """small_max None: the plan's own threshold (latency plan: segments of 1025..4096 elements take the
+    sampled path); SMALL_MAX: forced, so those segments are encoded whole in one block."""
+    if small_max is not None:
+        monkeypatch.setenv("COALAC_SMALL_MAX", str(small_max))
     rng = np.random.default_rng(7)
     segs = edge_segments(rng)
     plan, g, r = run_both([s.size for s in segs], ratio, bits, [segs], flags=flags)
@@ -104,7 +112,7 @@ def test_random_layout_resnet18(cuda, flags, delta):
     plan, g, r = run_both(sizes, 0.01, 8, xs, bases, flags)
     assert_same(plan, g, r)
     if flags == COALAC_FLAG_FORCE_EXACT:
-        assert g["fallbacks"] == plan.table.n_segments - sum(1 for s in sizes if s <= SMALL_MAX)
+        assert g["fallbacks"] == plan.table.n_segments - sum(1 for s in sizes if s <= small_limit(sizes))
 
 
 @pytest.mark.parametrize("ratio", [0.001, 0.01, 0.1])

@@ -110,6 +110,32 @@ def test_split_pipeline_resnet18_x3(cuda, split, delta, fused):
     assert pipe.fallbacks() == 0
 
 
+@pytest.mark.parametrize("lanes", [2, 3])
+def test_lane_pipeline_unjoined_alternating_inputs(cuda, lanes):
+    """LanePipeline.roundtrip(joined=False) back to back with TWO alternating inputs through one shared
+    Encoded and two dense outputs: a step's samplers / small segments (on C) overwrite idx / vals the
+    previous step's decodes (on S) read, so a missing 'decoded' dependency would mix the two inputs."""
+    t = SegmentTable(fp32_sizes("resnet50_tv"), 0.01, 4)
+    flats = [synth_batch(t, cuda, client_ids=range(4)), synth_batch(t, cuda, client_ids=range(10, 14))]
+    pipe = LanePipeline(t, 8, lanes=lanes, device=cuda)
+    enc = pipe.empty_encoded()
+    outs = [pipe.empty_flat().zero_(), pipe.empty_flat().zero_()]
+    torch.cuda.synchronize()
+    for i in range(6):
+        pipe.roundtrip(flats[i % 2], enc=enc, out=outs[i % 2], joined=False)
+    torch.cuda.synchronize()
+    assert pipe.timeouts() == 0
+    plan = CodecPlan(fp32_sizes("resnet50_tv"), 0.01, 8, clients=4, device=cuda)
+    for j in range(2):
+        e = plan.encode(flats[j])
+        d = plan.decode(e, out=torch.zeros_like(outs[j]))
+        torch.cuda.synchronize()
+        assert torch.equal(d.view(torch.int32), outs[j].view(torch.int32)), j
+    e1 = plan.encode(flats[1])  # the last step encoded flats[1]
+    torch.cuda.synchronize()
+    assert torch.equal(e1.idx, enc.idx) and torch.equal(e1.vals, enc.vals)
+
+
 def test_split_pipeline_unjoined_steps_match_single_plan(cuda):
     """The bench's schedule: 6 back-to-back unjoined roundtrips of 16 ResNet-50 updates as 2 x 8 (plus
     the batch's small segments forked per sub-plan) equal one plan over the whole batch, bit for bit."""

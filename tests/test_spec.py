@@ -62,6 +62,8 @@ def test_build_module_layout_order():
 def test_constants_mirror_kernel():
     src = open(__import__("coala_amd._build", fromlist=["SRC"]).SRC).read()
     assert f"constexpr uint32_t SMALL_MAX = {spec.SMALL_MAX};" in src
+    assert f"constexpr uint32_t SMALL_MAX_LATENCY = {spec.SMALL_MAX_LATENCY};" in src
+    assert f"constexpr uint32_t LATENCY_PLAN_UNITS = {spec.LATENCY_PLAN_UNITS};" in src
     assert f"constexpr uint32_t UNIT = {spec.UNIT};" in src
 
 
