@@ -81,6 +81,12 @@ constexpr int SEL_NT = 256;               // threads of a k_select block (4 wave
 #ifndef SCAN_NB
 #define SCAN_NB 1  // load batches per k_scan unit (weights mode): 1 = all 16 float4 per lane in flight
 #endif
+#ifndef LOAD_AUX
+#define LOAD_AUX 2   // cache policy of the streaming buffer loads (k_scan): 2 = non-temporal
+#endif
+#ifndef STORE_AUX
+#define STORE_AUX 2  // cache policy of the streaming buffer stores (k_decode): 2 = non-temporal
+#endif
 constexpr uint32_t STAGE_CAP = 512;       // candidate records staged in LDS per k_scan wave
 constexpr uint32_t GU = 32;               // units per select group (k_ghist / k_gwin block)
 constexpr uint32_t HB2 = 512;             // bins of the per-group band histograms
@@ -495,10 +501,10 @@ DEV __amdgpu_buffer_rsrc_t unit_rsrc(const float* p, uint32_t n) {
 template <bool DELTA>
 DEV float4 unit_load_x4(__amdgpu_buffer_rsrc_t rin, __amdgpu_buffer_rsrc_t rbase, uint32_t boff) {
   typedef unsigned int u4v __attribute__((ext_vector_type(4)));
-  const u4v a = __builtin_amdgcn_raw_buffer_load_b128(rin, (int)boff, 0, 2);
+  const u4v a = __builtin_amdgcn_raw_buffer_load_b128(rin, (int)boff, 0, LOAD_AUX);
   float4 v = make_float4(__uint_as_float(a.x), __uint_as_float(a.y), __uint_as_float(a.z), __uint_as_float(a.w));
   if (DELTA) {
-    const u4v b = __builtin_amdgcn_raw_buffer_load_b128(rbase, (int)boff, 0, 2);
+    const u4v b = __builtin_amdgcn_raw_buffer_load_b128(rbase, (int)boff, 0, LOAD_AUX);
     v.x = v.x - __uint_as_float(b.x);
     v.y = v.y - __uint_as_float(b.y);
     v.z = v.z - __uint_as_float(b.z);
@@ -508,18 +514,20 @@ DEV float4 unit_load_x4(__amdgpu_buffer_rsrc_t rin, __amdgpu_buffer_rsrc_t rbase
 }
 
 // non-temporal 16-byte buffer store (dropped when it lies past the resource's range)
+template <int AUX = STORE_AUX>
 DEV void unit_store_x4(__amdgpu_buffer_rsrc_t r, uint32_t boff, float4 v) {
   typedef unsigned int u4v __attribute__((ext_vector_type(4)));
   const u4v a = {__float_as_uint(v.x), __float_as_uint(v.y), __float_as_uint(v.z), __float_as_uint(v.w)};
-  __builtin_amdgcn_raw_buffer_store_b128(a, r, (int)boff, 0, 2);
+  __builtin_amdgcn_raw_buffer_store_b128(a, r, (int)boff, 0, AUX);
 }
 
 // the same 16 bytes as four dword stores: the range check drops exactly the dwords past the end
+template <int AUX = STORE_AUX>
 DEV void unit_store_x1x4(__amdgpu_buffer_rsrc_t r, uint32_t boff, float4 v) {
-  __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v.x), r, (int)boff, 0, 2);
-  __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v.y), r, (int)boff + 4, 0, 2);
-  __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v.z), r, (int)boff + 8, 0, 2);
-  __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v.w), r, (int)boff + 12, 0, 2);
+  __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v.x), r, (int)boff, 0, AUX);
+  __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v.y), r, (int)boff + 4, 0, AUX);
+  __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v.z), r, (int)boff + 8, 0, AUX);
+  __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v.w), r, (int)boff + 12, 0, AUX);
 }
 
 // non-temporal (read-once) 16-byte load of x (or x - base)
@@ -1662,8 +1670,11 @@ __global__ __launch_bounds__(SEL_NT) void k_select(Params P) {
 // unit's first 64 records are in flight before the first one is classified.
 // ------------------------------------------------------------------------------------------------
 #ifndef EMIT_UPW
-#define EMIT_UPW 8u  // large units per k_emit wave
+#define EMIT_UPW 8u  // large units per k_emit wave in batches (C3 share: +2 % over 2 units per wave)
 #endif
+// ... in latency-bound plans (<= LATENCY_PLAN_UNITS units): a wave's units are handled one after the other,
+// so fewer per wave shortens the launch (one ResNet-50 update: 8 per wave 13.1 us, 2 per wave 6.0 us)
+constexpr uint32_t EMIT_UPW_LATENCY = 2;
 #ifndef EMIT_ROWS
 #define EMIT_ROWS 1  // 64-record rows of every unit loaded before the first is classified (1 or 2)
 #endif
@@ -1721,13 +1732,13 @@ DEV void emit_raw_unit(const Params& P, const UnitDev& L, uint32_t T, uint32_t r
   });
 }
 
-// one wave emits the large units [lu0, lu1) (lu1 - lu0 <= EMIT_UPW)
-template <bool DELTA, bool RAW>
+// one wave emits the large units [lu0, lu1) (lu1 - lu0 <= UPW)
+template <bool DELTA, bool RAW, uint32_t UPW = EMIT_UPW>
 DEV void emit_units(const Params& P, uint32_t lu0, uint32_t lu1) {
   const uint32_t lane = lane_id();
-  // round 1 / 2: lane g < EMIT_UPW holds unit lu0 + g's count, offsets and its segment's T*, tie budget,
-  // mn, scale (lanes past EMIT_UPW or past the last unit repeat a valid unit; never used)
-  const uint32_t lug = min(lu0 + min(lane, EMIT_UPW - 1), lu1 - 1);
+  // round 1 / 2: lane g < UPW holds unit lu0 + g's count, offsets and its segment's T*, tie budget,
+  // mn, scale (lanes past UPW or past the last unit repeat a valid unit; never used)
+  const uint32_t lug = min(lu0 + min(lane, UPW - 1), lu1 - 1);
   const uint32_t nCg = min(P.cntC[lug], P.ccap);  // stored records (a raw-path unit may have dropped some)
   const uint32_t segg = P.lunits[lug].seg;
   const uint32_t stg = P.status[segg];             // != 0: the segment took the raw-data path
@@ -1739,16 +1750,16 @@ DEV void emit_units(const Params& P, uint32_t lu0, uint32_t lu1) {
   // every unit's first 2 x 64 records in flight before the first is classified (at ~1.5 % candidates a
   // unit holds ~60 records, so about half of the units need the second row: loading it inside the unit
   // loop made it one dependent round per unit, 8 in a row)
-  uint2 rec0[EMIT_UPW], rec1[EMIT_UPW];
+  uint2 rec0[UPW], rec1[UPW];
 #pragma unroll
-  for (uint32_t g = 0; g < EMIT_UPW; ++g) {
+  for (uint32_t g = 0; g < UPW; ++g) {
     const uint32_t lu = min(lu0 + g, lu1 - 1), nC = rl(nCg, g);
     const uint32_t last = nC ? nC - 1 : 0u;
     rec0[g] = P.cand[(uint64_t)lu * P.ccap + min(lane, last)];  // unconditional (clamped) loads
     if (EMIT_ROWS > 1) rec1[g] = P.cand[(uint64_t)lu * P.ccap + min(lane + 64, last)];
   }
 #pragma unroll
-  for (uint32_t g = 0; g < EMIT_UPW; ++g) {
+  for (uint32_t g = 0; g < UPW; ++g) {
     const uint32_t nC = rl(nCg, g);
     if (lu0 + g < lu1 && rl(stg, g) != 0) {
       const uint64_t so = ((uint64_t)rl((uint32_t)(sog >> 32), g) << 32) | rl((uint32_t)sog, g);
@@ -1786,14 +1797,14 @@ DEV void emit_units(const Params& P, uint32_t lu0, uint32_t lu1) {
   }
 }
 
-template <bool DELTA, bool RAW>
+template <bool DELTA, bool RAW, uint32_t UPW>
 __global__ __launch_bounds__(BLOCK) void k_emit(Params P) {
   const uint32_t wv = threadIdx.x >> 6;
-  const uint32_t lu0 = (blockIdx.x * WAVES + wv) * EMIT_UPW;
+  const uint32_t lu0 = (blockIdx.x * WAVES + wv) * UPW;
   if (lu0 >= P.n_lunits) return;
   const bool st = blockIdx.x < P.nseg;  // diagnostics rows: block index (slots 13-14)
   if (st) STAMP(P, blockIdx.x, 13);
-  emit_units<DELTA, RAW>(P, lu0, min(lu0 + EMIT_UPW, P.n_lunits));
+  emit_units<DELTA, RAW, UPW>(P, lu0, min(lu0 + UPW, P.n_lunits));
   if (st) STAMP(P, blockIdx.x, 14);
 }
 
@@ -2013,16 +2024,20 @@ DEV void wave_lower_bound(const int32_t* const (&L)[M], const uint32_t (&k)[M], 
   for (int m = 0; m < M; ++m) res[m] = a[m];
 }
 
-// units per wave of k_decode: 1 with a base (its 16 float4 of base per unit would double the registers)
-template <bool HASBASE>
-constexpr uint32_t decode_dpw() { return HASBASE ? 1u : 2u; }
+// units per wave of k_decode: 1 with a base (its 16 float4 of base per unit would double the registers) or
+// in the in-kernel search variant (latency-bound plans: twice the waves, each with half the serial merge)
+#ifndef DECODE_SEARCH_DPW
+#define DECODE_SEARCH_DPW 1u
+#endif
+template <bool HASBASE, bool SEARCH>
+constexpr uint32_t decode_dpw() { return HASBASE ? 1u : SEARCH ? DECODE_SEARCH_DPW : 2u; }
 
 // SEARCH: the units' entry ranges are found in-kernel (wave_lower_bound) instead of read from k_bounds'
 // ustart: one launch less, three more dependent load rounds per wave — worth it when the plan is small
 // and latency-bound (one update), not for a batch (the rounds then cost write-stream slots).
 template <bool RAW, bool HASBASE, bool SEARCH>
 __global__ __launch_bounds__(BLOCK, DECODE_WPE) void k_decode(Params P) {
-  constexpr uint32_t DPW = decode_dpw<HASBASE>();
+  constexpr uint32_t DPW = decode_dpw<HASBASE, SEARCH>();
   const uint32_t lane = lane_id(), wv = threadIdx.x >> 6;
   const uint32_t u0 = (blockIdx.x * WAVES + wv) * DPW;
   if (u0 >= P.n_units) return;
@@ -2104,12 +2119,15 @@ __global__ __launch_bounds__(BLOCK, DECODE_WPE) void k_decode(Params P) {
         b[it].w = a.w + ((m & 8u) ? b[it].w : 0.0f);
       }
     }
-    if ((len & 3u) == 0) {  // wave-uniform: one non-temporal float4 buffer store per slot
+    // non-temporal stores for batches; a latency-bound plan's output (~100 MB) stores plainly (measured
+    // 33.8 -> 30.8 us on one ResNet-50 update; a batch streams 15 % slower that way)
+    constexpr int SAUX = SEARCH ? 0 : STORE_AUX;
+    if ((len & 3u) == 0) {  // wave-uniform: one float4 buffer store per slot
 #pragma unroll
-      for (uint32_t it = 0; it < UNIT_IT; ++it) unit_store_x4(rout, (it * 64 + lane) * 16, b[it]);
+      for (uint32_t it = 0; it < UNIT_IT; ++it) unit_store_x4<SAUX>(rout, (it * 64 + lane) * 16, b[it]);
     } else {  // a segment's last unit with n % 4 != 0: dword stores (range-checked per dword)
 #pragma unroll
-      for (uint32_t it = 0; it < UNIT_IT; ++it) unit_store_x1x4(rout, (it * 64 + lane) * 16, b[it]);
+      for (uint32_t it = 0; it < UNIT_IT; ++it) unit_store_x1x4<SAUX>(rout, (it * 64 + lane) * 16, b[it]);
     }
   }
 }
@@ -2576,6 +2594,17 @@ constexpr int ENC_SPAN[4][2] = {{0, 1}, {1, 2}, {2, 4}, {0, 1}};  // SAMPLE, SCA
 constexpr int DEC_SPAN[2][2] = {{0, 1}, {1, 2}};                  // BOUNDS, DECODE
 
 template <bool DELTA, bool RAW>
+void launch_emit(const Params& P, coalac_plan_t plan, hipStream_t st) {
+  if (plan->n_lunits <= LATENCY_PLAN_UNITS) {
+    constexpr uint32_t U = EMIT_UPW_LATENCY * WAVES;
+    hipLaunchKernelGGL((k_emit<DELTA, RAW, EMIT_UPW_LATENCY>), dim3((plan->n_lunits + U - 1) / U), dim3(BLOCK), 0, st, P);
+  } else {
+    constexpr uint32_t U = EMIT_UPW * WAVES;
+    hipLaunchKernelGGL((k_emit<DELTA, RAW, EMIT_UPW>), dim3((plan->n_lunits + U - 1) / U), dim3(BLOCK), 0, st, P);
+  }
+}
+
+template <bool DELTA, bool RAW>
 int launch_encode(const Params& P, coalac_plan_t plan, hipStream_t st, const coalac_sched_t* sc) {
   const uint32_t gu = (plan->n_lunits + WAVES - 1) / WAVES;
   const unsigned all = COALAC_STAGE_SAMPLE | COALAC_STAGE_SCAN | COALAC_STAGE_SELECT | COALAC_STAGE_SMALL;
@@ -2628,7 +2657,7 @@ int launch_encode(const Params& P, coalac_plan_t plan, hipStream_t st, const coa
     hipLaunchKernelGGL((k_select<DELTA, RAW>), dim3(plan->n_large), dim3(SEL_NT), 0, st, P);
   }
   ENC_BOUNDARY(3);
-  if ((stages & COALAC_STAGE_SELECT) && plan->n_large) hipLaunchKernelGGL((k_emit<DELTA, RAW>), dim3((plan->n_lunits + WAVES * EMIT_UPW - 1) / (WAVES * EMIT_UPW)), dim3(BLOCK), 0, st, P);
+  if ((stages & COALAC_STAGE_SELECT) && plan->n_large) launch_emit<DELTA, RAW>(P, plan, st);
   if (fork) HIP_CHECK(hipStreamWaitEvent(st, plan->join, 0));
   ENC_BOUNDARY(4);
 #undef ENC_BOUNDARY
@@ -2673,8 +2702,7 @@ int launch_front(const Params& P, coalac_plan_t plan, hipStream_t st, const coal
   }
   BOUNDARY(3);
   if (plan->n_large)
-    hipLaunchKernelGGL((k_emit<DELTA, RAW>), dim3((plan->n_lunits + WAVES * EMIT_UPW - 1) / (WAVES * EMIT_UPW)), dim3(BLOCK), 0,
-                       st, P);
+    launch_emit<DELTA, RAW>(P, plan, st);
   BOUNDARY(4);
   return COALAC_OK;
 }
@@ -3033,7 +3061,10 @@ int coalac_decode_sched(coalac_plan_t plan, const int32_t* d_idx, const void* d_
   P.ustart = static_cast<const uint32_t*>(d_ws);
   hipStream_t st = static_cast<hipStream_t>(stream);
   const bool raw = plan->bits == 32, hb = d_base != nullptr;
-  const uint32_t upb = WAVES * (hb ? decode_dpw<true>() : decode_dpw<false>());  // units per block
+  // small plans: k_decode finds its units' entry ranges itself (one launch); batches: k_bounds first
+  const bool search = plan->n_units <= DECODE_SEARCH_MAX_UNITS;
+  const uint32_t upb = WAVES * (hb ? decode_dpw<true, false>()
+                                   : search ? decode_dpw<false, true>() : decode_dpw<false, false>());  // units per block
   const uint32_t g = (plan->n_units + upb - 1) / upb;
   const coalac_sched_t* sc = sched;
   auto B = [&](int i) { return at_boundary(stages, DEC_SPAN, 2, i) ? boundary(sc, i, st) : COALAC_OK; };
@@ -3042,8 +3073,6 @@ int coalac_decode_sched(coalac_plan_t plan, const int32_t* d_idx, const void* d_
     const int rc_ = B(i);     \
     if (rc_) return rc_;      \
   } while (0)
-  // small plans: k_decode finds its units' entry ranges itself (one launch); batches: k_bounds first
-  const bool search = plan->n_units <= DECODE_SEARCH_MAX_UNITS;
   DEC_BOUNDARY(0);
   if ((stages & COALAC_STAGE_BOUNDS) && plan->n_bchunks && !search)
     hipLaunchKernelGGL(k_bounds, dim3(plan->n_bchunks), dim3(BLOCK), 0, st, P, plan->bchunks,

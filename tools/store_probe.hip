@@ -1,0 +1,122 @@
+// Write-bandwidth probe for k_decode's store pattern (tools/store_probe <MiB> ...): for each buffer size,
+// the time of one launch writing it, per store flavour:
+//   unit_g    one wave per 16 KiB unit, 16 float4 global stores per lane (stride 1 KiB), plain
+//   unit_gnt  the same, non-temporal (__builtin_nontemporal_store)
+//   unit_b    buffer stores through a per-unit resource (k_decode's form), cache policy 0
+//   unit_bnt  the same, policy 2 (non-temporal: k_decode's default)
+//   flat1     one float4 per thread, grid = n/4/256 blocks (elementwise style)
+//   gs        grid-stride float4 loop, 8 blocks per CU
+// Prints TB/s of bytes written (launch time from hipEvents, mean of 20).
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstdlib>
+
+#define CK(x)                                                                   \
+  do {                                                                          \
+    hipError_t e_ = (x);                                                        \
+    if (e_ != hipSuccess) {                                                     \
+      fprintf(stderr, "%s:%d %s\n", __FILE__, __LINE__, hipGetErrorString(e_)); \
+      exit(1);                                                                  \
+    }                                                                           \
+  } while (0)
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(void* p, uint32_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(p, (short)0, (int)bytes, 0x00020000);
+}
+
+template <int MODE>
+__global__ __launch_bounds__(256) void unit_store(float4* __restrict__ out, size_t n4, float v) {
+  const size_t w = (size_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const unsigned lane = threadIdx.x & 63;
+  const size_t base = w * 1024;
+  if (base >= n4) return;
+  const float4 z = make_float4(v, v, v, v);
+  if (MODE == 0) {
+#pragma unroll
+    for (int i = 0; i < 16; ++i) out[base + i * 64 + lane] = z;
+  } else if (MODE == 1) {
+    typedef float f4v __attribute__((ext_vector_type(4)));
+    const f4v zz = {v, v, v, v};
+#pragma unroll
+    for (int i = 0; i < 16; ++i) __builtin_nontemporal_store(zz, reinterpret_cast<f4v*>(out + base + i * 64 + lane));
+  } else {
+    const __amdgpu_buffer_rsrc_t r = rsrc(out + base, 16384);
+    typedef unsigned int u4v __attribute__((ext_vector_type(4)));
+    const u4v a = {__float_as_uint(v), __float_as_uint(v), __float_as_uint(v), __float_as_uint(v)};
+#pragma unroll
+    for (int i = 0; i < 16; ++i)
+      __builtin_amdgcn_raw_buffer_store_b128(a, r, (int)((i * 64 + lane) * 16), 0, MODE == 2 ? 0 : 2);
+  }
+}
+
+// N float4 per lane per wave (a wave writes N KiB, strided rows), plain global stores
+template <int N>
+__global__ __launch_bounds__(256) void unit_n(float4* __restrict__ out, size_t n4, float v) {
+  const size_t w = (size_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const unsigned lane = threadIdx.x & 63;
+  const size_t base = w * 64 * N;
+  if (base >= n4) return;
+#pragma unroll
+  for (int i = 0; i < N; ++i) out[base + i * 64 + lane] = make_float4(v, v, v, v);
+}
+
+// a block owns 4 consecutive 16 KiB units; at step j its wave w writes row 4j + w of the 64 KiB (the
+// block's stores walk its region in order, 4 KiB per step)
+__global__ __launch_bounds__(256) void unit_blk(float4* __restrict__ out, size_t n4, float v) {
+  const unsigned wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const size_t base = (size_t)blockIdx.x * 4096;
+  if (base >= n4) return;
+#pragma unroll
+  for (int j = 0; j < 16; ++j) out[base + (j * 4 + wv) * 64 + lane] = make_float4(v, v, v, v);
+}
+
+__global__ __launch_bounds__(256) void flat1(float4* __restrict__ out, size_t n4, float v) {
+  const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
+  if (i < n4) out[i] = make_float4(v, v, v, v);
+}
+
+__global__ __launch_bounds__(256) void gs(float4* __restrict__ out, size_t n4, float v) {
+  for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n4; i += (size_t)gridDim.x * 256)
+    out[i] = make_float4(v, v, v, v);
+}
+
+int main(int argc, char** argv) {
+  int cus = 0;
+  CK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0));
+  for (int a = 1; a < argc; ++a) {
+    const size_t bytes = (size_t)atoll(argv[a]) << 20;
+    const size_t n4 = bytes / 16;
+    float4* out;
+    CK(hipMalloc(&out, bytes));
+    hipEvent_t e0, e1;
+    CK(hipEventCreate(&e0));
+    CK(hipEventCreate(&e1));
+    const unsigned gu = (unsigned)((n4 / 1024 + 3) / 4);
+    auto run = [&](const char* name, auto launch) {
+      for (int i = 0; i < 3; ++i) launch();
+      CK(hipDeviceSynchronize());
+      const int R = 20;
+      CK(hipEventRecord(e0));
+      for (int i = 0; i < R; ++i) launch();
+      CK(hipEventRecord(e1));
+      CK(hipEventSynchronize(e1));
+      float ms = 0;
+      CK(hipEventElapsedTime(&ms, e0, e1));
+      const double us = ms * 1e3 / R;
+      printf("%6zu MiB %-9s %8.1f us %6.2f TB/s\n", bytes >> 20, name, us, bytes / us / 1e6);
+    };
+    run("unit_g", [&] { hipLaunchKernelGGL(unit_store<0>, dim3(gu), dim3(256), 0, 0, out, n4, 1.0f); });
+    run("unit_gnt", [&] { hipLaunchKernelGGL(unit_store<1>, dim3(gu), dim3(256), 0, 0, out, n4, 1.0f); });
+    run("unit_b", [&] { hipLaunchKernelGGL(unit_store<2>, dim3(gu), dim3(256), 0, 0, out, n4, 1.0f); });
+    run("unit_bnt", [&] { hipLaunchKernelGGL(unit_store<3>, dim3(gu), dim3(256), 0, 0, out, n4, 1.0f); });
+    run("unit_n4", [&] { hipLaunchKernelGGL(unit_n<4>, dim3((unsigned)((n4 / 256 + 3) / 4)), dim3(256), 0, 0, out, n4, 1.0f); });
+    run("unit_n8", [&] { hipLaunchKernelGGL(unit_n<8>, dim3((unsigned)((n4 / 512 + 3) / 4)), dim3(256), 0, 0, out, n4, 1.0f); });
+    run("unit_n2", [&] { hipLaunchKernelGGL(unit_n<2>, dim3((unsigned)((n4 / 128 + 3) / 4)), dim3(256), 0, 0, out, n4, 1.0f); });
+    run("unit_blk", [&] { hipLaunchKernelGGL(unit_blk, dim3((unsigned)((n4 + 4095) / 4096)), dim3(256), 0, 0, out, n4, 1.0f); });
+    run("flat1", [&] { hipLaunchKernelGGL(flat1, dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, 0, out, n4, 1.0f); });
+    run("gs", [&] { hipLaunchKernelGGL(gs, dim3(cus * 8), dim3(256), 0, 0, out, n4, 1.0f); });
+    CK(hipFree(out));
+  }
+  return 0;
+}
