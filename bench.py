@@ -430,10 +430,18 @@ def main():
 
     import torch
     import torch.distributed as dist
+    # COALA_BENCH_DIST_BACKEND=gloo: a rehearsal of the N > 1 path with several ranks on fewer GPUs (ranks share
+    # devices round-robin; RCCL refuses two ranks on one GPU). The driver's runs use RCCL, one rank per GPU.
+    backend = os.environ.get("COALA_BENCH_DIST_BACKEND", "nccl")
+    if backend != "nccl":
+        local = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
 
     head = run_workload(a.config, a, dev, world, rank, headline=True)
     extras = {}
