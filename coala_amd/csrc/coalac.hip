@@ -138,6 +138,7 @@ struct Params {
   const UnitDev* lunits;  // units of large segments (encode)
   const uint32_t* small_list;
   const uint32_t* large_list;
+  const SegDev* lsegs;  // [n_large] the large segments' SegDev, in large_list order (one load round less)
   uint32_t nseg, n_small, n_large, n_units, n_lunits;
   uint32_t scan_small;  // small segments encoded by k_scan's first blocks (0 when forked to k_small)
   float levels;
@@ -1034,6 +1035,19 @@ DEV uint32_t chunk_prefix(const uint32_t* cnt, uint32_t cn, uint32_t cap, uint32
   return carry;
 }
 
+// The same prefix from counts already in registers (thread i < cn holds unit i's count, cn <= NT): the
+// loads were issued with the caller's other loads of the same round.
+template <int NT>
+DEV uint32_t reg_prefix(uint32_t c, uint32_t cn, uint32_t* upre, uint32_t* sh) {
+  const uint32_t t = threadIdx.x;
+  uint32_t tot;
+  const uint32_t ex = block_excl_scan<NT>(t < cn ? c : 0u, sh, tot);
+  if (t < cn) upre[t] = ex;
+  if (t == 0) upre[cn] = tot;
+  __syncthreads();
+  return tot;
+}
+
 // Wave w owns the units whose first record index (upre[u]) lies in [w*total/NW, (w+1)*total/NW):
 // contiguous unit ranges balanced by record count, so segment order = (wave, unit, lane) order. A wave
 // reads one unit at a time from its contiguous region (coalesced, trivial addressing, the unit is
@@ -1212,10 +1226,12 @@ struct Band {
 DEV void group_hist(const Params& P, uint32_t gi, uint32_t* hist, uint32_t* upre, uint32_t* sh) {
   const uint4 G = P.groups[gi];  // x: large-segment index, y: first large unit, z: units, w: segment
   const uint32_t t = threadIdx.x;
-  const uint32_t tlo = P.tlo[G.y], thi = P.thi[G.y];
-  const Band band(tlo, thi, P.shhi[G.x]);
+  // one load round for everything that depends on G only
+  const uint32_t tlo = P.tlo[G.y], thi = P.thi[G.y], hh = P.shhi[G.x];
+  const uint32_t c = t < G.z ? min(P.cntC[G.y + t], P.ccap) : 0u;  // stored records only
   for (uint32_t i = t; i < HB2; i += BLOCK) hist[i] = 0;
-  const uint32_t total = chunk_prefix<BLOCK>(P.cntC + G.y, G.z, P.ccap, upre, sh);  // barrier inside
+  const uint32_t total = reg_prefix<BLOCK>(c, G.z, upre, sh);  // barriers inside
+  const Band band(tlo, thi, hh);
   unit_sweep<WAVES, 4>(
       P.cand, P.ccap, G.y, upre, G.z, total,
       [&](float x, bool valid, uint32_t) {
@@ -1239,15 +1255,44 @@ __global__ __launch_bounds__(BLOCK) void k_ghist(Params P) {
 // generic single-block path (bracket miss, nothing to take from B, huge segment, test flags). Every group
 // block of the segment computes it (identically) at the start of k_gwin — cheaper than a launch of its
 // own between k_ghist and k_gwin. Returned to every thread.
-DEV uint4 segment_pick(const Params& P, uint32_t li, uint32_t* hist, uint32_t* sh) {
+DEV uint4 segment_pick(const Params& P, const SegDev& sd, const Band& band, uint32_t* hist, uint32_t* sh) {
   const uint32_t t = threadIdx.x;
-  const SegDev sd = P.segs[P.large_list[li]];
   const uint32_t lb = sd.lu_begin, nu = sd.unit_end - sd.unit_begin, k = sd.k;
   const uint32_t g0 = sd.g_begin, ng = (nu + GU - 1) / GU;
-  // the group histograms: both of this thread's bins, 8 groups' loads in flight at a time
+  // one load round: the group histograms (both of this thread's bins, up to 24 groups' loads in flight)
+  // and the per-unit counts (up to 3 per thread) together
   static_assert(HB2 == 2 * BLOCK, "two histogram bins per thread");
-  uint32_t h0 = 0, h1 = 0;
-  for (uint32_t g = 0; g < ng; g += 8) {
+  constexpr uint32_t GB = 24, CB = 3;
+  uint32_t h0 = 0, h1 = 0, sa = 0, sc = 0, ov = 0;
+  {
+    uint32_t v0[GB], v1[GB], ca[CB], cc[CB];
+#pragma unroll
+    for (uint32_t j = 0; j < GB; ++j) {
+      const uint64_t row = (uint64_t)(g0 + min(j, ng - 1)) * HB2;
+      v0[j] = P.ghist[row + t];
+      v1[j] = P.ghist[row + BLOCK + t];
+    }
+#pragma unroll
+    for (uint32_t j = 0; j < CB; ++j) {
+      const uint32_t i = min(t + j * BLOCK, nu - 1);
+      cc[j] = P.cntC[lb + i];
+      ca[j] = P.cntA[lb + i];
+    }
+#pragma unroll
+    for (uint32_t j = 0; j < GB; ++j) {
+      h0 += j < ng ? v0[j] : 0u;
+      h1 += j < ng ? v1[j] : 0u;
+    }
+#pragma unroll
+    for (uint32_t j = 0; j < CB; ++j) {
+      if (t + j * BLOCK < nu) {
+        sa += ca[j];
+        sc += cc[j];
+        ov += cc[j] > P.ccap ? 1u : 0u;
+      }
+    }
+  }
+  for (uint32_t g = GB; g < ng; g += 8) {  // segments of more than GB groups
     uint32_t v0[8], v1[8];
 #pragma unroll
     for (uint32_t j = 0; j < 8; ++j) {
@@ -1261,8 +1306,7 @@ DEV uint4 segment_pick(const Params& P, uint32_t li, uint32_t* hist, uint32_t* s
       h1 += g + j < ng ? v1[j] : 0u;
     }
   }
-  uint32_t sa = 0, sc = 0, ov = 0;
-  for (uint32_t i = t; i < nu; i += BLOCK) {
+  for (uint32_t i = t + CB * BLOCK; i < nu; i += BLOCK) {
     const uint32_t c = P.cntC[lb + i];
     sa += P.cntA[lb + i];
     sc += c;
@@ -1281,7 +1325,6 @@ DEV uint4 segment_pick(const Params& P, uint32_t li, uint32_t* hist, uint32_t* s
   uint32_t r = k - sa;
   const uint32_t b = hist_pick<BLOCK, HB2>(hist, r, sh);
   if (b == NONE) return make_uint4(0u, 0u, 0u, 1u);
-  const Band band(P.tlo[lb], P.thi[lb], P.shhi[li]);
   return make_uint4(band.wlo(b), band.whi(b), r, 0u);
 }
 
@@ -1297,15 +1340,16 @@ struct GwinSmem {
 template <int NT, bool DELTA, bool RAW>
 DEV void segment_select(const Params& P, uint32_t li, SelSmem& S);
 
-DEV void group_window(const Params& P, uint32_t gi, const uint4 G, const uint4 st, GwinSmem& W_, uint32_t* sh) {
+// (upre / total: the group's record prefix, already in W_.upre)
+DEV void group_window(const Params& P, uint32_t gi, const uint4 G, const uint4 st, uint32_t lu_begin, uint32_t total,
+                      GwinSmem& W_, uint32_t* sh) {
   uint32_t* upre = W_.upre;
   auto& slots = W_.slots;
   uint32_t* wcnt = W_.wcnt;
   float* shf = W_.shf;
   const uint32_t t = threadIdx.x, lane = lane_id(), wv = t >> 6;
   const uint32_t wlo = st.x, whi = st.y;
-  const uint32_t useg0 = G.y - P.segs[G.w].lu_begin;  // unit index (within the segment) of the group's first unit
-  const uint32_t total = chunk_prefix<BLOCK>(P.cntC + G.y, G.z, P.ccap, upre, sh);
+  const uint32_t useg0 = G.y - lu_begin;  // unit index (within the segment) of the group's first unit
   uint32_t wc = 0, ug = 0;
   float lmn = qnan(), lmx = qnan();
   unit_sweep<WAVES, 4>(
@@ -1353,13 +1397,19 @@ DEV void group_window(const Params& P, uint32_t gi, const uint4 G, const uint4 s
 
 DEV void group_pick_window(const Params& P, uint32_t gi, GwinSmem& W, uint32_t* hist, uint32_t* sh) {
   const uint4 G = P.groups[gi];
-  const uint4 st = segment_pick(P, G.x, hist, sh);
-  if (threadIdx.x == 0 && G.y == P.segs[G.w].lu_begin) {  // the segment's first group
+  // one load round for everything that depends on G only: the segment, its band, the group's counts
+  const SegDev sd = P.lsegs[G.x];
+  const uint32_t tlo = P.tlo[G.y], thi = P.thi[G.y], hh = P.shhi[G.x];
+  const uint32_t c = threadIdx.x < G.z ? min(P.cntC[G.y + threadIdx.x], P.ccap) : 0u;
+  const uint32_t total = reg_prefix<BLOCK>(c, G.z, W.upre, sh);
+  const Band band(tlo, thi, hh);
+  const uint4 st = segment_pick(P, sd, band, hist, sh);
+  if (threadIdx.x == 0 && G.y == sd.lu_begin) {  // the segment's first group
     uint2* ss = reinterpret_cast<uint2*>(P.sstate + G.x);
     pst(P, ss, make_uint2(st.x, st.y));
     pst(P, ss + 1, make_uint2(st.z, st.w));
   }
-  if (st.w == 0) group_window(P, gi, G, st, W, sh);
+  if (st.w == 0) group_window(P, gi, G, st, sd.lu_begin, total, W, sh);
 }
 
 __global__ __launch_bounds__(BLOCK) void k_gwin(Params P) {
@@ -1475,7 +1525,13 @@ DEV bool select_from_groups(const Params& P, const SegDev& sd, uint32_t lb, uint
                             uint32_t& T_out, uint32_t& rt_out, uint32_t& fp, uint32_t& fn, float& gmn, float& gmx) {
   const uint32_t t = threadIdx.x;
   const uint32_t g0 = sd.g_begin, ng = (nu + GU - 1) / GU;  // ng <= UCAP / GU = 64 <= NT
+  // one load round: the groups' list lengths, min / max above the window and the first per-unit counts
   const uint32_t c = t < ng ? P.gcnt[g0 + t] : 0u;
+  const float gmn0 = t < ng ? P.gmm[2 * (g0 + t)] : qnan(), gmx0 = t < ng ? P.gmm[2 * (g0 + t) + 1] : qnan();
+  constexpr uint32_t CB = 3;
+  uint32_t gtc[CB];
+#pragma unroll
+  for (uint32_t j = 0; j < CB; ++j) gtc[j] = P.gtC[lb + min(t + j * NT, nu - 1)];
   uint32_t W;
   const uint32_t gpre = block_excl_scan<NT>(c, S.sh, W);
   const uint32_t over = block_sum<NT>(c > GCAP ? 1u : 0u, S.sh);
@@ -1506,7 +1562,10 @@ DEV bool select_from_groups(const Params& P, const SegDev& sd, uint32_t lb, uint
       if (e < W) S.lst[e] = v[j];
     }
   }
-  for (uint32_t i = t; i < nu; i += NT) S.ge[i] = P.gtC[lb + i];
+#pragma unroll
+  for (uint32_t j = 0; j < CB; ++j)
+    if (t + j * NT < nu) S.ge[t + j * NT] = gtc[j];
+  for (uint32_t i = t + CB * NT; i < nu; i += NT) S.ge[i] = P.gtC[lb + i];
   __syncthreads();
   uint32_t rt = st.z;
   const uint32_t T = block_select<NT, SEL_HB>(
@@ -1533,10 +1592,8 @@ DEV bool select_from_groups(const Params& P, const SegDev& sd, uint32_t lb, uint
       ++leq;
     }
   }
-  for (uint32_t g = t; g < ng; g += NT) {
-    lmn = fmin_nan(lmn, P.gmm[2 * (g0 + g)]);
-    lmx = fmax_nan(lmx, P.gmm[2 * (g0 + g) + 1]);
-  }
+  lmn = fmin_nan(lmn, gmn0);  // ng <= NT: thread t < ng holds group t's
+  lmx = fmax_nan(lmx, gmx0);
   uint32_t teq;
   const uint32_t ex = block_excl_scan<NT>(leq, S.sh, teq);
   if (t == 0) {
@@ -1562,14 +1619,14 @@ DEV void segment_select(const Params& P, uint32_t li, SelSmem& S) {
   constexpr int NW = NT / 64;
   const uint32_t t = threadIdx.x, wv = t >> 6;
   const uint32_t s = P.large_list[li];
-  const SegDev sd = P.segs[s];
+  const SegDev sd = P.lsegs[li];  // (same load round as s and the select state)
+  const uint4 st = P.sstate[li];
   const float* xs = seg_in(P, s, sd.in_off);
   const float* bs = DELTA ? P.base + sd.in_off : xs;
   const uint32_t lb = sd.lu_begin, nu = sd.unit_end - sd.unit_begin, k = sd.k;
   STAMP(P, li, 0);
   uint32_t T, rt, fp_rank, fn_rank;
   float gmn, gmx;
-  const uint4 st = P.sstate[li];
   bool done = st.w == 0 && select_from_groups<NT>(P, sd, lb, nu, st, S, T, rt, fp_rank, fn_rank, gmn, gmx);
   STAMP(P, li, 1);
   if (!done) {
@@ -2501,6 +2558,7 @@ struct coalac_plan {
   UnitDev* lunits = nullptr;
   uint32_t* small_list = nullptr;
   uint32_t* large_list = nullptr;
+  SegDev* lsegs = nullptr;
   uint4* groups = nullptr;
   uint32_t n_groups = 0;
   BChunk* bchunks = nullptr;  // aggregate: k_bounds work list
@@ -2538,6 +2596,7 @@ void fill_meta(Params& P, coalac_plan_t plan) {
   P.lunits = plan->lunits;
   P.small_list = plan->small_list;
   P.large_list = plan->large_list;
+  P.lsegs = plan->lsegs;
   P.groups = plan->groups;
   P.n_groups = plan->n_groups;
   P.items = plan->items;
@@ -2827,7 +2886,10 @@ int coalac_plan_create(const coalac_seg_t* h_segs, int nseg, int bits, coalac_pl
   const size_t o_lunits = align_up(o_units + sizeof(UnitDev) * units.size(), 256);
   const size_t o_small = align_up(o_lunits + sizeof(UnitDev) * lunits.size(), 256);
   const size_t o_large = align_up(o_small + 4 * small_list.size(), 256);
-  const size_t o_grp = align_up(o_large + 4 * large_list.size(), 256);
+  std::vector<SegDev> lsegs;
+  for (uint32_t s2 : large_list) lsegs.push_back(segs[s2]);
+  const size_t o_lsegs = align_up(o_large + 4 * large_list.size(), 256);
+  const size_t o_grp = align_up(o_lsegs + sizeof(SegDev) * lsegs.size(), 256);
   const size_t o_bch = align_up(o_grp + sizeof(uint4) * groups.size(), 256);
   const size_t o_items = align_up(o_bch + sizeof(BChunk) * bchunks.size(), 256);
   const size_t o_fsched = align_up(o_items + 4 * F.items.size(), 256);
@@ -2841,6 +2903,7 @@ int coalac_plan_create(const coalac_seg_t* h_segs, int nseg, int bits, coalac_pl
   if (!lunits.empty()) memcpy(host.data() + o_lunits, lunits.data(), sizeof(UnitDev) * lunits.size());
   if (!small_list.empty()) memcpy(host.data() + o_small, small_list.data(), 4 * small_list.size());
   if (!large_list.empty()) memcpy(host.data() + o_large, large_list.data(), 4 * large_list.size());
+  if (!lsegs.empty()) memcpy(host.data() + o_lsegs, lsegs.data(), sizeof(SegDev) * lsegs.size());
   if (!groups.empty()) memcpy(host.data() + o_grp, groups.data(), sizeof(uint4) * groups.size());
   if (!bchunks.empty()) memcpy(host.data() + o_bch, bchunks.data(), sizeof(BChunk) * bchunks.size());
   if (!F.items.empty()) memcpy(host.data() + o_items, F.items.data(), 4 * F.items.size());
@@ -2865,6 +2928,7 @@ int coalac_plan_create(const coalac_seg_t* h_segs, int nseg, int bits, coalac_pl
   p->lunits = reinterpret_cast<UnitDev*>(m + o_lunits);
   p->small_list = reinterpret_cast<uint32_t*>(m + o_small);
   p->large_list = reinterpret_cast<uint32_t*>(m + o_large);
+  p->lsegs = reinterpret_cast<SegDev*>(m + o_lsegs);
   p->groups = reinterpret_cast<uint4*>(m + o_grp);
   p->bchunks = reinterpret_cast<BChunk*>(m + o_bch);
   p->items = reinterpret_cast<uint32_t*>(m + o_items);
