@@ -89,6 +89,9 @@ constexpr int SEL_NT = 256;               // threads of a k_select block (4 wave
 #endif
 constexpr uint32_t STAGE_CAP = 512;       // candidate records staged in LDS per k_scan wave
 constexpr uint32_t GU = 32;               // units per select group (k_ghist / k_gwin block)
+#ifndef GSWEEP
+#define GSWEEP 4  // units per record-load batch of a group sweep (8 measured equal on one update, lower on C3)
+#endif
 constexpr uint32_t HB2 = 512;             // bins of the per-group band histograms
 constexpr uint32_t GCAP = 256;            // in-window entries a group may hand to k_select
 constexpr uint32_t A_FLAG = 0x80000000u;  // candidate record flag: key > T_hi (kept for sure)
@@ -1232,7 +1235,7 @@ DEV void group_hist(const Params& P, uint32_t gi, uint32_t* hist, uint32_t* upre
   for (uint32_t i = t; i < HB2; i += BLOCK) hist[i] = 0;
   const uint32_t total = reg_prefix<BLOCK>(c, G.z, upre, sh);  // barriers inside
   const Band band(tlo, thi, hh);
-  unit_sweep<WAVES, 4>(
+  unit_sweep<WAVES, GSWEEP>(
       P.cand, P.ccap, G.y, upre, G.z, total,
       [&](float x, bool valid, uint32_t) {
         const uint32_t key = fkey(x);
@@ -1352,7 +1355,7 @@ DEV void group_window(const Params& P, uint32_t gi, const uint4 G, const uint4 s
   const uint32_t useg0 = G.y - lu_begin;  // unit index (within the segment) of the group's first unit
   uint32_t wc = 0, ug = 0;
   float lmn = qnan(), lmx = qnan();
-  unit_sweep<WAVES, 4>(
+  unit_sweep<WAVES, GSWEEP>(
       P.cand, P.ccap, G.y, upre, G.z, total,
       [&](float x, bool valid, uint32_t u) {
         const uint32_t key = fkey(x);
