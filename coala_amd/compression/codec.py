@@ -536,12 +536,6 @@ class UpdateCodec:
         return module_with_state(template, state)
 
 
-_MODULE_DICTS = ("_forward_hooks", "_forward_hooks_with_kwargs", "_forward_hooks_always_called",
-                 "_forward_pre_hooks", "_forward_pre_hooks_with_kwargs", "_backward_hooks",
-                 "_backward_pre_hooks", "_state_dict_hooks", "_state_dict_pre_hooks",
-                 "_load_state_dict_pre_hooks", "_load_state_dict_post_hooks")
-
-
 def module_with_state(template, state):
     """A new nn.Module shaped like `template` whose parameters / buffers ARE the tensors of `state`
     (views into the decode output: no parameter data is copied; `template` is never aliased).
@@ -550,6 +544,14 @@ def module_with_state(template, state):
     deep, fresh parameter / buffer / submodule tables and hook dicts) instead of copy.deepcopy, whose
     generic recursion cost ~8 ms per ResNet-50 on the server's per-upload path. Tensors outside the state
     (non-persistent buffers, unregistered tensors) are cloned."""
+    def shallow(v):  # a container one level deep; empty ones (most hook dicts) without copy.copy's reduce path
+        if not v:
+            try:
+                return v.__class__()
+            except TypeError:
+                pass
+        return copy.copy(v)
+
     def clone(mod, prefix):
         new = mod.__class__.__new__(mod.__class__)
         d = {}
@@ -557,7 +559,7 @@ def module_with_state(template, state):
             if isinstance(v, torch.Tensor):
                 v = v.clone()
             elif isinstance(v, (list, dict, set)) and k not in ("_parameters", "_buffers", "_modules"):
-                v = copy.copy(v)
+                v = shallow(v)  # (the hook dicts included: the clone never shares them)
             d[k] = v
         params = OrderedDict()
         for name, p in mod._parameters.items():
@@ -575,9 +577,6 @@ def module_with_state(template, state):
         d["_parameters"], d["_buffers"] = params, buffers
         d["_modules"] = OrderedDict((name, None if c is None else clone(c, prefix + name + "."))
                                     for name, c in mod._modules.items())
-        for k in _MODULE_DICTS:
-            if k in d:
-                d[k] = copy.copy(mod.__dict__[k])
         new.__dict__.update(d)
         return new
     return clone(template, "")
