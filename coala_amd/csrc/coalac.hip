@@ -2232,6 +2232,12 @@ __global__ __launch_bounds__(BLOCK) void k_bounds(Params P, const BChunk* chunks
   }
 }
 
+#ifndef AGG_WPE
+#define AGG_WPE 1  // k_aggregate launch-bounds blocks per CU (register budget)
+#endif
+#ifndef AGG_SPLIT
+#define AGG_SPLIT 2u  // waves per 4096-element unit in k_aggregate (each owns UNIT_IT / AGG_SPLIT rows)
+#endif
 #ifndef AGG_DEPTH
 #define AGG_DEPTH 8u  // clients whose entries k_aggregate keeps in flight (16 ResNet-50: 2 -> 92.5 us, 8 -> 73.7 us, 16 -> 93.5 us)
 #endif
@@ -2259,30 +2265,37 @@ struct AggArgs {
 // while client j is accumulated (rotating register slots). Clients are identical copies of one layout, so
 // client c's unit / segment / entry offsets are u + c*U0, seg + c*T, out_off + c*Kc (host-validated).
 template <bool RAW, bool HASBASE, int MODE>
-__global__ __launch_bounds__(BLOCK) void k_aggregate(Params P, AggArgs A) {
-  __shared__ float4 tiles[WAVES][UNIT / 4];
+__global__ __launch_bounds__(BLOCK, AGG_WPE) void k_aggregate(Params P, AggArgs A) {
+  // AGG_SPLIT waves per unit, each owning RI of its UNIT_IT rows: a smaller LDS tile and half the registers
+  // per wave, so twice the waves are resident
+  constexpr uint32_t RI = UNIT_IT / AGG_SPLIT, HE = UNIT / AGG_SPLIT;  // rows / elements per wave
+  __shared__ float4 tiles[WAVES][HE / 4];
   const uint32_t lane = lane_id(), wv = threadIdx.x >> 6;
-  const uint32_t u = blockIdx.x * WAVES + wv;
+  const uint32_t wid = blockIdx.x * WAVES + wv;
+  const uint32_t u = wid / AGG_SPLIT, h = wid % AGG_SPLIT;
   if (u >= A.U0) return;
   const UnitDev U = P.units[u];
   const uint32_t len = U.len, kseg = U.k;
+  const uint32_t e_lo = h * HE;  // first element (within the unit) of this wave's rows
+  if (e_lo >= len) return;
+  const uint32_t hlen = min(len - e_lo, HE);
   float4* tile = tiles[wv];
   float* tf = reinterpret_cast<float*>(tile);
 #pragma unroll
-  for (uint32_t it = 0; it < UNIT_IT; ++it) tile[it * 64 + lane] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-  float4 b[UNIT_IT], acc[UNIT_IT];
-  const float* bs = HASBASE ? P.base + U.off : nullptr;
+  for (uint32_t it = 0; it < RI; ++it) tile[it * 64 + lane] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+  float4 b[RI], acc[RI];
+  const float* bs = HASBASE ? P.base + U.off + e_lo : nullptr;
 #pragma unroll
-  for (uint32_t it = 0; it < UNIT_IT; ++it) {
+  for (uint32_t it = 0; it < RI; ++it) {
     const uint32_t e = (it * 64 + lane) * 4;
     if (HASBASE) {
-      if (len == UNIT) {
+      if (hlen == HE) {
         b[it] = *reinterpret_cast<const float4*>(bs + e);
       } else {
-        b[it].x = e + 0 < len ? bs[e + 0] : 0.0f;
-        b[it].y = e + 1 < len ? bs[e + 1] : 0.0f;
-        b[it].z = e + 2 < len ? bs[e + 2] : 0.0f;
-        b[it].w = e + 3 < len ? bs[e + 3] : 0.0f;
+        b[it].x = e + 0 < hlen ? bs[e + 0] : 0.0f;
+        b[it].y = e + 1 < hlen ? bs[e + 1] : 0.0f;
+        b[it].z = e + 2 < hlen ? bs[e + 2] : 0.0f;
+        b[it].w = e + 3 < hlen ? bs[e + 3] : 0.0f;
       }
     }
     acc[it] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
@@ -2304,7 +2317,7 @@ __global__ __launch_bounds__(BLOCK) void k_aggregate(Params P, AggArgs A) {
       const uint32_t lo = __builtin_amdgcn_readlane(m_lo, jj), hi = __builtin_amdgcn_readlane(m_hi, jj);
       const uint64_t oo = entries(jj);
       const uint32_t e = min(lo + lane, hi > lo ? hi - 1 : lo);  // kseg >= 1: entry lo always exists
-      pos = (uint32_t)P.cidx[oo + min(e, kseg - 1)] - U.start;
+      pos = (uint32_t)P.cidx[oo + min(e, kseg - 1)] - U.start - e_lo;  // wraps (>= hlen) outside this wave's rows
       q = load_code<RAW>(P, oo + min(e, kseg - 1));
     };
     auto process = [&](uint32_t j, uint32_t pos, uint32_t q) {
@@ -2314,16 +2327,16 @@ __global__ __launch_bounds__(BLOCK) void k_aggregate(Params P, AggArgs A) {
       const float w = __uint_as_float(__builtin_amdgcn_readlane(__float_as_uint(m_w), j));
       const uint32_t ne = hi - lo;
       const uint64_t oo = entries(j);
-      if (lane < ne && pos < len) tf[pos] = code_value<RAW>(q, mn, sc);
+      if (lane < ne && pos < hlen) tf[pos] = code_value<RAW>(q, mn, sc);
       for (uint32_t e = lo + 64 + lane; e < hi; e += 64) {  // more than 64 kept entries in this unit
-        const uint32_t p2 = (uint32_t)P.cidx[oo + e] - U.start;
+        const uint32_t p2 = (uint32_t)P.cidx[oo + e] - U.start - e_lo;
         const float v2 = load_val<RAW>(P, oo + e, mn, sc);
-        if (p2 < len) tf[p2] = v2;
+        if (p2 < hlen) tf[p2] = v2;
       }
       wave_fence();
       const bool first = c0 + j == 0;
 #pragma unroll
-      for (uint32_t it = 0; it < UNIT_IT; ++it) {
+      for (uint32_t it = 0; it < RI; ++it) {
         const float4 d = tile[it * 64 + lane];
         float4 x;
         x.x = HASBASE ? b[it].x + d.x : d.x;
@@ -2339,8 +2352,8 @@ __global__ __launch_bounds__(BLOCK) void k_aggregate(Params P, AggArgs A) {
       wave_fence();
       if (ne > 64) {
 #pragma unroll
-        for (uint32_t it = 0; it < UNIT_IT; ++it) tile[it * 64 + lane] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-      } else if (lane < ne && pos < len) {
+        for (uint32_t it = 0; it < RI; ++it) tile[it * 64 + lane] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+      } else if (lane < ne && pos < hlen) {
         tf[pos] = 0.0f;
       }
       wave_fence();
@@ -2358,9 +2371,9 @@ __global__ __launch_bounds__(BLOCK) void k_aggregate(Params P, AggArgs A) {
       }
     }
   }
-  float* out = P.out + U.off;
+  float* out = P.out + U.off + e_lo;
 #pragma unroll
-  for (uint32_t it = 0; it < UNIT_IT; ++it) {
+  for (uint32_t it = 0; it < RI; ++it) {
     float4 o;
     if (MODE == COALAC_AGG_DIV) {
       o = make_float4(acc[it].x / A.total, acc[it].y / A.total, acc[it].z / A.total, acc[it].w / A.total);
@@ -2371,13 +2384,13 @@ __global__ __launch_bounds__(BLOCK) void k_aggregate(Params P, AggArgs A) {
                       acc[it].w * A.inv_total);
     }
     const uint32_t e = (it * 64 + lane) * 4;
-    if (len == UNIT) {
+    if (hlen == HE) {
       *reinterpret_cast<float4*>(out + e) = o;
     } else {
-      if (e + 0 < len) out[e + 0] = o.x;
-      if (e + 1 < len) out[e + 1] = o.y;
-      if (e + 2 < len) out[e + 2] = o.z;
-      if (e + 3 < len) out[e + 3] = o.w;
+      if (e + 0 < hlen) out[e + 0] = o.x;
+      if (e + 1 < hlen) out[e + 1] = o.y;
+      if (e + 2 < hlen) out[e + 2] = o.z;
+      if (e + 3 < hlen) out[e + 3] = o.w;
     }
   }
 }
@@ -3235,7 +3248,7 @@ int coalac_aggregate_ev(coalac_plan_t plan, int clients, const int32_t* d_idx, c
     hipLaunchKernelGGL(k_bounds, dim3(plan->n_bchunks), dim3(BLOCK), 0, st, P, plan->bchunks,
                        static_cast<uint32_t*>(d_ws));
   BOUNDARY(1);
-  const uint32_t g = (U0 + WAVES - 1) / WAVES;
+  const uint32_t g = (U0 * AGG_SPLIT + WAVES - 1) / WAVES;
   const bool raw = plan->bits == 32, hb = d_base != nullptr;
 #define AGG(R, H, M) hipLaunchKernelGGL((k_aggregate<R, H, M>), dim3(g), dim3(BLOCK), 0, st, P, A)
 #define AGG_MODES(R, H)                     \
