@@ -2086,6 +2086,9 @@ DEV void wave_lower_bound(const int32_t* const (&L)[M], const uint32_t (&k)[M], 
 
 // units per wave of k_decode: 1 with a base (its 16 float4 of base per unit would double the registers) or
 // in the in-kernel search variant (latency-bound plans: twice the waves, each with half the serial merge)
+#ifndef DECODE_SCATTER
+#define DECODE_SCATTER 1  // latency-bound plans decode as k_fill + k_scatter (else k_decode with the search)
+#endif
 #ifndef DECODE_SEARCH_DPW
 #define DECODE_SEARCH_DPW 1u
 #endif
@@ -2192,6 +2195,38 @@ __global__ __launch_bounds__(BLOCK, DECODE_WPE) void k_decode(Params P) {
   }
 }
 
+// Latency-bound plans, DECODE_SCATTER: the background first (k_fill: every unit's 0 / base + 0.0f, no entry
+// lookup, so the write stream starts at once), then the kept values on top (k_scatter: one thread per entry,
+// per k_bounds chunk; bounds-checked like k_decode). Stream order puts every kept value after the fill.
+template <bool HASBASE>
+__global__ __launch_bounds__(BLOCK) void k_fill(Params P) {
+  const uint32_t lane = lane_id();
+  const uint32_t u = blockIdx.x * WAVES + (threadIdx.x >> 6);
+  if (u >= P.n_units) return;
+  const UnitDev U = P.units[u];
+  const __amdgpu_buffer_rsrc_t rout = unit_rsrc(P.out + U.off, U.len);
+  float4 b[UNIT_IT];
+  if (HASBASE) {
+    const __amdgpu_buffer_rsrc_t rb = unit_rsrc(P.base + U.off, U.len);
+#pragma unroll
+    for (uint32_t it = 0; it < UNIT_IT; ++it) {
+      const float4 a = unit_load_x4<false>(rb, rb, (it * 64 + lane) * 16);
+      b[it] = make_float4(a.x + 0.0f, a.y + 0.0f, a.z + 0.0f, a.w + 0.0f);
+    }
+  } else {
+#pragma unroll
+    for (uint32_t it = 0; it < UNIT_IT; ++it) b[it] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+  }
+  if ((U.len & 3u) == 0) {
+#pragma unroll
+    for (uint32_t it = 0; it < UNIT_IT; ++it) unit_store_x4<0>(rout, (it * 64 + lane) * 16, b[it]);
+  } else {
+#pragma unroll
+    for (uint32_t it = 0; it < UNIT_IT; ++it) unit_store_x1x4<0>(rout, (it * 64 + lane) * 16, b[it]);
+  }
+}
+
+
 // ------------------------------------------------------------------------------------------------
 // aggregate: fused server-side decode + FedAvg of C client updates of one layout
 // ------------------------------------------------------------------------------------------------
@@ -2241,6 +2276,37 @@ __global__ __launch_bounds__(BLOCK) void k_bounds(Params P, const BChunk* chunks
 #ifndef AGG_DEPTH
 #define AGG_DEPTH 8u  // clients whose entries k_aggregate keeps in flight (16 ResNet-50: 2 -> 92.5 us, 8 -> 73.7 us, 16 -> 93.5 us)
 #endif
+
+// k_scatter's work list: one chunk of <= BCHUNK entries of one segment, with the segment's offsets and
+// size inline (the entries, mn and scale then load in one round)
+struct SChunk {
+  uint64_t in_off, out_off;
+  uint32_t seg, n, e0, e1;
+};
+static_assert(sizeof(SChunk) == 32, "SChunk layout");
+
+template <bool RAW, bool HASBASE>
+__global__ __launch_bounds__(BLOCK) void k_scatter(Params P, const SChunk* chunks) {
+  constexpr uint32_t EPT = BCHUNK / BLOCK;
+  const SChunk C = chunks[blockIdx.x];
+  const float mn = RAW ? 0.0f : P.cmn[C.seg];
+  const float sc = RAW ? 0.0f : P.cscale[C.seg];
+  uint32_t ix[EPT], q[EPT];
+#pragma unroll
+  for (uint32_t j = 0; j < EPT; ++j) {  // coalesced: entry C.e0 + j * BLOCK + t (clamped: loads unconditional)
+    const uint64_t e = C.out_off + min(C.e0 + j * BLOCK + threadIdx.x, C.e1 - 1);
+    ix[j] = (uint32_t)P.cidx[e];
+    q[j] = load_code<RAW>(P, e);
+  }
+#pragma unroll
+  for (uint32_t j = 0; j < EPT; ++j) {
+    if (C.e0 + j * BLOCK + threadIdx.x < C.e1 && ix[j] < C.n) {  // an untrusted list stays in its segment
+      const float v = code_value<RAW>(q[j], mn, sc);
+      float* o = P.out + C.in_off + ix[j];
+      *o = HASBASE ? P.base[C.in_off + ix[j]] + v : v;
+    }
+  }
+}
 
 struct AggArgs {
   const uint32_t* ustart;  // [n_units] from k_bounds
@@ -2579,6 +2645,7 @@ struct coalac_plan {
   uint32_t n_groups = 0;
   BChunk* bchunks = nullptr;  // aggregate: k_bounds work list
   uint32_t n_bchunks = 0;
+  SChunk* schunks = nullptr;  // latency-bound decode: k_scatter work list (n_bchunks of them)
   // one-launch encode (k_fused): block work items, scan order, unit -> group, emit blocks
   uint32_t* items = nullptr;
   uint32_t n_items = 0;
@@ -2907,7 +2974,11 @@ int coalac_plan_create(const coalac_seg_t* h_segs, int nseg, int bits, coalac_pl
   const size_t o_lsegs = align_up(o_large + 4 * large_list.size(), 256);
   const size_t o_grp = align_up(o_lsegs + sizeof(SegDev) * lsegs.size(), 256);
   const size_t o_bch = align_up(o_grp + sizeof(uint4) * groups.size(), 256);
-  const size_t o_items = align_up(o_bch + sizeof(BChunk) * bchunks.size(), 256);
+  std::vector<SChunk> schunks;
+  for (const BChunk& c : bchunks)
+    schunks.push_back(SChunk{segs[c.seg].in_off, segs[c.seg].out_off, c.seg, segs[c.seg].n, c.e0, c.e1});
+  const size_t o_sch = align_up(o_bch + sizeof(BChunk) * bchunks.size(), 256);
+  const size_t o_items = align_up(o_sch + sizeof(SChunk) * schunks.size(), 256);
   const size_t o_fsched = align_up(o_items + 4 * F.items.size(), 256);
   const size_t o_lgroup = align_up(o_fsched + 4 * F.fsched.size(), 256);
   const size_t o_eblk = align_up(o_lgroup + 4 * F.lgroup.size(), 256);
@@ -2922,6 +2993,7 @@ int coalac_plan_create(const coalac_seg_t* h_segs, int nseg, int bits, coalac_pl
   if (!lsegs.empty()) memcpy(host.data() + o_lsegs, lsegs.data(), sizeof(SegDev) * lsegs.size());
   if (!groups.empty()) memcpy(host.data() + o_grp, groups.data(), sizeof(uint4) * groups.size());
   if (!bchunks.empty()) memcpy(host.data() + o_bch, bchunks.data(), sizeof(BChunk) * bchunks.size());
+  if (!schunks.empty()) memcpy(host.data() + o_sch, schunks.data(), sizeof(SChunk) * schunks.size());
   if (!F.items.empty()) memcpy(host.data() + o_items, F.items.data(), 4 * F.items.size());
   if (!F.fsched.empty()) memcpy(host.data() + o_fsched, F.fsched.data(), 4 * F.fsched.size());
   if (!F.lgroup.empty()) memcpy(host.data() + o_lgroup, F.lgroup.data(), 4 * F.lgroup.size());
@@ -2947,6 +3019,7 @@ int coalac_plan_create(const coalac_seg_t* h_segs, int nseg, int bits, coalac_pl
   p->lsegs = reinterpret_cast<SegDev*>(m + o_lsegs);
   p->groups = reinterpret_cast<uint4*>(m + o_grp);
   p->bchunks = reinterpret_cast<BChunk*>(m + o_bch);
+  p->schunks = reinterpret_cast<SChunk*>(m + o_sch);
   p->items = reinterpret_cast<uint32_t*>(m + o_items);
   p->fsched = reinterpret_cast<uint32_t*>(m + o_fsched);
   p->lgroup = reinterpret_cast<uint32_t*>(m + o_lgroup);
@@ -3142,8 +3215,10 @@ int coalac_decode_sched(coalac_plan_t plan, const int32_t* d_idx, const void* d_
   P.ustart = static_cast<const uint32_t*>(d_ws);
   hipStream_t st = static_cast<hipStream_t>(stream);
   const bool raw = plan->bits == 32, hb = d_base != nullptr;
-  // small plans: k_decode finds its units' entry ranges itself (one launch); batches: k_bounds first
+  // small plans: k_decode finds its units' entry ranges itself (one launch), or (DECODE_SCATTER) the
+  // background and then the kept values; batches: k_bounds first
   const bool search = plan->n_units <= DECODE_SEARCH_MAX_UNITS;
+  const bool scatter = search && DECODE_SCATTER;
   const uint32_t upb = WAVES * (hb ? decode_dpw<true, false>()
                                    : search ? decode_dpw<false, true>() : decode_dpw<false, false>());  // units per block
   const uint32_t g = (plan->n_units + upb - 1) / upb;
@@ -3168,7 +3243,24 @@ int coalac_decode_sched(coalac_plan_t plan, const int32_t* d_idx, const void* d_
   } while (0)
   if (!(stages & COALAC_STAGE_DECODE))
     ;
-  else if (raw && hb)
+  else if (scatter) {
+    const uint32_t gf = (plan->n_units + WAVES - 1) / WAVES;
+    if (hb)
+      hipLaunchKernelGGL((k_fill<true>), dim3(gf), dim3(BLOCK), 0, st, P);
+    else
+      hipLaunchKernelGGL((k_fill<false>), dim3(gf), dim3(BLOCK), 0, st, P);
+    if (plan->n_bchunks) {
+      const dim3 gs(plan->n_bchunks);
+      if (raw && hb)
+        hipLaunchKernelGGL((k_scatter<true, true>), gs, dim3(BLOCK), 0, st, P, plan->schunks);
+      else if (raw)
+        hipLaunchKernelGGL((k_scatter<true, false>), gs, dim3(BLOCK), 0, st, P, plan->schunks);
+      else if (hb)
+        hipLaunchKernelGGL((k_scatter<false, true>), gs, dim3(BLOCK), 0, st, P, plan->schunks);
+      else
+        hipLaunchKernelGGL((k_scatter<false, false>), gs, dim3(BLOCK), 0, st, P, plan->schunks);
+    }
+  } else if (raw && hb)
     DEC(true, true);
   else if (raw)
     DEC(true, false);

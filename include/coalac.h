@@ -120,7 +120,8 @@ int coalac_decode(coalac_plan_t plan, const int32_t* d_idx, const void* d_vals, 
  * encode (COALAC_FLAG_FRONT_LAUNCH): events[0] before the control-block memset, [1] before the front
  *         launch (samplers + scan + small segments), [2] after it, [3] after k_select, [4] after k_emit;
  * encode (COALAC_FLAG_ONE_LAUNCH): [0] before the memset, [1] before k_fused, [2] [3] [4] after it;
- * decode: [0] before k_bounds (plans of > 8192 units only), [1] before k_decode, [2] after it. NULL
+ * decode: [0] before k_bounds (plans of > 8192 units only), [1] before k_decode (plans of <= 8192 units:
+ *         before k_fill), [2] after it (after k_scatter). NULL
  *         array or NULL entries are skipped. */
 int coalac_encode_ev(coalac_plan_t plan, const float* d_in, const float* d_base, int32_t* d_idx,
                      void* d_vals, float* d_mn, float* d_scale, void* d_ws, uint64_t ws_bytes,
@@ -136,8 +137,10 @@ int coalac_decode_ev(coalac_plan_t plan, const int32_t* d_idx, const void* d_val
  *           COALAC_STAGE_SCAN    k_scan   (the one HBM read of the large segments) 1 .. 2
  *           COALAC_STAGE_SELECT  k_ghist k_gwin k_select k_emit                  2 .. 4
  *   decode  COALAC_STAGE_BOUNDS  k_bounds (plans of > 8192 units; smaller    boundaries 0 .. 1
- *                                 plans: k_decode finds its units' entry ranges itself)
- *           COALAC_STAGE_DECODE  k_decode                                  1 .. 2
+ *                                 plans need no bounds)
+ *           COALAC_STAGE_DECODE  k_decode (plans of <= 8192 units: k_fill     1 .. 2
+ *                                 writes the background, then k_scatter the
+ *                                 kept values)
  * SAMPLE, SCAN, SELECT of one encode (and BOUNDS, DECODE of one decode) must run in this order on the
  * same workspace; SMALL is independent of them. The caller orders them, e.g. with the events below.
  * (A whole encode places the small segments itself: beside k_scan on the plan's side stream for big
