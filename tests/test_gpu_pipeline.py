@@ -172,3 +172,30 @@ def test_split_pipeline_single_update_segment_ranges(cuda, split, delta):
     torch.cuda.synchronize()
     check(t, enc, dec, oracle_roundtrip(t, flat.cpu().numpy(), 8, None if base is None else base.cpu().numpy()))
     assert pipe.fallbacks() == 0
+
+
+def test_split_pipelines_share_pooled_streams(cuda):
+    """Every SplitPipeline of a process takes sub-batch g's stream from one pool (pooled_streams): two
+    pipelines over different tables share them, and their unjoined calls, interleaved, stay correct (the
+    shared stream orders them) and equal single plans."""
+    from coala_amd.compression.pipeline import pooled_streams
+    ta = SegmentTable(fp32_sizes("resnet18"), 0.01, 4)
+    tb = SegmentTable(fp32_sizes("lenet"), 0.05, 6)
+    pa, pb = SplitPipeline(ta, 8, split=2, device=cuda), SplitPipeline(tb, 8, split=3, device=cuda)
+    pool = pooled_streams(cuda, 3)
+    assert pa.streams == pool[:2] and pb.streams == pool[:3]
+    fa, fb = synth_batch(ta, cuda), synth_batch(tb, cuda, client_ids=range(20, 26))
+    ea, oa = pa.empty_encoded(), pa.empty_flat().zero_()
+    eb, ob = pb.empty_encoded(), pb.empty_flat().zero_()
+    torch.cuda.synchronize()
+    for _ in range(3):
+        pa.roundtrip(fa, enc=ea, out=oa, joined=False)
+        pb.roundtrip(fb, enc=eb, out=ob, joined=False)
+    torch.cuda.synchronize()
+    for t, f, e, o in ((ta, fa, ea, oa), (tb, fb, eb, ob)):
+        plan = CodecPlan(None, t.ratio, 8, table=t, device=cuda)
+        e1 = plan.encode(f)
+        d1 = plan.decode(e1, out=torch.zeros_like(o))
+        torch.cuda.synchronize()
+        assert torch.equal(e1.idx, e.idx) and torch.equal(e1.vals, e.vals)
+        assert torch.equal(d1.view(torch.int32), o.view(torch.int32))
