@@ -2089,6 +2089,12 @@ DEV void wave_lower_bound(const int32_t* const (&L)[M], const uint32_t (&k)[M], 
 #ifndef DECODE_SCATTER
 #define DECODE_SCATTER 1  // latency-bound plans decode as k_fill + k_scatter (else k_decode with the search)
 #endif
+#ifndef DECODE_SCATTER_ALL
+#define DECODE_SCATTER_ALL 0  // experiment: batches decode as k_fill + k_scatter too
+#endif
+#ifndef FILL_AUX
+#define FILL_AUX 0  // k_fill store cache policy (0 plain, 2 non-temporal)
+#endif
 #ifndef DECODE_SEARCH_DPW
 #define DECODE_SEARCH_DPW 1u
 #endif
@@ -2219,10 +2225,10 @@ __global__ __launch_bounds__(BLOCK) void k_fill(Params P) {
   }
   if ((U.len & 3u) == 0) {
 #pragma unroll
-    for (uint32_t it = 0; it < UNIT_IT; ++it) unit_store_x4<0>(rout, (it * 64 + lane) * 16, b[it]);
+    for (uint32_t it = 0; it < UNIT_IT; ++it) unit_store_x4<FILL_AUX>(rout, (it * 64 + lane) * 16, b[it]);
   } else {
 #pragma unroll
-    for (uint32_t it = 0; it < UNIT_IT; ++it) unit_store_x1x4<0>(rout, (it * 64 + lane) * 16, b[it]);
+    for (uint32_t it = 0; it < UNIT_IT; ++it) unit_store_x1x4<FILL_AUX>(rout, (it * 64 + lane) * 16, b[it]);
   }
 }
 
@@ -3218,7 +3224,7 @@ int coalac_decode_sched(coalac_plan_t plan, const int32_t* d_idx, const void* d_
   // small plans: k_decode finds its units' entry ranges itself (one launch), or (DECODE_SCATTER) the
   // background and then the kept values; batches: k_bounds first
   const bool search = plan->n_units <= DECODE_SEARCH_MAX_UNITS;
-  const bool scatter = search && DECODE_SCATTER;
+  const bool scatter = (search || DECODE_SCATTER_ALL) && DECODE_SCATTER;
   const uint32_t upb = WAVES * (hb ? decode_dpw<true, false>()
                                    : search ? decode_dpw<false, true>() : decode_dpw<false, false>());  // units per block
   const uint32_t g = (plan->n_units + upb - 1) / upb;
