@@ -93,3 +93,20 @@ def test_subtable_extents():
     assert sub.total_k == int(t.segs[4, 3] + t.segs[4, 2])
     assert sub.span == int(t.segs[4, 0] + t.segs[4, 1])
     assert sub.n_elements == int(t.segs[2:5, 1].sum())
+
+
+def test_small_limit_follows_plan_size(monkeypatch):
+    """spec.small_limit mirrors coalac_plan_create: latency-bound plans (<= LATENCY_PLAN_UNITS units)
+    encode segments of up to SMALL_MAX_LATENCY elements whole, bigger plans up to SMALL_MAX; the
+    COALAC_SMALL_MAX override is clamped to [1024, SMALL_MAX]."""
+    monkeypatch.delenv("COALAC_SMALL_MAX", raising=False)
+    one = fp32_sizes("resnet50_tv")
+    assert spec.small_limit(one) == spec.SMALL_MAX_LATENCY
+    assert spec.small_limit(one * 2) == spec.SMALL_MAX
+    units = spec.LATENCY_PLAN_UNITS
+    assert spec.small_limit([spec.UNIT] * units) == spec.SMALL_MAX_LATENCY
+    assert spec.small_limit([spec.UNIT] * (units + 1)) == spec.SMALL_MAX
+    monkeypatch.setenv("COALAC_SMALL_MAX", "4096")
+    assert spec.small_limit(one) == 4096
+    monkeypatch.setenv("COALAC_SMALL_MAX", "10")
+    assert spec.small_limit(one) == 1024
