@@ -81,6 +81,12 @@ constexpr int SEL_NT = 256;               // threads of a k_select block (4 wave
 #ifndef SCAN_NB
 #define SCAN_NB 1  // load batches per k_scan unit (weights mode): 1 = all 16 float4 per lane in flight
 #endif
+#ifndef DECODE_XCD
+#define DECODE_XCD 1  // batch k_decode: XCD-aware unit order (xcd_block)
+#endif
+#ifndef SCAN_XCD
+#define SCAN_XCD 0    // k_scan: XCD-aware unit order
+#endif
 #ifndef LOAD_AUX
 #define LOAD_AUX 2   // cache policy of the streaming buffer loads (k_scan): 2 = non-temporal
 #endif
@@ -206,6 +212,15 @@ DEV float fmax_nan(float a, float b) { return __builtin_fmaxf(a, b); }
 DEV float qnan() { return __int_as_float(0x7FC00000); }
 
 DEV uint32_t lane_id() { return __lane_id(); }
+
+// XCD-aware block order: workgroups are dispatched round-robin over the 8 XCDs (block b on XCD b % 8); the
+// remapped index gives XCD x the x-th contiguous share of [0, gridDim.x) (a bijection for any grid size), so
+// each XCD streams through one region instead of every eighth 64 KiB. NT stores of the unit pattern, 1.5 GiB:
+// 5.56 -> 6.38 TB/s (tools/store_probe.hip); reads and ~100 MB buffers gain nothing.
+DEV uint32_t xcd_block(uint32_t b) {
+  const uint32_t nb = gridDim.x, q = nb / 8, r = nb % 8, x = b % 8, i = b / 8;
+  return x * q + min(x, r) + i;
+}
 
 // number of set bits of `m` in lanes below this lane
 DEV uint32_t mbcnt(uint64_t m) {
@@ -1010,7 +1025,7 @@ __global__ __launch_bounds__(BLOCK, SCAN_WPE) void k_scan(Params P) {
   }
   uint2* stage = reinterpret_cast<uint2*>(arena);
   const uint32_t wv = threadIdx.x >> 6;
-  const uint32_t lu = (blockIdx.x - P.scan_small) * WAVES + wv;
+  const uint32_t lu = ((SCAN_XCD && !WITH_SMALL ? xcd_block(blockIdx.x) : blockIdx.x) - P.scan_small) * WAVES + wv;
   if (lu >= P.n_lunits) return;
   const UnitDev L = P.lunits[lu];
   // delta: 4 load batches (32 float4 in flight spill)
@@ -2108,7 +2123,7 @@ template <bool RAW, bool HASBASE, bool SEARCH>
 __global__ __launch_bounds__(BLOCK, DECODE_WPE) void k_decode(Params P) {
   constexpr uint32_t DPW = decode_dpw<HASBASE, SEARCH>();
   const uint32_t lane = lane_id(), wv = threadIdx.x >> 6;
-  const uint32_t u0 = (blockIdx.x * WAVES + wv) * DPW;
+  const uint32_t u0 = ((DECODE_XCD && !SEARCH ? xcd_block(blockIdx.x) : blockIdx.x) * WAVES + wv) * DPW;
   if (u0 >= P.n_units) return;
   UnitDev U[DPW];
   uint32_t lo[DPW], hi[DPW];

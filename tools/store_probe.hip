@@ -71,6 +71,49 @@ __global__ __launch_bounds__(256) void unit_blk(float4* __restrict__ out, size_t
   for (int j = 0; j < 16; ++j) out[base + (j * 4 + wv) * 64 + lane] = make_float4(v, v, v, v);
 }
 
+// k_decode's pattern with an XCD-aware block order: workgroups are dispatched round-robin over the 8 XCDs, so
+// block b runs on XCD b % 8; remapped, XCD x writes the contiguous x-th eighth of the buffer (MODE 0: plain
+// global stores, 1: non-temporal buffer stores)
+template <int MODE>
+__global__ __launch_bounds__(256) void unit_x(float4* __restrict__ out, size_t n4, float v) {
+  const unsigned nb = gridDim.x, per = (nb + 7) / 8;
+  const unsigned b = (blockIdx.x % 8) * per + blockIdx.x / 8;
+  const size_t w = (size_t)b * 4 + (threadIdx.x >> 6);
+  const unsigned lane = threadIdx.x & 63;
+  const size_t base = w * 1024;
+  if (base >= n4) return;
+  if (MODE == 0) {
+#pragma unroll
+    for (int i = 0; i < 16; ++i) out[base + i * 64 + lane] = make_float4(v, v, v, v);
+  } else {
+    const __amdgpu_buffer_rsrc_t r = rsrc(out + base, 16384);
+    typedef unsigned int u4v __attribute__((ext_vector_type(4)));
+    const u4v a = {__float_as_uint(v), __float_as_uint(v), __float_as_uint(v), __float_as_uint(v)};
+#pragma unroll
+    for (int i = 0; i < 16; ++i) __builtin_amdgcn_raw_buffer_store_b128(a, r, (int)((i * 64 + lane) * 16), 0, 2);
+  }
+}
+
+// read probes: one wave per 16 KiB unit (k_scan's pattern), in dispatch order or XCD-remapped
+template <bool XCD>
+__global__ __launch_bounds__(256) void read_u(const float4* __restrict__ in, size_t n4, float* sink) {
+  const unsigned nb = gridDim.x, per = (nb + 7) / 8;
+  const unsigned b = XCD ? (blockIdx.x % 8) * per + blockIdx.x / 8 : blockIdx.x;
+  const size_t w = (size_t)b * 4 + (threadIdx.x >> 6);
+  const unsigned lane = threadIdx.x & 63;
+  const size_t base = w * 1024;
+  if (base >= n4) return;
+  typedef float f4v __attribute__((ext_vector_type(4)));
+  const f4v* src = reinterpret_cast<const f4v*>(in);
+  f4v x[16];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) x[i] = __builtin_nontemporal_load(src + base + i * 64 + lane);
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) s += x[i].x + x[i].y + x[i].z + x[i].w;
+  if (s == 12345.678f) sink[0] = s;
+}
+
 __global__ __launch_bounds__(256) void flat1(float4* __restrict__ out, size_t n4, float v) {
   const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
   if (i < n4) out[i] = make_float4(v, v, v, v);
@@ -88,7 +131,9 @@ int main(int argc, char** argv) {
     const size_t bytes = (size_t)atoll(argv[a]) << 20;
     const size_t n4 = bytes / 16;
     float4* out;
+    float* sink;
     CK(hipMalloc(&out, bytes));
+    CK(hipMalloc(&sink, 4));
     hipEvent_t e0, e1;
     CK(hipEventCreate(&e0));
     CK(hipEventCreate(&e1));
@@ -114,6 +159,10 @@ int main(int argc, char** argv) {
     run("unit_n8", [&] { hipLaunchKernelGGL(unit_n<8>, dim3((unsigned)((n4 / 512 + 3) / 4)), dim3(256), 0, 0, out, n4, 1.0f); });
     run("unit_n2", [&] { hipLaunchKernelGGL(unit_n<2>, dim3((unsigned)((n4 / 128 + 3) / 4)), dim3(256), 0, 0, out, n4, 1.0f); });
     run("unit_blk", [&] { hipLaunchKernelGGL(unit_blk, dim3((unsigned)((n4 + 4095) / 4096)), dim3(256), 0, 0, out, n4, 1.0f); });
+    run("unit_xg", [&] { hipLaunchKernelGGL(unit_x<0>, dim3(gu), dim3(256), 0, 0, out, n4, 1.0f); });
+    run("unit_xbnt", [&] { hipLaunchKernelGGL(unit_x<1>, dim3(gu), dim3(256), 0, 0, out, n4, 1.0f); });
+    run("read_u", [&] { hipLaunchKernelGGL(read_u<false>, dim3(gu), dim3(256), 0, 0, out, n4, sink); });
+    run("read_ux", [&] { hipLaunchKernelGGL(read_u<true>, dim3(gu), dim3(256), 0, 0, out, n4, sink); });
     run("flat1", [&] { hipLaunchKernelGGL(flat1, dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, 0, out, n4, 1.0f); });
     run("gs", [&] { hipLaunchKernelGGL(gs, dim3(cus * 8), dim3(256), 0, 0, out, n4, 1.0f); });
     CK(hipFree(out));
