@@ -94,6 +94,24 @@ __global__ __launch_bounds__(256) void unit_x(float4* __restrict__ out, size_t n
   }
 }
 
+// XCD-aware order in chunks: XCD x takes chunks x, x + 8, x + 16, ... of C blocks (64 KiB each), so every
+// XCD streams through C contiguous blocks at a time while all XCDs advance through the buffer together
+// (the probe's grids are multiples of 8 * C)
+template <int C>
+__global__ __launch_bounds__(256) void unit_xc(float4* __restrict__ out, size_t n4, float v) {
+  const unsigned x = blockIdx.x % 8, i = blockIdx.x / 8;
+  const unsigned b = ((i / C) * 8 + x) * C + i % C;
+  const size_t w = (size_t)b * 4 + (threadIdx.x >> 6);
+  const unsigned lane = threadIdx.x & 63;
+  const size_t base = w * 1024;
+  if (base >= n4) return;
+  const __amdgpu_buffer_rsrc_t r = rsrc(out + base, 16384);
+  typedef unsigned int u4v __attribute__((ext_vector_type(4)));
+  const u4v a = {__float_as_uint(v), __float_as_uint(v), __float_as_uint(v), __float_as_uint(v)};
+#pragma unroll
+  for (int i2 = 0; i2 < 16; ++i2) __builtin_amdgcn_raw_buffer_store_b128(a, r, (int)((i2 * 64 + lane) * 16), 0, 2);
+}
+
 // read probes: one wave per 16 KiB unit (k_scan's pattern), in dispatch order or XCD-remapped
 template <bool XCD>
 __global__ __launch_bounds__(256) void read_u(const float4* __restrict__ in, size_t n4, float* sink) {
@@ -161,6 +179,9 @@ int main(int argc, char** argv) {
     run("unit_blk", [&] { hipLaunchKernelGGL(unit_blk, dim3((unsigned)((n4 + 4095) / 4096)), dim3(256), 0, 0, out, n4, 1.0f); });
     run("unit_xg", [&] { hipLaunchKernelGGL(unit_x<0>, dim3(gu), dim3(256), 0, 0, out, n4, 1.0f); });
     run("unit_xbnt", [&] { hipLaunchKernelGGL(unit_x<1>, dim3(gu), dim3(256), 0, 0, out, n4, 1.0f); });
+    run("unit_xc16", [&] { hipLaunchKernelGGL(unit_xc<16>, dim3(gu), dim3(256), 0, 0, out, n4, 1.0f); });
+    run("unit_xc64", [&] { hipLaunchKernelGGL(unit_xc<64>, dim3(gu), dim3(256), 0, 0, out, n4, 1.0f); });
+    run("unit_xc256", [&] { hipLaunchKernelGGL(unit_xc<256>, dim3(gu), dim3(256), 0, 0, out, n4, 1.0f); });
     run("read_u", [&] { hipLaunchKernelGGL(read_u<false>, dim3(gu), dim3(256), 0, 0, out, n4, sink); });
     run("read_ux", [&] { hipLaunchKernelGGL(read_u<true>, dim3(gu), dim3(256), 0, 0, out, n4, sink); });
     run("flat1", [&] { hipLaunchKernelGGL(flat1, dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, 0, out, n4, 1.0f); });
