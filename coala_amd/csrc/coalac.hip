@@ -87,6 +87,9 @@ constexpr int SEL_NT = 256;               // threads of a k_select block (4 wave
 #ifndef SCAN_XCD
 #define SCAN_XCD 0    // k_scan: XCD-aware unit order
 #endif
+#ifndef SCAN_HIST
+#define SCAN_HIST 1  // latency-bound plans: k_scan accumulates the group band histograms (no k_ghist)
+#endif
 #ifndef LOAD_AUX
 #define LOAD_AUX 2   // cache policy of the streaming buffer loads (k_scan): 2 = non-temporal
 #endif
@@ -156,6 +159,9 @@ struct Params {
   uint32_t *tstar, *rtie, *status;
   // per large unit
   uint32_t *tlo, *thi, *cntA, *cntC, *gtC, *eqC, *eqpre, *outoff;
+  uint32_t* thh;        // [n_lunits] histogram upper bound of the unit's segment (= shhi; scan_hist only)
+  uint32_t scan_hist;   // latency-bound plans: k_scan accumulates the group band histograms (no k_ghist); the
+                        // samplers zero them first
   uint2* cand;  // candidate records {index | A_FLAG, value bits}, ccap slots per large unit
   uint32_t ccap;  // record slots per large unit (< UNIT: a unit that finds more candidates overflows and its
                   // segment is selected and emitted from the raw data instead)
@@ -606,6 +612,20 @@ DEV uint32_t hash32(uint32_t x) {
   return x;
 }
 
+// Group-histogram geometry of a segment: bins of 2^shift keys over [tlo, hhi]; keys in (hhi, thi] are
+// clamped into the last bin, whose key window therefore ends at thi.
+struct Band {
+  uint32_t tlo, thi, hhi, last;
+  int shift;
+  DEV Band(uint32_t lo, uint32_t hi, uint32_t hh) : tlo(lo), thi(hi), hhi(hh) {
+    shift = band_shift(lo, hh, 9);
+    last = (hh - lo) >> shift;
+  }
+  DEV uint32_t bin(uint32_t key) const { return key > hhi ? last : (key - tlo) >> shift; }
+  DEV uint32_t wlo(uint32_t b) const { return tlo + (b << shift); }
+  DEV uint32_t whi(uint32_t b) const { return b == last ? thi : min(thi, wlo(b) + ((1u << shift) - 1u)); }
+};
+
 // ------------------------------------------------------------------------------------------------
 // streaming classify + ordered compaction of one large unit by one wave (k_scan, exact fallback)
 // Candidates (key >= tlo) are written in index order as 8-byte records {index | A_FLAG, value}; A_FLAG
@@ -618,8 +638,11 @@ DEV uint32_t hash32(uint32_t x) {
 // SC1 (k_fused): records and counts are stored write-through for the in-launch hand-off to the select
 // phases. get_t() returns {T_lo, T_hi}; it is called once the first batch of loads is in flight (k_fused
 // waits there for the sampler).
-template <bool DELTA, int NB, bool SC1 = false, class GetT>
-DEV void scan_unit_t(const Params& P, uint32_t lu, const UnitDev& L, GetT&& get_t, uint2* stage) {
+// HIST (latency-bound plans): every stored band record (not A) is also counted into its group's band
+// histogram `gh` (HB2 bins of `band`) with a device-scope atomic add, replacing k_ghist's pass.
+template <bool DELTA, int NB, bool SC1 = false, bool HIST = false, class GetT>
+DEV void scan_unit_t(const Params& P, uint32_t lu, const UnitDev& L, GetT&& get_t, uint2* stage,
+                     uint32_t* gh = nullptr, const Band* band = nullptr) {
   constexpr uint32_t IT = UNIT_IT / NB;
   const uint32_t lane = lane_id();
   const uint32_t len = L.len;
@@ -639,6 +662,7 @@ DEV void scan_unit_t(const Params& P, uint32_t lu, const UnitDev& L, GetT&& get_
       st_sc1(R + i, rec);
     else
       R[i] = rec;
+    if (HIST && !(rec.x & A_FLAG)) atomicAdd(gh + band->bin(rec.y & KEY_MAX), 1u);
   };
 
   for (uint32_t nb = 0; nb < (uint32_t)NB; ++nb) {
@@ -964,6 +988,7 @@ DEV void sample_segment(const Params& P, uint32_t li, uint32_t* hist, uint32_t* 
     thi = (uint32_t)min<uint64_t>(edge, kmax);
   }
   const uint32_t nu = sd.unit_end - sd.unit_begin;
+  const uint32_t hh = max(tlo, min(thi, kmax));  // the band histograms' upper bound (see below)
   for (uint32_t i = t; i < nu; i += NT) {
     if (SC1) {
       st_sc1(P.tlo + sd.lu_begin + i, tlo);
@@ -971,15 +996,20 @@ DEV void sample_segment(const Params& P, uint32_t li, uint32_t* hist, uint32_t* 
     } else {
       P.tlo[sd.lu_begin + i] = tlo;
       P.thi[sd.lu_begin + i] = thi;
+      if (P.scan_hist) P.thh[sd.lu_begin + i] = hh;
     }
+  }
+  if (!SC1 && P.scan_hist) {  // k_scan adds into the segment's group histograms
+    const uint32_t ng = (nu + GU - 1) / GU;
+    for (uint32_t i = t; i < ng * HB2; i += NT) P.ghist[(uint64_t)sd.g_begin * HB2 + i] = 0;
   }
   // The band histograms of the parallel select span [T_lo, min(T_hi, max sampled key)] (keys above go
   // to the last bin): with T_hi = KEY_MAX a full-range histogram would be too coarse.
   if (t == 0) {
     if (SC1) {
-      st_sc1(P.shhi + li, max(tlo, min(thi, kmax)));
+      st_sc1(P.shhi + li, hh);
     } else {
-      P.shhi[li] = max(tlo, min(thi, kmax));
+      P.shhi[li] = hh;
       P.status[s] = 0;  // (k_fused: the control block, status included, is zeroed before the launch)
     }
   }
@@ -1010,7 +1040,7 @@ __global__ __launch_bounds__(BLOCK) void k_presel(Params P) {
 
 // k_scan: streams the large units, one wave each. (WITH_SMALL: blocks [0, scan_small) first encode the
 // small segments — no longer launched: k_presel runs them beside the samplers.)
-template <bool DELTA, bool RAW, bool WITH_SMALL>
+template <bool DELTA, bool RAW, bool WITH_SMALL, bool HIST = false>
 __global__ __launch_bounds__(BLOCK, SCAN_WPE) void k_scan(Params P) {
   // one LDS arena: candidate staging (WAVES x STAGE_CAP records) or a small segment's values + histogram
   // (WITH_SMALL only: without it the block needs 16 KB of LDS instead of 24.8 KB)
@@ -1029,7 +1059,15 @@ __global__ __launch_bounds__(BLOCK, SCAN_WPE) void k_scan(Params P) {
   if (lu >= P.n_lunits) return;
   const UnitDev L = P.lunits[lu];
   // delta: 4 load batches (32 float4 in flight spill)
-  scan_unit<DELTA, DELTA ? 4 : SCAN_NB>(P, lu, L, P.tlo[lu], P.thi[lu], stage + wv * STAGE_CAP);
+  if (HIST) {
+    const uint32_t tlo = P.tlo[lu], thi = P.thi[lu];
+    const Band band(tlo, thi, P.thh[lu]);
+    uint32_t* gh = P.ghist + (uint64_t)P.lgroup[lu] * HB2;
+    scan_unit_t<DELTA, DELTA ? 4 : SCAN_NB, false, true>(P, lu, L, [&]() { return make_uint2(tlo, thi); },
+                                                          stage + wv * STAGE_CAP, gh, &band);
+  } else {
+    scan_unit<DELTA, DELTA ? 4 : SCAN_NB>(P, lu, L, P.tlo[lu], P.thi[lu], stage + wv * STAGE_CAP);
+  }
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -1224,20 +1262,6 @@ DEV void select_generic(const Params& P, uint32_t lb, uint32_t nu, uint32_t tlo,
 // ------------------------------------------------------------------------------------------------
 // parallel select, fast path: groups of GU units of one large segment, one 256-thread block each
 // ------------------------------------------------------------------------------------------------
-// Group-histogram geometry of a segment: bins of 2^shift keys over [tlo, hhi]; keys in (hhi, thi] are
-// clamped into the last bin, whose key window therefore ends at thi.
-struct Band {
-  uint32_t tlo, thi, hhi, last;
-  int shift;
-  DEV Band(uint32_t lo, uint32_t hi, uint32_t hh) : tlo(lo), thi(hi), hhi(hh) {
-    shift = band_shift(lo, hh, 9);
-    last = (hh - lo) >> shift;
-  }
-  DEV uint32_t bin(uint32_t key) const { return key > hhi ? last : (key - tlo) >> shift; }
-  DEV uint32_t wlo(uint32_t b) const { return tlo + (b << shift); }
-  DEV uint32_t whi(uint32_t b) const { return b == last ? thi : min(thi, wlo(b) + ((1u << shift) - 1u)); }
-};
-
 // k_ghist: the group's HB2-bin histogram of the band keys [tlo, thi] -> ghist[group]. (A fused variant in
 // which the segment's last-arriving group block ran segment_pick needed an agent-scope release fence in
 // every block — an L2 writeback on gfx950 — and was ~100x slower; kernel boundaries are cheaper.)
@@ -2509,7 +2533,7 @@ struct WsLayout {
   size_t ctl_bytes;  // the control block at offset 0: status and the k_fused hand-off words
   size_t status, hf_sampled, hf_ghist, hf_gwin, hf_sel, hf_err, hf_garr;
   size_t tstar, rtie;
-  size_t tlo, thi, cntA, cntC, gtC, eqC, eqpre, outoff;
+  size_t tlo, thi, thh, cntA, cntC, gtC, eqC, eqpre, outoff;
   size_t cand, stamps, ghist, gcnt, glist, gmm, sstate, shhi, istamps;
   size_t total;
 };
@@ -2537,6 +2561,7 @@ WsLayout ws_layout(size_t S, size_t LU, size_t NG, size_t NL, size_t NI, uint32_
   L.rtie = take(4 * S);
   L.tlo = take(4 * LU);
   L.thi = take(4 * LU);
+  L.thh = take(4 * LU);
   L.cntA = take(4 * LU);
   L.cntC = take(4 * LU);
   L.gtC = take(4 * LU);
@@ -2812,11 +2837,15 @@ int launch_encode(const Params& P, coalac_plan_t plan, hipStream_t st, const coa
   if (split && (stages & COALAC_STAGE_SMALL) && plan->n_small)
     hipLaunchKernelGGL((k_small<DELTA, RAW>), dim3(plan->n_small), dim3(BLOCK), 0, st, P);
   ENC_BOUNDARY(1);
-  if ((stages & COALAC_STAGE_SCAN) && gu)
-    hipLaunchKernelGGL((k_scan<DELTA, RAW, false>), dim3(gu), dim3(BLOCK), 0, st, Q);
+  if ((stages & COALAC_STAGE_SCAN) && gu) {
+    if (P.scan_hist)
+      hipLaunchKernelGGL((k_scan<DELTA, RAW, false, true>), dim3(gu), dim3(BLOCK), 0, st, Q);
+    else
+      hipLaunchKernelGGL((k_scan<DELTA, RAW, false>), dim3(gu), dim3(BLOCK), 0, st, Q);
+  }
   ENC_BOUNDARY(2);
   if ((stages & COALAC_STAGE_SELECT) && plan->n_large) {
-    hipLaunchKernelGGL(k_ghist, dim3(plan->n_groups), dim3(BLOCK), 0, st, P);
+    if (!P.scan_hist) hipLaunchKernelGGL(k_ghist, dim3(plan->n_groups), dim3(BLOCK), 0, st, P);
     hipLaunchKernelGGL(k_gwin, dim3(plan->n_groups), dim3(BLOCK), 0, st, P);
     hipLaunchKernelGGL((k_select<DELTA, RAW>), dim3(plan->n_large), dim3(SEL_NT), 0, st, P);
   }
@@ -3125,6 +3154,7 @@ int encode_impl(coalac_plan_t plan, const float* d_in, const float* const* d_inp
   P.status = reinterpret_cast<uint32_t*>(w + L.status);
   P.tlo = reinterpret_cast<uint32_t*>(w + L.tlo);
   P.thi = reinterpret_cast<uint32_t*>(w + L.thi);
+  P.thh = reinterpret_cast<uint32_t*>(w + L.thh);
   P.cntA = reinterpret_cast<uint32_t*>(w + L.cntA);
   P.cntC = reinterpret_cast<uint32_t*>(w + L.cntC);
   P.gtC = reinterpret_cast<uint32_t*>(w + L.gtC);
@@ -3146,6 +3176,8 @@ int encode_impl(coalac_plan_t plan, const float* d_in, const float* const* d_inp
   const bool one = whole && (flags & COALAC_FLAG_ONE_LAUNCH) && !(flags & COALAC_FLAG_STAMPS) && plan->n_items > 0;
   const bool front = whole && !one && (flags & COALAC_FLAG_FRONT_LAUNCH) && !(flags & COALAC_FLAG_STAMPS) &&
                      plan->n_front > 0;
+  // the kernel sequence of a latency-bound plan: band histograms from k_scan (one launch less)
+  P.scan_hist = (!one && !front && SCAN_HIST && plan->n_lunits <= LATENCY_PLAN_UNITS) ? 1u : 0u;
   if (front) {
     if (delta && raw)
       rc = launch_front<true, true>(P, plan, st, sched, d_ws);
