@@ -82,6 +82,9 @@ def parse():
     p.add_argument("--single-split", type=int, default=SINGLE_SPLIT,
                    help="config 'single': the update's segments cut into this many ranges, each a sub-plan on its "
                         "own stream (their latency-bound phases overlap)")
+    p.add_argument("--prefill", choices=["none", "start", "scan", "small"], default="none",
+                   help="latency-bound plans (single, C5): the decode's background (k_fill) on a second stream beside "
+                        "the encode, from the step's start or from the end of k_scan (SplitPipeline prefill)")
     p.add_argument("--cpu-seconds", type=float, default=8.0, help="CPU baseline time budget per leg")
     p.add_argument("--no-cpu-baseline", action="store_true")
     return p.parse_args()
@@ -251,7 +254,8 @@ def run_workload(cfg, a, dev, world, rank, headline):
         if a.pipe == "lane" and headline:
             p = LanePipeline(t, a.bits, lanes=split, device=dev, flags=a.flags)
         else:
-            p = SplitPipeline(t, a.bits, split=split, device=dev, flags=a.flags, fork=a.fork)
+            p = SplitPipeline(t, a.bits, split=split, device=dev, flags=a.flags, fork=a.fork,
+                              prefill=None if a.prefill == "none" else a.prefill)
         slots.append((p, p.empty_encoded(), p.empty_flat()))
     split = slots[0][0].n_parts
     pipes = [s[0] for s in slots]
@@ -321,8 +325,10 @@ def run_workload(cfg, a, dev, world, rank, headline):
     one = bool(a.flags & ONE_LAUNCH)
     multi = not one and not (a.flags & FRONT_LAUNCH)
     enc_kernel = "k_scan" if multi else "k_fused" if one else "k_front"
+    # prefill: the decode events bracket the background write (k_fill) on its own stream
+    dec_kernel = "k_fill" if any("fill" in q for q in getattr(pipes[0], "parts", [])) else "k_decode"
     stages = {}
-    for name, which in {enc_kernel: ev_e, "k_decode": ev_d}.items():
+    for name, which in {enc_kernel: ev_e, dec_kernel: ev_d}.items():
         per = [union([(e[1], e[2]) for e in which[i]]) for i in timed_steps]
         stages[name] = sum(per) / len(per)
     N, K, T = t.n_elements, t.total_k, t.n_segments
@@ -333,7 +339,9 @@ def run_workload(cfg, a, dev, world, rank, headline):
     alg = {  # algorithmic HBM bytes per timed interval
         enc_kernel: (4 * large_elems if multi else 4 * N + (4 + vb) * K + 8 * T if one else 4 * N) + (4 * N if delta else 0),
         "k_decode": 4 * N * (2 if delta else 1) + (4 + vb) * K + 8 * T,
+        "k_fill": 4 * N * (2 if delta else 1),
     }
+    alg = {k: alg[k] for k in stages}
     dom = max(alg, key=lambda k: stages[k])
     ach = alg[dom] / (stages[dom] * 1e-3) / 1e9
     step_ms = el / a.steps * 1e3

@@ -18,7 +18,7 @@ COALAC_FLAG_ONE_LAUNCH = 64    # the whole encode as one k_fused launch (select 
 COALAC_FLAG_FRONT_LAUNCH = 128 # samplers + scan + small segments as one launch, then the select kernels
 # stages of a split encode / decode (coalac_sched_t.stages; 0 = all)
 COALAC_STAGE_SAMPLE, COALAC_STAGE_SCAN, COALAC_STAGE_SELECT, COALAC_STAGE_SMALL = 1, 2, 4, 8
-COALAC_STAGE_BOUNDS, COALAC_STAGE_DECODE = 1, 2
+COALAC_STAGE_BOUNDS, COALAC_STAGE_DECODE, COALAC_STAGE_FILL, COALAC_STAGE_SCATTER = 1, 2, 4, 8
 COALAC_AGG_DIV = 0     # acc / total            (torch CPU division by a scalar)
 COALAC_AGG_RECIP = 1   # acc * (1.0f / total)   (torch GPU division by a host scalar)
 COALAC_AGG_SUM = 2     # acc                    (weighted_sum: the multi-GPU per-rank sum)

@@ -88,7 +88,9 @@ constexpr int SEL_NT = 256;               // threads of a k_select block (4 wave
 #define SCAN_XCD 0    // k_scan: XCD-aware unit order
 #endif
 #ifndef SCAN_HIST
-#define SCAN_HIST 1  // latency-bound plans: k_scan accumulates the group band histograms (no k_ghist)
+#define SCAN_HIST 0  // latency-bound plans: k_scan accumulates the group band histograms (no k_ghist). Off:
+                     // the per-record device atomics made one update's k_scan 25.0 -> 33.2 us for k_ghist's
+                     // 6.4 (single update 0.0897 -> 0.0927 ms)
 #endif
 #ifndef LOAD_AUX
 #define LOAD_AUX 2   // cache policy of the streaming buffer loads (k_scan): 2 = non-temporal
@@ -3244,12 +3246,20 @@ int coalac_decode_sched(coalac_plan_t plan, const int32_t* d_idx, const void* d_
                         const float* d_scale, const float* d_base, float* d_out, void* d_ws, uint64_t ws_bytes,
                         void* stream, const coalac_sched_t* sched) {
   const unsigned all = COALAC_STAGE_BOUNDS | COALAC_STAGE_DECODE;
-  const unsigned stages = (sched && (sched->stages & all)) ? (sched->stages & all) : all;
+  const unsigned known = all | COALAC_STAGE_FILL | COALAC_STAGE_SCATTER;
+  unsigned stages = (sched && (sched->stages & known)) ? (sched->stages & known) : all;
+  // DECODE = FILL + SCATTER: the background (k_fill) and the kept values (k_scatter, or k_decode for plans
+  // that merge the background in registers) as separately enqueued parts
+  if (stages & COALAC_STAGE_DECODE) stages |= COALAC_STAGE_FILL | COALAC_STAGE_SCATTER;
+  if (stages & (COALAC_STAGE_FILL | COALAC_STAGE_SCATTER)) stages |= COALAC_STAGE_DECODE;
   if (!plan) return fail(COALAC_EINVAL, "coalac_decode: plan is NULL");
   if (plan->n_units == 0) return COALAC_OK;
   if (!d_out) return fail(COALAC_EINVAL, "coalac_decode: output pointer is NULL");
-  if (plan->total_k && (!d_idx || !d_vals)) return fail(COALAC_EINVAL, "coalac_decode: idx/vals pointers are NULL");
-  if (plan->bits != 32 && (!d_mn || !d_scale)) return fail(COALAC_EINVAL, "coalac_decode: mn/scale pointers are NULL");
+  const bool payload = (stages & (COALAC_STAGE_BOUNDS | COALAC_STAGE_SCATTER)) != 0;  // reads the encoded arrays
+  if (payload && plan->total_k && (!d_idx || !d_vals))
+    return fail(COALAC_EINVAL, "coalac_decode: idx/vals pointers are NULL");
+  if (payload && plan->bits != 32 && (!d_mn || !d_scale))
+    return fail(COALAC_EINVAL, "coalac_decode: mn/scale pointers are NULL");
   if ((reinterpret_cast<uintptr_t>(d_out) | reinterpret_cast<uintptr_t>(d_base)) & 15)
     return fail(COALAC_EINVAL, "coalac_decode: output/base must be 16-byte aligned");
   if (!d_ws || ws_bytes < plan->dec_ws)
@@ -3298,11 +3308,13 @@ int coalac_decode_sched(coalac_plan_t plan, const int32_t* d_idx, const void* d_
     ;
   else if (scatter) {
     const uint32_t gf = (plan->n_units + WAVES - 1) / WAVES;
-    if (hb)
+    if (!(stages & COALAC_STAGE_FILL))
+      ;
+    else if (hb)
       hipLaunchKernelGGL((k_fill<true>), dim3(gf), dim3(BLOCK), 0, st, P);
     else
       hipLaunchKernelGGL((k_fill<false>), dim3(gf), dim3(BLOCK), 0, st, P);
-    if (plan->n_bchunks) {
+    if (plan->n_bchunks && (stages & COALAC_STAGE_SCATTER)) {
       const dim3 gs(plan->n_bchunks);
       if (raw && hb)
         hipLaunchKernelGGL((k_scatter<true, true>), gs, dim3(BLOCK), 0, st, P, plan->schunks);
@@ -3313,7 +3325,9 @@ int coalac_decode_sched(coalac_plan_t plan, const int32_t* d_idx, const void* d_
       else
         hipLaunchKernelGGL((k_scatter<false, false>), gs, dim3(BLOCK), 0, st, P, plan->schunks);
     }
-  } else if (raw && hb)
+  } else if (!(stages & COALAC_STAGE_SCATTER))
+    ;  // FILL alone: k_decode writes the background itself
+  else if (raw && hb)
     DEC(true, true);
   else if (raw)
     DEC(true, false);

@@ -141,6 +141,13 @@ int coalac_decode_ev(coalac_plan_t plan, const int32_t* d_idx, const void* d_val
  *           COALAC_STAGE_DECODE  k_decode (plans of <= 8192 units: k_fill     1 .. 2
  *                                 writes the background, then k_scatter the
  *                                 kept values)
+ *           COALAC_STAGE_FILL    the background only (k_fill: 0, or the base)  1 .. 2
+ *                                 of a plan of <= 8192 units; it reads no
+ *                                 encoded array, so it may run before the
+ *                                 payload exists. Other plans: nothing.
+ *           COALAC_STAGE_SCATTER the kept values only (k_scatter), after a     1 .. 2
+ *                                 FILL of the same d_out / d_base; other plans:
+ *                                 the whole k_decode. FILL + SCATTER = DECODE.
  * SAMPLE, SCAN, SELECT of one encode (and BOUNDS, DECODE of one decode) must run in this order on the
  * same workspace; SMALL is independent of them. The caller orders them, e.g. with the events below.
  * (A whole encode places the small segments itself: beside k_scan on the plan's side stream for big
@@ -156,7 +163,9 @@ enum {
   COALAC_STAGE_SELECT = 4,
   COALAC_STAGE_SMALL = 8,
   COALAC_STAGE_BOUNDS = 1,
-  COALAC_STAGE_DECODE = 2
+  COALAC_STAGE_DECODE = 2,
+  COALAC_STAGE_FILL = 4,
+  COALAC_STAGE_SCATTER = 8
 };
 typedef struct coalac_sched {
   void* wait[5];
