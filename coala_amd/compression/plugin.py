@@ -32,6 +32,14 @@ Behaviour:
     + decoded delta, fused in the decode kernel); anything else (plain modules, splitFL feature dicts,
     server/service.py:124-131) passes through unchanged. Safe to call from several threads
     (server/service.py:74 spawns one per upload).
+  * splitFL cut-layer features (opt-in, `codec_features = True`): the splitFL client uploads its
+    features as `{"content": [feature, label], "name": [...]}` through marshal_data("feature_label")
+    (application/splitFL/client/base_sfl.py:248-257) and the server reads them back through
+    decompression(codec.unmarshal(data)) (application/splitFL/server/base_sfl.py:207-209). With the flag,
+    the client mixin's marshal_data encodes the feature tensor on its training device (weights mode, no
+    dense .cpu() copy) into a CompressedUpdate that stands where the tensor stood, and the server mixin's
+    decompression decodes it back to a dense tensor of the same shape; labels and other entries travel
+    unchanged. Without the flag (default) the dict passes through exactly as before.
   * download direction (opt-in, `codec_download = True`): server compression()
     encodes the global model once per round into a CompressedModel (download.py) that stands where the
     global module stood during distribution; aggregation() restores the real module first. Client
@@ -39,12 +47,35 @@ Behaviour:
     set_model's load_state_dict). Delta-mode uploads are decoded against the server's reconstruction of
     its own download, which is bit-identical to what the clients decoded.
 """
+import copy
+import pickle
 import threading
 
 from torch import nn
 
 from .codec import CompressedUpdate, UpdateCodec
 from .download import CompressedModel, compress_model
+
+DATA_TYPE_FEATURE = 2  # coala/pb/common.proto: DataType.DATA_TYPE_FEATURE (protos/coala/pb/common.proto:26)
+FEATURE_CONTENT = "feature_label"  # application/splitFL/client/base_sfl.py:252
+
+
+def _marshal(obj):
+    """The reference's codec.marshal (coala/protocol/codec.py:4-5) when COALA is installed, else its
+    restatement (pickle.dumps)."""
+    try:
+        from coala.protocol.codec import marshal
+    except ImportError:
+        marshal = pickle.dumps
+    return marshal(obj)
+
+
+def _data_type_feature():
+    try:
+        from coala.pb import common_pb2
+        return common_pb2.DATA_TYPE_FEATURE
+    except ImportError:
+        return DATA_TYPE_FEATURE
 
 EQUAL_AVERAGE = "equal"                     # coala/server/base.py:37
 TRAIN_UPLOAD_COMPRESSION_RATIO = "train_upload_compression_ratio"  # tracked next to metric.TRAIN_UPLOAD_SIZE
@@ -72,6 +103,33 @@ class _CodecOwner:
 
 class CompressionClientMixin(_CodecOwner):
     """Mix in before coala's BaseClient: `class Client(CompressionClientMixin, BaseClient)`."""
+
+    codec_features = False        # splitFL: compress the uploaded cut-layer features as well
+    codec_feature_ratio = None    # their top-k ratio (None: codec_ratio)
+    codec_feature_bits = None     # their code width (None: codec_bits)
+
+    def _feature_codec(self):
+        c = self.__dict__.get("_feature_update_codec")
+        if c is None:
+            ratio = self.codec_feature_ratio if self.codec_feature_ratio is not None else self.codec_ratio
+            bits = self.codec_feature_bits if self.codec_feature_bits is not None else self.codec_bits
+            c = UpdateCodec(ratio, bits, "weights", self.codec_backend)
+            self.__dict__["_feature_update_codec"] = c
+        return c
+
+    def marshal_data(self, content):
+        """splitFL's upload serialiser (application/splitFL/client/base_sfl.py:248-257) with the feature
+        tensor encoded: the same dict, the same DATA_TYPE_FEATURE, a CompressedUpdate where the dense
+        `feature.detach().cpu()` was. Model uploads ("model") and uncompressed runs go to the parent."""
+        feature = getattr(self, "feature", None)
+        parent = getattr(super(), "marshal_data", None)
+        if content != FEATURE_CONTENT or not self.codec_features or feature is None:
+            if parent is None:
+                raise AttributeError("marshal_data: no parent implementation (not a splitFL client)")
+            return parent(content)
+        carrier = self._feature_codec().encode({"feature": feature.detach()})
+        customize_dict = {"content": [carrier, copy.deepcopy(self.label)], "name": ["feature", "label"]}
+        return _marshal(customize_dict), _data_type_feature()
 
     def set_model(self, model):
         # a compressed download decodes with this client's codec backend (inside the reference's
@@ -217,7 +275,28 @@ class CompressionServerMixin(_CodecOwner):
             if self.codec_fused_aggregate:
                 return model  # decoded together with the other uploads in aggregate()
             return self._decode_upload(model)
+        if isinstance(model, dict) and isinstance(model.get("content"), list):
+            return self._decode_features(model)
         return model
+
+    def _decode_features(self, upload):
+        """A splitFL feature upload (application/splitFL/server/base_sfl.py:207-209): every CompressedUpdate
+        in "content" (the client mixin's encoded features) back to a dense tensor of its shape on the
+        codec's device; everything else unchanged. A new dict; the received one is not modified."""
+        content = upload["content"]
+        if not any(isinstance(c, CompressedUpdate) for c in content):
+            return upload
+        codec = self._codec()
+        out = dict(upload)
+        out["content"] = [self._decode_feature(codec, c) if isinstance(c, CompressedUpdate) else c for c in content]
+        return out
+
+    @staticmethod
+    def _decode_feature(codec, carrier):
+        entries = carrier.header["entries"]
+        if carrier.header["mode"] != "weights" or len(entries) != 1:
+            raise ValueError("a splitFL feature carrier holds one tensor in weights mode")
+        return codec.decode_state(carrier)[entries[0]["name"]]
 
     def aggregate(self, models, weights):
         """server/base.py:573-601 with the fused decode: FedAvg in one kernel (single process), or in a
