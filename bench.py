@@ -13,6 +13,8 @@ collective on the data path — torch.distributed only for the barrier and the m
           client-side models at cut 1/2/4 + feature tensors up to 8,388,608 elements), MixedTable
   single  ONE ResNet-50 update per step, steps serialised (north_star's "a 25.6 M-param fp32 update at
           1 GPU"; latency-bound)
+  single_x2  ONE ResNet-50 update per step, two steps in flight on two streams (a server decoding
+          concurrent uploads, one thread each: coala/server/service.py:71-111)
   plugin  the hooks' own path per ResNet-50 client, delta mode: client compression() encoding the trained
           module's parameters in place + server decompression(model) into a new module on w_global
 value = 4 * N * clients * steps / elapsed (GB/s of fp32 update processed, whole job).
@@ -45,9 +47,13 @@ CONFIGS = {  # name -> (layout | "c5", clients per GPU, sub-batches: the best of
     "C4": ("vit_b16", 16, SPLIT),
     "C5": ("c5", None, 1),  # one latency-bound plan (<= 8192 units): 0.116 ms vs 0.122 as 2 sub-batches
     "single": ("resnet50_tv", 1, "single"),
+    "single_x2": ("resnet50_tv", 1, "single"),
 }
+# updates in flight per extra config: single_x2 = one update per step, consecutive steps on two streams (a
+# server decodes concurrent uploads from one thread each, coala/server/service.py:71-111)
+CONFIG_INFLIGHT = {"single_x2": 2}
 SINGLE_SPLIT = 1  # segment ranges of the single update run as this many concurrent sub-plans
-DEFAULT_EXTRAS = "C2,C4,C5,single,plugin"
+DEFAULT_EXTRAS = "C2,C4,C5,single,single_x2,plugin"
 
 
 def parse():
@@ -82,9 +88,6 @@ def parse():
     p.add_argument("--single-split", type=int, default=SINGLE_SPLIT,
                    help="config 'single': the update's segments cut into this many ranges, each a sub-plan on its "
                         "own stream (their latency-bound phases overlap)")
-    p.add_argument("--prefill", choices=["none", "start", "scan", "small"], default="none",
-                   help="latency-bound plans (single, C5): the decode's background (k_fill) on a second stream beside "
-                        "the encode, from the step's start or from the end of k_scan (SplitPipeline prefill)")
     p.add_argument("--cpu-seconds", type=float, default=8.0, help="CPU baseline time budget per leg")
     p.add_argument("--no-cpu-baseline", action="store_true")
     return p.parse_args()
@@ -248,14 +251,13 @@ def run_workload(cfg, a, dev, world, rank, headline):
     flat = synth_batch(t, dev, client_ids=ids)
     base = synth_batch(t, dev, client_ids=[10_000 + i for i in ids]) if a.mode == "delta" else None
     split = max(1, split)
-    inflight = max(1, a.inflight) if headline else 1
+    inflight = max(1, a.inflight) if headline else CONFIG_INFLIGHT.get(cfg, 1)
     slots = []
-    for _ in range(inflight):
+    for j in range(inflight):
         if a.pipe == "lane" and headline:
             p = LanePipeline(t, a.bits, lanes=split, device=dev, flags=a.flags)
-        else:
-            p = SplitPipeline(t, a.bits, split=split, device=dev, flags=a.flags, fork=a.fork,
-                              prefill=None if a.prefill == "none" else a.prefill)
+        else:  # slot j on its own pooled streams, so the slots' steps overlap
+            p = SplitPipeline(t, a.bits, split=split, device=dev, flags=a.flags, fork=a.fork, stream_base=j * split)
         slots.append((p, p.empty_encoded(), p.empty_flat()))
     split = slots[0][0].n_parts
     pipes = [s[0] for s in slots]
@@ -325,8 +327,7 @@ def run_workload(cfg, a, dev, world, rank, headline):
     one = bool(a.flags & ONE_LAUNCH)
     multi = not one and not (a.flags & FRONT_LAUNCH)
     enc_kernel = "k_scan" if multi else "k_fused" if one else "k_front"
-    # prefill: the decode events bracket the background write (k_fill) on its own stream
-    dec_kernel = "k_fill" if any("fill" in q for q in getattr(pipes[0], "parts", [])) else "k_decode"
+    dec_kernel = "k_decode"
     stages = {}
     for name, which in {enc_kernel: ev_e, dec_kernel: ev_d}.items():
         per = [union([(e[1], e[2]) for e in which[i]]) for i in timed_steps]
@@ -339,9 +340,7 @@ def run_workload(cfg, a, dev, world, rank, headline):
     alg = {  # algorithmic HBM bytes per timed interval
         enc_kernel: (4 * large_elems if multi else 4 * N + (4 + vb) * K + 8 * T if one else 4 * N) + (4 * N if delta else 0),
         "k_decode": 4 * N * (2 if delta else 1) + (4 + vb) * K + 8 * T,
-        "k_fill": 4 * N * (2 if delta else 1),
     }
-    alg = {k: alg[k] for k in stages}
     dom = max(alg, key=lambda k: stages[k])
     ach = alg[dom] / (stages[dom] * 1e-3) / 1e9
     step_ms = el / a.steps * 1e3
@@ -476,7 +475,8 @@ def main():
             "stage_timing": head["stage_timing"], "sample_fallbacks": head["sample_fallbacks"],
             "wait_timeouts": head["wait_timeouts"],
             "configs": {k: {f: v[f] for f in ("value", "ms_per_step", "step_roofline", "roofline", "stages_ms", "desc",
-                                              "elements_per_gpu", "segments_per_gpu", "split", "sample_fallbacks")}
+                                              "elements_per_gpu", "segments_per_gpu", "split", "inflight",
+                                              "sample_fallbacks")}
                         for k, v in extras.items()},
         }
         if plugin is not None:

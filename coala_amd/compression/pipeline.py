@@ -30,7 +30,7 @@ import torch
 
 from . import _lib
 from .plan import CodecPlan, Encoded
-from .spec import LATENCY_PLAN_UNITS, SegmentTable, small_limit
+from .spec import SegmentTable, small_limit
 
 _IN_LAUNCH = _lib.COALAC_FLAG_ONE_LAUNCH | _lib.COALAC_FLAG_FRONT_LAUNCH  # encodes with in-launch waits
 
@@ -319,7 +319,7 @@ class SplitPipeline:
     per sub-batch index.
     """
 
-    def __init__(self, table: SegmentTable, bits=8, split=2, device=None, flags=0, fork=False, prefill=None):
+    def __init__(self, table: SegmentTable, bits=8, split=2, device=None, flags=0, fork=False, stream_base=0):
         self.table = table
         self.bits = int(bits)
         self.flags = int(flags)
@@ -336,7 +336,9 @@ class SplitPipeline:
             if S <= C:  # client ranges: ordinary plans over views of the batch buffers
                 cuts = balanced_cuts(table.client_elements(), S)
                 so, ko, to = table.client_span_off, table.client_k_off, table.client_seg_off
-                streams = pooled_streams(self.device, len(cuts) - 1)
+                # stream_base: pipelines meant to run side by side (several batches in flight) take
+                # disjoint pool ranges; by default every pipeline starts at pooled stream 0
+                streams = pooled_streams(self.device, stream_base + len(cuts) - 1)[stream_base:]
                 for c0, c1, st in zip(cuts[:-1], cuts[1:], streams):
                     plan = CodecPlan(None, table.ratio, self.bits, device=self.device, table=table.sub_table(c0, c1))
                     self.parts.append(dict(x=slice(so[c0], so[c1]), k=slice(ko[c0], ko[c1]), t=slice(to[c0], to[c1]),
@@ -347,37 +349,11 @@ class SplitPipeline:
                 # element count, each a plan over absolute segment rows that reads / writes the whole
                 # buffers in place (its own segments only) — the ranges' latency-bound phases overlap
                 ranges = split_lanes(table.segs[:, 1].tolist(), S)
-                for (s0, s1), st in zip(ranges, pooled_streams(self.device, len(ranges))):
+                for (s0, s1), st in zip(ranges, pooled_streams(self.device, stream_base + len(ranges))[stream_base:]):
                     plan = CodecPlan.from_segments(table.segs[s0:s1], self.bits, device=self.device)
                     self.parts.append(dict(x=slice(None), k=slice(None), t=slice(s0, s1), plan=plan,
                                            ws=plan.empty_workspace(), dws=plan.empty_decode_workspace(),
                                            stream=st))
-            self._setup_prefill(prefill)
-
-    def _setup_prefill(self, prefill):
-        """prefill ("start" | "scan" | None): roundtrip() writes the decode's background (k_fill: 0, or the
-        base) of every latency-bound part (<= LATENCY_PLAN_UNITS units, the plans that decode as k_fill +
-        k_scatter) on a second stream, beside that part's own encode, and the part's stream then scatters the
-        kept values after it (COALAC_STAGE_FILL / COALAC_STAGE_SCATTER). The background depends on nothing
-        the encode produces (a server can write it before the upload arrives); one update's encode is a
-        chain of latency-bound kernels that leaves HBM idle, and the fill streams into that. "start": the
-        fill waits for the start of the part's step (its previous scatter: same output buffer); "scan": for
-        the end of the part's k_scan, so it overlaps the select chain only; "small": from the step's start,
-        and the encode's small segments (COALAC_STAGE_SMALL, k_small) run on that stream too, ahead of the
-        fill, so the part's own stream runs k_sample -> k_scan -> select -> emit -> k_scatter only. Batches
-        (k_decode merges the background in registers) are not affected."""
-        if prefill not in (None, "start", "scan", "small"):
-            raise ValueError(f"prefill must be None, 'start', 'scan' or 'small', got {prefill!r}")
-        self.prefill = prefill
-        if prefill is None:
-            return
-        lat = [P for P in self.parts if P["plan"].n_units <= LATENCY_PLAN_UNITS]
-        side = pooled_streams(self.device, len(self.parts) + len(lat))[len(self.parts):]
-        for P, st in zip(lat, side):
-            go, filled = torch.cuda.Event(), torch.cuda.Event()
-            go.record(P["stream"])  # torch creates the HIP event on first record
-            filled.record(st)
-            P["fill"] = dict(stream=st, go=go, filled=filled)
 
     @property
     def n_parts(self):
@@ -449,35 +425,8 @@ class SplitPipeline:
             out = self.empty_flat() if base is None else torch.empty_like(base)
 
         def both(g, P):
-            F = P.get("fill")
-            if F is None:
-                self._encode_part(g, P, flat, base, enc, enc_events)
-                self._decode_part(g, P, enc, base, out, dec_events)
-                return
-            ev = list(enc_events[g]) if enc_events is not None else [None] * 5
-            go = F["go"]
-            fs = F["stream"]
-            eargs = dict(base=self._x(base, P), out=self._enc(enc, P), workspace=P["ws"], flags=self.flags | self.fork_flag)
-            if self.prefill in ("start", "small"):
-                go.record(P["stream"])
-            elif ev[2] is not None:
-                go = ev[2]  # the caller's timing event sits on the same boundary (after k_scan)
-            else:
-                ev[2] = go
-            if self.prefill == "small":
-                large = _lib.COALAC_STAGE_SAMPLE | _lib.COALAC_STAGE_SCAN | _lib.COALAC_STAGE_SELECT
-                P["plan"].encode(self._x(flat, P), **eargs, sched=(None, ev, large))
-                P["plan"].encode(self._x(flat, P), **eargs, stream=fs,
-                                 sched=([go, None, None, None, None], None, _lib.COALAC_STAGE_SMALL))
-                go = None  # the fill follows k_small on that stream
-            else:
-                P["plan"].encode(self._x(flat, P), **eargs, events=ev)
-            de = dec_events[g] if dec_events is not None else [None] * 3
-            P["plan"].decode(self._enc(enc, P), base=self._x(base, P), out=self._x(out, P), workspace=P["dws"],
-                             stream=fs, sched=([None, go, None], [None, de[1], de[2]], _lib.COALAC_STAGE_FILL))
-            F["filled"].record(fs)
-            P["plan"].decode(self._enc(enc, P), base=self._x(base, P), out=self._x(out, P), workspace=P["dws"],
-                             sched=([None, F["filled"], None], [None, None, None], _lib.COALAC_STAGE_SCATTER))
+            self._encode_part(g, P, flat, base, enc, enc_events)
+            self._decode_part(g, P, enc, base, out, dec_events)
         self._run(both, joined)
         return enc, out
 

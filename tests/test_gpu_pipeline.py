@@ -201,40 +201,6 @@ def test_split_pipelines_share_pooled_streams(cuda):
         assert torch.equal(d1.view(torch.int32), o.view(torch.int32))
 
 
-@pytest.mark.parametrize("prefill", ["start", "scan", "small"])
-@pytest.mark.parametrize("delta", [False, True])
-def test_split_pipeline_prefill_unjoined_alternating(cuda, prefill, delta):
-    """SplitPipeline(prefill=...): one update's decode background (k_fill) on a second stream beside its
-    encode, the kept values scattered after it. Six unjoined back-to-back roundtrips alternate two inputs
-    (and bases) through ONE output buffer: a fill that overtook the previous step's scatter would leave
-    that step's kept values in the output. Every step's result equals a plain plan's, the last one the
-    oracle's, bit for bit."""
-    t = SegmentTable(fp32_sizes("resnet50_tv"), 0.01, 1)
-    flats = [synth_batch(t, cuda, client_ids=[4]), synth_batch(t, cuda, client_ids=[5])]
-    bases = [synth_batch(t, cuda, client_ids=[40]), synth_batch(t, cuda, client_ids=[50])] if delta else [None, None]
-    pipe = SplitPipeline(t, 8, split=1, device=cuda, prefill=prefill)
-    assert "fill" in pipe.parts[0]
-    plan = CodecPlan(fp32_sizes("resnet50_tv"), 0.01, 8, clients=1, device=cuda)
-    refs = []
-    for j in range(2):
-        e = plan.encode(flats[j], base=bases[j])
-        refs.append((e, plan.decode(e, base=bases[j], out=torch.zeros_like(flats[j]))))
-    enc, out = pipe.empty_encoded(), pipe.empty_flat().zero_()
-    torch.cuda.synchronize()
-    for i in range(6):
-        pipe.roundtrip(flats[i % 2], base=bases[i % 2], enc=enc, out=out, joined=False)
-        if i >= 4:  # the last two steps, one per input, checked after their own step
-            cur = torch.cuda.current_stream(cuda)
-            for s in pipe.streams:
-                cur.wait_stream(s)
-            torch.cuda.synchronize()
-            e1, d1 = refs[i % 2]
-            assert torch.equal(e1.idx, enc.idx) and torch.equal(e1.vals, enc.vals), i
-            assert torch.equal(d1.view(torch.int32), out.view(torch.int32)), i
-    ref = oracle_roundtrip(t, flats[1].cpu().numpy(), 8, None if bases[1] is None else bases[1].cpu().numpy())
-    check(t, enc, out, ref)
-
-
 def test_decode_fill_scatter_stages(cuda):
     """COALAC_STAGE_FILL then COALAC_STAGE_SCATTER = COALAC_STAGE_DECODE, for a latency-bound plan (k_fill +
     k_scatter) and for a batch plan (FILL is nothing, SCATTER the whole k_decode); FILL alone writes the
@@ -263,3 +229,26 @@ def test_decode_fill_scatter_stages(cuda):
         for off, n, _, _ in segs:
             np.testing.assert_array_equal(o[off:off + n].view(np.uint32), r[off:off + n].view(np.uint32),
                                           err_msg=f"clients={clients} segment at {off}")
+
+
+def test_split_pipelines_in_flight_on_disjoint_streams(cuda):
+    """bench.py's single_x2: two single-update pipelines on disjoint pooled streams (stream_base), steps
+    alternating between them unjoined, so consecutive updates overlap; each keeps its own buffers and the
+    results equal a plain plan's, bit for bit."""
+    from coala_amd.compression.pipeline import pooled_streams
+    t = SegmentTable(fp32_sizes("resnet50_tv"), 0.01, 1)
+    flats = [synth_batch(t, cuda, client_ids=[7]), synth_batch(t, cuda, client_ids=[8])]
+    pipes = [SplitPipeline(t, 8, split=1, device=cuda, stream_base=j) for j in range(2)]
+    assert pipes[0].streams == pooled_streams(cuda, 1) and pipes[1].streams == pooled_streams(cuda, 2)[1:]
+    bufs = [(p.empty_encoded(), p.empty_flat().zero_()) for p in pipes]
+    torch.cuda.synchronize()
+    for i in range(6):
+        pipes[i % 2].roundtrip(flats[i % 2], enc=bufs[i % 2][0], out=bufs[i % 2][1], joined=False)
+    torch.cuda.synchronize()
+    plan = CodecPlan(fp32_sizes("resnet50_tv"), 0.01, 8, clients=1, device=cuda)
+    for j in range(2):
+        e = plan.encode(flats[j])
+        d = plan.decode(e, out=torch.zeros_like(flats[j]))
+        torch.cuda.synchronize()
+        assert torch.equal(e.idx, bufs[j][0].idx) and torch.equal(e.vals, bufs[j][0].vals), j
+        assert torch.equal(d.view(torch.int32), bufs[j][1].view(torch.int32)), j
