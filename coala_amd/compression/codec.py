@@ -74,24 +74,64 @@ def layout_of(state):
     return [(k, str(v.dtype).replace("torch.", ""), tuple(v.shape)) for k, v in state.items()]
 
 
+_DTYPE_NAMES = {}
+
+
+def _dtype_name(dt):
+    n = _DTYPE_NAMES.get(dt)
+    if n is None:
+        n = _DTYPE_NAMES[dt] = str(dt).replace("torch.", "")
+    return n
+
+
+class _Layout:
+    """The header entries of one state_dict layout (the (name, dtype, shape) sequence) and the names of its
+    fp32 segments / raw passthrough entries. Built once per layout: a model's layout is fixed for a whole FL
+    task, and the per-entry Python of building them was most of a ResNet-50 encode call's host time. The
+    entries are shared by every header of that layout and never mutated."""
+
+    def __init__(self, items):
+        self.entries, self.seg_names, self.raw_names = [], [], []
+        off = seg = 0
+        for name, dt, shape in items:
+            n = 1
+            for d in shape:
+                n *= d
+            e = {"name": name, "dtype": _dtype_name(dt), "shape": list(shape)}
+            if dt == torch.float32 and n > 0:
+                e.update(kind="seg", seg=seg, off=off, n=n)
+                self.seg_names.append(name)
+                off = align_up(off + n)
+                seg += 1
+            else:
+                e["kind"] = "raw"
+                self.raw_names.append(name)
+            self.entries.append(e)
+        self.sizes = [e["n"] for e in self.entries if e["kind"] == "seg"]
+
+
+_LAYOUTS = OrderedDict()
+_LAYOUTS_LOCK = threading.Lock()
+
+
+def _layout(state):
+    sig = tuple((k, v.dtype, v.shape) for k, v in state.items())
+    with _LAYOUTS_LOCK:
+        L = _LAYOUTS.get(sig)
+        if L is None:
+            L = _LAYOUTS[sig] = _Layout(sig)
+            while len(_LAYOUTS) > 16:
+                _LAYOUTS.popitem(last=False)
+    return L
+
+
 def describe_state(state):
     """state_dict -> (entries as flatten_state would write them, fp32 segment tensors in order, raw
     passthrough entries), WITHOUT copying the fp32 data: the zero-copy encode reads the tensors in place."""
-    entries, segs, raw = [], [], OrderedDict()
-    off = seg = 0
-    for name, t in state.items():
-        e = {"name": name, "dtype": str(t.dtype).replace("torch.", ""), "shape": list(t.shape)}
-        if t.dtype == torch.float32 and t.numel() > 0:
-            n = t.numel()
-            e.update(kind="seg", seg=seg, off=off, n=n)
-            segs.append(t)  # read in place by the kernels (pointer, numel, dtype, contiguity only)
-            off = align_up(off + n)
-            seg += 1
-        else:
-            e.update(kind="raw")
-            raw[name] = t.detach()
-        entries.append(e)
-    return entries, segs, _snapshot_raw(raw)
+    L = _layout(state)
+    segs = [state[n] for n in L.seg_names]  # read in place by the kernels (pointer, numel, dtype, contiguity)
+    raw = OrderedDict((n, state[n].detach()) for n in L.raw_names)
+    return L.entries, segs, _snapshot_raw(raw)
 
 
 def _snapshot_raw(raw):
@@ -367,10 +407,12 @@ class UpdateCodec:
             base_flat = base.flat_on(device)
         plan = self.plan_for(sizes, device)
         ws = self._workspace(plan)
+        dev_index = device.index if device.type == "cuda" else -1  # (Tensor.get_device(): -1 on the CPU)
         in_place = getattr(plan, "encode_segments", None) is not None and all(
-            t.device == device and t.is_contiguous() and t.data_ptr() % 16 == 0 for t in segs)
+            t.get_device() == dev_index and t.is_contiguous() and t.data_ptr() % 16 == 0 for t in segs)
         if in_place:  # read the parameters where they live: no flattening copy (+8 B/element of traffic)
-            enc = plan.encode_segments(segs, base=base_flat, workspace=ws)
+            # (dtype and sizes hold by construction: the plan was made from this layout's segments)
+            enc = plan.encode_segments(segs, base=base_flat, workspace=ws, checked=True)
         else:
             fs = flatten_state(state, device=device)
             enc = plan.encode(fs.flat, base=base_flat, workspace=ws)
@@ -434,7 +476,6 @@ class UpdateCodec:
         sizes = [e["n"] for e in h["entries"] if e["kind"] == "seg"]
         state = OrderedDict()
         flat = None
-        offs = None
         if sizes:
             if device is None:
                 device = self.backend.default_device()
@@ -445,7 +486,6 @@ class UpdateCodec:
                 _check_same_layout(h["entries"], base.entries)
                 base_flat = base.flat_on(device)
             plan = self.plan_for(sizes, device, ratio=h["ratio"], bits=h["bits"])
-            offs = plan.table.offsets  # the decoder's own offsets, never the (untrusted) header's
             if device.type == "cuda":
                 # this thread's own stream (the remote server decodes from one thread per upload,
                 # coala/server/service.py:74): pinned H2D of the payload + decode, then wait for it
@@ -459,10 +499,10 @@ class UpdateCodec:
             else:
                 enc = update.encoded.to(device, non_blocking=True)
                 flat = plan.decode(enc, base=base_flat)
+        views = _segment_views(flat, plan.table, h["entries"]) if sizes else None
         for e in h["entries"]:
             if e["kind"] == "seg":
-                o = offs[e["seg"]]
-                state[e["name"]] = flat[o:o + e["n"]].view(e["shape"])
+                state[e["name"]] = views[e["seg"]]
             else:
                 t = update.raw[e["name"]]
                 state[e["name"]] = t.to(device) if device is not None else t
@@ -536,6 +576,36 @@ class UpdateCodec:
         return module_with_state(template, state)
 
 
+def _segment_views(flat, table, entries):
+    """Views of the decoded flat buffer, one per fp32 segment (in segment order), shaped like the header's
+    entries, at the decoder's own offsets (never the untrusted header's): ONE split of the buffer into
+    segments and alignment pads, and a view only where a shape is not already the 1-D piece (a slice +
+    view per entry cost ~3 us each, ~1 ms per ResNet-50 decode)."""
+    split = table.__dict__.get("_split")
+    if split is None:
+        sizes, keep, prev = [], [], 0
+        for off, n in zip(table.offsets, table.sizes):
+            if off > prev:
+                sizes.append(off - prev)
+            keep.append(len(sizes))
+            sizes.append(n)
+            prev = off + n
+        split = table.__dict__["_split"] = (sizes, keep, prev)
+    sizes, keep, end = split
+    pieces = flat[:end].split_with_sizes(sizes)
+    seg_entries = [e for e in entries if e["kind"] == "seg"]
+    out = []
+    for j, e in zip(keep, seg_entries):
+        t, shape = pieces[j], e["shape"]
+        out.append(t if len(shape) == 1 else t.view(shape))
+    return out
+
+
+_PLAIN_TYPES = frozenset((bool, int, float, str, type(None), tuple))
+_CONTAINER_TYPES = frozenset((dict, OrderedDict, list, set))
+_MODULE_TABLES = frozenset(("_parameters", "_buffers", "_modules"))
+
+
 def module_with_state(template, state):
     """A new nn.Module shaped like `template` whose parameters / buffers ARE the tensors of `state`
     (views into the decode output: no parameter data is copied; `template` is never aliased).
@@ -553,27 +623,32 @@ def module_with_state(template, state):
         return copy.copy(v)
 
     def clone(mod, prefix):
-        new = mod.__class__.__new__(mod.__class__)
+        cls = mod.__class__
+        new = cls.__new__(cls)
         d = {}
         for k, v in mod.__dict__.items():
-            if isinstance(v, torch.Tensor):
+            tv = type(v)
+            if tv in _PLAIN_TYPES:  # most of a module's attributes: nothing to copy
+                pass
+            elif tv in _CONTAINER_TYPES:
+                if k not in _MODULE_TABLES:
+                    v = shallow(v)  # (the hook dicts included: the clone never shares them)
+            elif isinstance(v, torch.Tensor):
                 v = v.clone()
-            elif isinstance(v, (list, dict, set)) and k not in ("_parameters", "_buffers", "_modules"):
-                v = shallow(v)  # (the hook dicts included: the clone never shares them)
+            elif isinstance(v, (list, dict, set)) and k not in _MODULE_TABLES:
+                v = shallow(v)
             d[k] = v
         params = OrderedDict()
         for name, p in mod._parameters.items():
-            key = prefix + name
             if p is None:
                 params[name] = None
-            elif key in state:
-                params[name] = nn.Parameter(state[key], requires_grad=p.requires_grad)
-            else:
-                params[name] = nn.Parameter(p.detach().clone(), requires_grad=p.requires_grad)
+                continue
+            t = state.get(prefix + name)
+            params[name] = nn.Parameter(t if t is not None else p.detach().clone(), requires_grad=p.requires_grad)
         buffers = OrderedDict()
         for name, b in mod._buffers.items():
-            key = prefix + name
-            buffers[name] = None if b is None else (state[key] if key in state else b.clone())
+            t = None if b is None else state.get(prefix + name)
+            buffers[name] = None if b is None else (t if t is not None else b.clone())
         d["_parameters"], d["_buffers"] = params, buffers
         d["_modules"] = OrderedDict((name, None if c is None else clone(c, prefix + name + "."))
                                     for name, c in mod._modules.items())

@@ -172,13 +172,14 @@ class CodecPlan:
         _lib.check(rc, "coalac_encode")
         return out
 
-    def segment_pointers(self, tensors):
+    def segment_pointers(self, tensors, checked=False):
         """Device array of the tensors' data pointers (one per segment), for encode_segments; cached per
-        pointer tuple (a model's parameter storage does not move between rounds)."""
+        pointer tuple (a model's parameter storage does not move between rounds). checked: the caller has
+        verified device, dtype, contiguity, alignment and sizes (UpdateCodec.encode)."""
         segs = self.table.segs
         if len(tensors) != len(segs):
             raise ValueError(f"need {len(segs)} segment tensors, got {len(tensors)}")
-        for i, t in enumerate(tensors):
+        for i, t in enumerate(() if checked else tensors):
             if t.device != self.device or t.dtype != torch.float32 or not t.is_contiguous():
                 raise ValueError(f"segment {i}: need a contiguous float32 tensor on {self.device}")
             if t.numel() != int(segs[i, 1]):
@@ -195,10 +196,10 @@ class CodecPlan:
             cache[key] = d
         return d
 
-    def encode_segments(self, tensors, base=None, out=None, workspace=None, flags=0, stream=None):
+    def encode_segments(self, tensors, base=None, out=None, workspace=None, flags=0, stream=None, checked=False):
         """Encode with segment i read from tensors[i] itself (coalac_encode_segptr): e.g. a model's
         parameters, no flattening copy. base: flat fp32[span] (delta mode), as encode()."""
-        ptrs = self.segment_pointers(tensors)
+        ptrs = self.segment_pointers(tensors, checked=checked)
         self._check_flat(base, "base")
         with _on(stream):
             out = self.empty_encoded() if out is None else out
