@@ -92,6 +92,9 @@ constexpr int SEL_NT = 256;               // threads of a k_select block (4 wave
                      // the per-record device atomics made one update's k_scan 25.0 -> 33.2 us for k_ghist's
                      // 6.4 (single update 0.0897 -> 0.0927 ms)
 #endif
+#ifndef RANK_SELECT
+#define RANK_SELECT 1  // block_select: rank the <= RANK_MAX keys of the chosen bin instead of more radix passes
+#endif
 #ifndef LOAD_AUX
 #define LOAD_AUX 2   // cache policy of the streaming buffer loads (k_scan): 2 = non-temporal
 #endif
@@ -397,7 +400,54 @@ DEV void block_minmax(float& mn, float& mx, float* shf) {
 // enumerates (each thread enumerates its own share; the union is the key multiset). Returns T with
 // count(key in (T, hi]) < r <= count(key in [T, hi]) and leaves in r the number of keys == T to take
 // (r - count(key in (T, hi])). Radix narrowing with 2048-bin LDS histograms: at most 3 passes over the
-// keys for a full 31-bit range. sh needs >= 64 words (broadcast slots sh[40], sh[41]).
+// keys for a full 31-bit range. Once the bin holding the r-th key has at most RANK_MAX keys, they are
+// gathered into LDS (one more enumeration) and ranked against each other instead of further radix passes
+// (a small segment's keys crowd a few exponent bins: 3 passes -> 1 pass + gather + rank). sh needs >= 64
+// words (broadcast slots sh[36]-sh[41]).
+constexpr uint32_t RANK_MAX = 256;
+
+template <int NT, class ForEach>
+DEV uint32_t rank_select(ForEach&& for_each, uint32_t lo, uint32_t hi, uint32_t& r, uint32_t* cand, uint32_t* sh) {
+  const uint32_t t = threadIdx.x, lane = lane_id();
+  if (t == 0) {
+    sh[39] = 0;
+    sh[36] = lo;
+    sh[37] = r;
+  }
+  __syncthreads();
+  for_each([&](uint32_t key) {  // wave-aggregated append of the bin's keys
+    const bool in = key >= lo && key <= hi;
+    const uint64_t m = __ballot(in);
+    if (m) {
+      const uint32_t leader = (uint32_t)__ffsll((long long)m) - 1u;
+      uint32_t base = 0;
+      if (lane == leader) base = atomicAdd(&sh[39], (uint32_t)__popcll(m));
+      base = (uint32_t)__shfl((int)base, (int)leader, 64);
+      if (in) cand[base + mbcnt(m)] = key;
+    }
+  });
+  __syncthreads();
+  const uint32_t c = sh[39];
+  for (uint32_t i = t; i < c; i += NT) {
+    const uint32_t ki = cand[i];
+    uint32_t g = 0, e = 0;
+    for (uint32_t j = 0; j < c; ++j) {  // every thread reads the same word: LDS broadcast
+      const uint32_t kj = cand[j];
+      g += kj > ki ? 1u : 0u;
+      e += kj == ki ? 1u : 0u;
+    }
+    if (g < r && r <= g + e) {  // the r-th key (every tie of it writes the same two words)
+      sh[36] = ki;
+      sh[37] = r - g;
+    }
+  }
+  __syncthreads();
+  const uint32_t T = sh[36];
+  r = sh[37];
+  __syncthreads();
+  return T;
+}
+
 template <int NT, int NB = HIST_BINS, class ForEach>
 DEV uint32_t block_select(ForEach&& for_each, uint32_t lo, uint32_t hi, uint32_t& r, uint32_t* hist,
                           uint32_t* sh) {
@@ -432,27 +482,32 @@ DEV uint32_t block_select(ForEach&& for_each, uint32_t lo, uint32_t hi, uint32_t
     }
     __syncthreads();
     if (above < r && r <= above + s) {
-      uint32_t acc = above;
+      uint32_t acc = above, cb = 0;
       int b = (int)(t * BPT);
 #pragma unroll
       for (int j = BPT - 1; j >= 0; --j) {
         if (acc + c[j] >= r) {
           b = (int)(t * BPT) + j;
+          cb = c[j];
           break;
         }
         acc += c[j];
       }
       sh[40] = (uint32_t)b;
       sh[41] = r - acc;
+      sh[38] = cb;  // keys in the chosen bin
     }
     __syncthreads();
     const uint32_t b = sh[40];
     r = sh[41];
+    const uint32_t bc = sh[38];
     __syncthreads();
     if (b == NONE) return lo;  // precondition violated (cannot happen for valid inputs)
     lo = lo + (b << shift);
     const uint32_t nhi = lo + ((1u << shift) - 1u);
     hi = nhi < hi ? nhi : hi;
+    if (RANK_SELECT && lo < hi && bc <= RANK_MAX && NB >= (int)RANK_MAX)
+      return rank_select<NT>(for_each, lo, hi, r, hist, sh);
   }
   return lo;
 }
