@@ -92,6 +92,9 @@ constexpr int SEL_NT = 256;               // threads of a k_select block (4 wave
                      // the per-record device atomics made one update's k_scan 25.0 -> 33.2 us for k_ghist's
                      // 6.4 (single update 0.0897 -> 0.0927 ms)
 #endif
+#ifndef SCAN_SMALL_LAT
+#define SCAN_SMALL_LAT 1  // latency-bound plans: small segments in k_scan's first blocks (k_sample alone ahead)
+#endif
 #ifndef RANK_SELECT
 #define RANK_SELECT 1  // block_select: rank the <= RANK_MAX keys of the chosen bin instead of more radix passes
 #endif
@@ -2859,8 +2862,10 @@ int launch_encode(const Params& P, coalac_plan_t plan, hipStream_t st, const coa
   // split encode: only in stage SMALL (k_small)
   const bool split = stages != all;
   const bool fork = plan->n_small && !split && plan->n_lunits >= FORK_MIN_LUNITS && !(P.flags & COALAC_FLAG_NO_FORK);
-  // otherwise (whole encode) the small segments run beside the samplers in k_presel
+  // otherwise (whole encode) the small segments run beside the samplers in k_presel, or (latency-bound
+  // plans, SCAN_SMALL_LAT) in k_scan's first blocks, beside the streaming waves: k_sample alone ahead of it
   const bool presel = !split && !fork && plan->n_small;
+  const bool small_in_scan = presel && SCAN_SMALL_LAT && plan->n_lunits <= LATENCY_PLAN_UNITS && !P.scan_hist;
   Params Q = P;
   Q.scan_small = 0u;
   std::unique_lock<std::mutex> lk(plan->mu, std::defer_lock);
@@ -2887,14 +2892,17 @@ int launch_encode(const Params& P, coalac_plan_t plan, hipStream_t st, const coa
     hipLaunchKernelGGL((k_small<DELTA, RAW>), dim3(plan->n_small), dim3(BLOCK), 0, plan->side, P);
     HIP_CHECK(hipEventRecord(plan->join, plan->side));
   }
-  if (presel)
+  if (presel && !small_in_scan)
     hipLaunchKernelGGL((k_presel<DELTA, RAW>), dim3(plan->n_large + plan->n_small), dim3(BLOCK), 0, st, P);
   else if ((stages & COALAC_STAGE_SAMPLE) && plan->n_large)
     hipLaunchKernelGGL((k_sample<DELTA, RAW>), dim3(plan->n_large), dim3(BLOCK), 0, st, P);
   if (split && (stages & COALAC_STAGE_SMALL) && plan->n_small)
     hipLaunchKernelGGL((k_small<DELTA, RAW>), dim3(plan->n_small), dim3(BLOCK), 0, st, P);
   ENC_BOUNDARY(1);
-  if ((stages & COALAC_STAGE_SCAN) && gu) {
+  if (small_in_scan) {
+    Q.scan_small = plan->n_small;
+    hipLaunchKernelGGL((k_scan<DELTA, RAW, true>), dim3(gu + plan->n_small), dim3(BLOCK), 0, st, Q);
+  } else if ((stages & COALAC_STAGE_SCAN) && gu) {
     if (P.scan_hist)
       hipLaunchKernelGGL((k_scan<DELTA, RAW, false, true>), dim3(gu), dim3(BLOCK), 0, st, Q);
     else
