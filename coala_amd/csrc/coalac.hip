@@ -95,6 +95,9 @@ constexpr int SEL_NT = 256;               // threads of a k_select block (4 wave
 #ifndef SCAN_SMALL_LAT
 #define SCAN_SMALL_LAT 1  // latency-bound plans: small segments in k_scan's first blocks (k_sample alone ahead)
 #endif
+#ifndef SAMPLE_PICK2
+#define SAMPLE_PICK2 1  // k_sample: both bracket bins from one block scan of the histogram
+#endif
 #ifndef RANK_SELECT
 #define RANK_SELECT 1  // block_select: rank the <= RANK_MAX keys of the chosen bin instead of more radix passes
 #endif
@@ -854,6 +857,51 @@ DEV uint32_t hist_pick(const uint32_t* hist, uint32_t& r, uint32_t* sh) {
   return b;
 }
 
+// hist_pick for two ranks at once (r1, r2; 0 = not wanted): ONE block scan of the bins instead of two.
+// Returns the bins in b1 / b2 (NONE when not wanted). sh needs >= 64 words (slots 40-43).
+template <int NT, int NB = HIST_BINS>
+DEV void hist_pick2(const uint32_t* hist, uint32_t r1, uint32_t r2, uint32_t& b1, uint32_t& b2, uint32_t* sh) {
+  constexpr int BPT = NB / NT;
+  const uint32_t t = threadIdx.x;
+  uint32_t c[BPT];
+  uint32_t s = 0;
+#pragma unroll
+  for (int j = 0; j < BPT; ++j) {
+    c[j] = hist[t * BPT + j];
+    s += c[j];
+  }
+  uint32_t total;
+  const uint32_t ex = block_excl_scan<NT>(s, sh, total);
+  const uint32_t above = total - ex - s;
+  if (t == 0) {
+    sh[40] = NONE;
+    sh[41] = NONE;
+  }
+  __syncthreads();
+  const uint32_t rr[2] = {r1, r2};
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    const uint32_t r = rr[q];
+    if (r != 0 && above < r && r <= above + s) {
+      uint32_t acc = above;
+      int b = (int)(t * BPT);
+#pragma unroll
+      for (int j = BPT - 1; j >= 0; --j) {
+        if (acc + c[j] >= r) {
+          b = (int)(t * BPT) + j;
+          break;
+        }
+        acc += c[j];
+      }
+      sh[40 + q] = (uint32_t)b;
+    }
+  }
+  __syncthreads();
+  b1 = sh[40];
+  b2 = sh[41];
+  __syncthreads();
+}
+
 // ------------------------------------------------------------------------------------------------
 // small segments (n <= SMALL_MAX): one 256-thread block, values in LDS, exact radix select, ordered
 // compaction, min/max, codes. Runs as its own kernel (k_small) on the plan's side stream, concurrently
@@ -1036,15 +1084,17 @@ DEV void sample_segment(const Params& P, uint32_t li, uint32_t* hist, uint32_t* 
   }
   __syncthreads();
   uint32_t tlo = 0u, thi = KEY_MAX;
-  if (rlo < (double)m) {
-    uint32_t r1 = (uint32_t)rlo;
-    const uint32_t b = hist_pick<NT>(hist, r1, sh);
-    tlo = kmin + (b << shift);
+  uint32_t blo = 0, bhi = 0;  // both bracket bins from one scan of the histogram
+  if (SAMPLE_PICK2) {
+    hist_pick2<NT>(hist, rlo < (double)m ? (uint32_t)rlo : 0u, rhi >= 1.0 ? (uint32_t)rhi : 0u, blo, bhi, sh);
+  } else {
+    uint32_t r1 = (uint32_t)rlo, r2 = (uint32_t)rhi;
+    if (rlo < (double)m) blo = hist_pick<NT>(hist, r1, sh);
+    if (rhi >= 1.0) bhi = hist_pick<NT>(hist, r2, sh);
   }
+  if (rlo < (double)m) tlo = kmin + (blo << shift);
   if (rhi >= 1.0) {
-    uint32_t r2 = (uint32_t)rhi;
-    const uint32_t b = hist_pick<NT>(hist, r2, sh);
-    const uint64_t edge = (uint64_t)kmin + (((uint64_t)b + 1) << shift) - 1;
+    const uint64_t edge = (uint64_t)kmin + (((uint64_t)bhi + 1) << shift) - 1;
     thi = (uint32_t)min<uint64_t>(edge, kmax);
   }
   const uint32_t nu = sd.unit_end - sd.unit_begin;
