@@ -108,7 +108,10 @@ constexpr int SEL_NT = 256;               // threads of a k_select block (4 wave
 #define STORE_AUX 2  // cache policy of the streaming buffer stores (k_decode): 2 = non-temporal
 #endif
 constexpr uint32_t STAGE_CAP = 512;       // candidate records staged in LDS per k_scan wave
-constexpr uint32_t GU = 32;               // units per select group (k_ghist / k_gwin block)
+#ifndef GU_UNITS
+#define GU_UNITS 32
+#endif
+constexpr uint32_t GU = GU_UNITS;               // units per select group (k_ghist / k_gwin block)
 #ifndef GSWEEP
 #define GSWEEP 4  // units per record-load batch of a group sweep (8 measured equal on one update, lower on C3)
 #endif

@@ -23,3 +23,8 @@ for v in coala_amd/lib/variants/*.so; do
   echo "== $n"; grep -E "^single|^C3" $O/$n.txt
 done
 cp $O/in_tree.so.bak coala_amd/lib/libcoalac.so && rm $O/in_tree.so.bak
+# optional: single-update lines of the in-tree library with extra bench flags, e.g. EXTRA_FLAGS="0 64 128"
+for f in ${EXTRA_FLAGS}; do
+  timeout -k 10 120 python bench.py --config single --extras none --no-cpu-baseline --steps 300 --warmup 20 --flags $f \
+    | python -c "import json,sys; d=json.loads(sys.stdin.read()); print('single flags=$f', d['value'], d['ms_per_step'])"
+done

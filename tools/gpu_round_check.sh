@@ -1,6 +1,6 @@
 #!/bin/bash
 # Round check on the GPU box: GPU tests (one process), smoke(), the default bench line (all extras), and
-# the single-update prefill A/B lines. tools/gpu_round_check.sh <tag>
+# a 300-step single-update line. tools/gpu_round_check.sh <tag>
 set -e
 TAG=${1:-r02}
 O=gpurun_out/rc_${TAG}
@@ -20,8 +20,6 @@ for k, v in d["configs"].items():
     print(k, v["value"], v.get("ms_per_step", v.get("ms_per_client")), v["step_roofline"]["frac"])
 print("cpu", d["cpu_baseline"]["value"], d["cpu_baseline"]["cores"])
 PY
-for pf in ${PF:-none small}; do
-  timeout -k 10 120 python bench.py --config single --extras none --no-cpu-baseline --steps 300 --warmup 20 \
-    --prefill $pf > $O/single_$pf.json 2>> $O/bench.err || { tail -20 $O/bench.err; exit 1; }
-  python -c "import json,sys; d=json.load(open('$O/single_$pf.json')); print('single prefill=$pf', d['value'], d['ms_per_step'])"
-done
+timeout -k 10 120 python bench.py --config single --extras none --no-cpu-baseline --steps 300 --warmup 20 \
+  > $O/single.json 2>> $O/bench.err || { tail -20 $O/bench.err; exit 1; }
+python -c "import json,sys; d=json.load(open('$O/single.json')); print('single', d['value'], d['ms_per_step'])"
