@@ -93,7 +93,8 @@ constexpr int SEL_NT = 256;               // threads of a k_select block (4 wave
                      // 6.4 (single update 0.0897 -> 0.0927 ms)
 #endif
 #ifndef SCAN_SMALL_LAT
-#define SCAN_SMALL_LAT 1  // latency-bound plans: small segments in k_scan's first blocks (k_sample alone ahead)
+#define SCAN_SMALL_LAT 1  // latency-bound plans: small segments in k_scan's first blocks (k_sample alone ahead;
+                          // batches measured the same either way and keep k_presel)
 #endif
 #ifndef SAMPLE_PICK2
 #define SAMPLE_PICK2 1  // k_sample: both bracket bins from one block scan of the histogram
