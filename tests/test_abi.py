@@ -56,3 +56,14 @@ def test_null_arguments():
     assert lib.coalac_plan_destroy(None) == 0
     assert lib.coalac_encode(None, None, None, None, None, None, None, None, 0, 0, None) == -1
     assert lib.coalac_decode(None, None, None, None, None, None, None, None, 0, None) == -1
+
+
+def test_enum_constants_match_header():
+    """Every COALAC_FLAG_* / COALAC_STAGE_* / COALAC_AGG_* value the Python binding uses is the header's."""
+    hdr = open(_build.HDR).read()
+    declared = {k: int(v) for k, v in re.findall(r"\b(COALAC_(?:FLAG|STAGE|AGG)_\w+)\s*=\s*(\d+)", hdr)}
+    assert {"COALAC_STAGE_FILL", "COALAC_STAGE_SCATTER", "COALAC_STAGE_DECODE", "COALAC_AGG_SUM"} <= set(declared)
+    for name, value in declared.items():
+        if hasattr(_lib, name):
+            assert getattr(_lib, name) == value, name
+    assert _lib.COALAC_STAGE_FILL | _lib.COALAC_STAGE_SCATTER != _lib.COALAC_STAGE_DECODE  # separate bits
