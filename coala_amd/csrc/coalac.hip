@@ -96,6 +96,9 @@ constexpr int SEL_NT = 256;               // threads of a k_select block (4 wave
 #define SCAN_SMALL_LAT 1  // latency-bound plans: small segments in k_scan's first blocks (k_sample alone ahead;
                           // batches measured the same either way and keep k_presel)
 #endif
+#ifndef DECODE_FS
+#define DECODE_FS 1  // latency-bound plans: the whole decode as k_fillscatter (else k_fill + k_scatter)
+#endif
 #ifndef SAMPLE_PICK2
 #define SAMPLE_PICK2 1  // k_sample: both bracket bins from one block scan of the histogram
 #endif
@@ -2357,12 +2360,9 @@ __global__ __launch_bounds__(BLOCK, DECODE_WPE) void k_decode(Params P) {
 // Latency-bound plans, DECODE_SCATTER: the background first (k_fill: every unit's 0 / base + 0.0f, no entry
 // lookup, so the write stream starts at once), then the kept values on top (k_scatter: one thread per entry,
 // per k_bounds chunk; bounds-checked like k_decode). Stream order puts every kept value after the fill.
+// one wave writes unit U's background: 0, or base + 0.0f (-0 -> +0, as the oracle's base + dense)
 template <bool HASBASE>
-__global__ __launch_bounds__(BLOCK) void k_fill(Params P) {
-  const uint32_t lane = lane_id();
-  const uint32_t u = blockIdx.x * WAVES + (threadIdx.x >> 6);
-  if (u >= P.n_units) return;
-  const UnitDev U = P.units[u];
+DEV void fill_unit(const Params& P, const UnitDev& U, uint32_t lane) {
   const __amdgpu_buffer_rsrc_t rout = unit_rsrc(P.out + U.off, U.len);
   float4 b[UNIT_IT];
   if (HASBASE) {
@@ -2382,6 +2382,49 @@ __global__ __launch_bounds__(BLOCK) void k_fill(Params P) {
   } else {
 #pragma unroll
     for (uint32_t it = 0; it < UNIT_IT; ++it) unit_store_x1x4<FILL_AUX>(rout, (it * 64 + lane) * 16, b[it]);
+  }
+}
+
+template <bool HASBASE>
+__global__ __launch_bounds__(BLOCK) void k_fill(Params P) {
+  const uint32_t u = blockIdx.x * WAVES + (threadIdx.x >> 6);
+  if (u >= P.n_units) return;
+  fill_unit<HASBASE>(P, P.units[u], lane_id());
+}
+
+// k_fillscatter (latency-bound plans, DECODE_FS): k_fill and k_scatter as one launch, one wave per unit. The
+// wave stores its unit's background first (nothing to wait for), finds the unit's kept entries [lo, hi) in
+// its segment's sorted idx list in-kernel (wave_lower_bound, while the stores drain), waits until its own
+// stores have completed, and then writes the kept values on top: every output element is written by the
+// wave that owns its unit, background before value. Entries are bounds-checked against the unit (an
+// untrusted list cannot write outside it). Same bytes as k_fill + k_scatter, one launch and no second pass
+// over the payload's chunk list.
+template <bool RAW, bool HASBASE>
+__global__ __launch_bounds__(BLOCK) void k_fillscatter(Params P) {
+  const uint32_t lane = lane_id();
+  const uint32_t u = blockIdx.x * WAVES + (threadIdx.x >> 6);
+  if (u >= P.n_units) return;
+  const UnitDev U = P.units[u];
+  fill_unit<HASBASE>(P, U, lane);
+  const int32_t* L[2] = {P.cidx + U.out_off, P.cidx + U.out_off};
+  const uint32_t kk[2] = {U.k, U.last ? 0u : U.k};  // a segment's last unit ends at k: no search
+  const uint32_t tg[2] = {U.start, U.last ? 0xFFFFFFFFu : U.start + U.len};
+  uint32_t res[2];
+  wave_lower_bound<2>(L, kk, tg, res);
+  const uint32_t lo = min(res[0], U.k), hi = max(lo, min(U.last ? U.k : res[1], U.k));
+  const float mn = RAW ? 0.0f : P.cmn[U.seg];
+  const float sc = RAW ? 0.0f : P.cscale[U.seg];
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the background stores have completed
+  for (uint32_t e0 = lo; e0 < hi; e0 += 64) {
+    const uint32_t e = e0 + lane;
+    if (e < hi) {
+      const uint64_t ge = U.out_off + e;
+      const uint32_t pos = (uint32_t)P.cidx[ge] - U.start;
+      if (pos < U.len) {
+        const float v = code_value<RAW>(load_code<RAW>(P, ge), mn, sc);
+        P.out[U.off + pos] = HASBASE ? P.base[U.off + pos] + v : v;
+      }
+    }
   }
 }
 
@@ -3423,7 +3466,17 @@ int coalac_decode_sched(coalac_plan_t plan, const int32_t* d_idx, const void* d_
   } while (0)
   if (!(stages & COALAC_STAGE_DECODE))
     ;
-  else if (scatter) {
+  else if (scatter && DECODE_FS && (stages & COALAC_STAGE_FILL) && (stages & COALAC_STAGE_SCATTER)) {
+    const dim3 gf((plan->n_units + WAVES - 1) / WAVES);
+    if (raw && hb)
+      hipLaunchKernelGGL((k_fillscatter<true, true>), gf, dim3(BLOCK), 0, st, P);
+    else if (raw)
+      hipLaunchKernelGGL((k_fillscatter<true, false>), gf, dim3(BLOCK), 0, st, P);
+    else if (hb)
+      hipLaunchKernelGGL((k_fillscatter<false, true>), gf, dim3(BLOCK), 0, st, P);
+    else
+      hipLaunchKernelGGL((k_fillscatter<false, false>), gf, dim3(BLOCK), 0, st, P);
+  } else if (scatter) {
     const uint32_t gf = (plan->n_units + WAVES - 1) / WAVES;
     if (!(stages & COALAC_STAGE_FILL))
       ;
