@@ -70,8 +70,10 @@ constexpr uint32_t SMALL_MAX_LATENCY = 1024;  // ... in latency-bound plans (<= 
                                               // the length of k_presel; bigger segments take the sampled path
 constexpr uint32_t LATENCY_PLAN_UNITS = 8192;  // ~1.3 ResNet-50 updates
 constexpr uint32_t SAMPLE_MAX = 8192;     // sampled keys per large segment
-constexpr int SEL_NT = 256;               // threads of a k_select block (4 waves: one per SIMD, so a
-                                          // block finds room beside a streaming kernel's waves)
+constexpr int SEL_NT = 256;               // threads of a k_select block in batches (4 waves: one per SIMD, so
+                                          // a block finds room beside a streaming kernel's waves)
+constexpr int SEL_NT_LAT = 512;           // ... in latency-bound plans, where nothing streams beside it (one
+                                          // ResNet-50 update: k_select 11.3 -> 10.2 us; batches measured slower)
 #ifndef SCAN_WPE
 #define SCAN_WPE 5
 #endif
@@ -1281,9 +1283,9 @@ struct SelSmem {
   uint32_t upre[UCAP + 1];
   uint32_t ge[UCAP];   // per unit of the chunk: count above T* (bits 0-15) | count equal T* (bits 16-31)
   uint2 lst[WLIST];    // in-window entries {value bits, unit}, all waves concatenated = index order
-  uint32_t wcnt[SEL_NT / 64];
+  uint32_t wcnt[SEL_NT_LAT / 64];
   uint32_t sh[64];
-  float shf[2 * (SEL_NT / 64)];
+  float shf[2 * (SEL_NT_LAT / 64)];
 };
 static_assert(sizeof(SelSmem) <= 29 * 1024, "select LDS budget");
 
@@ -1871,10 +1873,10 @@ DEV void segment_select(const Params& P, uint32_t li, SelSmem& S) {
   STAMP(P, li, 12);
 }
 
-template <bool DELTA, bool RAW>
-__global__ __launch_bounds__(SEL_NT) void k_select(Params P) {
+template <bool DELTA, bool RAW, int NT = SEL_NT>
+__global__ __launch_bounds__(NT) void k_select(Params P) {
   __shared__ SelSmem S;
-  segment_select<SEL_NT, DELTA, RAW>(P, blockIdx.x, S);
+  segment_select<NT, DELTA, RAW>(P, blockIdx.x, S);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -3009,7 +3011,10 @@ int launch_encode(const Params& P, coalac_plan_t plan, hipStream_t st, const coa
   if ((stages & COALAC_STAGE_SELECT) && plan->n_large) {
     if (!P.scan_hist) hipLaunchKernelGGL(k_ghist, dim3(plan->n_groups), dim3(BLOCK), 0, st, P);
     hipLaunchKernelGGL(k_gwin, dim3(plan->n_groups), dim3(BLOCK), 0, st, P);
-    hipLaunchKernelGGL((k_select<DELTA, RAW>), dim3(plan->n_large), dim3(SEL_NT), 0, st, P);
+    if (plan->n_lunits <= LATENCY_PLAN_UNITS)
+      hipLaunchKernelGGL((k_select<DELTA, RAW, SEL_NT_LAT>), dim3(plan->n_large), dim3(SEL_NT_LAT), 0, st, P);
+    else
+      hipLaunchKernelGGL((k_select<DELTA, RAW>), dim3(plan->n_large), dim3(SEL_NT), 0, st, P);
   }
   ENC_BOUNDARY(3);
   if ((stages & COALAC_STAGE_SELECT) && plan->n_large) launch_emit<DELTA, RAW>(P, plan, st);
