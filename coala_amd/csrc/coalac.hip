@@ -72,6 +72,9 @@ constexpr uint32_t LATENCY_PLAN_UNITS = 8192;  // ~1.3 ResNet-50 updates
 constexpr uint32_t SAMPLE_MAX = 8192;     // sampled keys per large segment
 constexpr int SEL_NT = 256;               // threads of a k_select block in batches (4 waves: one per SIMD, so
                                           // a block finds room beside a streaming kernel's waves)
+#ifndef GHIST_NT_LAT
+#define GHIST_NT_LAT 1024  // k_ghist block in latency-bound plans (256 / 512 / 1024: 6.5 / 5.7 / 5.3 us on one update)
+#endif
 constexpr int SEL_NT_LAT = 512;           // ... in latency-bound plans, where nothing streams beside it (one
                                           // ResNet-50 update: k_select 11.3 -> 10.2 us; batches measured slower)
 #ifndef SCAN_WPE
@@ -1384,16 +1387,17 @@ DEV void select_generic(const Params& P, uint32_t lb, uint32_t nu, uint32_t tlo,
 // k_ghist: the group's HB2-bin histogram of the band keys [tlo, thi] -> ghist[group]. (A fused variant in
 // which the segment's last-arriving group block ran segment_pick needed an agent-scope release fence in
 // every block — an L2 writeback on gfx950 — and was ~100x slower; kernel boundaries are cheaper.)
+template <int NT = BLOCK>
 DEV void group_hist(const Params& P, uint32_t gi, uint32_t* hist, uint32_t* upre, uint32_t* sh) {
   const uint4 G = P.groups[gi];  // x: large-segment index, y: first large unit, z: units, w: segment
   const uint32_t t = threadIdx.x;
   // one load round for everything that depends on G only
   const uint32_t tlo = P.tlo[G.y], thi = P.thi[G.y], hh = P.shhi[G.x];
   const uint32_t c = t < G.z ? min(P.cntC[G.y + t], P.ccap) : 0u;  // stored records only
-  for (uint32_t i = t; i < HB2; i += BLOCK) hist[i] = 0;
-  const uint32_t total = reg_prefix<BLOCK>(c, G.z, upre, sh);  // barriers inside
+  for (uint32_t i = t; i < HB2; i += NT) hist[i] = 0;
+  const uint32_t total = reg_prefix<NT>(c, G.z, upre, sh);  // barriers inside
   const Band band(tlo, thi, hh);
-  unit_sweep<WAVES, GSWEEP>(
+  unit_sweep<NT / 64, GSWEEP>(
       P.cand, P.ccap, G.y, upre, G.z, total,
       [&](float x, bool valid, uint32_t) {
         const uint32_t key = fkey(x);
@@ -1401,14 +1405,16 @@ DEV void group_hist(const Params& P, uint32_t gi, uint32_t* hist, uint32_t* upre
       },
       [&](uint32_t) {});
   __syncthreads();
-  for (uint32_t i = t; i < HB2; i += BLOCK) pst(P, P.ghist + (uint64_t)gi * HB2 + i, hist[i]);
+  for (uint32_t i = t; i < HB2; i += NT) pst(P, P.ghist + (uint64_t)gi * HB2 + i, hist[i]);
 }
 
-__global__ __launch_bounds__(BLOCK) void k_ghist(Params P) {
+// NT: 256 threads in batches, GHIST_NT_LAT in latency-bound plans (nothing streams beside the block)
+template <int NT = BLOCK>
+__global__ __launch_bounds__(NT) void k_ghist(Params P) {
   __shared__ uint32_t hist[HB2];
   __shared__ uint32_t upre[GU + 1];
   __shared__ uint32_t sh[64];
-  group_hist(P, blockIdx.x, hist, upre, sh);
+  group_hist<NT>(P, blockIdx.x, hist, upre, sh);
 }
 
 // segment_pick: per large segment — validate the sampled bracket, sum the group histograms, pick the bin of
@@ -3009,7 +3015,12 @@ int launch_encode(const Params& P, coalac_plan_t plan, hipStream_t st, const coa
   }
   ENC_BOUNDARY(2);
   if ((stages & COALAC_STAGE_SELECT) && plan->n_large) {
-    if (!P.scan_hist) hipLaunchKernelGGL(k_ghist, dim3(plan->n_groups), dim3(BLOCK), 0, st, P);
+    if (!P.scan_hist) {
+      if (plan->n_lunits <= LATENCY_PLAN_UNITS)
+        hipLaunchKernelGGL(k_ghist<GHIST_NT_LAT>, dim3(plan->n_groups), dim3(GHIST_NT_LAT), 0, st, P);
+      else
+        hipLaunchKernelGGL(k_ghist<BLOCK>, dim3(plan->n_groups), dim3(BLOCK), 0, st, P);
+    }
     hipLaunchKernelGGL(k_gwin, dim3(plan->n_groups), dim3(BLOCK), 0, st, P);
     if (plan->n_lunits <= LATENCY_PLAN_UNITS)
       hipLaunchKernelGGL((k_select<DELTA, RAW, SEL_NT_LAT>), dim3(plan->n_large), dim3(SEL_NT_LAT), 0, st, P);
@@ -3056,7 +3067,7 @@ int launch_front(const Params& P, coalac_plan_t plan, hipStream_t st, const coal
   hipLaunchKernelGGL((k_fused<DELTA, RAW>), dim3(plan->n_front), dim3(BLOCK), 0, st, Q);
   BOUNDARY(2);
   if (plan->n_large) {
-    hipLaunchKernelGGL(k_ghist, dim3(plan->n_groups), dim3(BLOCK), 0, st, P);
+    hipLaunchKernelGGL(k_ghist<BLOCK>, dim3(plan->n_groups), dim3(BLOCK), 0, st, P);
     hipLaunchKernelGGL(k_gwin, dim3(plan->n_groups), dim3(BLOCK), 0, st, P);
     hipLaunchKernelGGL((k_select<DELTA, RAW>), dim3(plan->n_large), dim3(SEL_NT), 0, st, P);
   }
