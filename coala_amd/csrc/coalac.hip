@@ -72,6 +72,9 @@ constexpr uint32_t LATENCY_PLAN_UNITS = 8192;  // ~1.3 ResNet-50 updates
 constexpr uint32_t SAMPLE_MAX = 8192;     // sampled keys per large segment
 constexpr int SEL_NT = 256;               // threads of a k_select block in batches (4 waves: one per SIMD, so
                                           // a block finds room beside a streaming kernel's waves)
+#ifndef GWIN_NT_LAT
+#define GWIN_NT_LAT 512  // k_gwin block in latency-bound plans (256 or 512: one or two histogram bins per thread)
+#endif
 #ifndef GHIST_NT_LAT
 #define GHIST_NT_LAT 1024  // k_ghist block in latency-bound plans (256 / 512 / 1024: 6.5 / 5.7 / 5.3 us on one update)
 #endif
@@ -1422,13 +1425,15 @@ __global__ __launch_bounds__(NT) void k_ghist(Params P) {
 // generic single-block path (bracket miss, nothing to take from B, huge segment, test flags). Every group
 // block of the segment computes it (identically) at the start of k_gwin — cheaper than a launch of its
 // own between k_ghist and k_gwin. Returned to every thread.
+template <int NT = BLOCK>
 DEV uint4 segment_pick(const Params& P, const SegDev& sd, const Band& band, uint32_t* hist, uint32_t* sh) {
   const uint32_t t = threadIdx.x;
   const uint32_t lb = sd.lu_begin, nu = sd.unit_end - sd.unit_begin, k = sd.k;
   const uint32_t g0 = sd.g_begin, ng = (nu + GU - 1) / GU;
-  // one load round: the group histograms (both of this thread's bins, up to 24 groups' loads in flight)
-  // and the per-unit counts (up to 3 per thread) together
-  static_assert(HB2 == 2 * BLOCK, "two histogram bins per thread");
+  // one load round: the group histograms (this thread's bins t and t + NT, up to 24 groups' loads in
+  // flight) and the per-unit counts (up to 3 per thread) together
+  static_assert(HB2 == 2 * NT || HB2 == NT, "one or two histogram bins per thread");
+  constexpr bool TWO = HB2 == 2 * NT;
   constexpr uint32_t GB = 24, CB = 3;
   uint32_t h0 = 0, h1 = 0, sa = 0, sc = 0, ov = 0;
   {
@@ -1437,11 +1442,11 @@ DEV uint4 segment_pick(const Params& P, const SegDev& sd, const Band& band, uint
     for (uint32_t j = 0; j < GB; ++j) {
       const uint64_t row = (uint64_t)(g0 + min(j, ng - 1)) * HB2;
       v0[j] = P.ghist[row + t];
-      v1[j] = P.ghist[row + BLOCK + t];
+      v1[j] = TWO ? P.ghist[row + NT + t] : 0u;
     }
 #pragma unroll
     for (uint32_t j = 0; j < CB; ++j) {
-      const uint32_t i = min(t + j * BLOCK, nu - 1);
+      const uint32_t i = min(t + j * NT, nu - 1);
       cc[j] = P.cntC[lb + i];
       ca[j] = P.cntA[lb + i];
     }
@@ -1452,7 +1457,7 @@ DEV uint4 segment_pick(const Params& P, const SegDev& sd, const Band& band, uint
     }
 #pragma unroll
     for (uint32_t j = 0; j < CB; ++j) {
-      if (t + j * BLOCK < nu) {
+      if (t + j * NT < nu) {
         sa += ca[j];
         sc += cc[j];
         ov += cc[j] > P.ccap ? 1u : 0u;
@@ -1465,7 +1470,7 @@ DEV uint4 segment_pick(const Params& P, const SegDev& sd, const Band& band, uint
     for (uint32_t j = 0; j < 8; ++j) {
       const uint64_t row = (uint64_t)(g0 + min(g + j, ng - 1)) * HB2;
       v0[j] = P.ghist[row + t];
-      v1[j] = P.ghist[row + BLOCK + t];
+      v1[j] = TWO ? P.ghist[row + NT + t] : 0u;
     }
 #pragma unroll
     for (uint32_t j = 0; j < 8; ++j) {
@@ -1473,43 +1478,47 @@ DEV uint4 segment_pick(const Params& P, const SegDev& sd, const Band& band, uint
       h1 += g + j < ng ? v1[j] : 0u;
     }
   }
-  for (uint32_t i = t + CB * BLOCK; i < nu; i += BLOCK) {
+  for (uint32_t i = t + CB * NT; i < nu; i += NT) {
     const uint32_t c = P.cntC[lb + i];
     sa += P.cntA[lb + i];
     sc += c;
     ov += c > P.ccap ? 1u : 0u;
   }
   hist[t] = h0;
-  hist[BLOCK + t] = h1;
-  sa = block_sum<BLOCK>(sa, sh);  // barriers inside (also publish hist)
-  sc = block_sum<BLOCK>(sc, sh);
-  ov = block_sum<BLOCK>(ov, sh);
+  if (TWO) hist[NT + t] = h1;
+  sa = block_sum<NT>(sa, sh);  // barriers inside (also publish hist)
+  sc = block_sum<NT>(sc, sh);
+  ov = block_sum<NT>(ov, sh);
   // (a unit that overflowed its record slots sends the segment to the raw-data path in segment_select)
   const bool generic = (P.flags & (COALAC_FLAG_FORCE_EXACT | COALAC_FLAG_GENERIC_SELECT)) || !(sa < k && k <= sc) ||
                        nu > UCAP || ov != 0;
   if (generic) return make_uint4(0u, 0u, 0u, 1u);
   __syncthreads();
   uint32_t r = k - sa;
-  const uint32_t b = hist_pick<BLOCK, HB2>(hist, r, sh);
+  const uint32_t b = hist_pick<NT, HB2>(hist, r, sh);
   if (b == NONE) return make_uint4(0u, 0u, 0u, 1u);
   return make_uint4(band.wlo(b), band.whi(b), r, 0u);
 }
 
 // k_gwin: per group — per-unit counts of keys above the window (-> gtC), the group's in-window entries
 // in index order (-> glist, count -> gcnt), min/max of the values above the window (-> gmm)
-struct GwinSmem {
+template <int NW = WAVES>
+struct GwinSmemT {
   uint32_t upre[GU + 1];
-  uint2 slots[WAVES][GCAP];
-  uint32_t wcnt[WAVES];
-  float shf[2 * WAVES];
+  uint2 slots[NW][GCAP];
+  uint32_t wcnt[NW];
+  float shf[2 * NW];
 };
+using GwinSmem = GwinSmemT<WAVES>;
 
 template <int NT, bool DELTA, bool RAW>
 DEV void segment_select(const Params& P, uint32_t li, SelSmem& S);
 
 // (upre / total: the group's record prefix, already in W_.upre)
+template <int NT = BLOCK>
 DEV void group_window(const Params& P, uint32_t gi, const uint4 G, const uint4 st, uint32_t lu_begin, uint32_t total,
-                      GwinSmem& W_, uint32_t* sh) {
+                      GwinSmemT<NT / 64>& W_, uint32_t* sh) {
+  constexpr int NW = NT / 64;
   uint32_t* upre = W_.upre;
   auto& slots = W_.slots;
   uint32_t* wcnt = W_.wcnt;
@@ -1519,7 +1528,7 @@ DEV void group_window(const Params& P, uint32_t gi, const uint4 G, const uint4 s
   const uint32_t useg0 = G.y - lu_begin;  // unit index (within the segment) of the group's first unit
   uint32_t wc = 0, ug = 0;
   float lmn = qnan(), lmx = qnan();
-  unit_sweep<WAVES, GSWEEP>(
+  unit_sweep<NW, GSWEEP>(
       P.cand, P.ccap, G.y, upre, G.z, total,
       [&](float x, bool valid, uint32_t u) {
         const uint32_t key = fkey(x);
@@ -1547,14 +1556,14 @@ DEV void group_window(const Params& P, uint32_t gi, const uint4 G, const uint4 s
   __syncthreads();
   uint32_t wpre = 0, W = 0;
 #pragma unroll
-  for (int i = 0; i < WAVES; ++i) {
+  for (int i = 0; i < NW; ++i) {
     const uint32_t c = wcnt[i];
     if (i < (int)wv) wpre += c;
     W += c;
   }
   for (uint32_t q = lane; q < wc && q < GCAP; q += 64)
     if (wpre + q < GCAP) pst(P, P.glist + (uint64_t)gi * GCAP + wpre + q, slots[wv][q]);
-  block_minmax<BLOCK>(lmn, lmx, shf);
+  block_minmax<NT>(lmn, lmx, shf);
   if (t == 0) {
     pst(P, P.gcnt + gi, W);
     pst(P, P.gmm + 2 * gi, lmn);
@@ -1562,28 +1571,31 @@ DEV void group_window(const Params& P, uint32_t gi, const uint4 G, const uint4 s
   }
 }
 
-DEV void group_pick_window(const Params& P, uint32_t gi, GwinSmem& W, uint32_t* hist, uint32_t* sh) {
+template <int NT = BLOCK>
+DEV void group_pick_window(const Params& P, uint32_t gi, GwinSmemT<NT / 64>& W, uint32_t* hist, uint32_t* sh) {
   const uint4 G = P.groups[gi];
   // one load round for everything that depends on G only: the segment, its band, the group's counts
   const SegDev sd = P.lsegs[G.x];
   const uint32_t tlo = P.tlo[G.y], thi = P.thi[G.y], hh = P.shhi[G.x];
   const uint32_t c = threadIdx.x < G.z ? min(P.cntC[G.y + threadIdx.x], P.ccap) : 0u;
-  const uint32_t total = reg_prefix<BLOCK>(c, G.z, W.upre, sh);
+  const uint32_t total = reg_prefix<NT>(c, G.z, W.upre, sh);
   const Band band(tlo, thi, hh);
-  const uint4 st = segment_pick(P, sd, band, hist, sh);
+  const uint4 st = segment_pick<NT>(P, sd, band, hist, sh);
   if (threadIdx.x == 0 && G.y == sd.lu_begin) {  // the segment's first group
     uint2* ss = reinterpret_cast<uint2*>(P.sstate + G.x);
     pst(P, ss, make_uint2(st.x, st.y));
     pst(P, ss + 1, make_uint2(st.z, st.w));
   }
-  if (st.w == 0) group_window(P, gi, G, st, sd.lu_begin, total, W, sh);
+  if (st.w == 0) group_window<NT>(P, gi, G, st, sd.lu_begin, total, W, sh);
 }
 
-__global__ __launch_bounds__(BLOCK) void k_gwin(Params P) {
-  __shared__ GwinSmem W;
+// NT: 256 threads in batches, GWIN_NT_LAT in latency-bound plans (nothing streams beside the block)
+template <int NT = BLOCK>
+__global__ __launch_bounds__(NT) void k_gwin(Params P) {
+  __shared__ GwinSmemT<NT / 64> W;
   __shared__ uint32_t hist[HB2];
   __shared__ uint32_t sh[64];
-  group_pick_window(P, blockIdx.x, W, hist, sh);
+  group_pick_window<NT>(P, blockIdx.x, W, hist, sh);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -3021,7 +3033,10 @@ int launch_encode(const Params& P, coalac_plan_t plan, hipStream_t st, const coa
       else
         hipLaunchKernelGGL(k_ghist<BLOCK>, dim3(plan->n_groups), dim3(BLOCK), 0, st, P);
     }
-    hipLaunchKernelGGL(k_gwin, dim3(plan->n_groups), dim3(BLOCK), 0, st, P);
+    if (plan->n_lunits <= LATENCY_PLAN_UNITS)
+      hipLaunchKernelGGL(k_gwin<GWIN_NT_LAT>, dim3(plan->n_groups), dim3(GWIN_NT_LAT), 0, st, P);
+    else
+      hipLaunchKernelGGL(k_gwin<BLOCK>, dim3(plan->n_groups), dim3(BLOCK), 0, st, P);
     if (plan->n_lunits <= LATENCY_PLAN_UNITS)
       hipLaunchKernelGGL((k_select<DELTA, RAW, SEL_NT_LAT>), dim3(plan->n_large), dim3(SEL_NT_LAT), 0, st, P);
     else
@@ -3068,7 +3083,7 @@ int launch_front(const Params& P, coalac_plan_t plan, hipStream_t st, const coal
   BOUNDARY(2);
   if (plan->n_large) {
     hipLaunchKernelGGL(k_ghist<BLOCK>, dim3(plan->n_groups), dim3(BLOCK), 0, st, P);
-    hipLaunchKernelGGL(k_gwin, dim3(plan->n_groups), dim3(BLOCK), 0, st, P);
+    hipLaunchKernelGGL(k_gwin<BLOCK>, dim3(plan->n_groups), dim3(BLOCK), 0, st, P);
     hipLaunchKernelGGL((k_select<DELTA, RAW>), dim3(plan->n_large), dim3(SEL_NT), 0, st, P);
   }
   BOUNDARY(3);
