@@ -107,6 +107,12 @@ constexpr int SEL_NT_LAT = 512;           // ... in latency-bound plans, where n
 #ifndef DECODE_FS
 #define DECODE_FS 1  // latency-bound plans: the whole decode as k_fillscatter (else k_fill + k_scatter)
 #endif
+#ifndef SCAN_WPE_LAT
+#define SCAN_WPE_LAT 5  // latency-bound plans' k_scan: blocks per CU
+#endif
+#ifndef SCAN_NB_LAT
+#define SCAN_NB_LAT 1   // ... and load batches per unit
+#endif
 #ifndef SAMPLE_PICK2
 #define SAMPLE_PICK2 1  // k_sample: both bracket bins from one block scan of the histogram
 #endif
@@ -1165,8 +1171,10 @@ __global__ __launch_bounds__(BLOCK) void k_presel(Params P) {
 
 // k_scan: streams the large units, one wave each. (WITH_SMALL: blocks [0, scan_small) first encode the
 // small segments — no longer launched: k_presel runs them beside the samplers.)
-template <bool DELTA, bool RAW, bool WITH_SMALL, bool HIST = false>
-__global__ __launch_bounds__(BLOCK, SCAN_WPE) void k_scan(Params P) {
+// (WPE / NB: launch-bound blocks per CU and load batches; the latency-bound plans' instantiation, the one
+// WITH_SMALL, takes its own — nothing streams beside it)
+template <bool DELTA, bool RAW, bool WITH_SMALL, bool HIST = false, int WPE = SCAN_WPE, int NB = SCAN_NB>
+__global__ __launch_bounds__(BLOCK, WPE) void k_scan(Params P) {
   // one LDS arena: candidate staging (WAVES x STAGE_CAP records) or a small segment's values + histogram
   // (WITH_SMALL only: without it the block needs 16 KB of LDS instead of 24.8 KB)
   constexpr size_t SMALL_BYTES = WITH_SMALL ? (SMALL_MAX + HIST_BINS + 64) * 4 : 0;
@@ -1191,7 +1199,7 @@ __global__ __launch_bounds__(BLOCK, SCAN_WPE) void k_scan(Params P) {
     scan_unit_t<DELTA, DELTA ? 4 : SCAN_NB, false, true>(P, lu, L, [&]() { return make_uint2(tlo, thi); },
                                                           stage + wv * STAGE_CAP, gh, &band);
   } else {
-    scan_unit<DELTA, DELTA ? 4 : SCAN_NB>(P, lu, L, P.tlo[lu], P.thi[lu], stage + wv * STAGE_CAP);
+    scan_unit<DELTA, DELTA ? 4 : NB>(P, lu, L, P.tlo[lu], P.thi[lu], stage + wv * STAGE_CAP);
   }
 }
 
@@ -3018,7 +3026,8 @@ int launch_encode(const Params& P, coalac_plan_t plan, hipStream_t st, const coa
   ENC_BOUNDARY(1);
   if (small_in_scan) {
     Q.scan_small = plan->n_small;
-    hipLaunchKernelGGL((k_scan<DELTA, RAW, true>), dim3(gu + plan->n_small), dim3(BLOCK), 0, st, Q);
+    hipLaunchKernelGGL((k_scan<DELTA, RAW, true, false, SCAN_WPE_LAT, SCAN_NB_LAT>), dim3(gu + plan->n_small),
+                       dim3(BLOCK), 0, st, Q);
   } else if ((stages & COALAC_STAGE_SCAN) && gu) {
     if (P.scan_hist)
       hipLaunchKernelGGL((k_scan<DELTA, RAW, false, true>), dim3(gu), dim3(BLOCK), 0, st, Q);
