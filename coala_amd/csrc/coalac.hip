@@ -108,10 +108,11 @@ constexpr int SEL_NT_LAT = 512;           // ... in latency-bound plans, where n
 #define DECODE_FS 1  // latency-bound plans: the whole decode as k_fillscatter (else k_fill + k_scatter)
 #endif
 #ifndef SCAN_WPE_LAT
-#define SCAN_WPE_LAT 5  // latency-bound plans' k_scan: blocks per CU
+#define SCAN_WPE_LAT 6  // latency-bound plans' k_scan: blocks per CU (5 / 1 batch: 24.5 us, 6 / 2: 23.0, 6 / 1
+                        // spills: 31.7, 8 / 4: 24.2 on one update; batches keep SCAN_WPE / SCAN_NB)
 #endif
 #ifndef SCAN_NB_LAT
-#define SCAN_NB_LAT 1   // ... and load batches per unit
+#define SCAN_NB_LAT 2   // ... and load batches per unit
 #endif
 #ifndef SAMPLE_PICK2
 #define SAMPLE_PICK2 1  // k_sample: both bracket bins from one block scan of the histogram
