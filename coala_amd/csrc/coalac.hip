@@ -1919,7 +1919,10 @@ __global__ __launch_bounds__(NT) void k_select(Params P) {
 #endif
 // ... in latency-bound plans (<= LATENCY_PLAN_UNITS units): a wave's units are handled one after the other,
 // so fewer per wave shortens the launch (one ResNet-50 update: 8 per wave 13.1 us, 2 per wave 6.0 us)
-constexpr uint32_t EMIT_UPW_LATENCY = 2;
+#ifndef EMIT_UPW_LAT
+#define EMIT_UPW_LAT 2u
+#endif
+constexpr uint32_t EMIT_UPW_LATENCY = EMIT_UPW_LAT;
 #ifndef EMIT_ROWS
 #define EMIT_ROWS 1  // 64-record rows of every unit loaded before the first is classified (1 or 2)
 #endif
