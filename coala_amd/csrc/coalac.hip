@@ -1918,9 +1918,10 @@ __global__ __launch_bounds__(NT) void k_select(Params P) {
 #define EMIT_UPW 8u  // large units per k_emit wave in batches (C3 share: +2 % over 2 units per wave)
 #endif
 // ... in latency-bound plans (<= LATENCY_PLAN_UNITS units): a wave's units are handled one after the other,
-// so fewer per wave shortens the launch (one ResNet-50 update: 8 per wave 13.1 us, 2 per wave 6.0 us)
+// so fewer per wave shortens the launch (one ResNet-50 update: 8 per wave 13.1 us, 2 per wave 6.0, 1 per
+// wave 5.1)
 #ifndef EMIT_UPW_LAT
-#define EMIT_UPW_LAT 2u
+#define EMIT_UPW_LAT 1u
 #endif
 constexpr uint32_t EMIT_UPW_LATENCY = EMIT_UPW_LAT;
 #ifndef EMIT_ROWS
