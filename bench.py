@@ -88,6 +88,9 @@ def parse():
     p.add_argument("--single-split", type=int, default=SINGLE_SPLIT,
                    help="config 'single': the update's segments cut into this many ranges, each a sub-plan on its "
                         "own stream (their latency-bound phases overlap)")
+    p.add_argument("--graph", choices=["auto", "on", "off"], default="auto",
+                   help="replay each timed step as a captured hipGraph: auto = the latency-bound configs "
+                        f"({', '.join(GRAPH_CONFIGS) if 'GRAPH_CONFIGS' in globals() else 'single, single_x2, C5'})")
     p.add_argument("--cpu-seconds", type=float, default=8.0, help="CPU baseline time budget per leg")
     p.add_argument("--no-cpu-baseline", action="store_true")
     return p.parse_args()
@@ -240,6 +243,13 @@ def build_table(cfg, a, rank, headline):
                            "segments_per_client": len(t.sizes)}
 
 
+GRAPH_CONFIGS = ("single", "single_x2", "C5")  # latency-bound plans: step time ~ host launch time
+
+
+def use_graph(cfg, a):
+    return a.graph == "on" or (a.graph == "auto" and cfg in GRAPH_CONFIGS)
+
+
 def run_workload(cfg, a, dev, world, rank, headline):
     import torch
     import torch.distributed as dist
@@ -275,6 +285,32 @@ def run_workload(cfg, a, dev, world, rank, headline):
         step(j=w)
     fallbacks = sum(p.fallbacks() for p in pipes)
     timeouts = sum(p.timeouts() for p in pipes)
+
+    # Latency-bound configs: each slot's step captured once as a hipGraph and replayed on that slot's stream
+    # (the same kernels on the same buffers, one graph launch per step instead of the per-call Python checks,
+    # ctypes calls and ~8 kernel launches, which take about as long as the ~80 us of GPU work of one update:
+    # on a box with a slower host the eager single step measured 0.138 ms for 0.080 ms of kernels; with a
+    # fast host the graph costs ~4 us per step more than eager — single 0.084 vs 0.080, single_x2 0.058 vs
+    # 0.064, C5 0.097 vs 0.093 ms — and it is the stable one)
+    graphs = None
+    if use_graph(cfg, a):
+        torch.cuda.synchronize()
+        graphs = []
+        for p, enc, out in slots:
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, stream=p.streams[0]):
+                p.roundtrip(flat, base=base, enc=enc, out=out, joined=False)
+            graphs.append((g, p.streams[0]))
+        torch.cuda.synchronize()
+
+        def step(i=None, j=0, joined=a.joined, eager=step):  # noqa: F811 (the timed steps only)
+            if i is not None:
+                return eager(i, j, joined)
+            g, st = graphs[j % len(graphs)]
+            with torch.cuda.stream(st):
+                g.replay()
+        for w in range(len(graphs)):
+            step(j=w)
 
     # The timed region carries no timing event (each recorded event costs a dispatch gap) and its
     # sub-batch streams are not joined per step, so consecutive steps overlap.
@@ -357,6 +393,7 @@ def run_workload(cfg, a, dev, world, rank, headline):
         "stages_ms": {k: round(v, 4) for k, v in stages.items()},
         "sample_fallbacks": fallbacks,
         "wait_timeouts": timeouts,
+        "graph": graphs is not None,
     }
     if headline:
         traffic, src = pmc_traffic(dom, cfg, a, split)
@@ -483,7 +520,7 @@ def main():
             "wait_timeouts": head["wait_timeouts"],
             "configs": {k: {f: v[f] for f in ("value", "ms_per_step", "step_roofline", "roofline", "stages_ms", "desc",
                                               "elements_per_gpu", "segments_per_gpu", "split", "inflight",
-                                              "sample_fallbacks")}
+                                              "graph", "sample_fallbacks")}
                         for k, v in extras.items()},
         }
         if plugin is not None:

@@ -252,3 +252,32 @@ def test_split_pipelines_in_flight_on_disjoint_streams(cuda):
         torch.cuda.synchronize()
         assert torch.equal(e.idx, bufs[j][0].idx) and torch.equal(e.vals, bufs[j][0].vals), j
         assert torch.equal(d.view(torch.int32), bufs[j][1].view(torch.int32)), j
+
+
+def test_single_update_roundtrip_graph_replay(cuda):
+    """bench.py's latency-bound configs replay each step as a captured hipGraph: the captured roundtrip of
+    one update (every kernel of the encode and the decode, launched through the C ABI on the capture
+    stream) replayed on new input data in the same buffers gives exactly the eager result."""
+    t = SegmentTable(fp32_sizes("resnet50_tv"), 0.01, 1)
+    flat = synth_batch(t, cuda, client_ids=[21])
+    pipe = SplitPipeline(t, 8, split=1, device=cuda)
+    enc, out = pipe.empty_encoded(), pipe.empty_flat().zero_()
+    pipe.roundtrip(flat, enc=enc, out=out, joined=False)  # warm-up (eager)
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, stream=pipe.streams[0]):
+        pipe.roundtrip(flat, enc=enc, out=out, joined=False)
+    torch.cuda.synchronize()
+    flat.copy_(synth_batch(t, cuda, client_ids=[22]))  # new data, same buffers
+    torch.cuda.synchronize()
+    for _ in range(3):
+        with torch.cuda.stream(pipe.streams[0]):
+            g.replay()
+    torch.cuda.synchronize()
+    plan = CodecPlan(fp32_sizes("resnet50_tv"), 0.01, 8, clients=1, device=cuda)
+    e = plan.encode(flat)
+    d = plan.decode(e, out=torch.zeros_like(flat))
+    torch.cuda.synchronize()
+    assert torch.equal(e.idx, enc.idx) and torch.equal(e.vals, enc.vals)
+    assert torch.equal(e.mn, enc.mn) and torch.equal(e.scale, enc.scale)
+    assert torch.equal(d.view(torch.int32), out.view(torch.int32))
