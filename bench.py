@@ -91,6 +91,9 @@ def parse():
     p.add_argument("--graph", choices=["auto", "on", "off"], default="auto",
                    help="replay each timed step as a captured hipGraph: auto = the latency-bound configs "
                         f"({', '.join(GRAPH_CONFIGS) if 'GRAPH_CONFIGS' in globals() else 'single, single_x2, C5'})")
+    p.add_argument("--graph-steps", type=int, default=10,
+                   help="timed steps captured in one graph (--graph): one graph launch per this many steps (1 / 4 / "
+                        "10 measured 0.0845 / 0.0803 / 0.0796 ms per single step; eager 0.080-0.083)")
     p.add_argument("--cpu-seconds", type=float, default=8.0, help="CPU baseline time budget per leg")
     p.add_argument("--no-cpu-baseline", action="store_true")
     return p.parse_args()
@@ -290,27 +293,29 @@ def run_workload(cfg, a, dev, world, rank, headline):
     # (the same kernels on the same buffers, one graph launch per step instead of the per-call Python checks,
     # ctypes calls and ~8 kernel launches, which take about as long as the ~80 us of GPU work of one update:
     # on a box with a slower host the eager single step measured 0.138 ms for 0.080 ms of kernels; with a
-    # fast host the graph costs ~4 us per step more than eager — single 0.084 vs 0.080, single_x2 0.058 vs
-    # 0.064, C5 0.097 vs 0.093 ms — and it is the stable one)
+    # fast host a graph per step costs ~4 us more than eager, a graph of 10 steps does not — single 0.0796 vs
+    # 0.0804-0.0827, single_x2 0.0588 vs 0.071-0.079, C5 0.0921 vs 0.092-0.094 ms; tools/graph_ab.sh)
     graphs = None
     if use_graph(cfg, a):
         torch.cuda.synchronize()
-        graphs = []
-        for p, enc, out in slots:
-            g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g, stream=p.streams[0]):
-                p.roundtrip(flat, base=base, enc=enc, out=out, joined=False)
-            graphs.append((g, p.streams[0]))
-        torch.cuda.synchronize()
+        gk = max(1, a.graph_steps)  # steps per graph (one graph launch per gk steps)
 
-        def step(i=None, j=0, joined=a.joined, eager=step):  # noqa: F811 (the timed steps only)
-            if i is not None:
-                return eager(i, j, joined)
-            g, st = graphs[j % len(graphs)]
+        def capture(n):
+            gs = []
+            for p, enc, out in slots:
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g, stream=p.streams[0]):
+                    for _ in range(n):
+                        p.roundtrip(flat, base=base, enc=enc, out=out, joined=False)
+                gs.append((g, p.streams[0]))
+            return gs
+        graphs = {gk: capture(gk)}
+        if a.steps % gk:
+            graphs[1] = capture(1)
+        torch.cuda.synchronize()
+        for g, st in graphs[gk]:  # one replay of each before the timed region
             with torch.cuda.stream(st):
                 g.replay()
-        for w in range(len(graphs)):
-            step(j=w)
 
     # The timed region carries no timing event (each recorded event costs a dispatch gap) and its
     # sub-batch streams are not joined per step, so consecutive steps overlap.
@@ -320,8 +325,18 @@ def run_workload(cfg, a, dev, world, rank, headline):
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for i in range(a.steps):
-        step(j=i)
+    if graphs is None:
+        for i in range(a.steps):
+            step(j=i)
+    else:  # chunks of gk steps (the last ones one by one), slots in turn
+        i = c = 0
+        while i < a.steps:
+            n = gk if a.steps - i >= gk else 1
+            g, st = graphs[n][c % len(slots)]
+            with torch.cuda.stream(st):
+                g.replay()
+            i += n
+            c += 1
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -393,7 +408,7 @@ def run_workload(cfg, a, dev, world, rank, headline):
         "stages_ms": {k: round(v, 4) for k, v in stages.items()},
         "sample_fallbacks": fallbacks,
         "wait_timeouts": timeouts,
-        "graph": graphs is not None,
+        "graph": graphs is not None and f"{gk} step(s) per graph launch",
     }
     if headline:
         traffic, src = pmc_traffic(dom, cfg, a, split)
