@@ -296,6 +296,7 @@ def run_workload(cfg, a, dev, world, rank, headline):
     # fast host a graph per step costs ~4 us more than eager, a graph of 10 steps does not — single 0.0796 vs
     # 0.0804-0.0827, single_x2 0.0588 vs 0.071-0.079, C5 0.0921 vs 0.092-0.094 ms; tools/graph_ab.sh)
     graphs = None
+    graph_error = None
     if use_graph(cfg, a):
         torch.cuda.synchronize()
         gk = max(1, a.graph_steps)  # steps per graph (one graph launch per gk steps)
@@ -309,13 +310,18 @@ def run_workload(cfg, a, dev, world, rank, headline):
                         p.roundtrip(flat, base=base, enc=enc, out=out, joined=False)
                 gs.append((g, p.streams[0]))
             return gs
-        graphs = {gk: capture(gk)}
-        if a.steps % gk:
-            graphs[1] = capture(1)
-        torch.cuda.synchronize()
-        for g, st in graphs[gk]:  # one replay of each before the timed region
-            with torch.cuda.stream(st):
-                g.replay()
+        try:
+            graphs = {gk: capture(gk)}
+            if a.steps % gk:
+                graphs[1] = capture(1)
+            torch.cuda.synchronize()
+            for g, st in graphs[gk]:  # one replay of each before the timed region
+                with torch.cuda.stream(st):
+                    g.replay()
+        except RuntimeError as e:  # a runtime that cannot capture: time the eager steps instead (reported)
+            graph_error = f"capture failed, eager steps: {e}"[:200]
+            graphs = None
+            torch.cuda.synchronize()
 
     # The timed region carries no timing event (each recorded event costs a dispatch gap) and its
     # sub-batch streams are not joined per step, so consecutive steps overlap.
@@ -408,7 +414,7 @@ def run_workload(cfg, a, dev, world, rank, headline):
         "stages_ms": {k: round(v, 4) for k, v in stages.items()},
         "sample_fallbacks": fallbacks,
         "wait_timeouts": timeouts,
-        "graph": graphs is not None and f"{gk} step(s) per graph launch",
+        "graph": graph_error or (graphs is not None and f"{gk} step(s) per graph launch"),
     }
     if headline:
         traffic, src = pmc_traffic(dom, cfg, a, split)
