@@ -297,7 +297,9 @@ def run_workload(cfg, a, dev, world, rank, headline):
     # 0.0804-0.0827, single_x2 0.0588 vs 0.071-0.079, C5 0.0921 vs 0.092-0.094 ms; tools/graph_ab.sh)
     graphs = None
     graph_error = None
-    if use_graph(cfg, a):
+    # (one process per GPU and N = 1 only: with a process group alive, other threads — RCCL's watchdog — make
+    # HIP calls that a capture must not see; the scaling runs time the headline, which is never captured)
+    if use_graph(cfg, a) and world == 1:
         torch.cuda.synchronize()
         gk = max(1, a.graph_steps)  # steps per graph (one graph launch per gk steps)
 
@@ -305,7 +307,7 @@ def run_workload(cfg, a, dev, world, rank, headline):
             gs = []
             for p, enc, out in slots:
                 g = torch.cuda.CUDAGraph()
-                with torch.cuda.graph(g, stream=p.streams[0]):
+                with torch.cuda.graph(g, stream=p.streams[0], capture_error_mode="thread_local"):
                     for _ in range(n):
                         p.roundtrip(flat, base=base, enc=enc, out=out, joined=False)
                 gs.append((g, p.streams[0]))
