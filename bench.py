@@ -36,8 +36,6 @@ sys.path.insert(0, ROOT)
 
 METRIC = "encode+decode GB/s over fp32 weight updates (device-resident), 1/2/4/8 GPU"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md: 8.0 TB/s)
-ONE_LAUNCH = 64     # COALAC_FLAG_ONE_LAUNCH: the whole encode as one k_fused launch
-FRONT_LAUNCH = 128  # COALAC_FLAG_FRONT_LAUNCH: samplers + scan + small segments as one launch
 SPLIT = 2  # sub-batches per step: two independent pipelines side by side fill the CUs the other leaves
            # idle in its latency-bound stages and launch tails (+11 % over one 16-client pipeline)
 ROOF_STEPS = 8  # joined steps after the timed region that carry the per-kernel timing events
@@ -71,9 +69,6 @@ def parse():
     p.add_argument("--split", type=int, default=None,
                    help="the step's clients are cut into this many sub-batches (balanced by elements), each an "
                         "independent pipeline (own plan, buffers, HIP stream) launched side by side")
-    p.add_argument("--pipe", choices=["split", "lane"], default="split",
-                   help="split: SplitPipeline sub-batches, free-running side by side; lane: LanePipeline (the "
-                        "streaming kernels of all lanes back to back on one stream, latency stages beside them)")
     p.add_argument("--fork", action="store_true", help="keep the per-plan small-segment side streams with --split > 1")
     p.add_argument("--joined", action="store_true",
                    help="join the sub-batch streams with the caller's stream on entry/exit of every step")
@@ -91,9 +86,10 @@ def parse():
     p.add_argument("--graph", choices=["auto", "on", "off"], default="auto",
                    help="replay each timed step as a captured hipGraph: auto = the latency-bound configs "
                         f"({', '.join(GRAPH_CONFIGS) if 'GRAPH_CONFIGS' in globals() else 'single, single_x2, C5'})")
-    p.add_argument("--graph-steps", type=int, default=10,
-                   help="timed steps captured in one graph (--graph): one graph launch per this many steps (1 / 4 / "
-                        "10 measured 0.0845 / 0.0803 / 0.0796 ms per single step; eager 0.080-0.083)")
+    p.add_argument("--graph-steps", type=int, default=12,
+                   help="timed steps captured in one graph (--graph; rounded up to whole input rotations): one graph "
+                        "launch per this many steps (1 / 4 / 10 measured 0.0845 / 0.0803 / 0.0796 ms per single step; "
+                        "eager 0.080-0.083)")
     p.add_argument("--cpu-seconds", type=float, default=8.0, help="CPU baseline time budget per leg")
     p.add_argument("--no-cpu-baseline", action="store_true")
     return p.parse_args()
@@ -137,8 +133,10 @@ def _oracle_worker(args):
 
 
 def host_cores():
+    """(affinity cores, pool size). The pool is capped at the job's CPU share: OMP_NUM_THREADS, which the GPU
+    box sets to 16 for a one-GPU job (its affinity mask shows the whole host, 256 cores); 16 without it."""
     aff = len(os.sched_getaffinity(0))
-    cap = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or 16  # the box's CPU share (16 per GPU)
+    cap = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or 16
     return aff, max(1, min(aff, cap))
 
 
@@ -175,6 +173,8 @@ def cpu_baseline(layout, ratio, bits, budget_s):
             "sample": f"{doneW} x {layout} client updates ({N} fp32 elements each) in {wall:.1f} s: numpy oracle "
                       f"encode+decode, {W} worker processes (one client stream each)",
             "host_cores_affinity": aff, "torch_threads": torch.get_num_threads(),
+            "cores_note": f"pool capped at this job's CPU share (OMP_NUM_THREADS={os.environ.get('OMP_NUM_THREADS')}; "
+                          f"{aff} cores in the affinity mask, which on the GPU box is the whole 8-GPU host)",
             "single_thread": {"value": round(4.0 * N * done1 / el1 / 1e9, 4), "unit": "GB/s", "cores": 1,
                               "sample": f"{done1} updates, {el1:.1f} s, one thread"},
             "reference_identity_pickle": {
@@ -192,8 +192,8 @@ def pmc_traffic(kernel, cfg, a, split):
     doubled (gfx950 reports half the bytes of wide coalesced streaming reads, MI355X_MICROARCH.md §HBM)
     + WRITE_SIZE. Only reported for the default configuration the summary was collected on."""
     import glob
-    default = (cfg, a.layout, a.clients, a.ratio, a.bits, a.mode, a.inflight, split, a.pipe) == \
-        ("C3", None, None, 0.01, 8, "weights", 1, SPLIT, "split")
+    default = (cfg, a.layout, a.clients, a.ratio, a.bits, a.mode, a.inflight, split) == \
+        ("C3", None, None, 0.01, 8, "weights", 1, SPLIT)
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_summary.json")))
     if not default or not files:
         return None, None
@@ -210,7 +210,7 @@ def large_elements(pipe):
     in k_presel; each plan's threshold follows its size, spec.small_limit)."""
     from coala_amd.compression.spec import small_limit
     tot = 0
-    for q in getattr(pipe, "parts", None) or pipe.lanes:
+    for q in pipe.parts:
         n = q["plan"].table.segs[:, 1].astype("int64")
         tot += int(n[n > small_limit(n)].sum())
     return tot
@@ -253,81 +253,101 @@ def use_graph(cfg, a):
     return a.graph == "on" or (a.graph == "auto" and cfg in GRAPH_CONFIGS)
 
 
-def run_workload(cfg, a, dev, world, rank, headline):
-    import torch
-    import torch.distributed as dist
+# configs whose timed steps rotate over ROTATE distinct input / output buffer sets (one ResNet-50 update is
+# 102 MB in + 102 MB out: a single set would stay resident in the 256 MB Infinity Cache, step after step)
+ROTATE_CONFIGS = ("single", "single_x2")
+ROTATE = 3
 
-    from coala_amd.compression import LanePipeline, SplitPipeline
+
+def setup_workload(cfg, a, dev, rank, headline):
+    """Buffers, pipelines and synthetic inputs of one config (nothing timed)."""
+    import torch
+
+    from coala_amd.compression import SplitPipeline
     from coala_amd.workload import synth_batch
 
     t, ids, split, desc = build_table(cfg, a, rank, headline)
-    flat = synth_batch(t, dev, client_ids=ids)
+    rot = ROTATE if cfg in ROTATE_CONFIGS and not headline else 1
+    flats = [synth_batch(t, dev, client_ids=[1000 * r + i for i in ids]) for r in range(rot)]
     base = synth_batch(t, dev, client_ids=[10_000 + i for i in ids]) if a.mode == "delta" else None
     split = max(1, split)
     inflight = max(1, a.inflight) if headline else CONFIG_INFLIGHT.get(cfg, 1)
     slots = []
-    for j in range(inflight):
-        if a.pipe == "lane" and headline:
-            p = LanePipeline(t, a.bits, lanes=split, device=dev, flags=a.flags)
-        else:  # slot j on its own pooled streams, so the slots' steps overlap
-            p = SplitPipeline(t, a.bits, split=split, device=dev, flags=a.flags, fork=a.fork, stream_base=j * split)
-        slots.append((p, p.empty_encoded(), p.empty_flat()))
-    split = slots[0][0].n_parts
-    pipes = [s[0] for s in slots]
+    for j in range(inflight):  # slot j on its own pooled streams, so the slots' steps overlap
+        p = SplitPipeline(t, a.bits, split=split, device=dev, flags=a.flags, fork=a.fork, stream_base=j * split)
+        slots.append((p, [(p.empty_encoded(), p.empty_flat()) for _ in range(rot)]))
     torch.cuda.synchronize()
+    return {"cfg": cfg, "headline": headline, "table": t, "desc": desc, "flats": flats, "base": base, "rot": rot,
+            "slots": slots, "split": slots[0][0].n_parts, "graphs": None, "graph_error": None}
 
-    def step(i=None, j=0, joined=a.joined):
-        p, enc, out = slots[j % len(slots)]
-        ee = ev_e[i] if i is not None else None
-        de = ev_d[i] if i is not None else None
-        # sub-batch streams ordered by themselves step after step (each slot's buffers are used by its own
-        # streams only): no joins with the caller's stream inside the timed loop
-        p.roundtrip(flat, base=base, enc=enc, out=out, enc_events=ee, dec_events=de, joined=joined)
 
-    for w in range(max(a.warmup, len(slots))):
-        step(j=w)
-    fallbacks = sum(p.fallbacks() for p in pipes)
-    timeouts = sum(p.timeouts() for p in pipes)
+def _step(W, i, joined, enc_events=None, dec_events=None):
+    """Step i: slot i % inflight, buffer set (i // inflight) % rot."""
+    p, bufs = W["slots"][i % len(W["slots"])]
+    r = (i // len(W["slots"])) % W["rot"]
+    enc, out = bufs[r]
+    p.roundtrip(W["flats"][r], base=W["base"], enc=enc, out=out, enc_events=enc_events, dec_events=dec_events,
+                joined=joined)
 
-    # Latency-bound configs: each slot's step captured once as a hipGraph and replayed on that slot's stream
-    # (the same kernels on the same buffers, one graph launch per step instead of the per-call Python checks,
-    # ctypes calls and ~8 kernel launches, which take about as long as the ~80 us of GPU work of one update:
-    # on a box with a slower host the eager single step measured 0.138 ms for 0.080 ms of kernels; with a
-    # fast host a graph per step costs ~4 us more than eager, a graph of 10 steps does not — single 0.0796 vs
-    # 0.0804-0.0827, single_x2 0.0588 vs 0.071-0.079, C5 0.0921 vs 0.092-0.094 ms; tools/graph_ab.sh)
-    graphs = None
-    graph_error = None
-    # (one process per GPU and N = 1 only: with a process group alive, other threads — RCCL's watchdog — make
-    # HIP calls that a capture must not see; the scaling runs time the headline, which is never captured)
-    if use_graph(cfg, a) and world == 1:
+
+def warm_workload(W, a):
+    import torch
+    for w in range(max(a.warmup, len(W["slots"]) * W["rot"])):
+        _step(W, w, a.joined)
+    torch.cuda.synchronize()
+    W["fallbacks"] = sum(p.fallbacks() for p, _ in W["slots"])
+
+
+def capture_graphs(W, a):
+    """Latency-bound configs: each slot's steps captured as hipGraphs and replayed on the slot's first stream
+    (the same kernels on the same buffers: one graph launch per gk steps instead of the per-call Python checks,
+    ctypes calls and ~8 kernel launches per step, which take about as long as the ~80 us of GPU work of one
+    update — a box with a slower host measured the eager single step at 0.138 ms for 0.080 ms of kernels).
+    Captured on a stream of its own with the pipeline's JOINED roundtrip, so every sub-batch stream forks
+    from the capture and joins back into it (all parts land in the graph). Runs before any process group
+    exists (no other thread makes HIP calls during the capture)."""
+    import torch
+    S = len(W["slots"])
+    gk = max(1, a.graph_steps)
+    gk = -(-gk // W["rot"]) * W["rot"]  # whole rotations per graph
+    W["gk"] = gk
+
+    def capture(steps_of_slot):  # {slot: [buffer-set index per captured step]}
+        gs = []
+        for j, (p, _) in enumerate(W["slots"]):
+            cap = torch.cuda.Stream(p.device)
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, stream=cap, capture_error_mode="thread_local"):
+                for r in steps_of_slot:
+                    _step(W, r * S + j, True)
+            gs.append((g, p.streams[0]))
+        return gs
+    try:
         torch.cuda.synchronize()
-        gk = max(1, a.graph_steps)  # steps per graph (one graph launch per gk steps)
+        W["graphs"] = {gk: capture(list(range(gk)))}
+        for r in range(W["rot"]):  # single steps for the remainder, one per buffer set
+            W["graphs"][(1, r)] = capture([r])
+        torch.cuda.synchronize()
+        for g, st in W["graphs"][gk]:  # one replay of each before the timed region
+            with torch.cuda.stream(st):
+                g.replay()
+        torch.cuda.synchronize()
+    except RuntimeError as e:  # a runtime that cannot capture: time the eager steps instead (reported)
+        W["graph_error"] = f"capture failed, eager steps: {e}"[:200]
+        W["graphs"] = None
+        torch.cuda.synchronize()
 
-        def capture(n):
-            gs = []
-            for p, enc, out in slots:
-                g = torch.cuda.CUDAGraph()
-                with torch.cuda.graph(g, stream=p.streams[0], capture_error_mode="thread_local"):
-                    for _ in range(n):
-                        p.roundtrip(flat, base=base, enc=enc, out=out, joined=False)
-                gs.append((g, p.streams[0]))
-            return gs
-        try:
-            graphs = {gk: capture(gk)}
-            if a.steps % gk:
-                graphs[1] = capture(1)
-            torch.cuda.synchronize()
-            for g, st in graphs[gk]:  # one replay of each before the timed region
-                with torch.cuda.stream(st):
-                    g.replay()
-        except RuntimeError as e:  # a runtime that cannot capture: time the eager steps instead (reported)
-            graph_error = f"capture failed, eager steps: {e}"[:200]
-            graphs = None
-            torch.cuda.synchronize()
 
-    # The timed region carries no timing event (each recorded event costs a dispatch gap) and its
-    # sub-batch streams are not joined per step, so consecutive steps overlap.
-    ev_e = ev_d = [None] * a.steps
+def time_workload(W, a, dev, world):
+    import torch
+    import torch.distributed as dist
+
+    slots = W["slots"]
+    pipes = [p for p, _ in slots]
+    split, t, headline = W["split"], W["table"], W["headline"]
+    graphs = W["graphs"]
+    # The timed region carries no timing event (each recorded event costs a dispatch gap) and its sub-batch
+    # streams are not joined per step, so consecutive steps overlap.
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -335,12 +355,17 @@ def run_workload(cfg, a, dev, world, rank, headline):
     t0 = time.perf_counter()
     if graphs is None:
         for i in range(a.steps):
-            step(j=i)
-    else:  # chunks of gk steps (the last ones one by one), slots in turn
+            _step(W, i, a.joined)
+    else:  # chunks of gk steps per slot launch; the remainder one graph per step
+        gk, S = W["gk"], len(slots)
         i = c = 0
         while i < a.steps:
-            n = gk if a.steps - i >= gk else 1
-            g, st = graphs[n][c % len(slots)]
+            if a.steps - i >= gk:
+                g, st = graphs[gk][c % S]
+                n = gk
+            else:
+                g, st = graphs[(1, (c // S) % W["rot"])][c % S]
+                n = 1
             with torch.cuda.stream(st):
                 g.replay()
             i += n
@@ -370,7 +395,7 @@ def run_workload(cfg, a, dev, world, rank, headline):
     ev_d = [part_events(3) for _ in timed_steps]
     torch.cuda.synchronize()
     for i in timed_steps:
-        step(i, i, joined=True)
+        _step(W, i, True, ev_e[i], ev_d[i])
     torch.cuda.synchronize()
 
     # Per-kernel durations (ms, averaged over the event-carrying steps) from HIP events on each
@@ -381,23 +406,16 @@ def run_workload(cfg, a, dev, world, rank, headline):
     def union(pairs):
         ref = pairs[0][0]
         return max(ref.elapsed_time(e) for _, e in pairs) - min(ref.elapsed_time(s) for s, _ in pairs)
-    # events [1] / [2] bracket the encode's streaming launch: k_scan (the default kernel sequence), the front
-    # launch (samplers + scan + small segments) or the whole k_fused (one launch)
-    one = bool(a.flags & ONE_LAUNCH)
-    multi = not one and not (a.flags & FRONT_LAUNCH)
-    enc_kernel = "k_scan" if multi else "k_fused" if one else "k_front"
-    dec_kernel = "k_decode"
     stages = {}
-    for name, which in {enc_kernel: ev_e, dec_kernel: ev_d}.items():
+    for name, which in {"k_scan": ev_e, "k_decode": ev_d}.items():
         per = [union([(e[1], e[2]) for e in which[i]]) for i in timed_steps]
         stages[name] = sum(per) / len(per)
     N, K, T = t.n_elements, t.total_k, t.n_segments
     delta = a.mode == "delta"
     vb = 4 if a.bits == 32 else 1
-    segs = t.segs.astype("int64")
     large_elems = large_elements(pipes[0])
     alg = {  # algorithmic HBM bytes per timed interval
-        enc_kernel: (4 * large_elems if multi else 4 * N + (4 + vb) * K + 8 * T if one else 4 * N) + (4 * N if delta else 0),
+        "k_scan": 4 * large_elems + (4 * N if delta else 0),
         "k_decode": 4 * N * (2 if delta else 1) + (4 + vb) * K + 8 * T,
     }
     dom = max(alg, key=lambda k: stages[k])
@@ -406,7 +424,7 @@ def run_workload(cfg, a, dev, world, rank, headline):
     step_alg = t.algorithmic_bytes(a.bits, delta)
     res = {
         "value": round(4.0 * N * world * a.steps / el / 1e9, 2), "ms_per_step": round(step_ms, 4),
-        "desc": desc, "split": split, "inflight": len(slots), "pipe": a.pipe if headline else "split",
+        "desc": W["desc"], "split": split, "inflight": len(slots), "rotation": W["rot"],
         "elements_per_gpu": N, "segments_per_gpu": T, "kept_per_gpu": K,
         "roofline": {"bound": "hbm", "kernel": dom if split == 1 else f"{dom} x{split} concurrent launches (union interval)",
                      "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4),
@@ -414,22 +432,25 @@ def run_workload(cfg, a, dev, world, rank, headline):
         "step_roofline": {"alg_bytes_per_step": step_alg, "achieved_GBs": round(step_alg / (step_ms * 1e-3) / 1e9, 1),
                           "frac": round(step_alg / (step_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)},
         "stages_ms": {k: round(v, 4) for k, v in stages.items()},
-        "sample_fallbacks": fallbacks,
-        "wait_timeouts": timeouts,
-        "graph": graph_error or (graphs is not None and f"{gk} step(s) per graph launch"),
+        "sample_fallbacks": W.get("fallbacks", 0),
+        "graph": W["graph_error"] or (graphs is not None and f"{W['gk']} step(s) per graph launch"),
     }
     if headline:
-        traffic, src = pmc_traffic(dom, cfg, a, split)
+        traffic, src = pmc_traffic(dom, W["cfg"], a, split)
         res["roofline"]["traffic"] = traffic * split if traffic is not None else None
         res["roofline"]["traffic_source"] = src
-        res["stage_timing"] = (f"HIP events on each sub-batch stream around {enc_kernel} / k_decode, union over the "
+        res["stage_timing"] = (f"HIP events on each sub-batch stream around k_scan / k_decode, union over the "
                                f"{split} concurrent launches, mean of {len(timed_steps)} joined steps run after the "
                                f"timed region")
-    for p in pipes:
-        p.close()
-    del slots, pipes, flat, base
-    torch.cuda.empty_cache()
     return res
+
+
+def release_workload(W):
+    import torch
+    for p, _ in W["slots"]:
+        p.close()
+    W.clear()
+    torch.cuda.empty_cache()
 
 
 def run_plugin(a, dev, steps):
@@ -490,13 +511,52 @@ def run_plugin(a, dev, steps):
                     "host-side Python included; flattened = the round-1 path (torch.cat copy first)"}
 
 
+def launch_ranks(a):
+    """`--gpus N` (N > 1) without a launcher: start N rank processes of this script, one per GPU (RANK /
+    LOCAL_RANK / WORLD_SIZE / MASTER_* in their environment, as torch.distributed.run sets them), before this
+    process touches the GPU; rank 0 prints the JSON line. Mirrors the reference's own launcher, one
+    process per GPU (examples/distributed_mp.py:77-84). Returns the exit code (the first failing rank's)."""
+    import socket
+    import subprocess
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    procs = []
+    for r in range(a.gpus):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(a.gpus), LOCAL_WORLD_SIZE=str(a.gpus),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    rc = 0
+    try:
+        pending = list(procs)
+        while pending:
+            for p in list(pending):
+                code = p.poll()
+                if code is None:
+                    continue
+                pending.remove(p)
+                if code and not rc:
+                    rc = code
+                    for q in pending:  # one rank failed: the others would wait in a collective forever
+                        q.terminate()
+            time.sleep(0.05)
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+                p.wait()
+    return rc
+
+
 def main():
     a = parse()
+    if a.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(a))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != a.gpus:
-        raise SystemExit(f"--gpus {a.gpus} but WORLD_SIZE={world} (launch N>1 with torch.distributed.run)")
+        raise SystemExit(f"--gpus {a.gpus} but WORLD_SIZE={world}")
     cpu = None
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         layout = a.layout or CONFIGS[a.config][0]
@@ -511,20 +571,35 @@ def main():
         local = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
+
+    order = [a.config] + ([] if a.extras == "none" else [c for c in a.extras.split(",") if c and c != a.config])
+    # latency-bound configs: set up, warmed and captured as hipGraphs BEFORE the process group exists (with one
+    # alive, RCCL's watchdog thread makes HIP calls while a capture runs); small buffers, kept until timed
+    pre = {}
+    for cfg in order:
+        if cfg in CONFIGS and use_graph(cfg, a):
+            W = setup_workload(cfg, a, dev, rank, headline=cfg == a.config)
+            warm_workload(W, a)
+            capture_graphs(W, a)
+            pre[cfg] = W
     if world > 1:
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=dev)
         else:
             dist.init_process_group(backend)
 
-    head = run_workload(a.config, a, dev, world, rank, headline=True)
-    extras = {}
-    plugin = None
-    for cfg in ([] if a.extras == "none" else [c for c in a.extras.split(",") if c and c != a.config]):
+    results, plugin = {}, None
+    for cfg in order:
         if cfg == "plugin":
             plugin = run_plugin(a, dev, a.steps)
-        else:
-            extras[cfg] = run_workload(cfg, a, dev, world, rank, headline=False)
+            continue
+        W = pre.pop(cfg, None)
+        if W is None:
+            W = setup_workload(cfg, a, dev, rank, headline=cfg == a.config)
+            warm_workload(W, a)
+        results[cfg] = time_workload(W, a, dev, world)
+        release_workload(W)
+    head = results.pop(a.config)
 
     if rank == 0:
         d = head["desc"]
@@ -540,11 +615,11 @@ def main():
                        "parallelism": f"replicas{world}"},
             "roofline": head["roofline"], "step_roofline": head["step_roofline"], "stages_ms": head["stages_ms"],
             "stage_timing": head["stage_timing"], "sample_fallbacks": head["sample_fallbacks"],
-            "wait_timeouts": head["wait_timeouts"],
+            "graph": head["graph"],
             "configs": {k: {f: v[f] for f in ("value", "ms_per_step", "step_roofline", "roofline", "stages_ms", "desc",
-                                              "elements_per_gpu", "segments_per_gpu", "split", "inflight",
+                                              "elements_per_gpu", "segments_per_gpu", "split", "inflight", "rotation",
                                               "graph", "sample_fallbacks")}
-                        for k, v in extras.items()},
+                        for k, v in results.items()},
         }
         if plugin is not None:
             res["configs"]["plugin"] = plugin

@@ -11,11 +11,11 @@ Public surface:
 from . import wire
 from .codec import CompressedUpdate, FlatState, HipBackend, UpdateCodec, flatten_state, module_with_state
 from .download import CompressedModel, compress_model, skeleton_of
-from .pipeline import LanePipeline, SplitPipeline, split_lanes
+from .pipeline import SplitPipeline, split_lanes
 from .plan import CodecPlan, Encoded
 from .plugin import CompressionClientMixin, CompressionServerMixin
 from .spec import ALIGN, RAW_BITS, SegmentTable, SubTable, k_for
 
-__all__ = ["wire", "SplitPipeline", "CompressedModel", "compress_model", "skeleton_of", "LanePipeline", "split_lanes", "SubTable", "CompressedUpdate", "FlatState", "HipBackend", "UpdateCodec", "flatten_state", "module_with_state",
+__all__ = ["wire", "SplitPipeline", "CompressedModel", "compress_model", "skeleton_of", "split_lanes", "SubTable", "CompressedUpdate", "FlatState", "HipBackend", "UpdateCodec", "flatten_state", "module_with_state",
            "CodecPlan", "Encoded", "CompressionClientMixin", "CompressionServerMixin", "ALIGN", "RAW_BITS",
            "SegmentTable", "k_for"]

@@ -13,12 +13,10 @@ COALAC_FLAG_FORCE_EXACT = 1
 COALAC_FLAG_GENERIC_SELECT = 2
 COALAC_FLAG_STAMPS = 4
 COALAC_FLAG_NO_FORK = 8
-COALAC_FLAG_ITEM_STAMPS = 32   # diagnostics: per-work-item timestamps of k_fused
-COALAC_FLAG_ONE_LAUNCH = 64    # the whole encode as one k_fused launch (select phases as in-launch work items)
-COALAC_FLAG_FRONT_LAUNCH = 128 # samplers + scan + small segments as one launch, then the select kernels
 # stages of a split encode / decode (coalac_sched_t.stages; 0 = all)
 COALAC_STAGE_SAMPLE, COALAC_STAGE_SCAN, COALAC_STAGE_SELECT, COALAC_STAGE_SMALL = 1, 2, 4, 8
 COALAC_STAGE_BOUNDS, COALAC_STAGE_DECODE, COALAC_STAGE_FILL, COALAC_STAGE_SCATTER = 1, 2, 4, 8
+COALAC_STAGE_BOUNDS_DONE = 16  # decode: BOUNDS was enqueued by an earlier call on this workspace (batch plans)
 COALAC_AGG_DIV = 0     # acc / total            (torch CPU division by a scalar)
 COALAC_AGG_RECIP = 1   # acc * (1.0f / total)   (torch GPU division by a host scalar)
 COALAC_AGG_SUM = 2     # acc                    (weighted_sum: the multi-GPU per-rank sum)
@@ -54,11 +52,9 @@ SIGNATURES = [
     ("coalac_aggregate_ev", _I, [_P, _I, _P, _P, _P, _P, _P, ctypes.c_float, _I, _P, _P, _P, _U64, _P, _P]),
     ("coalac_workspace_fallbacks", _I, [_P, _P, _P, ctypes.POINTER(_I)]),
     ("coalac_debug_stamps", _I, [_P, _P, _P, ctypes.POINTER(ctypes.c_uint64), _I]),
-    ("coalac_workspace_timeouts", _I, [_P, _P, _P, ctypes.POINTER(_I)]),
-    ("coalac_debug_item_stamps", _I, [_P, _P, _P, ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_uint64), _I]),
 ]
 
-ABI_VERSION = 2
+ABI_VERSION = 3
 
 
 class CodecError(RuntimeError):

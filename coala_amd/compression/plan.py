@@ -83,7 +83,8 @@ class CodecPlan:
     def from_segments(cls, segs, bits=8, device=None):
         """Plan over explicit coalac_seg_t rows (in_off, n, k, out_off), offsets absolute: e.g. a
         contiguous slice of a SegmentTable, whose results land in the buffers of the whole table
-        (LanePipeline). mn / scale of such a plan are indexed by row of `segs`."""
+        (SplitPipeline's segment ranges of one update). mn / scale of such a plan are indexed by row of
+        `segs`."""
         return cls(None, None, bits, device=device, table=SubTable(segs))
 
     # -- lifetime ---------------------------------------------------------------------------------
@@ -281,16 +282,6 @@ class CodecPlan:
                 rc = self._lib.coalac_aggregate_ev(*args, _event_array(events, 3))
         _lib.check(rc, "coalac_aggregate")
         return out  # w was allocated on the launch stream: its memory is reused only after the kernel
-
-    def timeouts(self, workspace, stream=None):
-        """1 if a bounded in-launch wait of the last one-launch / front-launch encode with this workspace
-        gave up (its results are then invalid; never expected), else 0 (synchronises). Meaningless after a
-        kernel-sequence encode (nothing zeroes or sets the word then)."""
-        c = ctypes.c_int()
-        with torch.cuda.device(self.device):
-            _lib.check(self._lib.coalac_workspace_timeouts(self._h, _ptr(workspace), _stream_handle(stream),
-                                                           ctypes.byref(c)), "coalac_workspace_timeouts")
-        return c.value
 
     def fallbacks(self, workspace, stream=None):
         """Segments of the last encode with this workspace whose sampled bracket missed (synchronises)."""

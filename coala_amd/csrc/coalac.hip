@@ -50,7 +50,6 @@
 #include <cstdlib>
 #include <cstring>
 #include <mutex>
-#include <queue>
 #include <string>
 #include <vector>
 
@@ -94,11 +93,6 @@ constexpr int SEL_NT_LAT = 512;           // ... in latency-bound plans, where n
 #endif
 #ifndef SCAN_XCD
 #define SCAN_XCD 0    // k_scan: XCD-aware unit order
-#endif
-#ifndef SCAN_HIST
-#define SCAN_HIST 0  // latency-bound plans: k_scan accumulates the group band histograms (no k_ghist). Off:
-                     // the per-record device atomics made one update's k_scan 25.0 -> 33.2 us for k_ghist's
-                     // 6.4 (single update 0.0897 -> 0.0927 ms)
 #endif
 #ifndef SCAN_SMALL_LAT
 #define SCAN_SMALL_LAT 1  // latency-bound plans: small segments in k_scan's first blocks (k_sample alone ahead;
@@ -192,9 +186,6 @@ struct Params {
   uint32_t *tstar, *rtie, *status;
   // per large unit
   uint32_t *tlo, *thi, *cntA, *cntC, *gtC, *eqC, *eqpre, *outoff;
-  uint32_t* thh;        // [n_lunits] histogram upper bound of the unit's segment (= shhi; scan_hist only)
-  uint32_t scan_hist;   // latency-bound plans: k_scan accumulates the group band histograms (no k_ghist); the
-                        // samplers zero them first
   uint2* cand;  // candidate records {index | A_FLAG, value bits}, ccap slots per large unit
   uint32_t ccap;  // record slots per large unit (< UNIT: a unit that finds more candidates overflows and its
                   // segment is selected and emitted from the raw data instead)
@@ -207,21 +198,6 @@ struct Params {
   float* gmm;              // [n_groups][2] min/max of the group's values above the window
   uint4* sstate;           // [n_large] {wlo, whi, rank inside the window, path: 0 fast / 1 generic}
   uint32_t* shhi;          // [n_large] histogram upper bound: min(T_hi, largest sampled key)
-
-  // one-launch encode (k_fused): per-block work items, the scan order, and the hand-off words (the
-  // workspace's control block, zeroed before every launch)
-  const uint32_t* items;   // [grid] role << 28 | index
-  const uint32_t* fsched;  // large units in scan order (segments by descending size)
-  const uint32_t* lgroup;  // [n_lunits] select group of each large unit
-  const uint4* eblocks;    // emit blocks {first large unit, units (<= 32), segment, 0}
-  uint32_t* hf_sampled;    // [nseg] sampler done
-  uint32_t* hf_garr;       // [n_groups] units of the group scanned
-  uint32_t* hf_ghist;      // [nseg] group histograms done
-  uint32_t* hf_gwin;       // [nseg] group windows done
-  uint32_t* hf_sel;        // [nseg] segment selected
-  uint32_t* hf_err;        // [4] [0]: a bounded wait gave up
-  uint32_t wt;             // 1 in k_fused: data another block of the launch reads is stored write-through
-  uint64_t* istamps;       // diagnostics (COALAC_FLAG_ITEM_STAMPS): per item {start, inputs ready, end}
 
   // decode workspace
   const uint32_t* ustart;  // [n_units + 1] first kept entry of every unit (k_bounds; aggregate only)
@@ -305,73 +281,10 @@ DEV void wave_fence() {
   __builtin_amdgcn_wave_barrier();
 }
 
-// ---- in-launch hand-offs (k_fused), the agent-scope forms of cdna_hip_programming.md §6 Guideline 16:
-// a producer's payload is either stored write-through (sc1: relaxed agent-scope atomic stores, global
-// address space) and drained, or plain-stored and published by ONE agent-scope release (L2 write-back)
-// after every storing wave has drained and met the block barrier; the signal is an agent-scope atomic. A
-// consumer polls ONE word relaxed (bounded, with s_sleep), then either reads the payload with sc1 loads
-// only, or runs ONE agent-scope acquire (L1 invalidate) before a barrier and plain loads.
-typedef __attribute__((address_space(1))) uint32_t gu32;
-typedef __attribute__((address_space(1))) uint64_t gu64;
-constexpr uint32_t SPIN_MAX = 1u << 18;  // >= 0.1 s of polling: a wait that long means a broken schedule
-
-DEV uint32_t ld_sc1(const uint32_t* p) {
-  return __hip_atomic_load((gu32*)(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-DEV void st_sc1(uint32_t* p, uint32_t v) { __hip_atomic_store((gu32*)(p), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
-DEV void st_sc1(uint2* p, uint2 v) {
-  __hip_atomic_store((gu64*)(p), ((uint64_t)v.y << 32) | v.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-DEV void add_sc1(uint32_t* p, uint32_t v) {
-  (void)__hip_atomic_fetch_add((gu32*)(p), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-// a store another block of the same launch will read (k_fused: write-through, so no release is needed)
-DEV void pst(const Params& P, uint32_t* p, uint32_t v) {
-  if (P.wt)
-    st_sc1(p, v);
-  else
-    *p = v;
-}
-DEV void pst(const Params& P, float* p, float v) { pst(P, reinterpret_cast<uint32_t*>(p), __float_as_uint(v)); }
-DEV void pst(const Params& P, uint2* p, uint2 v) {
-  if (P.wt)
-    st_sc1(p, v);
-  else
-    *p = v;
-}
-DEV void drain() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
-DEV void acquire_agent() { __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent"); }
-
-// one lane waits until *p >= target (relaxed agent-scope polls); false (and hf_err[0] set) on timeout
-DEV bool wait_ge(const uint32_t* p, uint32_t target, uint32_t* err) {
-  for (uint32_t it = 0;; ++it) {
-    if (ld_sc1(p) >= target) return true;
-    if (it >= SPIN_MAX) {
-      st_sc1(err, 1u);
-      return false;
-    }
-    __builtin_amdgcn_s_sleep(2);
-  }
-}
-
-// block-level consume: thread 0 polls, ONE acquire, every wave then reads after the barrier
-DEV void block_wait(const uint32_t* p, uint32_t target, uint32_t* err) {
-  if (threadIdx.x == 0) {
-    wait_ge(p, target, err);
-    acquire_agent();
-  }
-  drain();
-  __syncthreads();
-}
-
-// block-level publish of write-through (sc1) stores: every storing wave drains, barrier, then ONE lane
-// signals (no release: nothing the consumer reads sits dirty in an L2; a release would write back the
-// whole XCD L2, including other kernels' dirty output, once per block)
-DEV void block_publish_add(uint32_t* counter, uint32_t v) {
-  drain();
-  __syncthreads();
-  if (threadIdx.x == 0) add_sc1(counter, v);
-}
+// stores of the select phases' per-group / per-segment results (plain global stores)
+DEV void pst(const Params&, uint32_t* p, uint32_t v) { *p = v; }
+DEV void pst(const Params&, float* p, float v) { *p = v; }
+DEV void pst(const Params&, uint2* p, uint2 v) { *p = v; }
 
 // Block-wide exclusive scan over NT threads. sh needs >= NT/64 words. Returns the exclusive prefix and
 // the block total. Contains barriers: call from all threads.
@@ -720,14 +633,9 @@ struct Band {
 // The unit is loaded in NB batches of UNIT_IT/NB float4 per lane: NB = 1 for the streaming pass (all
 // loads in flight at once), more for the register-lean fallback inside k_select.
 // ------------------------------------------------------------------------------------------------
-// SC1 (k_fused): records and counts are stored write-through for the in-launch hand-off to the select
-// phases. get_t() returns {T_lo, T_hi}; it is called once the first batch of loads is in flight (k_fused
-// waits there for the sampler).
-// HIST (latency-bound plans): every stored band record (not A) is also counted into its group's band
-// histogram `gh` (HB2 bins of `band`) with a device-scope atomic add, replacing k_ghist's pass.
-template <bool DELTA, int NB, bool SC1 = false, bool HIST = false, class GetT>
-DEV void scan_unit_t(const Params& P, uint32_t lu, const UnitDev& L, GetT&& get_t, uint2* stage,
-                     uint32_t* gh = nullptr, const Band* band = nullptr) {
+template <bool DELTA, int NB>
+DEV void scan_unit(const Params& P, uint32_t lu, const UnitDev& L, const uint32_t tlo, const uint32_t thi,
+                   uint2* stage) {
   constexpr uint32_t IT = UNIT_IT / NB;
   const uint32_t lane = lane_id();
   const uint32_t len = L.len;
@@ -735,7 +643,6 @@ DEV void scan_unit_t(const Params& P, uint32_t lu, const UnitDev& L, GetT&& get_
   uint2* R = P.cand + (uint64_t)lu * P.ccap;
   const uint32_t cap = P.ccap;
   uint32_t cC = 0, cA = 0;
-  uint32_t tlo = 0, thi = 0;
   // buffer resources over exactly this unit: one shared lane offset for all loads (constant offsets
   // fold into the instruction), and loads past len return 0 — no separate partial-unit path
   const float* xin = P.inptr != nullptr ? P.inptr[L.seg] + L.start : P.in + off;
@@ -743,23 +650,13 @@ DEV void scan_unit_t(const Params& P, uint32_t lu, const UnitDev& L, GetT&& get_
   const __amdgpu_buffer_rsrc_t rbase = unit_rsrc(DELTA ? P.base + off : xin, len);
   auto put = [&](uint32_t i, uint2 rec) {
     if (i >= cap) return;  // overflow: counted, not stored (the segment goes to the raw-data path)
-    if (SC1)
-      st_sc1(R + i, rec);
-    else
-      R[i] = rec;
-    if (HIST && !(rec.x & A_FLAG)) atomicAdd(gh + band->bin(rec.y & KEY_MAX), 1u);
+    R[i] = rec;
   };
 
   for (uint32_t nb = 0; nb < (uint32_t)NB; ++nb) {
     float4 v[IT];
 #pragma unroll
     for (uint32_t i = 0; i < IT; ++i) v[i] = unit_load_x4<DELTA>(rin, rbase, ((nb * IT + i) * 64 + lane) * 16);
-    if (nb == 0) {
-      asm volatile("" ::: "memory");  // the loads above stay ahead of a wait inside get_t
-      const uint2 tt = get_t();
-      tlo = tt.x;
-      thi = tt.y;
-    }
 #pragma unroll
     for (uint32_t i = 0; i < IT; ++i) {
       const uint32_t e0 = ((nb * IT + i) * 64 + lane) * 4;
@@ -821,19 +718,9 @@ DEV void scan_unit_t(const Params& P, uint32_t lu, const UnitDev& L, GetT&& get_
     for (uint32_t i = lane; i < cC && i < STAGE_CAP; i += 64) put(i, stage[i]);
   }
   if (lane == 0) {
-    if (SC1) {
-      st_sc1(P.cntA + lu, cA);
-      st_sc1(P.cntC + lu, cC);
-    } else {
-      P.cntA[lu] = cA;
-      P.cntC[lu] = cC;
-    }
+    P.cntA[lu] = cA;
+    P.cntC[lu] = cC;
   }
-}
-
-template <bool DELTA, int NB>
-DEV void scan_unit(const Params& P, uint32_t lu, const UnitDev& L, uint32_t tlo, uint32_t thi, uint2* stage) {
-  scan_unit_t<DELTA, NB, false>(P, lu, L, [&]() { return make_uint2(tlo, thi); }, stage);
 }
 
 
@@ -1032,7 +919,7 @@ __global__ __launch_bounds__(BLOCK) void k_small(Params P) {
 // ------------------------------------------------------------------------------------------------
 // k_sample: per large segment, sampled thresholds [T_lo, T_hi] for every unit of the segment
 // ------------------------------------------------------------------------------------------------
-template <bool DELTA, bool SC1>
+template <bool DELTA>
 DEV void sample_segment(const Params& P, uint32_t li, uint32_t* hist, uint32_t* sh) {
   constexpr int NT = BLOCK;
   constexpr uint32_t MAXIT = SAMPLE_MAX / 16 / 64;  // run batches per block (64 runs of 16 per batch)
@@ -1122,28 +1009,14 @@ DEV void sample_segment(const Params& P, uint32_t li, uint32_t* hist, uint32_t* 
   const uint32_t nu = sd.unit_end - sd.unit_begin;
   const uint32_t hh = max(tlo, min(thi, kmax));  // the band histograms' upper bound (see below)
   for (uint32_t i = t; i < nu; i += NT) {
-    if (SC1) {
-      st_sc1(P.tlo + sd.lu_begin + i, tlo);
-      st_sc1(P.thi + sd.lu_begin + i, thi);
-    } else {
-      P.tlo[sd.lu_begin + i] = tlo;
-      P.thi[sd.lu_begin + i] = thi;
-      if (P.scan_hist) P.thh[sd.lu_begin + i] = hh;
-    }
-  }
-  if (!SC1 && P.scan_hist) {  // k_scan adds into the segment's group histograms
-    const uint32_t ng = (nu + GU - 1) / GU;
-    for (uint32_t i = t; i < ng * HB2; i += NT) P.ghist[(uint64_t)sd.g_begin * HB2 + i] = 0;
+    P.tlo[sd.lu_begin + i] = tlo;
+    P.thi[sd.lu_begin + i] = thi;
   }
   // The band histograms of the parallel select span [T_lo, min(T_hi, max sampled key)] (keys above go
   // to the last bin): with T_hi = KEY_MAX a full-range histogram would be too coarse.
   if (t == 0) {
-    if (SC1) {
-      st_sc1(P.shhi + li, hh);
-    } else {
-      P.shhi[li] = hh;
-      P.status[s] = 0;  // (k_fused: the control block, status included, is zeroed before the launch)
-    }
+    P.shhi[li] = hh;
+    P.status[s] = 0;
   }
 }
 
@@ -1151,7 +1024,7 @@ template <bool DELTA, bool RAW>
 __global__ __launch_bounds__(BLOCK) void k_sample(Params P) {
   __shared__ uint32_t hist[HIST_BINS];
   __shared__ uint32_t sh[64];
-  sample_segment<DELTA, false>(P, blockIdx.x, hist, sh);
+  sample_segment<DELTA>(P, blockIdx.x, hist, sh);
 }
 
 // k_presel: the samplers (blocks [0, n_large)) and the small segments (blocks after them) as one launch —
@@ -1163,7 +1036,7 @@ __global__ __launch_bounds__(BLOCK) void k_presel(Params P) {
   __shared__ __attribute__((aligned(16))) uint8_t arena[(SMALL_MAX + HIST_BINS + 64) * 4];
   uint32_t* hist = reinterpret_cast<uint32_t*>(arena) + SMALL_MAX;
   if (blockIdx.x < P.n_large) {
-    sample_segment<DELTA, false>(P, blockIdx.x, hist, hist + HIST_BINS);
+    sample_segment<DELTA>(P, blockIdx.x, hist, hist + HIST_BINS);
   } else {
     small_encode<DELTA, RAW>(P, P.small_list[blockIdx.x - P.n_large], reinterpret_cast<float*>(arena), hist,
                              hist + HIST_BINS);
@@ -1174,7 +1047,7 @@ __global__ __launch_bounds__(BLOCK) void k_presel(Params P) {
 // small segments — no longer launched: k_presel runs them beside the samplers.)
 // (WPE / NB: launch-bound blocks per CU and load batches; the latency-bound plans' instantiation, the one
 // WITH_SMALL, takes its own — nothing streams beside it)
-template <bool DELTA, bool RAW, bool WITH_SMALL, bool HIST = false, int WPE = SCAN_WPE, int NB = SCAN_NB>
+template <bool DELTA, bool RAW, bool WITH_SMALL, int WPE = SCAN_WPE, int NB = SCAN_NB>
 __global__ __launch_bounds__(BLOCK, WPE) void k_scan(Params P) {
   // one LDS arena: candidate staging (WAVES x STAGE_CAP records) or a small segment's values + histogram
   // (WITH_SMALL only: without it the block needs 16 KB of LDS instead of 24.8 KB)
@@ -1193,15 +1066,7 @@ __global__ __launch_bounds__(BLOCK, WPE) void k_scan(Params P) {
   if (lu >= P.n_lunits) return;
   const UnitDev L = P.lunits[lu];
   // delta: 4 load batches (32 float4 in flight spill)
-  if (HIST) {
-    const uint32_t tlo = P.tlo[lu], thi = P.thi[lu];
-    const Band band(tlo, thi, P.thh[lu]);
-    uint32_t* gh = P.ghist + (uint64_t)P.lgroup[lu] * HB2;
-    scan_unit_t<DELTA, DELTA ? 4 : SCAN_NB, false, true>(P, lu, L, [&]() { return make_uint2(tlo, thi); },
-                                                          stage + wv * STAGE_CAP, gh, &band);
-  } else {
-    scan_unit<DELTA, DELTA ? 4 : NB>(P, lu, L, P.tlo[lu], P.thi[lu], stage + wv * STAGE_CAP);
-  }
+  scan_unit<DELTA, DELTA ? 4 : NB>(P, lu, L, P.tlo[lu], P.thi[lu], stage + wv * STAGE_CAP);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -2058,141 +1923,6 @@ __global__ __launch_bounds__(BLOCK) void k_emit(Params P) {
 }
 
 // ------------------------------------------------------------------------------------------------
-// k_fused: the whole encode as ONE launch (no kernel boundaries; the select phases of a segment run while
-// later segments still stream). Every block runs one work item, named by P.items[blockIdx.x]:
-//   SAMPLE(li)  the sampler of large segment li                                    k_sample
-//   SMALL(i)    small segment i, whole, in LDS                                     k_small
-//   SCAN(j)     4 large units of the scan order, one wave each; the loads go out before the wave waits
-//               for its segment's sampler                                           k_scan
-//   GHIST(g)    band histogram of group g, once its units are scanned              k_ghist
-//   GWIN(g)     window + per-unit counts of group g, once the segment's histograms are in   k_gwin
-//   SELECT(li)  exact k-th key, offsets, min/max of segment li, once its windows are in     k_select
-//   EMIT(e)     up to 32 units of one segment (8 per wave), once it is selected   k_emit
-// The host orders the items so that every item comes after everything it waits for (plan_create:
-// fused_schedule); workgroups are dispatched in order, so a waiting block only ever waits for blocks
-// that were dispatched before it. Every wait is bounded (hf_err[0] records a give-up).
-// Hand-offs: sampler -> scan: T_lo/T_hi stored write-through, flag, read by the scan wave with sc1 loads.
-// scan -> GHIST: records and counts stored write-through, drained, one atomic add per wave; the group
-// blocks acquire. GHIST -> GWIN -> SELECT -> EMIT: write-through stores (Params::wt), drained, barrier,
-// one atomic per block; one acquire per consuming block.
-// ------------------------------------------------------------------------------------------------
-enum : uint32_t { R_SAMPLE = 0, R_SMALL = 1, R_SCAN = 2, R_GHIST = 3, R_GWIN = 4, R_SELECT = 5, R_EMIT = 6 };
-constexpr uint32_t EMIT_BLOCK_UNITS = WAVES * EMIT_UPW;
-
-struct GhistSmem {
-  uint32_t hist[HB2];
-  uint32_t upre[GU + 1];
-  uint32_t sh[64];
-};
-struct GwinAll {
-  GwinSmem w;
-  uint32_t hist[HB2];
-  uint32_t sh[64];
-};
-struct SmallSmem {
-  float vals[SMALL_MAX];
-  uint32_t hist[HIST_BINS];
-  uint32_t sh[64];
-};
-constexpr size_t cmax(size_t a, size_t b) { return a > b ? a : b; }
-constexpr size_t FUSED_LDS =
-    cmax(cmax(sizeof(SelSmem), sizeof(SmallSmem)), cmax(cmax(sizeof(GwinAll), sizeof(GhistSmem)), WAVES * STAGE_CAP * sizeof(uint2)));
-static_assert(FUSED_LDS <= 32 * 1024, "k_fused keeps five blocks per CU (160 KB of LDS)");
-
-template <bool DELTA, bool RAW>
-DEV void k_fused_item(const Params& P, uint32_t role, uint32_t idx, uint8_t* arena, uint64_t* stamp);
-
-template <bool DELTA, bool RAW>
-__global__ __launch_bounds__(BLOCK, SCAN_WPE) void k_fused(Params P) {
-  __shared__ __attribute__((aligned(16))) uint8_t arena[FUSED_LDS];
-  const uint32_t item = P.items[blockIdx.x];
-  const uint32_t role = item >> 28, idx = item & 0x0FFFFFFFu;
-  const uint32_t t = threadIdx.x, lane = lane_id(), wv = t >> 6;
-  uint64_t* const stamp = P.istamps != nullptr ? P.istamps + 3 * (uint64_t)blockIdx.x : nullptr;
-  if (stamp != nullptr && t == 0) stamp[0] = __builtin_amdgcn_s_memrealtime();
-  k_fused_item<DELTA, RAW>(P, role, idx, arena, stamp);
-  if (stamp != nullptr) {
-    __syncthreads();
-    if (t == 0) stamp[2] = __builtin_amdgcn_s_memrealtime();
-  }
-}
-
-template <bool DELTA, bool RAW>
-DEV void k_fused_item(const Params& P, uint32_t role, uint32_t idx, uint8_t* arena, uint64_t* stamp) {
-  const uint32_t t = threadIdx.x, lane = lane_id(), wv = t >> 6;
-  auto ready = [&]() {  // inputs available (after the wait)
-    if (stamp != nullptr && t == 0) stamp[1] = __builtin_amdgcn_s_memrealtime();
-  };
-  if (role == R_SCAN) {
-    const uint32_t q = idx * WAVES + wv;
-    if (q >= P.n_lunits) return;
-    const uint32_t lu = P.fsched[q];
-    const UnitDev L = P.lunits[lu];
-    uint2* stage = reinterpret_cast<uint2*>(arena) + wv * STAGE_CAP;
-    auto get_t = [&]() {
-      uint32_t lo = 0, hi = 0;
-      if (lane == 0) {
-        wait_ge(P.hf_sampled + L.seg, 1u, P.hf_err);
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // compiler order only: sc1 loads follow
-        lo = ld_sc1(P.tlo + lu);
-        hi = ld_sc1(P.thi + lu);
-        if (stamp != nullptr && wv == 0) stamp[1] = __builtin_amdgcn_s_memrealtime();
-      }
-      return make_uint2(__builtin_amdgcn_readfirstlane(lo), __builtin_amdgcn_readfirstlane(hi));
-    };
-    if (P.wt) {  // one launch: the group blocks of this launch read the records
-      scan_unit_t<DELTA, DELTA ? 4 : SCAN_NB, true>(P, lu, L, get_t, stage);
-      drain();  // every lane's write-through stores have landed
-      if (lane == 0) add_sc1(P.hf_garr + P.lgroup[lu], 1u);
-    } else {  // front launch: the select kernels after this launch read them
-      scan_unit_t<DELTA, DELTA ? 4 : SCAN_NB, false>(P, lu, L, get_t, stage);
-    }
-  } else if (role == R_SAMPLE) {
-    uint32_t* hist = reinterpret_cast<uint32_t*>(arena);
-    ready();
-    sample_segment<DELTA, true>(P, idx, hist, hist + HIST_BINS);
-    drain();
-    __syncthreads();
-    if (t == 0) st_sc1(P.hf_sampled + P.large_list[idx], 1u);
-  } else if (role == R_SMALL) {
-    SmallSmem& S = *reinterpret_cast<SmallSmem*>(arena);
-    ready();
-    small_encode<DELTA, RAW>(P, P.small_list[idx], S.vals, S.hist, S.sh);
-  } else if (role == R_GHIST) {
-    GhistSmem& S = *reinterpret_cast<GhistSmem*>(arena);
-    const uint4 G = P.groups[idx];
-    block_wait(P.hf_garr + idx, G.z, P.hf_err);
-    ready();
-    group_hist(P, idx, S.hist, S.upre, S.sh);
-    block_publish_add(P.hf_ghist + G.w, 1u);
-  } else if (role == R_GWIN) {
-    GwinAll& S = *reinterpret_cast<GwinAll*>(arena);
-    const uint4 G = P.groups[idx];
-    const SegDev sd = P.segs[G.w];
-    const uint32_t ng = (sd.unit_end - sd.unit_begin + GU - 1) / GU;
-    block_wait(P.hf_ghist + G.w, ng, P.hf_err);
-    ready();
-    group_pick_window(P, idx, S.w, S.hist, S.sh);
-    block_publish_add(P.hf_gwin + G.w, 1u);
-  } else if (role == R_SELECT) {
-    SelSmem& S = *reinterpret_cast<SelSmem*>(arena);
-    const uint32_t s = P.large_list[idx];
-    const SegDev sd = P.segs[s];
-    const uint32_t ng = (sd.unit_end - sd.unit_begin + GU - 1) / GU;
-    block_wait(P.hf_gwin + s, ng, P.hf_err);
-    ready();
-    segment_select<BLOCK, DELTA, RAW>(P, idx, S);
-    block_publish_add(P.hf_sel + s, 1u);
-  } else if (role == R_EMIT) {
-    const uint4 E = P.eblocks[idx];  // {first large unit, units, segment, 0}
-    block_wait(P.hf_sel + E.z, 1u, P.hf_err);
-    ready();
-    const uint32_t u0 = E.x + wv * EMIT_UPW, u1 = min(u0 + EMIT_UPW, E.x + E.y);
-    if (u0 < u1) emit_units<DELTA, RAW>(P, u0, u1);
-  }
-}
-
-// ------------------------------------------------------------------------------------------------
 // decode
 // ------------------------------------------------------------------------------------------------
 // k_decode: DPW = 2 units per wave (1 in delta mode), all loads issued up front. Partial units (a
@@ -2720,38 +2450,26 @@ int fail(int code, const char* fmt, ...) {
 size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 
 struct WsLayout {
-  size_t ctl_bytes;  // the control block at offset 0: status and the k_fused hand-off words
-  size_t status, hf_sampled, hf_ghist, hf_gwin, hf_sel, hf_err, hf_garr;
+  size_t status;
   size_t tstar, rtie;
-  size_t tlo, thi, thh, cntA, cntC, gtC, eqC, eqpre, outoff;
-  size_t cand, stamps, ghist, gcnt, glist, gmm, sstate, shhi, istamps;
+  size_t tlo, thi, cntA, cntC, gtC, eqC, eqpre, outoff;
+  size_t cand, stamps, ghist, gcnt, glist, gmm, sstate, shhi;
   size_t total;
 };
 
-WsLayout ws_layout(size_t S, size_t LU, size_t NG, size_t NL, size_t NI, uint32_t CC) {
+WsLayout ws_layout(size_t S, size_t LU, size_t NG, size_t NL, uint32_t CC) {
   WsLayout L{};
-  // control block: words k_fused polls, zeroed by one memset before every launch (a block of its own at
-  // the workspace start, a multiple of 16 bytes: Guideline 16 "Re-initialise every call")
-  size_t c = 0;
-  L.status = c; c += 4 * S;
-  L.hf_sampled = c; c += 4 * S;
-  L.hf_ghist = c; c += 4 * S;
-  L.hf_gwin = c; c += 4 * S;
-  L.hf_sel = c; c += 4 * S;
-  L.hf_err = c; c += 16;
-  L.hf_garr = c; c += 4 * NG;
-  L.ctl_bytes = align_up(c, 16);
-  size_t o = align_up(L.ctl_bytes, 256);
+  size_t o = 0;
   auto take = [&](size_t bytes) {
     size_t r = o;
     o = align_up(o + bytes, 256);
     return r;
   };
+  L.status = take(4 * S);
   L.tstar = take(4 * S);
   L.rtie = take(4 * S);
   L.tlo = take(4 * LU);
   L.thi = take(4 * LU);
-  L.thh = take(4 * LU);
   L.cntA = take(4 * LU);
   L.cntC = take(4 * LU);
   L.gtC = take(4 * LU);
@@ -2766,99 +2484,8 @@ WsLayout ws_layout(size_t S, size_t LU, size_t NG, size_t NL, size_t NI, uint32_
   L.gmm = take(8 * NG);
   L.sstate = take(sizeof(uint4) * NL);
   L.shhi = take(4 * NL);
-  L.istamps = take(24 * NI);
   L.total = std::max<size_t>(o, 256);
   return L;
-}
-
-// k_fused work items in launch order (see k_fused). Scan order: large segments by descending size, so the
-// long select chains of the big segments start while the small ones still stream. Each waiting item is
-// placed `delay` items after the last item it waits for (a block dispatched much earlier would hold a CU
-// slot while it spins); dependencies always precede their dependents, so in-order dispatch cannot
-// deadlock.
-struct FusedSchedule {
-  std::vector<uint32_t> items, fsched, lgroup, front;  // front: SAMPLE + SCAN + SMALL only
-  std::vector<uint4> eblocks;
-};
-
-FusedSchedule fused_schedule(const std::vector<SegDev>& segs, const std::vector<uint32_t>& large_list,
-                             uint32_t n_small, uint32_t n_lunits, const std::vector<uint4>& groups, uint32_t delay) {
-  FusedSchedule F;
-  const uint32_t NL = (uint32_t)large_list.size();
-  std::vector<uint32_t> order(NL);
-  for (uint32_t i = 0; i < NL; ++i) order[i] = i;
-  std::stable_sort(order.begin(), order.end(),
-                   [&](uint32_t a, uint32_t b) { return segs[large_list[a]].n > segs[large_list[b]].n; });
-  F.lgroup.assign(n_lunits, 0);
-  std::vector<uint32_t> ng(NL), eb_first(NL), eb_count(NL);
-  std::vector<std::vector<uint32_t>> done_at;
-  for (uint32_t li : order) {
-    const SegDev& d = segs[large_list[li]];
-    const uint32_t nu = d.unit_end - d.unit_begin;
-    ng[li] = (nu + GU - 1) / GU;
-    for (uint32_t u = 0; u < nu; ++u) {
-      F.lgroup[d.lu_begin + u] = d.g_begin + u / GU;
-      F.fsched.push_back(d.lu_begin + u);
-      if ((u + 1) % GU == 0 || u + 1 == nu) {  // the group's last unit: its block completes the group
-        const uint32_t blk = (uint32_t)(F.fsched.size() - 1) / WAVES;
-        if (done_at.size() <= blk) done_at.resize(blk + 1);
-        done_at[blk].push_back(d.g_begin + u / GU);
-      }
-    }
-    eb_first[li] = (uint32_t)F.eblocks.size();
-    for (uint32_t u0 = 0; u0 < nu; u0 += EMIT_BLOCK_UNITS)
-      F.eblocks.push_back(make_uint4(d.lu_begin + u0, std::min(EMIT_BLOCK_UNITS, nu - u0), large_list[li], 0u));
-    eb_count[li] = (uint32_t)F.eblocks.size() - eb_first[li];
-  }
-  const uint32_t nscan = (n_lunits + WAVES - 1) / WAVES;
-  auto mk = [](uint32_t role, uint32_t idx) { return (role << 28) | idx; };
-  for (uint32_t li : order) F.items.push_back(mk(R_SAMPLE, li));
-  // pending items: (ready position, sequence, item)
-  typedef std::pair<std::pair<uint64_t, uint64_t>, uint32_t> Pending;
-  std::priority_queue<Pending, std::vector<Pending>, std::greater<Pending>> q;
-  uint64_t seq = 0;
-  // small segments (independent, latency-bound) spread evenly over the scan blocks: ahead of them they
-  // would hold the CUs before the first byte streams
-  for (uint32_t i = 0; i < n_small; ++i)
-    q.push(Pending({(uint64_t)F.items.size() + (uint64_t)(i + 1) * nscan / (n_small + 1), seq++}, mk(R_SMALL, i)));
-  std::vector<uint32_t> gh_done(NL, 0), gw_done(NL, 0);
-  auto push = [&](uint32_t item) { q.push(Pending({(uint64_t)F.items.size() + delay, seq++}, item)); };
-  auto place = [&](uint32_t item) {
-    F.items.push_back(item);
-    const uint32_t role = item >> 28, idx = item & 0x0FFFFFFFu;
-    if (role == R_SCAN) {
-      if (idx < done_at.size())
-        for (uint32_t g : done_at[idx]) push(mk(R_GHIST, g));
-    } else if (role == R_GHIST) {
-      const uint32_t li = groups[idx].x;
-      if (++gh_done[li] == ng[li])
-        for (uint32_t g = 0; g < ng[li]; ++g) push(mk(R_GWIN, segs[large_list[li]].g_begin + g));
-    } else if (role == R_GWIN) {
-      const uint32_t li = groups[idx].x;
-      if (++gw_done[li] == ng[li]) push(mk(R_SELECT, li));
-    } else if (role == R_SELECT) {
-      for (uint32_t e = 0; e < eb_count[idx]; ++e) push(mk(R_EMIT, eb_first[idx] + e));
-    }
-  };
-  // the front launch: samplers, then the scan blocks with the small segments spread among them
-  for (uint32_t li : order) F.front.push_back(mk(R_SAMPLE, li));
-  for (uint32_t j = 0, i = 0; j < nscan || i < n_small; ) {
-    if (i < n_small && (j == nscan || (uint64_t)(i + 1) * nscan / (n_small + 1) <= j))
-      F.front.push_back(mk(R_SMALL, i++));
-    else
-      F.front.push_back(mk(R_SCAN, j++));
-  }
-  uint32_t j = 0;
-  while (j < nscan || !q.empty()) {
-    if (!q.empty() && (q.top().first.first <= F.items.size() || j == nscan)) {
-      const uint32_t item = q.top().second;
-      q.pop();
-      place(item);
-    } else {
-      place(mk(R_SCAN, j++));
-    }
-  }
-  return F;
 }
 
 }  // namespace
@@ -2882,14 +2509,6 @@ struct coalac_plan {
   BChunk* bchunks = nullptr;  // aggregate: k_bounds work list
   uint32_t n_bchunks = 0;
   SChunk* schunks = nullptr;  // latency-bound decode: k_scatter work list (n_bchunks of them)
-  // one-launch encode (k_fused): block work items, scan order, unit -> group, emit blocks
-  uint32_t* items = nullptr;
-  uint32_t n_items = 0;
-  uint32_t* front = nullptr;  // the front launch (samplers + scan + small segments)
-  uint32_t n_front = 0;
-  uint32_t* fsched = nullptr;
-  uint32_t* lgroup = nullptr;
-  uint4* eblocks = nullptr;
   std::vector<SegDev> hsegs;  // host copy (aggregate validates the client-copy structure)
   // encode fork/join: k_small runs on `side`, concurrently with k_sample / k_scan on the caller's stream
   hipStream_t side = nullptr;
@@ -2918,10 +2537,6 @@ void fill_meta(Params& P, coalac_plan_t plan) {
   P.lsegs = plan->lsegs;
   P.groups = plan->groups;
   P.n_groups = plan->n_groups;
-  P.items = plan->items;
-  P.fsched = plan->fsched;
-  P.lgroup = plan->lgroup;
-  P.eblocks = plan->eblocks;
   P.nseg = (uint32_t)plan->nseg;
   P.n_small = plan->n_small;
   P.n_large = plan->n_large;
@@ -2995,7 +2610,7 @@ int launch_encode(const Params& P, coalac_plan_t plan, hipStream_t st, const coa
   // otherwise (whole encode) the small segments run beside the samplers in k_presel, or (latency-bound
   // plans, SCAN_SMALL_LAT) in k_scan's first blocks, beside the streaming waves: k_sample alone ahead of it
   const bool presel = !split && !fork && plan->n_small;
-  const bool small_in_scan = presel && SCAN_SMALL_LAT && plan->n_lunits <= LATENCY_PLAN_UNITS && !P.scan_hist;
+  const bool small_in_scan = presel && SCAN_SMALL_LAT && plan->n_lunits <= LATENCY_PLAN_UNITS;
   Params Q = P;
   Q.scan_small = 0u;
   std::unique_lock<std::mutex> lk(plan->mu, std::defer_lock);
@@ -3031,22 +2646,17 @@ int launch_encode(const Params& P, coalac_plan_t plan, hipStream_t st, const coa
   ENC_BOUNDARY(1);
   if (small_in_scan) {
     Q.scan_small = plan->n_small;
-    hipLaunchKernelGGL((k_scan<DELTA, RAW, true, false, SCAN_WPE_LAT, SCAN_NB_LAT>), dim3(gu + plan->n_small),
+    hipLaunchKernelGGL((k_scan<DELTA, RAW, true, SCAN_WPE_LAT, SCAN_NB_LAT>), dim3(gu + plan->n_small),
                        dim3(BLOCK), 0, st, Q);
   } else if ((stages & COALAC_STAGE_SCAN) && gu) {
-    if (P.scan_hist)
-      hipLaunchKernelGGL((k_scan<DELTA, RAW, false, true>), dim3(gu), dim3(BLOCK), 0, st, Q);
-    else
-      hipLaunchKernelGGL((k_scan<DELTA, RAW, false>), dim3(gu), dim3(BLOCK), 0, st, Q);
+    hipLaunchKernelGGL((k_scan<DELTA, RAW, false>), dim3(gu), dim3(BLOCK), 0, st, Q);
   }
   ENC_BOUNDARY(2);
   if ((stages & COALAC_STAGE_SELECT) && plan->n_large) {
-    if (!P.scan_hist) {
-      if (plan->n_lunits <= LATENCY_PLAN_UNITS)
-        hipLaunchKernelGGL(k_ghist<GHIST_NT_LAT>, dim3(plan->n_groups), dim3(GHIST_NT_LAT), 0, st, P);
-      else
-        hipLaunchKernelGGL(k_ghist<BLOCK>, dim3(plan->n_groups), dim3(BLOCK), 0, st, P);
-    }
+    if (plan->n_lunits <= LATENCY_PLAN_UNITS)
+      hipLaunchKernelGGL(k_ghist<GHIST_NT_LAT>, dim3(plan->n_groups), dim3(GHIST_NT_LAT), 0, st, P);
+    else
+      hipLaunchKernelGGL(k_ghist<BLOCK>, dim3(plan->n_groups), dim3(BLOCK), 0, st, P);
     if (plan->n_lunits <= LATENCY_PLAN_UNITS)
       hipLaunchKernelGGL(k_gwin<GWIN_NT_LAT>, dim3(plan->n_groups), dim3(GWIN_NT_LAT), 0, st, P);
     else
@@ -3061,49 +2671,6 @@ int launch_encode(const Params& P, coalac_plan_t plan, hipStream_t st, const coa
   if (fork) HIP_CHECK(hipStreamWaitEvent(st, plan->join, 0));
   ENC_BOUNDARY(4);
 #undef ENC_BOUNDARY
-  return COALAC_OK;
-}
-
-// The one-launch encode: zero the control block, then k_fused. Events (the _ev / _sched boundaries):
-// [0] before the memset, [1] before k_fused, [2] [3] [4] after it.
-template <bool DELTA, bool RAW>
-int launch_fused(const Params& P, coalac_plan_t plan, hipStream_t st, const coalac_sched_t* sc, void* ws) {
-  BOUNDARY(0);
-  HIP_CHECK(hipMemsetAsync(ws, 0, plan->ws.ctl_bytes, st));
-  BOUNDARY(1);
-  Params Q = P;
-  Q.wt = 1;
-  hipLaunchKernelGGL((k_fused<DELTA, RAW>), dim3(plan->n_items), dim3(BLOCK), 0, st, Q);
-  BOUNDARY(2);
-  BOUNDARY(3);
-  BOUNDARY(4);
-  return COALAC_OK;
-}
-
-// COALAC_FLAG_FRONT_LAUNCH: ONE front launch (samplers, the scan, the small segments; the scan waves issue
-// their loads before they wait for their segment's sampler), then the select kernels k_ghist, k_gwin,
-// k_select, k_emit. Measured no faster than the kernel sequence: the waves holding loaded
-// data while they wait keep the next waves from streaming. Events: [0] before the control-block memset,
-// [1] before the front launch, [2] after it, [3] after k_select, [4] after k_emit.
-template <bool DELTA, bool RAW>
-int launch_front(const Params& P, coalac_plan_t plan, hipStream_t st, const coalac_sched_t* sc, void* ws) {
-  BOUNDARY(0);
-  HIP_CHECK(hipMemsetAsync(ws, 0, plan->ws.ctl_bytes, st));
-  BOUNDARY(1);
-  Params Q = P;
-  Q.wt = 0;
-  Q.items = plan->front;
-  hipLaunchKernelGGL((k_fused<DELTA, RAW>), dim3(plan->n_front), dim3(BLOCK), 0, st, Q);
-  BOUNDARY(2);
-  if (plan->n_large) {
-    hipLaunchKernelGGL(k_ghist<BLOCK>, dim3(plan->n_groups), dim3(BLOCK), 0, st, P);
-    hipLaunchKernelGGL(k_gwin<BLOCK>, dim3(plan->n_groups), dim3(BLOCK), 0, st, P);
-    hipLaunchKernelGGL((k_select<DELTA, RAW>), dim3(plan->n_large), dim3(SEL_NT), 0, st, P);
-  }
-  BOUNDARY(3);
-  if (plan->n_large)
-    launch_emit<DELTA, RAW>(P, plan, st);
-  BOUNDARY(4);
   return COALAC_OK;
 }
 
@@ -3205,12 +2772,6 @@ int coalac_plan_create(const coalac_seg_t* h_segs, int nseg, int bits, coalac_pl
   p->n_bchunks = (uint32_t)bchunks.size();
   p->hsegs = segs;
   p->dec_ws = align_up(4 * (units.size() + 1), 256);  // decode / aggregate: per-unit bounds
-  uint32_t delay = 1024;  // k_fused: items between a waiting item and what it waits for (~ the blocks
-                          // resident at once: a waiting block is dispatched as its inputs complete)
-  if (const char* e = getenv("COALAC_FUSED_DELAY")) delay = (uint32_t)atoi(e);
-  const FusedSchedule F = fused_schedule(segs, large_list, p->n_small, p->n_lunits, groups, delay);
-  p->n_items = (uint32_t)F.items.size();
-  p->n_front = (uint32_t)F.front.size();
   // record slots per large unit: the candidates a unit can expect at the plan's largest ratio (kept
   // share + the sampled band + margin), so the workspace is ~1 B/element at ratio 0.01 instead of 8
   double rmax = 0.0;
@@ -3219,7 +2780,7 @@ int coalac_plan_create(const coalac_seg_t* h_segs, int nseg, int bits, coalac_pl
   if (const char* e = getenv("COALAC_CCAP")) ccap = (uint32_t)atoi(e);  // tests: force overflow
   ccap = std::max<uint32_t>(STAGE_CAP, std::min<uint32_t>(UNIT, ccap));
   p->ccap = ccap;
-  p->ws = ws_layout((size_t)nseg, lunits.size(), groups.size(), large_list.size(), F.items.size(), ccap);
+  p->ws = ws_layout((size_t)nseg, lunits.size(), groups.size(), large_list.size(), ccap);
 
   const size_t o_segs = 0;
   const size_t o_units = align_up(o_segs + sizeof(SegDev) * segs.size(), 256);
@@ -3235,12 +2796,7 @@ int coalac_plan_create(const coalac_seg_t* h_segs, int nseg, int bits, coalac_pl
   for (const BChunk& c : bchunks)
     schunks.push_back(SChunk{segs[c.seg].in_off, segs[c.seg].out_off, c.seg, segs[c.seg].n, c.e0, c.e1});
   const size_t o_sch = align_up(o_bch + sizeof(BChunk) * bchunks.size(), 256);
-  const size_t o_items = align_up(o_sch + sizeof(SChunk) * schunks.size(), 256);
-  const size_t o_fsched = align_up(o_items + 4 * F.items.size(), 256);
-  const size_t o_lgroup = align_up(o_fsched + 4 * F.fsched.size(), 256);
-  const size_t o_eblk = align_up(o_lgroup + 4 * F.lgroup.size(), 256);
-  const size_t o_front = align_up(o_eblk + sizeof(uint4) * F.eblocks.size(), 256);
-  const size_t bytes = align_up(o_front + 4 * F.front.size(), 256) + 256;
+  const size_t bytes = align_up(o_sch + sizeof(SChunk) * schunks.size(), 256) + 256;
   std::vector<uint8_t> host(bytes, 0);
   if (!segs.empty()) memcpy(host.data() + o_segs, segs.data(), sizeof(SegDev) * segs.size());
   if (!units.empty()) memcpy(host.data() + o_units, units.data(), sizeof(UnitDev) * units.size());
@@ -3251,11 +2807,6 @@ int coalac_plan_create(const coalac_seg_t* h_segs, int nseg, int bits, coalac_pl
   if (!groups.empty()) memcpy(host.data() + o_grp, groups.data(), sizeof(uint4) * groups.size());
   if (!bchunks.empty()) memcpy(host.data() + o_bch, bchunks.data(), sizeof(BChunk) * bchunks.size());
   if (!schunks.empty()) memcpy(host.data() + o_sch, schunks.data(), sizeof(SChunk) * schunks.size());
-  if (!F.items.empty()) memcpy(host.data() + o_items, F.items.data(), 4 * F.items.size());
-  if (!F.fsched.empty()) memcpy(host.data() + o_fsched, F.fsched.data(), 4 * F.fsched.size());
-  if (!F.lgroup.empty()) memcpy(host.data() + o_lgroup, F.lgroup.data(), 4 * F.lgroup.size());
-  if (!F.eblocks.empty()) memcpy(host.data() + o_eblk, F.eblocks.data(), sizeof(uint4) * F.eblocks.size());
-  if (!F.front.empty()) memcpy(host.data() + o_front, F.front.data(), 4 * F.front.size());
   hipError_t e = hipMalloc(&p->meta, bytes);
   if (e != hipSuccess) {
     delete p;
@@ -3277,11 +2828,6 @@ int coalac_plan_create(const coalac_seg_t* h_segs, int nseg, int bits, coalac_pl
   p->groups = reinterpret_cast<uint4*>(m + o_grp);
   p->bchunks = reinterpret_cast<BChunk*>(m + o_bch);
   p->schunks = reinterpret_cast<SChunk*>(m + o_sch);
-  p->items = reinterpret_cast<uint32_t*>(m + o_items);
-  p->fsched = reinterpret_cast<uint32_t*>(m + o_fsched);
-  p->lgroup = reinterpret_cast<uint32_t*>(m + o_lgroup);
-  p->eblocks = reinterpret_cast<uint4*>(m + o_eblk);
-  p->front = reinterpret_cast<uint32_t*>(m + o_front);
   *out = p;
   return COALAC_OK;
 }
@@ -3349,19 +2895,11 @@ int encode_impl(coalac_plan_t plan, const float* d_in, const float* const* d_inp
   P.flags = flags;
   uint8_t* w = static_cast<uint8_t*>(d_ws);
   const WsLayout& L = plan->ws;
-  P.hf_sampled = reinterpret_cast<uint32_t*>(w + L.hf_sampled);
-  P.hf_ghist = reinterpret_cast<uint32_t*>(w + L.hf_ghist);
-  P.hf_gwin = reinterpret_cast<uint32_t*>(w + L.hf_gwin);
-  P.hf_sel = reinterpret_cast<uint32_t*>(w + L.hf_sel);
-  P.hf_err = reinterpret_cast<uint32_t*>(w + L.hf_err);
-  P.hf_garr = reinterpret_cast<uint32_t*>(w + L.hf_garr);
-  P.istamps = (flags & COALAC_FLAG_ITEM_STAMPS) ? reinterpret_cast<uint64_t*>(w + L.istamps) : nullptr;
   P.tstar = reinterpret_cast<uint32_t*>(w + L.tstar);
   P.rtie = reinterpret_cast<uint32_t*>(w + L.rtie);
   P.status = reinterpret_cast<uint32_t*>(w + L.status);
   P.tlo = reinterpret_cast<uint32_t*>(w + L.tlo);
   P.thi = reinterpret_cast<uint32_t*>(w + L.thi);
-  P.thh = reinterpret_cast<uint32_t*>(w + L.thh);
   P.cntA = reinterpret_cast<uint32_t*>(w + L.cntA);
   P.cntC = reinterpret_cast<uint32_t*>(w + L.cntC);
   P.gtC = reinterpret_cast<uint32_t*>(w + L.gtC);
@@ -3378,32 +2916,7 @@ int encode_impl(coalac_plan_t plan, const float* d_in, const float* const* d_inp
   P.shhi = reinterpret_cast<uint32_t*>(w + L.shhi);
   hipStream_t st = static_cast<hipStream_t>(stream);
   const bool delta = d_base != nullptr, raw = plan->bits == 32;
-  const unsigned all = COALAC_STAGE_SAMPLE | COALAC_STAGE_SCAN | COALAC_STAGE_SELECT | COALAC_STAGE_SMALL;
-  const bool whole = !(sched && (sched->stages & all) && (sched->stages & all) != all);
-  const bool one = whole && (flags & COALAC_FLAG_ONE_LAUNCH) && !(flags & COALAC_FLAG_STAMPS) && plan->n_items > 0;
-  const bool front = whole && !one && (flags & COALAC_FLAG_FRONT_LAUNCH) && !(flags & COALAC_FLAG_STAMPS) &&
-                     plan->n_front > 0;
-  // the kernel sequence of a latency-bound plan: band histograms from k_scan (one launch less)
-  P.scan_hist = (!one && !front && SCAN_HIST && plan->n_lunits <= LATENCY_PLAN_UNITS) ? 1u : 0u;
-  if (front) {
-    if (delta && raw)
-      rc = launch_front<true, true>(P, plan, st, sched, d_ws);
-    else if (delta)
-      rc = launch_front<true, false>(P, plan, st, sched, d_ws);
-    else if (raw)
-      rc = launch_front<false, true>(P, plan, st, sched, d_ws);
-    else
-      rc = launch_front<false, false>(P, plan, st, sched, d_ws);
-  } else if (one) {
-    if (delta && raw)
-      rc = launch_fused<true, true>(P, plan, st, sched, d_ws);
-    else if (delta)
-      rc = launch_fused<true, false>(P, plan, st, sched, d_ws);
-    else if (raw)
-      rc = launch_fused<false, true>(P, plan, st, sched, d_ws);
-    else
-      rc = launch_fused<false, false>(P, plan, st, sched, d_ws);
-  } else if (delta && raw)
+  if (delta && raw)
     rc = launch_encode<true, true>(P, plan, st, sched);
   else if (delta)
     rc = launch_encode<true, false>(P, plan, st, sched);
@@ -3459,6 +2972,14 @@ int coalac_decode_sched(coalac_plan_t plan, const int32_t* d_idx, const void* d_
   if (stages & (COALAC_STAGE_FILL | COALAC_STAGE_SCATTER)) stages |= COALAC_STAGE_DECODE;
   if (!plan) return fail(COALAC_EINVAL, "coalac_decode: plan is NULL");
   if (plan->n_units == 0) return COALAC_OK;
+  // plans of > DECODE_SEARCH_MAX_UNITS units read the per-unit entry bounds k_bounds leaves in the workspace:
+  // the kept values need BOUNDS in this call, or the caller's word (BOUNDS_DONE) that an earlier call
+  // enqueued it on this workspace for these arrays, ordered before this one (else stale bounds mis-decode)
+  if (plan->n_units > DECODE_SEARCH_MAX_UNITS && (stages & COALAC_STAGE_SCATTER) && !(stages & COALAC_STAGE_BOUNDS) &&
+      !(sched && (sched->stages & COALAC_STAGE_BOUNDS_DONE)))
+    return fail(COALAC_EINVAL, "coalac_decode: a plan of %u units decodes its kept values from the bounds of "
+                "COALAC_STAGE_BOUNDS: pass BOUNDS in the same call, or BOUNDS_DONE after a BOUNDS call on this "
+                "workspace", plan->n_units);
   if (!d_out) return fail(COALAC_EINVAL, "coalac_decode: output pointer is NULL");
   const bool payload = (stages & (COALAC_STAGE_BOUNDS | COALAC_STAGE_SCATTER)) != 0;  // reads the encoded arrays
   if (payload && plan->total_k && (!d_idx || !d_vals))
@@ -3668,29 +3189,6 @@ int coalac_workspace_fallbacks(coalac_plan_t plan, const void* d_ws, void* strea
   int c = 0;
   for (uint32_t s2 : large) c += st[s2] == 1;
   *out = c;
-  return COALAC_OK;
-}
-
-int coalac_debug_item_stamps(coalac_plan_t plan, const void* d_ws, void* stream, uint32_t* items,
-                             uint64_t* stamps, int n) {
-  if (!plan || !d_ws || n < 0) return fail(COALAC_EINVAL, "coalac_debug_item_stamps: bad argument");
-  const int cnt = std::min<int>(n, (int)plan->n_items);
-  hipStream_t s = static_cast<hipStream_t>(stream);
-  if (items) HIP_CHECK(hipMemcpyAsync(items, plan->items, 4 * (size_t)cnt, hipMemcpyDeviceToHost, s));
-  if (stamps)
-    HIP_CHECK(hipMemcpyAsync(stamps, static_cast<const uint8_t*>(d_ws) + plan->ws.istamps, 24 * (size_t)cnt,
-                             hipMemcpyDeviceToHost, s));
-  HIP_CHECK(hipStreamSynchronize(s));
-  return cnt;
-}
-
-int coalac_workspace_timeouts(coalac_plan_t plan, const void* d_ws, void* stream, int* out) {
-  if (!plan || !d_ws || !out) return fail(COALAC_EINVAL, "coalac_workspace_timeouts: NULL argument");
-  uint32_t e[4] = {0, 0, 0, 0};
-  hipStream_t s = static_cast<hipStream_t>(stream);
-  HIP_CHECK(hipMemcpyAsync(e, static_cast<const uint8_t*>(d_ws) + plan->ws.hf_err, sizeof(e), hipMemcpyDeviceToHost, s));
-  HIP_CHECK(hipStreamSynchronize(s));
-  *out = (int)e[0];
   return COALAC_OK;
 }
 

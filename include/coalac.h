@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define COALAC_ABI_VERSION 2
+#define COALAC_ABI_VERSION 3
 
 enum {
   COALAC_OK = 0,
@@ -49,16 +49,11 @@ enum {
   COALAC_FLAG_FORCE_EXACT = 1,    /* test hook: re-select every large segment exactly (no sampling) */
   COALAC_FLAG_GENERIC_SELECT = 2, /* test hook: resolve the k-th key with the multi-pass select only */
   COALAC_FLAG_STAMPS = 4,         /* diagnostics: record per-block phase timestamps of k_select */
-  COALAC_FLAG_NO_FORK = 8,        /* encode small segments inside k_scan, never on the plan's side stream
+  COALAC_FLAG_NO_FORK = 8         /* encode small segments inside k_scan, never on the plan's side stream
                                      (for callers that run several plans concurrently themselves) */
-  COALAC_FLAG_ITEM_STAMPS = 32,   /* diagnostics: k_fused records per work item {start, inputs ready, end}
-                                     (100 MHz ticks; coalac_debug_item_stamps) */
-  COALAC_FLAG_ONE_LAUNCH = 64,    /* encode as ONE launch: k_fused, every phase an in-launch work item
-                                     behind per-segment hand-offs (default: the kernel sequence k_sample,
-                                     k_scan, k_ghist, k_gwin, k_select, k_emit) */
-  COALAC_FLAG_FRONT_LAUNCH = 128  /* samplers + scan + small segments as one launch, then the select
-                                     kernels */
 };
+/* (ABI 3 dropped ABI 2's COALAC_FLAG_ONE_LAUNCH / FRONT_LAUNCH / ITEM_STAMPS: the one-launch encode variants
+ * measured slower than the kernel sequence) */
 
 /* One fp32 segment (= one flattened tensor of the state_dict). Offsets are in ELEMENTS.
  *   in_off : start of the segment in the flat input / dense output buffer; must be a multiple of 4
@@ -114,12 +109,8 @@ int coalac_decode(coalac_plan_t plan, const int32_t* d_idx, const void* d_vals, 
                   void* stream);
 
 /* Profiling variants: identical work, plus hipEventRecord(events[i], stream) between kernels.
- * encode (default): [0] before k_sample, [1] after k_sample, [2] after k_scan, [3] after the select
- *         kernels (k_ghist, k_gwin, k_select), [4] after k_emit (recorded even if the plan has no large
- *         segment);
- * encode (COALAC_FLAG_FRONT_LAUNCH): events[0] before the control-block memset, [1] before the front
- *         launch (samplers + scan + small segments), [2] after it, [3] after k_select, [4] after k_emit;
- * encode (COALAC_FLAG_ONE_LAUNCH): [0] before the memset, [1] before k_fused, [2] [3] [4] after it;
+ * encode: [0] before k_sample, [1] after k_sample, [2] after k_scan, [3] after the select kernels
+ *         (k_ghist, k_gwin, k_select), [4] after k_emit (recorded even if the plan has no large segment);
  * decode: [0] before k_bounds (plans of > 8192 units only), [1] before k_decode (plans of <= 8192 units:
  *         before k_fill), [2] after it (after k_scatter). NULL
  *         array or NULL entries are skipped. */
@@ -149,7 +140,10 @@ int coalac_decode_ev(coalac_plan_t plan, const int32_t* d_idx, const void* d_val
  *                                 FILL of the same d_out / d_base; other plans:
  *                                 the whole k_decode. FILL + SCATTER = DECODE.
  * SAMPLE, SCAN, SELECT of one encode (and BOUNDS, DECODE of one decode) must run in this order on the
- * same workspace; SMALL is independent of them. The caller orders them, e.g. with the events below.
+ * same workspace; SMALL is independent of them. A decode call of a plan of > 8192 units that enqueues the
+ * kept values (DECODE or SCATTER) without BOUNDS must set COALAC_STAGE_BOUNDS_DONE: the caller states that
+ * an earlier call enqueued BOUNDS for the same arrays on the same workspace, ordered before this one;
+ * without it the call returns COALAC_EINVAL (stale bounds would mis-decode silently). The caller orders them, e.g. with the events below.
  * (A whole encode places the small segments itself: beside k_scan on the plan's side stream for big
  * batches, inside k_scan otherwise.) At every boundary an enqueued stage starts or ends at, the call first makes
  * `stream` wait for wait[i] (hipStreamWaitEvent; an event another stream recorded) and then records
@@ -165,7 +159,8 @@ enum {
   COALAC_STAGE_BOUNDS = 1,
   COALAC_STAGE_DECODE = 2,
   COALAC_STAGE_FILL = 4,
-  COALAC_STAGE_SCATTER = 8
+  COALAC_STAGE_SCATTER = 8,
+  COALAC_STAGE_BOUNDS_DONE = 16
 };
 typedef struct coalac_sched {
   void* wait[5];
@@ -207,17 +202,6 @@ int coalac_aggregate_ev(coalac_plan_t plan, int clients, const int32_t* d_idx, c
 /* Diagnostics: number of segments whose sampled thresholds were rejected and re-selected exactly in
  * the last encode that used workspace d_ws (synchronises `stream`). */
 int coalac_workspace_fallbacks(coalac_plan_t plan, const void* d_ws, void* stream, int* out);
-
-/* Diagnostics: 1 if a bounded in-launch wait of the last one-launch / front-launch encode with d_ws gave up
- * (its results are then not valid; never expected), else 0 (synchronises `stream`). Only those encodes
- * zero and set the word: after a kernel-sequence encode it holds whatever the workspace held. */
-int coalac_workspace_timeouts(coalac_plan_t plan, const void* d_ws, void* stream, int* out);
-
-/* Diagnostics: the k_fused work items (role << 28 | index, launch order) and, after a
- * COALAC_FLAG_ITEM_STAMPS encode with d_ws, their {start, inputs ready, end} timestamps (3 per item);
- * either pointer may be NULL. Copies up to n items (synchronises `stream`); returns the count copied. */
-int coalac_debug_item_stamps(coalac_plan_t plan, const void* d_ws, void* stream, uint32_t* items,
-                             uint64_t* stamps, int n);
 
 /* Diagnostics: copy up to n phase timestamps (16 per k_select block = per large segment, 100 MHz
  * ticks; 0 = phase not reached) of the last COALAC_FLAG_STAMPS encode with d_ws to host (synchronises

@@ -1,13 +1,13 @@
-"""GPU parity of the lane pipeline (coala_amd/compression/pipeline.py): L sub-plans over contiguous
-segment ranges, on their own streams, ordered by events through coalac_encode_sched /
-coalac_decode_sched. Bar: bit-identical to the oracle (and so to a single plan), for every lane count,
-including a single client split into lanes and delta mode. Repeated steps check that the event chain
-never lets a lane read a buffer another lane is still writing."""
+"""GPU parity of the batched pipelines (coala_amd/compression/pipeline.py): SplitPipeline sub-batches
+(client ranges, or segment ranges of one update) on their own streams, writing the whole batch's buffers.
+Bar: bit-identical to the oracle (and so to a single plan), for every split, including a single client
+cut into segment ranges and delta mode. Repeated and alternating unjoined steps check that no sub-batch
+reads a buffer another step is still writing; graph capture must record every sub-batch."""
 import numpy as np
 import pytest
 import torch
 
-from coala_amd.compression import CodecPlan, LanePipeline, SegmentTable, SplitPipeline
+from coala_amd.compression import CodecPlan, SegmentTable, SplitPipeline
 from coala_amd.layouts import fp32_sizes
 from coala_amd.workload import synth_batch
 from oracle import codec_oracle as O
@@ -33,32 +33,13 @@ def check(table, enc, dec, ref):
         np.testing.assert_array_equal(d[off:off + n].view(np.uint32), rdec[off:off + n].view(np.uint32))
 
 
-@pytest.mark.parametrize("lanes", [1, 2, 3, 4])
-@pytest.mark.parametrize("delta", [False, True])
-@pytest.mark.parametrize("fused", [False, True])
-def test_pipeline_resnet18_x2(cuda, lanes, delta, fused):
-    t = SegmentTable(fp32_sizes("resnet18"), 0.01, 2)
-    flat = synth_batch(t, cuda, client_ids=[5, 6])
-    base = synth_batch(t, cuda, client_ids=[50, 60]) if delta else None
-    pipe = LanePipeline(t, 8, lanes=lanes, device=cuda)
-    assert pipe.n_lanes == lanes
-    if fused:
-        enc, dec = pipe.roundtrip(flat, base=base)
-    else:
-        enc = pipe.encode(flat, base=base)
-        dec = pipe.decode(enc, base=base)
-    torch.cuda.synchronize()
-    ref = oracle_roundtrip(t, flat.cpu().numpy(), 8, None if base is None else base.cpu().numpy())
-    check(t, enc, dec, ref)
-    assert pipe.fallbacks() == 0
-
-
 @pytest.mark.parametrize("bits", [4, 32])
 def test_pipeline_single_client_split(cuda, bits):
-    """One client's update cut into 3 lanes by segment ranges (idx / vals shared, mn / scale sliced)."""
+    """One client's update cut into 3 segment ranges (idx / vals shared, mn / scale sliced)."""
     t = SegmentTable(fp32_sizes("vit_b16"), 0.02, 1)
     flat = synth_batch(t, cuda, client_ids=[9])
-    pipe = LanePipeline(t, bits, lanes=3, device=cuda)
+    pipe = SplitPipeline(t, bits, split=3, device=cuda)
+    assert pipe.n_parts == 3
     enc = pipe.encode(flat)
     dec = pipe.decode(enc)
     torch.cuda.synchronize()
@@ -66,11 +47,11 @@ def test_pipeline_single_client_split(cuda, bits):
 
 
 def test_pipeline_repeated_steps_stable(cuda):
-    """Five back-to-back encode+decode steps into the same buffers on 4 lanes: every step's result equals
-    the first (a missing cross-lane dependency would let decode read idx/vals mid-write)."""
+    """Five back-to-back encode+decode steps into the same buffers as 4 sub-batches: every step's result
+    equals the first (a missing dependency would let decode read idx/vals mid-write)."""
     t = SegmentTable(fp32_sizes("resnet50_tv"), 0.01, 4)
     flat = synth_batch(t, cuda)
-    pipe = LanePipeline(t, 8, lanes=4, device=cuda)
+    pipe = SplitPipeline(t, 8, split=4, device=cuda)
     enc, out = pipe.empty_encoded(), pipe.empty_flat()
     out.zero_()  # decode writes segments only; the alignment pads keep what was there (the oracle: 0)
     pipe.roundtrip(flat, enc=enc, out=out)
@@ -110,21 +91,20 @@ def test_split_pipeline_resnet18_x3(cuda, split, delta, fused):
     assert pipe.fallbacks() == 0
 
 
-@pytest.mark.parametrize("lanes", [2, 3])
-def test_lane_pipeline_unjoined_alternating_inputs(cuda, lanes):
-    """LanePipeline.roundtrip(joined=False) back to back with TWO alternating inputs through one shared
-    Encoded and two dense outputs: a step's samplers / small segments (on C) overwrite idx / vals the
-    previous step's decodes (on S) read, so a missing 'decoded' dependency would mix the two inputs."""
+@pytest.mark.parametrize("split", [2, 3])
+def test_split_pipeline_unjoined_alternating_inputs(cuda, split):
+    """SplitPipeline.roundtrip(joined=False) back to back with TWO alternating inputs through one shared
+    Encoded and two dense outputs: each step's encode overwrites idx / vals the previous step's decode
+    read, so anything but stream order per sub-batch would mix the two inputs."""
     t = SegmentTable(fp32_sizes("resnet50_tv"), 0.01, 4)
     flats = [synth_batch(t, cuda, client_ids=range(4)), synth_batch(t, cuda, client_ids=range(10, 14))]
-    pipe = LanePipeline(t, 8, lanes=lanes, device=cuda)
+    pipe = SplitPipeline(t, 8, split=split, device=cuda)
     enc = pipe.empty_encoded()
     outs = [pipe.empty_flat().zero_(), pipe.empty_flat().zero_()]
     torch.cuda.synchronize()
     for i in range(6):
         pipe.roundtrip(flats[i % 2], enc=enc, out=outs[i % 2], joined=False)
     torch.cuda.synchronize()
-    assert pipe.timeouts() == 0
     plan = CodecPlan(fp32_sizes("resnet50_tv"), 0.01, 8, clients=4, device=cuda)
     for j in range(2):
         e = plan.encode(flats[j])
@@ -231,6 +211,39 @@ def test_decode_fill_scatter_stages(cuda):
                                           err_msg=f"clients={clients} segment at {off}")
 
 
+def test_decode_scatter_without_bounds_is_refused(cuda):
+    """A batch plan (> 8192 units) decodes its kept values from the per-unit bounds k_bounds leaves in the
+    workspace. SCATTER alone on a fresh workspace would read stale bounds: the ABI refuses it (EINVAL)
+    unless the caller sets BOUNDS_DONE after its own BOUNDS call — which then decodes exactly."""
+    from coala_amd.compression import _lib
+    t = SegmentTable(fp32_sizes("resnet50_tv"), 0.01, 4)
+    assert CodecPlan(None, 0.01, 8, table=t, device=cuda).n_units > 8192
+    flat = synth_batch(t, cuda, client_ids=range(4))
+    plan = CodecPlan(None, 0.01, 8, table=t, device=cuda)
+    e = plan.encode(flat)
+    ref = plan.decode(e, out=torch.zeros_like(flat))
+    ws = torch.full((plan.dec_ws_bytes,), 0xAB, dtype=torch.uint8, device=cuda)  # garbage bounds
+    out = torch.zeros_like(flat)
+    for stages in (_lib.COALAC_STAGE_SCATTER, _lib.COALAC_STAGE_DECODE):
+        with pytest.raises(_lib.CodecError, match="BOUNDS"):
+            plan.decode(e, out=out, workspace=ws, sched=(None, None, stages))
+    plan.decode(e, out=out, workspace=ws, sched=(None, None, _lib.COALAC_STAGE_BOUNDS))
+    plan.decode(e, out=out, workspace=ws, sched=(None, None, _lib.COALAC_STAGE_SCATTER | _lib.COALAC_STAGE_BOUNDS_DONE))
+    torch.cuda.synchronize()
+    assert torch.equal(out.view(torch.int32), ref.view(torch.int32))
+    # a latency-bound plan searches its entry ranges in-kernel: SCATTER alone is fine there
+    t1 = SegmentTable(fp32_sizes("resnet50_tv"), 0.01, 1)
+    p1 = CodecPlan(None, 0.01, 8, table=t1, device=cuda)
+    f1 = flat[:t1.span]
+    e1 = p1.encode(f1)
+    r1 = p1.decode(e1, out=torch.zeros_like(f1))
+    o1 = torch.zeros_like(f1)
+    p1.decode(e1, out=o1, sched=(None, None, _lib.COALAC_STAGE_FILL))
+    p1.decode(e1, out=o1, sched=(None, None, _lib.COALAC_STAGE_SCATTER))
+    torch.cuda.synchronize()
+    assert torch.equal(o1.view(torch.int32), r1.view(torch.int32))
+
+
 def test_split_pipelines_in_flight_on_disjoint_streams(cuda):
     """bench.py's single_x2: two single-update pipelines on disjoint pooled streams (stream_base), steps
     alternating between them unjoined, so consecutive updates overlap; each keeps its own buffers and the
@@ -280,4 +293,38 @@ def test_single_update_roundtrip_graph_replay(cuda):
     torch.cuda.synchronize()
     assert torch.equal(e.idx, enc.idx) and torch.equal(e.vals, enc.vals)
     assert torch.equal(e.mn, enc.mn) and torch.equal(e.scale, enc.scale)
+    assert torch.equal(d.view(torch.int32), out.view(torch.int32))
+
+
+@pytest.mark.parametrize("split", [1, 2])
+def test_split_pipeline_graph_capture_records_every_part(cuda, split):
+    """bench.py captures its latency-bound steps as hipGraphs on a capture stream of its own with the
+    pipeline's joined roundtrip, so every sub-batch stream forks from and joins back into the capture: a
+    replay re-runs ALL parts (an unjoined capture on part 0's stream left parts 1.. out of the
+    graph). Replayed on new data in the same buffers, the graph gives the eager result for split 1 and 2."""
+    t = SegmentTable(fp32_sizes("resnet50_tv"), 0.01, 2)
+    flat = synth_batch(t, cuda, client_ids=[31, 32])
+    pipe = SplitPipeline(t, 8, split=split, device=cuda)
+    assert pipe.n_parts == split
+    enc, out = pipe.empty_encoded(), pipe.empty_flat().zero_()
+    pipe.roundtrip(flat, enc=enc, out=out)  # warm-up (eager)
+    torch.cuda.synchronize()
+    cap = torch.cuda.Stream(cuda)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, stream=cap):
+        for _ in range(2):
+            pipe.roundtrip(flat, enc=enc, out=out, joined=True)
+    torch.cuda.synchronize()
+    flat.copy_(synth_batch(t, cuda, client_ids=[41, 42]))
+    enc.idx.zero_()
+    out.zero_()
+    torch.cuda.synchronize()
+    with torch.cuda.stream(pipe.streams[0]):
+        g.replay()
+    torch.cuda.synchronize()
+    plan = CodecPlan(None, 0.01, 8, table=t, device=cuda)
+    e = plan.encode(flat)
+    d = plan.decode(e, out=torch.zeros_like(flat))
+    torch.cuda.synchronize()
+    assert torch.equal(e.idx, enc.idx) and torch.equal(e.vals, enc.vals)
     assert torch.equal(d.view(torch.int32), out.view(torch.int32))
