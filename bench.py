@@ -481,7 +481,7 @@ def run_plugin(a, dev, steps):
             ts.append((time.perf_counter() - t0) * 1e3)
         ts.sort()
         return ts[len(ts) // 2], sum(ts) / len(ts)
-    for name, fn in (("in_place", lambda: codec.encode(state, base=base)),
+    for name, fn in (("in_place", lambda: codec.encode_module(m, base=base)),
                      ("flattened", lambda: codec.plan_for(
                          [e["n"] for e in base.entries if e["kind"] == "seg"], dev).encode(
                          flatten_state(state).flat, base=base.flat))):
@@ -491,7 +491,7 @@ def run_plugin(a, dev, steps):
         med, mean = per_call(fn, max(steps, 20))
         res[f"compression_{name}_ms"] = round(med, 4)
         res[f"compression_{name}_mean_ms"] = round(mean, 4)
-    up = codec.encode(state, base=base)
+    up = codec.encode_module(m, base=base)
     for _ in range(3):
         codec.decode_module(up, g, base=base)
     torch.cuda.synchronize()
@@ -506,7 +506,7 @@ def run_plugin(a, dev, steps):
             "alg_bytes_per_client": alg,
             "step_roofline": {"achieved_GBs": round(alg / (ms * 1e-3) / 1e9, 1),
                               "frac": round(alg / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)},
-            "desc": "UpdateCodec.encode(state_dict, base) + decode_module(update, template, base): what "
+            "desc": "UpdateCodec.encode_module(module, base) + decode_module(update, template, base): what "
                     "CompressionClientMixin.compression() / CompressionServerMixin.decompression() run, "
                     "host-side Python included; flattened = the round-1 path (torch.cat copy first)"}
 

@@ -17,6 +17,8 @@ import copy
 import math
 import threading
 from collections import OrderedDict
+from itertools import repeat
+from operator import attrgetter, is_
 
 import numpy as np
 import torch
@@ -92,8 +94,9 @@ class _Layout:
 
     def __init__(self, items):
         self.entries, self.seg_names, self.raw_names = [], [], []
+        self.seg_idx, self.raw_idx = [], []
         off = seg = 0
-        for name, dt, shape in items:
+        for i, (name, dt, shape) in enumerate(items):
             n = 1
             for d in shape:
                 n *= d
@@ -101,13 +104,16 @@ class _Layout:
             if dt == torch.float32 and n > 0:
                 e.update(kind="seg", seg=seg, off=off, n=n)
                 self.seg_names.append(name)
+                self.seg_idx.append(i)
                 off = align_up(off + n)
                 seg += 1
             else:
                 e["kind"] = "raw"
                 self.raw_names.append(name)
+                self.raw_idx.append(i)
             self.entries.append(e)
         self.sizes = [e["n"] for e in self.entries if e["kind"] == "seg"]
+        self.sizes_key = tuple(self.sizes)
 
 
 _LAYOUTS = OrderedDict()
@@ -115,7 +121,10 @@ _LAYOUTS_LOCK = threading.Lock()
 
 
 def _layout(state):
-    sig = tuple((k, v.dtype, v.shape) for k, v in state.items())
+    return _layout_sig(tuple((k, v.dtype, v.shape) for k, v in state.items()))
+
+
+def _layout_sig(sig):
     with _LAYOUTS_LOCK:
         L = _LAYOUTS.get(sig)
         if L is None:
@@ -125,13 +134,90 @@ def _layout(state):
     return L
 
 
+class _StateWalk:
+    """The tensors of a module's state_dict, in state_dict order, without building the state_dict: the
+    module tree walked once (pre-order, as Module.state_dict recurses), then per call each module's
+    parameter and persistent-buffer tables read in place (no per-entry detach, no prefix strings, no
+    state-dict hooks: the reference's models register none). Re-walked when a table's size changes."""
+
+    def __init__(self, module):
+        self.mods, names = [], []
+        self.sizes = []
+        self.hooked = False
+        for prefix, m in module.named_modules(remove_duplicate=False):
+            self.hooked = self.hooked or bool(m._state_dict_hooks or m._state_dict_pre_hooks)
+            pn = tuple(k for k, v in m._parameters.items() if v is not None)
+            bn = tuple(k for k, v in m._buffers.items() if v is not None and k not in m._non_persistent_buffers_set)
+            self.mods.append((m, pn, bn))
+            self.sizes.append((len(m._parameters), len(m._buffers)))
+            p = prefix + "." if prefix else ""
+            names.extend(p + k for k in pn + bn)
+        self.names = tuple(names)
+
+    def tensors(self):
+        out = []
+        for (m, pn, bn), (np_, nb) in zip(self.mods, self.sizes):
+            P, B = m._parameters, m._buffers
+            if len(P) != np_ or len(B) != nb:
+                return None
+            out.extend(map(P.__getitem__, pn))
+            out.extend(map(B.__getitem__, bn))
+        return out
+
+
+_WALKS = {}  # id(module) -> (weakref, _StateWalk)
+
+
+def module_tensors(module):
+    """(names, tensors) of module.state_dict() — the same names and tensor storage, in the same order — via a
+    cached _StateWalk. A module tree with state-dict hooks takes state_dict() itself."""
+    if module._state_dict_hooks or module._state_dict_pre_hooks:
+        st = module.state_dict()
+        return tuple(st), list(st.values())
+    hit = _WALKS.get(id(module))
+    w = hit[1] if hit is not None and hit[0]() is module else None
+    ts = w.tensors() if w is not None else None
+    if ts is None:  # first call, another module at this id, or a table changed size: walk again
+        import weakref
+        w = _StateWalk(module)
+        with _LAYOUTS_LOCK:
+            _WALKS[id(module)] = (weakref.ref(module), w)
+            if len(_WALKS) > 64:
+                for k in [k for k, (r, _) in _WALKS.items() if r() is None]:
+                    del _WALKS[k]
+        ts = w.tensors()
+    if w.hooked:
+        st = module.state_dict()
+        return tuple(st), list(st.values())
+    return w.names, ts
+
+
+_get_dtype, _get_shape = attrgetter("dtype"), attrgetter("shape")
+
+
+def describe_tensors(names, tensors):
+    """describe_state() over (names, tensors) in state_dict order (module_tensors)."""
+    L = _layout_sig(tuple(zip(names, map(_get_dtype, tensors), map(_get_shape, tensors))))
+    segs = list(map(tensors.__getitem__, L.seg_idx))
+    raw = OrderedDict((n, tensors[i].detach()) for n, i in zip(L.raw_names, L.raw_idx))
+    return L, segs, _snapshot_raw(raw)
+
+
 def describe_state(state):
     """state_dict -> (entries as flatten_state would write them, fp32 segment tensors in order, raw
     passthrough entries), WITHOUT copying the fp32 data: the zero-copy encode reads the tensors in place."""
+    L, segs, raw = _describe(state)
+    return L.entries, segs, raw
+
+
+def _describe(state):
     L = _layout(state)
     segs = [state[n] for n in L.seg_names]  # read in place by the kernels (pointer, numel, dtype, contiguity)
     raw = OrderedDict((n, state[n].detach()) for n in L.raw_names)
-    return L.entries, segs, _snapshot_raw(raw)
+    return L, segs, _snapshot_raw(raw)
+
+
+_data_ptr, _is_contig, _get_device = torch.Tensor.data_ptr, torch.Tensor.is_contiguous, torch.Tensor.get_device
 
 
 def _snapshot_raw(raw):
@@ -366,7 +452,7 @@ class UpdateCodec:
         self.ratio, self.bits, self.mode = float(ratio), int(bits), mode
         self.backend = backend if backend is not None else HipBackend()
         self._plans = {}
-        self._ws = {}
+        self._ws = OrderedDict()
         self._lock = threading.Lock()
         self._tls = threading.local()
 
@@ -387,11 +473,25 @@ class UpdateCodec:
         `device`: where to flatten and encode (default: where the state lives if the backend runs there,
         else the backend's default device — a model trained on the CPU is encoded on the GPU)."""
         if device is None:
-            device = self._device_for(state)
+            device = self._device_for(state.values())
+        L, segs, raw = _describe(state)
+        return self._encode(L, segs, raw, base, device, lambda: state)
+
+    def encode_module(self, module, base=None, device=None):
+        """module -> CompressedUpdate of its state_dict (what CompressionClientMixin.compression() runs): the
+        same result as encode(module.state_dict(), ...), with the state read through a cached walk of the
+        module tree (module_tensors) instead of building the state_dict."""
+        names, tensors = module_tensors(module)
+        if device is None:
+            device = self._device_for(tensors)
+        L, segs, raw = describe_tensors(names, tensors)
+        return self._encode(L, segs, raw, base, device, lambda: OrderedDict(zip(names, tensors)))
+
+    def _encode(self, L, segs, raw, base, device, state_fn):
         if self.mode == "delta" and base is None:
             raise ValueError("delta mode needs the global-model snapshot (base)")
-        entries, segs, raw = describe_state(state)
-        sizes = [e["n"] for e in entries if e["kind"] == "seg"]
+        entries = L.entries
+        sizes = L.sizes
         header = {"ratio": self.ratio, "bits": self.bits, "mode": self.mode, "n_segments": len(sizes),
                   "entries": entries}
         if not sizes:
@@ -405,16 +505,19 @@ class UpdateCodec:
             # the snapshot may have been taken where the global model arrived (the reference client's
             # set_model runs before pretrain moves the model to its device, client/base.py:138 vs :245)
             base_flat = base.flat_on(device)
-        plan = self.plan_for(sizes, device)
+        plan = self.plan_for(L.sizes_key, device)
         ws = self._workspace(plan)
         dev_index = device.index if device.type == "cuda" else -1  # (Tensor.get_device(): -1 on the CPU)
-        in_place = getattr(plan, "encode_segments", None) is not None and all(
-            t.get_device() == dev_index and t.is_contiguous() and t.data_ptr() % 16 == 0 for t in segs)
+        in_place = getattr(plan, "encode_segments", None) is not None
+        if in_place:  # every segment on the plan's device, contiguous, 16-B aligned (one pass per property)
+            ptrs = tuple(map(_data_ptr, segs))
+            in_place = (all(map(_is_contig, segs)) and all(d == dev_index for d in map(_get_device, segs))
+                        and not any(p & 15 for p in ptrs))
         if in_place:  # read the parameters where they live: no flattening copy (+8 B/element of traffic)
             # (dtype and sizes hold by construction: the plan was made from this layout's segments)
-            enc = plan.encode_segments(segs, base=base_flat, workspace=ws, checked=True)
+            enc = plan.encode_segments(segs, base=base_flat, workspace=ws, checked=True, ptrs=ptrs)
         else:
-            fs = flatten_state(state, device=device)
+            fs = flatten_state(state_fn(), device=device)
             enc = plan.encode(fs.flat, base=base_flat, workspace=ws)
         header["total_k"] = int(plan.table.total_k)
         return CompressedUpdate(header, enc, raw)
@@ -432,31 +535,52 @@ class UpdateCodec:
         return s
 
     def _staging(self, nbytes):
-        """This thread's pinned host staging buffer of at least nbytes (grown by doubling; reused once the
-        thread's stream has finished with it, which decode_state waits for)."""
+        """This thread's pinned host staging buffer of at least nbytes (grown by doubling). Reused only once
+        the copy out of it that the previous decode enqueued has completed (its event, _staged)."""
+        ev = getattr(self._tls, "staging_event", None)
+        if ev is not None:
+            ev.synchronize()
+            self._tls.staging_event = None
         buf = getattr(self._tls, "staging", None)
         if buf is None or buf.numel() < nbytes:
             buf = torch.empty(max(nbytes, 2 * (buf.numel() if buf is not None else 0), 1 << 20),
                               dtype=torch.uint8, pin_memory=True)
             self._tls.staging = buf
+        self._tls.staging_used = True
         return buf
 
+    def _staged(self, stream):
+        """After encoded_to: if it staged through this thread's pinned buffer, mark the copy's completion."""
+        if getattr(self._tls, "staging_used", False):
+            self._tls.staging_used = False
+            ev = torch.cuda.Event()
+            ev.record(stream)
+            self._tls.staging_event = ev
+
+    WS_CACHE = 16  # encode workspaces kept per codec (one per plan and launch stream in use)
+
     def _workspace(self, plan):
-        """The encode workspace of `plan` for the calling thread and its current stream, reused across
-        calls (kernels on one stream run in order, so consecutive encodes can share it)."""
+        """The encode workspace of `plan` for the current stream, reused across calls (kernels on one stream
+        run in order, so consecutive encodes can share it). A bounded LRU: an evicted workspace was allocated
+        on its stream, whose later allocations are the only ones that can reuse it (stream-ordered)."""
         if not hasattr(plan, "empty_workspace"):
             return None
         stream = torch.cuda.current_stream(plan.device) if plan.device.type == "cuda" else None
-        key = (id(plan), threading.get_ident(), None if stream is None else stream.cuda_stream)
+        key = (id(plan), None if stream is None else stream.cuda_stream)
         with self._lock:
-            ws = self._ws.get(key)
-            if ws is None:
-                ws = plan.empty_workspace()
-                self._ws[key] = ws
+            hit = self._ws.get(key)
+            if hit is not None and hit[0] is plan:
+                self._ws.move_to_end(key)
+                return hit[1]
+            ws = plan.empty_workspace()
+            self._ws[key] = (plan, ws)
+            self._ws.move_to_end(key)
+            while len(self._ws) > self.WS_CACHE:
+                self._ws.popitem(last=False)
         return ws
 
-    def _device_for(self, state):
-        for t in state.values():
+    def _device_for(self, tensors):
+        for t in tensors:
             if t.dtype == torch.float32 and t.numel() > 0:
                 runs = getattr(self.backend, "runs_on", None)
                 return t.device if runs is None or runs(t.device) else self.backend.default_device()
@@ -467,16 +591,20 @@ class UpdateCodec:
         where the codec will run: the state's own device if the backend runs there, else the backend's
         default device)."""
         state = module_or_state.state_dict() if isinstance(module_or_state, nn.Module) else module_or_state
-        return flatten_state(state, device=device if device is not None else self._device_for(state))
+        return flatten_state(state, device=device if device is not None else self._device_for(state.values()))
 
     # -- decode -----------------------------------------------------------------------------------
     def decode_state(self, update, base=None, device=None):
-        """CompressedUpdate -> OrderedDict state (fp32 entries are views into one fresh flat buffer)."""
+        """CompressedUpdate -> OrderedDict state (fp32 entries are views into one fresh flat buffer).
+
+        On a GPU the decode runs on this thread's own stream (the remote server decodes from one thread per
+        upload, coala/server/service.py:74), after a pinned H2D of a received payload; the caller's current
+        stream waits for it (no host synchronisation), so the returned tensors are ready for any work the
+        caller enqueues next."""
         h = update.header  # self-describing: decode with the blob's own ratio/bits/mode
-        sizes = [e["n"] for e in h["entries"] if e["kind"] == "seg"]
-        state = OrderedDict()
-        flat = None
-        if sizes:
+        D = _decode_layout(h["entries"])
+        flat = plan = None
+        if D.sizes:
             if device is None:
                 device = self.backend.default_device()
             base_flat = None
@@ -485,28 +613,29 @@ class UpdateCodec:
                     raise ValueError("delta-mode update needs the global model (base) to decode")
                 _check_same_layout(h["entries"], base.entries)
                 base_flat = base.flat_on(device)
-            plan = self.plan_for(sizes, device, ratio=h["ratio"], bits=h["bits"])
+            plan = self.plan_for(D.sizes, device, ratio=h["ratio"], bits=h["bits"])
             if device.type == "cuda":
-                # this thread's own stream (the remote server decodes from one thread per upload,
-                # coala/server/service.py:74): pinned H2D of the payload + decode, then wait for it
+                cur = torch.cuda.current_stream(device)
                 side = self._thread_stream(device)
-                side.wait_stream(torch.cuda.current_stream(device))
-                out = torch.empty(plan.span, dtype=torch.float32, device=device)
+                side.wait_stream(cur)
+                out = torch.empty(plan.span, dtype=torch.float32, device=device)  # (the caller's stream's pool)
                 with torch.cuda.stream(side):
                     enc = update.encoded_to(device, staging=self._staging)
+                    self._staged(side)
                     flat = plan.decode(enc, base=base_flat, out=out, stream=side)
-                side.synchronize()
+                cur.wait_stream(side)
             else:
                 enc = update.encoded.to(device, non_blocking=True)
                 flat = plan.decode(enc, base=base_flat)
-        views = _segment_views(flat, plan.table, h["entries"]) if sizes else None
-        for e in h["entries"]:
-            if e["kind"] == "seg":
-                state[e["name"]] = views[e["seg"]]
-            else:
-                t = update.raw[e["name"]]
-                state[e["name"]] = t.to(device) if device is not None else t
-        return state
+        vals = [None] * len(D.names)
+        if D.sizes:
+            for pos, v in zip(D.seg_pos, _segment_views(flat, plan.table, h["entries"])):
+                vals[pos] = v
+        raw = update.raw
+        for pos, name in D.raw:
+            t = raw[name]
+            vals[pos] = t.to(device) if device is not None else t
+        return OrderedDict(zip(D.names, vals))
 
     def decode_module(self, update, template, base=None):
         """CompressedUpdate -> new nn.Module shaped like `template` holding the decoded state.
@@ -601,67 +730,224 @@ def _segment_views(flat, table, entries):
     return out
 
 
-_PLAIN_TYPES = frozenset((bool, int, float, str, type(None), tuple))
+_PLAIN_TYPES = frozenset((bool, int, float, complex, str, bytes, type(None), torch.dtype, torch.device))
 _CONTAINER_TYPES = frozenset((dict, OrderedDict, list, set))
 _MODULE_TABLES = frozenset(("_parameters", "_buffers", "_modules"))
+_make_param = torch.Tensor._make_subclass
+
+
+def _plain(v):
+    """An attribute value a clone may share with the template: immutable and holding no tensor / module."""
+    tv = type(v)
+    if tv in _PLAIN_TYPES:
+        return True
+    if tv is tuple or tv is frozenset:
+        return all(_plain(x) for x in v)
+    return False
+
+
+class _TreeRecipe:
+    """How to rebuild a template's module tree around new tensors, classified once per template (the
+    server's global model is one object for the whole task): the modules in pre-order (a submodule shared
+    by several parents is cloned once, as copy.deepcopy would), and per module the attributes a clone
+    shares (immutable plain values), gets as fresh empty containers (hook dicts, ...), deep-copies (any
+    other object: non-empty containers, hook objects, unregistered modules — with a memo that maps the
+    template's modules / parameters / buffers to the clone's, so bound hooks are rebound as deepcopy would)
+    or clones (unregistered tensors), plus its parameter / buffer / child slots. A module whose attribute
+    set, table sizes or special attribute types changed since is re-classified."""
+
+    def __init__(self, template):
+        self.mods, self.prefixes, self.index = [], [], {}
+        stack = [(template, "")]
+        while stack:
+            m, prefix = stack.pop()
+            if id(m) in self.index:
+                continue
+            self.index[id(m)] = len(self.mods)
+            self.mods.append(m)
+            self.prefixes.append(prefix)
+            stack.extend((c, prefix + n + ".") for n, c in reversed(list(m._modules.items())) if c is not None)
+        self.info = [self.classify(m, p) for m, p in zip(self.mods, self.prefixes)]
+
+    def classify(self, m, prefix):
+        d = m.__dict__
+        fresh, deep, tens = [], [], []
+        for k, v in d.items():
+            if k in _MODULE_TABLES or _plain(v):
+                continue
+            tv = type(v)
+            if tv in _CONTAINER_TYPES and not v:
+                fresh.append((k, tv))
+            elif isinstance(v, torch.Tensor):
+                tens.append((k, tv))
+            else:
+                deep.append((k, tv))
+        params = tuple((n, prefix + n, p is None or p.requires_grad) for n, p in m._parameters.items())
+        buffers = tuple((n, prefix + n) for n in m._buffers)
+        children = tuple((n, None if c is None else self.index[id(c)]) for n, c in m._modules.items())
+        sizes = (len(d), len(m._parameters), len(m._buffers), len(m._modules))
+        return sizes, tuple(fresh), tuple(deep), tuple(tens), params, buffers, children
+
+    def valid(self, i):
+        """Cheap per-call check that module i still matches its classification: attribute / table sizes, its
+        fresh containers still empty (a hook registered later must be deep-copied, not dropped) and the
+        types of its deep-copied / cloned attributes."""
+        m = self.mods[i]
+        sizes, fresh, deep, tens = self.info[i][:4]
+        d = m.__dict__
+        if sizes != (len(d), len(m._parameters), len(m._buffers), len(m._modules)):
+            return False
+        g = self.getters[i]
+        if g is not None and any(g(d)):
+            return False
+        return not (tens or deep) or all(type(d.get(k)) is tv for k, tv in tens + deep)
+
+    def _getters(self):
+        from operator import itemgetter
+        self.getters = []
+        for info in self.info:
+            keys = [k for k, _ in info[1]]
+            self.getters.append(None if not keys else itemgetter(*keys) if len(keys) > 1 else
+                                (lambda d, k=keys[0]: (d[k],)))
+
+    def build(self, state):
+        mods, info = self.mods, self.info
+        if not hasattr(self, "getters"):
+            self._getters()
+        stale = [i for i in range(len(mods)) if not self.valid(i)]
+        if stale:
+            for i in stale:
+                info[i] = self.classify(mods[i], self.prefixes[i])
+            self._getters()
+        fast = self.__dict__.get("fast")
+        if fast is None or stale:
+            fast = self.fast = [self._fast(x) for x in info]
+        new = [m.__class__.__new__(m.__class__) for m in mods]
+        get = state.get
+        deep_todo = []
+        for i, m in enumerate(mods):
+            pnames, pkeys, prgs, bnames, bkeys, fkeys, ftypes, cnames, cidx, tens, deep = fast[i]
+            ts = list(map(get, pkeys))
+            if any(map(is_, ts, repeat(None))):  # a parameter the state lacks (or a None slot): the template's, cloned
+                src = m._parameters
+                ts = [t if t is not None else (None if src[n] is None else src[n].detach().clone())
+                      for n, t in zip(pnames, ts)]
+                P = {n: None if t is None else _make_param(nn.Parameter, t, rg) for n, t, rg in zip(pnames, ts, prgs)}
+            else:
+                P = dict(zip(pnames, map(_make_param, repeat(nn.Parameter), ts, prgs)))
+            B = dict(zip(bnames, map(get, bkeys)))
+            if any(map(is_, B.values(), repeat(None))):
+                srcb = m._buffers
+                B = {n: (t if t is not None else (None if srcb[n] is None else srcb[n].clone())) for n, t in B.items()}
+            d = m.__dict__.copy()  # plain attributes shared (read now: e.g. `training` follows the template)
+            if fkeys:
+                d.update(zip(fkeys, [tv() for tv in ftypes]))
+            for k in tens:
+                d[k] = d[k].clone()
+            d["_parameters"] = P
+            d["_buffers"] = B
+            d["_modules"] = dict(zip(cnames, [None if j is None else new[j] for j in cidx]))
+            new[i].__dict__.update(d)  # (a fresh object's dict: no Module.__setattr__ on the way)
+            if deep:
+                deep_todo.append((i, deep))
+        if deep_todo:  # after every clone is filled in, so the memo maps every module / tensor
+            memo = self._memo(new, state)
+            for i, deep in deep_todo:
+                nd = new[i].__dict__
+                for k in deep:
+                    nd[k] = copy.deepcopy(nd[k], memo)
+        return new[0]
+
+    @staticmethod
+    def _fast(x):
+        _, fresh, deep, tens, params, buffers, children = x
+        return (tuple(n for n, _, _ in params), tuple(k for _, k, _ in params), tuple(rg for _, _, rg in params),
+                tuple(n for n, _ in buffers), tuple(k for _, k in buffers),
+                tuple(k for k, _ in fresh), tuple(tv for _, tv in fresh),
+                tuple(n for n, _ in children), tuple(j for _, j in children),
+                tuple(k for k, _ in tens), tuple(k for k, _ in deep))
+
+    def _memo(self, new, state):
+        """deepcopy memo: template module / parameter / buffer -> its counterpart in the clone."""
+        memo = {}
+        for m, c in zip(self.mods, new):
+            memo[id(m)] = c
+        for m, c, p in zip(self.mods, new, self.prefixes):
+            for name, t in m._parameters.items():
+                if t is not None and name in c.__dict__.get("_parameters", {}):
+                    memo[id(t)] = c._parameters[name]
+            for name, t in m._buffers.items():
+                if t is not None and name in c.__dict__.get("_buffers", {}):
+                    memo[id(t)] = c._buffers[name]
+        return memo
+
+
+_RECIPES = {}  # id(template) -> (weakref to it, recipe)
+_RECIPES_LOCK = threading.Lock()
 
 
 def module_with_state(template, state):
     """A new nn.Module shaped like `template` whose parameters / buffers ARE the tensors of `state`
     (views into the decode output: no parameter data is copied; `template` is never aliased).
 
-    The module tree is rebuilt directly (new objects of the same classes, their __dict__ copied one level
-    deep, fresh parameter / buffer / submodule tables and hook dicts) instead of copy.deepcopy, whose
-    generic recursion cost ~8 ms per ResNet-50 on the server's per-upload path. Tensors outside the state
-    (non-persistent buffers, unregistered tensors) are cloned."""
-    def shallow(v):  # a container one level deep; empty ones (most hook dicts) without copy.copy's reduce path
-        if not v:
-            try:
-                return v.__class__()
-            except TypeError:
-                pass
-        return copy.copy(v)
+    The module tree is rebuilt from a per-template recipe (_TreeRecipe) — new objects of the same classes,
+    their __dict__ copied one level deep with fresh tables and hook dicts, other attributes deep-copied —
+    instead of copy.deepcopy, whose generic recursion cost ~8 ms per ResNet-50 on the server's per-upload
+    path. Tensors outside the state (non-persistent buffers, unregistered tensors) are cloned."""
+    key = id(template)
+    with _RECIPES_LOCK:
+        hit = _RECIPES.get(key)
+        if hit is None or hit[0]() is not template:
+            import weakref
+            hit = (weakref.ref(template), _TreeRecipe(template))
+            _RECIPES[key] = hit
+            if len(_RECIPES) > 32:
+                for k in [k for k, (r, _) in _RECIPES.items() if r() is None]:
+                    del _RECIPES[k]
+    return hit[1].build(state)
 
-    def clone(mod, prefix):
-        cls = mod.__class__
-        new = cls.__new__(cls)
-        d = {}
-        for k, v in mod.__dict__.items():
-            tv = type(v)
-            if tv in _PLAIN_TYPES:  # most of a module's attributes: nothing to copy
-                pass
-            elif tv in _CONTAINER_TYPES:
-                if k not in _MODULE_TABLES:
-                    v = shallow(v)  # (the hook dicts included: the clone never shares them)
-            elif isinstance(v, torch.Tensor):
-                v = v.clone()
-            elif isinstance(v, (list, dict, set)) and k not in _MODULE_TABLES:
-                v = shallow(v)
-            d[k] = v
-        params = OrderedDict()
-        for name, p in mod._parameters.items():
-            if p is None:
-                params[name] = None
-                continue
-            t = state.get(prefix + name)
-            params[name] = nn.Parameter(t if t is not None else p.detach().clone(), requires_grad=p.requires_grad)
-        buffers = OrderedDict()
-        for name, b in mod._buffers.items():
-            t = None if b is None else state.get(prefix + name)
-            buffers[name] = None if b is None else (t if t is not None else b.clone())
-        d["_parameters"], d["_buffers"] = params, buffers
-        d["_modules"] = OrderedDict((name, None if c is None else clone(c, prefix + name + "."))
-                                    for name, c in mod._modules.items())
-        new.__dict__.update(d)
-        return new
-    return clone(template, "")
+
+_SAME_LAYOUT = OrderedDict()  # (id(a), id(b)) -> (a, b): pairs of entry lists already found equal
 
 
 def _check_same_layout(entries, base_entries):
+    key = (id(entries), id(base_entries))
+    hit = _SAME_LAYOUT.get(key)
+    if hit is not None and hit[0] is entries and hit[1] is base_entries:
+        return
     a = [(e["name"], e["dtype"], tuple(e["shape"])) for e in entries]
     b = [(e["name"], e["dtype"], tuple(e["shape"])) for e in base_entries]
     if a != b:
         raise ValueError("update and base model have different state_dict layouts")
+    with _LAYOUTS_LOCK:  # (the header entries are never mutated: the pair stays equal)
+        _SAME_LAYOUT[key] = (entries, base_entries)
+        while len(_SAME_LAYOUT) > 64:
+            _SAME_LAYOUT.popitem(last=False)
+
+
+class _DecodeLayout:
+    """Per header-entries list: the state names, the fp32 segment sizes and where segments / raw entries sit."""
+
+    def __init__(self, entries):
+        self.names = tuple(e["name"] for e in entries)
+        self.sizes = tuple(e["n"] for e in entries if e["kind"] == "seg")
+        self.seg_pos = [i for i, e in enumerate(entries) if e["kind"] == "seg"]
+        self.raw = [(i, e["name"]) for i, e in enumerate(entries) if e["kind"] != "seg"]
+
+
+_DECODE_LAYOUTS = OrderedDict()  # id(entries) -> (entries, _DecodeLayout)
+
+
+def _decode_layout(entries):
+    hit = _DECODE_LAYOUTS.get(id(entries))
+    if hit is not None and hit[0] is entries:
+        return hit[1]
+    D = _DecodeLayout(entries)
+    with _LAYOUTS_LOCK:
+        _DECODE_LAYOUTS[id(entries)] = (entries, D)
+        while len(_DECODE_LAYOUTS) > 64:
+            _DECODE_LAYOUTS.popitem(last=False)
+    return D
 
 
 def as_numpy(t):

@@ -173,10 +173,12 @@ class CodecPlan:
         _lib.check(rc, "coalac_encode")
         return out
 
-    def segment_pointers(self, tensors, checked=False):
+    def segment_pointers(self, tensors, checked=False, ptrs=None, stream=None):
         """Device array of the tensors' data pointers (one per segment), for encode_segments; cached per
         pointer tuple (a model's parameter storage does not move between rounds). checked: the caller has
-        verified device, dtype, contiguity, alignment and sizes (UpdateCodec.encode)."""
+        verified device, dtype, contiguity, alignment and sizes (UpdateCodec.encode); ptrs: their data
+        pointers, if the caller has them. The array is marked as in use by `stream` (the launch stream), so
+        an eviction from the cache never hands its memory to other work while a kernel still reads it."""
         segs = self.table.segs
         if len(tensors) != len(segs):
             raise ValueError(f"need {len(segs)} segment tensors, got {len(tensors)}")
@@ -187,20 +189,27 @@ class CodecPlan:
                 raise ValueError(f"segment {i}: {t.numel()} elements, the plan says {int(segs[i, 1])}")
             if t.data_ptr() % 16:
                 raise ValueError(f"segment {i}: storage must be 16-byte aligned")
-        key = tuple(t.data_ptr() for t in tensors)
+        key = ptrs if ptrs is not None else tuple(t.data_ptr() for t in tensors)
         cache = self.__dict__.setdefault("_segptr_cache", {})
+        st = torch.cuda.current_stream(self.device) if stream is None else stream
         d = cache.get(key)
         if d is None:
-            if len(cache) > 8:
-                cache.clear()
-            d = torch.tensor(key, dtype=torch.int64).to(self.device)
-            cache[key] = d
+            if len(cache) >= 8:  # LRU-ish: drop the oldest entry (dicts keep insertion order)
+                cache.pop(next(iter(cache)))
+            with torch.cuda.stream(st):
+                d = torch.tensor(key, dtype=torch.int64).to(self.device, non_blocking=False)
+            cache[key] = (d, st)
+        else:
+            d, home = d
+            if home != st:
+                d.record_stream(st)
         return d
 
-    def encode_segments(self, tensors, base=None, out=None, workspace=None, flags=0, stream=None, checked=False):
+    def encode_segments(self, tensors, base=None, out=None, workspace=None, flags=0, stream=None, checked=False,
+                        ptrs=None):
         """Encode with segment i read from tensors[i] itself (coalac_encode_segptr): e.g. a model's
         parameters, no flattening copy. base: flat fp32[span] (delta mode), as encode()."""
-        ptrs = self.segment_pointers(tensors, checked=checked)
+        ptrs = self.segment_pointers(tensors, checked=checked, ptrs=ptrs, stream=stream)
         self._check_flat(base, "base")
         with _on(stream):
             out = self.empty_encoded() if out is None else out

@@ -155,7 +155,7 @@ class CompressionClientMixin(_CodecOwner):
             return
         codec = self._codec()
         base = getattr(self, "_codec_base", None) if codec.mode == "delta" else None
-        update = codec.encode(model.state_dict(), base=base)
+        update = codec.encode_module(model, base=base)
         self._codec_trained_model = model
         self.model = update
         # §8(f) 3: the compression ratio next to TRAIN_UPLOAD_SIZE (client/base.py:155); an unknown

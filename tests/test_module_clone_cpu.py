@@ -1,0 +1,100 @@
+"""module_with_state (the server decompression's module rebuild) keeps copy.deepcopy's semantics where a
+template holds more than plain values: hooks bound to the template are rebound to the clone,
+tensors inside container attributes are copied, unregistered submodules are deep-copied, and plain
+attributes follow the template's CURRENT values (the recipe is cached per template). Also: the cached
+state walk (module_tensors) returns exactly state_dict()'s names and storage, and follows changes."""
+import copy
+
+import torch
+from torch import nn
+
+from coala_amd.compression.codec import module_tensors, module_with_state
+
+
+class Block(nn.Module):
+    def __init__(self):
+        super().__init__()
+        self.conv = nn.Conv2d(2, 3, 3)
+        self.bn = nn.BatchNorm2d(3)
+        self.calls = []
+        self.register_forward_hook(self._record)
+        self.extra = [torch.ones(3), 5]
+        self.table = {"w": torch.zeros(2)}
+        self.__dict__["aux"] = nn.Linear(2, 2)  # an unregistered module attribute
+
+    def _record(self, mod, inp, out):
+        self.calls.append(out.shape)
+
+    def forward(self, x):
+        return self.bn(self.conv(x))
+
+
+class Net(nn.Module):
+    def __init__(self):
+        super().__init__()
+        self.b1 = Block()
+        self.shared = nn.Linear(4, 4)
+        self.b2 = nn.Sequential(self.shared, nn.ReLU(), self.shared)  # shared submodule
+        self.register_buffer("scratch", torch.zeros(2), persistent=False)
+
+
+def _new_state(m):
+    return {k: torch.randn_like(v) if v.is_floating_point() else v.clone() for k, v in m.state_dict().items()}
+
+
+def test_clone_has_the_state_and_no_aliasing():
+    m = Net()
+    st = _new_state(m)
+    c = module_with_state(m, st)
+    cs = c.state_dict()
+    assert list(cs) == list(m.state_dict())
+    for k, v in st.items():  # (a shared submodule is cloned once, from its first name: "shared.")
+        if not k.startswith("b2."):
+            assert cs[k].data_ptr() == v.data_ptr()
+    assert all(isinstance(p, nn.Parameter) for p in c.parameters())
+    assert c.b2[0] is c.b2[2] is c.shared and c.shared is not m.shared  # sharing kept, template not aliased
+    assert c.scratch is not m.scratch and torch.equal(c.scratch, m.scratch)  # non-persistent: cloned
+
+
+def test_hooks_rebound_and_containers_copied_like_deepcopy():
+    m = Net()
+    c = module_with_state(m, _new_state(m))
+    ref = copy.deepcopy(m)
+    x = torch.randn(1, 2, 5, 5)
+    c.b1(x)
+    assert len(c.b1.calls) == 1 and m.b1.calls == []  # the clone's hook records on the clone
+    ref.b1(x)
+    assert len(ref.b1.calls) == 1
+    assert c.b1.extra is not m.b1.extra and c.b1.extra[0] is not m.b1.extra[0] and c.b1.extra[1] == 5
+    assert torch.equal(c.b1.extra[0], m.b1.extra[0])
+    assert c.b1.table["w"] is not m.b1.table["w"]
+    assert c.b1.aux is not m.b1.aux and torch.equal(c.b1.aux.weight, m.b1.aux.weight)
+    # a hook registered on the template after the first clone is carried by the next clone
+    seen = []
+    m.b2.register_forward_hook(lambda mod, i, o: seen.append(1))
+    c2 = module_with_state(m, _new_state(m))
+    c2.b2(torch.randn(1, 4))
+    assert seen == [1]
+
+
+def test_plain_attributes_follow_the_template():
+    m = Net()
+    module_with_state(m, _new_state(m))
+    m.eval()
+    c = module_with_state(m, _new_state(m))
+    assert not c.training and not c.b1.bn.training
+    m.train()
+    assert module_with_state(m, _new_state(m)).b1.bn.training
+
+
+def test_module_tensors_matches_state_dict_and_follows_changes():
+    m = Net()
+    names, ts = module_tensors(m)
+    st = m.state_dict()
+    assert names == tuple(st) and [t.data_ptr() for t in ts] == [v.data_ptr() for v in st.values()]
+    m.b1.register_buffer("extra_buf", torch.ones(1))
+    names2, ts2 = module_tensors(m)
+    assert names2 == tuple(m.state_dict()) and "b1.extra_buf" in names2
+    m.b1.conv.weight = nn.Parameter(torch.zeros(3, 2, 3, 3))  # replaced parameter: same table size
+    _, ts3 = module_tensors(m)
+    assert any(t is m.b1.conv.weight for t in ts3)
