@@ -86,10 +86,10 @@ def parse():
     p.add_argument("--graph", choices=["auto", "on", "off"], default="auto",
                    help="replay each timed step as a captured hipGraph: auto = the latency-bound configs "
                         f"({', '.join(GRAPH_CONFIGS) if 'GRAPH_CONFIGS' in globals() else 'single, single_x2, C5'})")
-    p.add_argument("--graph-steps", type=int, default=12,
-                   help="timed steps captured in one graph (--graph; rounded up to whole input rotations): one graph "
-                        "launch per this many steps (1 / 4 / 10 measured 0.0845 / 0.0803 / 0.0796 ms per single step; "
-                        "eager 0.080-0.083)")
+    p.add_argument("--graph-steps", type=int, default=30,
+                   help="at most this many timed steps captured in one graph (--graph; whole input rotations, the "
+                        "count that needs the fewest launches): 1 / 4 / 10 steps per launch measured 0.0845 / 0.0803 / "
+                        "0.0796 ms per single step (eager 0.080-0.083)")
     p.add_argument("--cpu-seconds", type=float, default=8.0, help="CPU baseline time budget per leg")
     p.add_argument("--no-cpu-baseline", action="store_true")
     return p.parse_args()
@@ -298,28 +298,40 @@ def warm_workload(W, a):
     W["fallbacks"] = sum(p.fallbacks() for p, _ in W["slots"])
 
 
+def _graph_plan(W, a):
+    """Per slot: how its share of the timed steps is replayed — whole-rotation graphs of gk steps, then single
+    steps — with gk the multiple of the rotation (<= --graph-steps) that needs the fewest graph launches."""
+    S, rot = len(W["slots"]), W["rot"]
+    per = [a.steps // S + (1 if j < a.steps % S else 0) for j in range(S)]
+    n = max(1, min(per))
+    cands = [m * rot for m in range(1, max(1, a.graph_steps // rot) + 1)] or [rot]
+    gk = min(cands, key=lambda g: (max(p // g + p % g for p in per), -g)) if n >= rot else rot
+    return gk, per
+
+
 def capture_graphs(W, a):
     """Latency-bound configs: each slot's steps captured as hipGraphs and replayed on the slot's first stream
     (the same kernels on the same buffers: one graph launch per gk steps instead of the per-call Python checks,
     ctypes calls and ~8 kernel launches per step, which take about as long as the ~80 us of GPU work of one
     update — a box with a slower host measured the eager single step at 0.138 ms for 0.080 ms of kernels).
-    Captured on a stream of its own with the pipeline's JOINED roundtrip, so every sub-batch stream forks
-    from the capture and joins back into it (all parts land in the graph). Runs before any process group
-    exists (no other thread makes HIP calls during the capture)."""
+    A one-part pipeline is captured on its own stream, unjoined (each join would add graph nodes: ~3.5 us per
+    step); a pipeline of several sub-batches is captured on a stream of its own with the JOINED roundtrip, so
+    every sub-batch stream forks from the capture and joins back into it (all parts land in the graph).
+    Runs before any process group exists (no other thread makes HIP calls during the capture)."""
     import torch
     S = len(W["slots"])
-    gk = max(1, a.graph_steps)
-    gk = -(-gk // W["rot"]) * W["rot"]  # whole rotations per graph
-    W["gk"] = gk
+    gk, per = _graph_plan(W, a)
+    W["gk"], W["per_slot"] = gk, per
 
-    def capture(steps_of_slot):  # {slot: [buffer-set index per captured step]}
+    def capture(steps_of_slot):  # buffer-set index per captured step
         gs = []
         for j, (p, _) in enumerate(W["slots"]):
-            cap = torch.cuda.Stream(p.device)
+            joined = p.n_parts > 1
+            cap = torch.cuda.Stream(p.device) if joined else p.streams[0]
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g, stream=cap, capture_error_mode="thread_local"):
                 for r in steps_of_slot:
-                    _step(W, r * S + j, True)
+                    _step(W, r * S + j, joined)
             gs.append((g, p.streams[0]))
         return gs
     try:
@@ -356,20 +368,18 @@ def time_workload(W, a, dev, world):
     if graphs is None:
         for i in range(a.steps):
             _step(W, i, a.joined)
-    else:  # chunks of gk steps per slot launch; the remainder one graph per step
+    else:  # per slot: its whole-rotation graphs, then its single steps; slots round-robin
         gk, S = W["gk"], len(slots)
-        i = c = 0
-        while i < a.steps:
-            if a.steps - i >= gk:
-                g, st = graphs[gk][c % S]
-                n = gk
-            else:
-                g, st = graphs[(1, (c // S) % W["rot"])][c % S]
-                n = 1
-            with torch.cuda.stream(st):
-                g.replay()
-            i += n
-            c += 1
+        ops = []
+        for j, n in enumerate(W["per_slot"]):
+            big = n // gk
+            ops.append([graphs[gk][j]] * big + [graphs[(1, r % W["rot"])][j] for r in range(n - big * gk)])
+        for t in range(max(len(o) for o in ops)):
+            for o in ops:
+                if t < len(o):
+                    g, st = o[t]
+                    with torch.cuda.stream(st):
+                        g.replay()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()

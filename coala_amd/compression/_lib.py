@@ -48,8 +48,8 @@ SIGNATURES = [
     ("coalac_decode_ev", _I, [_P, _P, _P, _P, _P, _P, _P, _P, _U64, _P, _P]),
     ("coalac_encode_sched", _I, [_P, _P, _P, _P, _P, _P, _P, _P, _U64, ctypes.c_uint, _P, _P]),
     ("coalac_decode_sched", _I, [_P, _P, _P, _P, _P, _P, _P, _P, _U64, _P, _P]),
-    ("coalac_aggregate", _I, [_P, _I, _P, _P, _P, _P, _P, ctypes.c_float, _I, _P, _P, _P, _U64, _P]),
-    ("coalac_aggregate_ev", _I, [_P, _I, _P, _P, _P, _P, _P, ctypes.c_float, _I, _P, _P, _P, _U64, _P, _P]),
+    ("coalac_aggregate", _I, [_P, _I, _P, _P, _P, _P, _P, ctypes.c_float, _I, _P, _P, _P, _P, _U64, _P]),
+    ("coalac_aggregate_ev", _I, [_P, _I, _P, _P, _P, _P, _P, ctypes.c_float, _I, _P, _P, _P, _P, _U64, _P, _P]),
     ("coalac_workspace_fallbacks", _I, [_P, _P, _P, ctypes.POINTER(_I)]),
     ("coalac_debug_stamps", _I, [_P, _P, _P, ctypes.POINTER(ctypes.c_uint64), _I]),
 ]

@@ -648,7 +648,7 @@ class UpdateCodec:
 
 
     # -- fused server-side aggregation ------------------------------------------------------------
-    def aggregate(self, updates, weights, template, base=None, mode="recip", device=None):
+    def aggregate(self, updates, weights, template, base=None, mode="recip", device=None, params_only=False):
         """Fused decode + FedAvg of several CompressedUpdates of one layout -> new nn.Module.
 
         Equivalent to decode_module() of every update followed by the reference's
@@ -659,7 +659,10 @@ class UpdateCodec:
         multi-GPU server passes to reduce_models (coala/distributed/distributed.py:42-57). Non-fp32
         entries (int64 BatchNorm counters) are combined with the same torch ops as the reference, on the
         output device. Weights follow federated_averaging / weighted_sum: empty or all-zero weights
-        become 1 per update.
+        become 1 per update. params_only (aggregation_content "parameters", coala/server/base.py:588-591):
+        only the template's parameters are averaged (federated_averaging_only_params /
+        weighted_sum_only_params, strategies.py:32-54, 93-124); every buffer keeps update 0's decoded value,
+        as the reference's deepcopy(models[0]) does.
         """
         if not updates:
             return None
@@ -685,17 +688,25 @@ class UpdateCodec:
         state = OrderedDict()
         flat = None
         offs = None
+        if params_only:
+            pnames = {n for n, _ in template.named_parameters(remove_duplicate=False)}
         if sizes:
             C = len(updates)
             plan = self.plan_for(sizes, device, ratio=h0["ratio"], bits=h0["bits"], clients=C)
             encs = [u.encoded.to(device, non_blocking=True) for u in updates]
             batched = Encoded(*(torch.cat([getattr(e, f) for e in encs]) for f in ("idx", "vals", "mn", "scale")))
-            flat = plan.aggregate(batched, weights, total=total, base=base_flat, mode=mode)
+            avg_mask = None
+            if params_only:
+                pnames = {n for n, _ in template.named_parameters(remove_duplicate=False)}
+                avg_mask = [e["name"] in pnames for e in h0["entries"] if e["kind"] == "seg"]
+            flat = plan.aggregate(batched, weights, total=total, base=base_flat, mode=mode, avg_mask=avg_mask)
             offs = plan.table.offsets
         for e in h0["entries"]:
             if e["kind"] == "seg":
                 o = offs[e["seg"]]
                 state[e["name"]] = flat[o:o + e["n"]].view(e["shape"])
+            elif params_only and e["name"] not in pnames:  # a buffer: update 0's (deepcopy(models[0]))
+                state[e["name"]] = updates[0].raw[e["name"]].to(device).clone()
             else:  # restated weighted_sum (+ torch.div) on the raw entries
                 acc = updates[0].raw[e["name"]].to(device).clone()
                 acc *= weights[0]

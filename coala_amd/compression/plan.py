@@ -250,7 +250,7 @@ class CodecPlan:
         return out
 
     def aggregate(self, enc, weights, total=None, base=None, out=None, workspace=None, mode="recip", stream=None,
-                  events=None):
+                  events=None, avg_mask=None):
         """Fused decode + FedAvg of the plan's `clients` updates (coalac_aggregate).
 
         enc: the batched Encoded of all clients (client-major, as encode() produces). weights: one
@@ -260,6 +260,8 @@ class CodecPlan:
         modules — mode "recip" reproduces torch on the GPU (division by a host scalar becomes a multiply
         by its fp32 reciprocal), "div" torch on the CPU, "sum" stops before the division (weighted_sum,
         strategies.py:57-90: what a multi-GPU server hands to reduce_models, distributed.py:42-57).
+        avg_mask: one bool per segment of a client (None: all True); a False segment is not averaged but
+        takes client 0's decoded value — aggregation_content "parameters" (strategies.py:32-54, 93-124).
         """
         self._check_encoded(enc)
         if not getattr(self.table, "uniform", False):
@@ -277,12 +279,17 @@ class CodecPlan:
             out = torch.empty(n_out, dtype=torch.float32, device=self.device) if out is None else out
             ws = self.empty_decode_workspace() if workspace is None else workspace
             w = torch.tensor([float(x) for x in weights], dtype=torch.float64).to(torch.float32).to(self.device)
+            m = None
+            if avg_mask is not None:
+                if len(avg_mask) != len(self.table.sizes):
+                    raise ValueError(f"avg_mask: need {len(self.table.sizes)} entries, got {len(avg_mask)}")
+                m = torch.tensor([1 if x else 0 for x in avg_mask], dtype=torch.uint8).to(self.device)
         self._check_flat(out, "output", n_out)
         if ws.device != self.device or ws.numel() * ws.element_size() < self.dec_ws_bytes:
             raise ValueError(f"aggregate workspace: need {self.dec_ws_bytes} bytes on {self.device}")
         total = float(sum(weights)) if total is None else float(total)
         args = (self._h, C, _ptr(enc.idx), _ptr(enc.vals), _ptr(enc.mn), _ptr(enc.scale), _ptr(w),
-                ctypes.c_float(total), modes[mode],
+                ctypes.c_float(total), modes[mode], _ptr(m),
                 _ptr(base), _ptr(out), _ptr(ws), ctypes.c_uint64(self.dec_ws_bytes), _stream_handle(stream))
         with torch.cuda.device(self.device):
             if events is None:
@@ -290,7 +297,7 @@ class CodecPlan:
             else:
                 rc = self._lib.coalac_aggregate_ev(*args, _event_array(events, 3))
         _lib.check(rc, "coalac_aggregate")
-        return out  # w was allocated on the launch stream: its memory is reused only after the kernel
+        return out  # w / m were allocated on the launch stream: their memory is reused only after the kernel
 
     def fallbacks(self, workspace, stream=None):
         """Segments of the last encode with this workspace whose sampled bracket missed (synchronises)."""

@@ -183,14 +183,15 @@ class CompressionClientMixin(_CodecOwner):
         return _bit_to_megabyte(sum(p.numel() for p in model.parameters()) * param_size)
 
 
-def reduce_models():
-    """The reference's reduce_models (coala/distributed/distributed.py:42-57) when COALA is installed,
-    else its restatement (coala_amd/fl/distributed.py)."""
+def reduce_models(params_only=False):
+    """The reference's reduce_models / reduce_models_only_params (coala/distributed/distributed.py:42-57,
+    60-74) when COALA is installed, else their restatements (coala_amd/fl/distributed.py)."""
+    name = "reduce_models_only_params" if params_only else "reduce_models"
     try:
-        from coala.distributed.distributed import reduce_models as fn
+        from coala.distributed import distributed as mod
     except ImportError:
-        from ..fl.distributed import reduce_models as fn
-    return fn
+        from ..fl import distributed as mod
+    return getattr(mod, name)
 
 
 class CompressionServerMixin(_CodecOwner):
@@ -306,8 +307,7 @@ class CompressionServerMixin(_CodecOwner):
         server_conf = getattr(conf, "server", None)
         distributed = bool(getattr(conf, "is_distributed", False))
         params_only = getattr(server_conf, "aggregation_content", "all") == AGGREGATION_CONTENT_PARAMS
-        fusable = (self.codec_fused_aggregate and models and not params_only
-                   and all(isinstance(m, CompressedUpdate) for m in models))
+        fusable = self.codec_fused_aggregate and models and all(isinstance(m, CompressedUpdate) for m in models)
         if fusable:
             if getattr(server_conf, "aggregation_strategy", None) == EQUAL_AVERAGE:
                 weights = [1 for _ in models]
@@ -323,14 +323,16 @@ class CompressionServerMixin(_CodecOwner):
                     import torch.distributed as dist
                     dist.barrier()
                     sample_sum = sum(weights)  # weighted_sum returns the caller's sum (0 stays 0)
-                    model = codec.aggregate(models, weights, self._real_global(), base=base, mode="sum", device=dev)
-                    reduce_models()(model, torch.tensor(sample_sum).to(getattr(conf, "device", dev)))
+                    model = codec.aggregate(models, weights, self._real_global(), base=base, mode="sum", device=dev,
+                                            params_only=params_only)
+                    reduce_models(params_only)(model, torch.tensor(sample_sum).to(getattr(conf, "device", dev)))
                     return model
                 mode = "div" if dev.type == "cpu" else "recip"  # torch's division semantics on that device
-                return codec.aggregate(models, weights, self._real_global(), base=base, mode=mode, device=dev)
+                return codec.aggregate(models, weights, self._real_global(), base=base, mode=mode, device=dev,
+                                       params_only=params_only)
         models = [self._decode_upload(m) if isinstance(m, CompressedUpdate) else m for m in models]
         parent = getattr(super(), "aggregate", None)
         if parent is not None:
             return parent(models, weights)
-        from ..fl.strategies import federated_averaging
-        return federated_averaging(models, weights)
+        from ..fl.strategies import federated_averaging, federated_averaging_only_params
+        return (federated_averaging_only_params if params_only else federated_averaging)(models, weights)

@@ -2279,9 +2279,13 @@ struct AggArgs {
   uint32_t clients, T, U0; // clients, segments per client, units per client
   uint64_t Kc;             // kept entries per client (out_off stride between clients)
   float total, inv_total;  // sum of weights; 1.0f / total (fp32 division)
+  const uint8_t* avg_mask; // [T] 1: segment averaged, 0: client 0's value passed through; null: all averaged
 };
 
-// k_aggregate: one wave per 4096-element unit of the (client-0) layout. For client i in order:
+// k_aggregate: one wave per 4096-element unit of the (client-0) layout. For client i in order (segments
+// the avg mask leaves out — the buffers of aggregation_content "parameters" — take client 0's x_0 as is,
+// as strategies.weighted_sum_only_params / federated_averaging_only_params leave models[0]'s buffers,
+// coala/server/strategies.py:32-54, 93-124):
 //   x_i = base + d_i   (d_i = decoded value where client i kept the element, +0.0f elsewhere: exactly
 //                       what coalac_decode with a base writes; without a base x_i = d_i)
 //   acc = x_0 * w_0, then acc = acc + (x_i * w_i)        (torch: params *= w0; params += s_i * w_i)
@@ -2307,6 +2311,8 @@ __global__ __launch_bounds__(BLOCK, AGG_WPE) void k_aggregate(Params P, AggArgs 
   if (u >= A.U0) return;
   const UnitDev U = P.units[u];
   const uint32_t len = U.len, kseg = U.k;
+  const bool avg = A.avg_mask == nullptr || A.avg_mask[U.seg] != 0;
+  const uint32_t nclients = avg ? A.clients : 1u;
   const uint32_t e_lo = h * HE;  // first element (within the unit) of this wave's rows
   if (e_lo >= len) return;
   const uint32_t hlen = min(len - e_lo, HE);
@@ -2331,8 +2337,8 @@ __global__ __launch_bounds__(BLOCK, AGG_WPE) void k_aggregate(Params P, AggArgs 
     }
     acc[it] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
   }
-  for (uint32_t c0 = 0; c0 < A.clients; c0 += 64) {
-    const uint32_t cn = min(64u, A.clients - c0);
+  for (uint32_t c0 = 0; c0 < nclients; c0 += 64) {
+    const uint32_t cn = min(64u, nclients - c0);
     // lane j: metadata of client c0 + j (unconditional loads at a clamped client index)
     const uint32_t cl = c0 + min(lane, cn - 1);
     const uint32_t ucl = u + cl * A.U0;
@@ -2341,7 +2347,7 @@ __global__ __launch_bounds__(BLOCK, AGG_WPE) void k_aggregate(Params P, AggArgs 
     const uint32_t sl = U.seg + cl * A.T;
     const float m_mn = RAW ? 0.0f : P.cmn[sl];
     const float m_sc = RAW ? 0.0f : P.cscale[sl];
-    const float m_w = A.weights[cl];
+    const float m_w = avg ? A.weights[cl] : 1.0f;  // (x_0 * 1.0f == x_0)
     auto entries = [&](uint32_t j) -> uint64_t { return U.out_off + (uint64_t)(c0 + j) * A.Kc; };
     auto fetch = [&](uint32_t j, uint32_t& pos, uint32_t& q) {
       const uint32_t jj = min(j, cn - 1);
@@ -2406,7 +2412,9 @@ __global__ __launch_bounds__(BLOCK, AGG_WPE) void k_aggregate(Params P, AggArgs 
 #pragma unroll
   for (uint32_t it = 0; it < RI; ++it) {
     float4 o;
-    if (MODE == COALAC_AGG_DIV) {
+    if (!avg) {
+      o = acc[it];
+    } else if (MODE == COALAC_AGG_DIV) {
       o = make_float4(acc[it].x / A.total, acc[it].y / A.total, acc[it].z / A.total, acc[it].w / A.total);
     } else if (MODE == COALAC_AGG_SUM) {
       o = acc[it];
@@ -3086,8 +3094,8 @@ int coalac_decode(coalac_plan_t plan, const int32_t* d_idx, const void* d_vals, 
 
 int coalac_aggregate_ev(coalac_plan_t plan, int clients, const int32_t* d_idx, const void* d_vals,
                         const float* d_mn, const float* d_scale, const float* d_weights, float total, int mode,
-                        const float* d_base, float* d_out, void* d_ws, uint64_t ws_bytes, void* stream,
-                        void* const* events) {
+                        const uint8_t* d_avg_mask, const float* d_base, float* d_out, void* d_ws,
+                        uint64_t ws_bytes, void* stream, void* const* events) {
   if (!plan) return fail(COALAC_EINVAL, "coalac_aggregate: plan is NULL");
   if (clients < 1 || plan->nseg % clients) return fail(COALAC_EINVAL, "coalac_aggregate: %d segments are not %d copies "
                                                        "of one layout", plan->nseg, clients);
@@ -3135,6 +3143,7 @@ int coalac_aggregate_ev(coalac_plan_t plan, int clients, const int32_t* d_idx, c
   A.Kc = Kc;
   A.total = total;
   A.inv_total = 1.0f / total;
+  A.avg_mask = d_avg_mask;
   hipStream_t st = static_cast<hipStream_t>(stream);
   const coalac_sched_t s = record_only(events, 3);
   const coalac_sched_t* sc = events ? &s : nullptr;
@@ -3168,10 +3177,10 @@ int coalac_aggregate_ev(coalac_plan_t plan, int clients, const int32_t* d_idx, c
 }
 
 int coalac_aggregate(coalac_plan_t plan, int clients, const int32_t* d_idx, const void* d_vals, const float* d_mn,
-                     const float* d_scale, const float* d_weights, float total, int mode, const float* d_base,
-                     float* d_out, void* d_ws, uint64_t ws_bytes, void* stream) {
-  return coalac_aggregate_ev(plan, clients, d_idx, d_vals, d_mn, d_scale, d_weights, total, mode, d_base, d_out,
-                             d_ws, ws_bytes, stream, nullptr);
+                     const float* d_scale, const float* d_weights, float total, int mode, const uint8_t* d_avg_mask,
+                     const float* d_base, float* d_out, void* d_ws, uint64_t ws_bytes, void* stream) {
+  return coalac_aggregate_ev(plan, clients, d_idx, d_vals, d_mn, d_scale, d_weights, total, mode, d_avg_mask, d_base,
+                             d_out, d_ws, ws_bytes, stream, nullptr);
 }
 
 int coalac_workspace_fallbacks(coalac_plan_t plan, const void* d_ws, void* stream, int* out) {

@@ -15,7 +15,7 @@ from dataclasses import dataclass, field
 
 import torch
 
-from .strategies import federated_averaging
+from .strategies import federated_averaging, federated_averaging_only_params
 
 DATA_TYPE_PARAMS = 0  # coala/pb common.proto DataType (tests/golden/hooks.json)
 
@@ -170,5 +170,8 @@ class LoopbackServer:
         agg = self.aggregate(list(self.uploaded.values()), list(self.weights.values()))
         self.model.load_state_dict(agg.state_dict())  # set_model(load_dict=True), server/base.py:571
 
-    def aggregate(self, models, weights):  # server/base.py:573-601, non-distributed "all" branch
+    def aggregate(self, models, weights):  # server/base.py:573-601, non-distributed branch
+        server = getattr(getattr(self, "conf", None), "server", None)
+        if getattr(server, "aggregation_content", "all") == "parameters":  # base.py:588-591
+            return federated_averaging_only_params(models, weights)
         return federated_averaging(models, weights)

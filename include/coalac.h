@@ -187,17 +187,22 @@ int coalac_decode_sched(coalac_plan_t plan, const int32_t* d_idx, const void* d_
  *         = acc                       (mode COALAC_AGG_SUM: strategies.weighted_sum, :57-90 — the
  *                                      multi-GPU server's per-rank sum before reduce_models'
  *                                      all_reduce + division, coala/server/base.py:595-598)
+ * d_avg_mask: DEVICE uint8[segments per client] or NULL (= every segment averaged). A segment whose byte
+ * is 0 is not averaged: d_out = x_0, client 0's decoded value — aggregation_content "parameters"
+ * (coala/server/base.py:588-591), where strategies.weighted_sum_only_params / federated_averaging_only_params
+ * average the parameters only and keep models[0]'s buffers (coala/server/strategies.py:32-54, 93-124).
  * d_weights: DEVICE fp32[clients] = float(w_i); total: float(sum of the weights). d_out / d_base are
  * indexed like client 0's segments. Workspace: dec_ws_bytes of coalac_plan_query. Events (the _ev
  * variant): [0] before the unit-bounds pass, [1] before k_aggregate, [2] after. */
 enum { COALAC_AGG_DIV = 0, COALAC_AGG_RECIP = 1, COALAC_AGG_SUM = 2 };
 int coalac_aggregate(coalac_plan_t plan, int clients, const int32_t* d_idx, const void* d_vals,
                      const float* d_mn, const float* d_scale, const float* d_weights, float total, int mode,
-                     const float* d_base, float* d_out, void* d_ws, uint64_t ws_bytes, void* stream);
+                     const uint8_t* d_avg_mask, const float* d_base, float* d_out, void* d_ws, uint64_t ws_bytes,
+                     void* stream);
 int coalac_aggregate_ev(coalac_plan_t plan, int clients, const int32_t* d_idx, const void* d_vals,
                         const float* d_mn, const float* d_scale, const float* d_weights, float total, int mode,
-                        const float* d_base, float* d_out, void* d_ws, uint64_t ws_bytes, void* stream,
-                        void* const* events);
+                        const uint8_t* d_avg_mask, const float* d_base, float* d_out, void* d_ws,
+                        uint64_t ws_bytes, void* stream, void* const* events);
 
 /* Diagnostics: number of segments whose sampled thresholds were rejected and re-selected exactly in
  * the last encode that used workspace d_ws (synchronises `stream`). */

@@ -170,7 +170,8 @@ def decode(idx, vals, mn, scale, segs, bits, span, base=None, out=None):
 AGG_DIV, AGG_RECIP, AGG_SUM = 0, 1, 2
 
 
-def aggregate(idx, vals, mn, scale, segs, bits, clients, weights, total, mode, base=None, out_span=None):
+def aggregate(idx, vals, mn, scale, segs, bits, clients, weights, total, mode, base=None, out_span=None,
+              avg_mask=None):
     """Fused decode + FedAvg restated: decode every client (decode_segment, i.e. coalac_decode with the
     same base), then the reference's weighted average over the decoded fp32 entries, in client order:
 
@@ -183,6 +184,11 @@ def aggregate(idx, vals, mn, scale, segs, bits, clients, weights, total, mode, b
     sum a multi-GPU server hands to reduce_models, distributed.py:42-57). weights / total are taken as fp32 (torch converts the Python scalars to the tensor's
     fp32 compute type). segs: [clients * T, 4] client-major copies of one layout; the output is
     indexed like client 0's segments (positions outside them: 0).
+
+    avg_mask (one bool per segment of a client, None = all True): a False segment is not averaged; it
+    keeps client 0's decoded value, as weighted_sum_only_params / federated_averaging_only_params keep
+    models[0]'s buffers (coala/server/strategies.py:32-54, 93-124: deepcopy(models[0]), then only
+    named_parameters() are summed and divided).
     """
     segs = np.asarray(segs, dtype=np.int64).reshape(-1, 4)
     T = len(segs) // clients
@@ -194,6 +200,10 @@ def aggregate(idx, vals, mn, scale, segs, bits, clients, weights, total, mode, b
         for t in range(T):
             off0, n = int(segs[t, 0]), int(segs[t, 1])
             b = None if base is None else base[off0:off0 + n]
+            if avg_mask is not None and not avg_mask[t]:
+                off, n_, k, oo = (int(v) for v in segs[t])
+                out[off0:off0 + n] = decode_segment(idx[oo:oo + k], vals[oo:oo + k], mn[t], scale[t], n, bits, b)
+                continue
             acc = None
             for c in range(clients):
                 off, n_, k, oo = (int(v) for v in segs[c * T + t])

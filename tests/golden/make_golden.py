@@ -149,6 +149,30 @@ def make_fedavg():
           sorted({str(v.dtype) for v in avg.state_dict().values()}))
 
 
+def make_fedavg_params():
+    """aggregation_content "parameters" (coala/server/base.py:588-591): the reference's
+    federated_averaging_only_params / weighted_sum_only_params (coala/server/strategies.py:32-54, 93-124) on
+    the fedavg.npz inputs, plus the zero-weights case of weighted_sum_only_params."""
+    from coala.server import strategies
+    models = [_seeded_tiny(s) for s in (11, 12, 13)]
+    weights = [3, 5, 2]
+    avg = strategies.federated_averaging_only_params([copy.deepcopy(m) for m in models], list(weights))
+    wsum, total = strategies.weighted_sum_only_params([copy.deepcopy(m) for m in models], list(weights))
+    wzero, tz = strategies.weighted_sum_only_params([copy.deepcopy(m) for m in models], [0, 0, 0])
+    arrays = {}
+    for i, m in enumerate(models):
+        for k, v in m.state_dict().items():
+            arrays[f"in{i}/{k}"] = v.numpy()
+    for tag, mod in (("avg", avg), ("sum", wsum), ("sum0", wzero)):
+        for k, v in mod.state_dict().items():
+            arrays[f"{tag}/{k}"] = v.detach().numpy()
+    arrays["weights"] = np.array(weights, dtype=np.int64)
+    arrays["total"] = np.array([total], dtype=np.int64)
+    arrays["total0"] = np.array([tz], dtype=np.int64)
+    np.savez(os.path.join(HERE, "fedavg_params.npz"), **arrays)
+    print("fedavg_params.npz:", len(arrays), "arrays")
+
+
 def make_hooks():
     from coala.client.base import BaseClient
     from coala.pb import common_pb2 as common_pb
@@ -291,7 +315,7 @@ if __name__ == "__main__":
         sys.exit("run with PYTHONDONTWRITEBYTECODE=1 so nothing is written into /root/reference")
     sys.dont_write_bytecode = True
     _stub_coala()
-    make_layouts()
-    make_fedavg()
-    make_hooks()
-    make_plugin_fixture()
+    parts = {"layouts": make_layouts, "fedavg": make_fedavg, "fedavg_params": make_fedavg_params,
+             "hooks": make_hooks, "plugin": make_plugin_fixture}
+    for name in (sys.argv[1:] or list(parts)):  # e.g. `make_golden.py fedavg_params`: that fixture only
+        parts[name]()

@@ -29,13 +29,13 @@ class OraclePlan:
                  self.table.segs.astype(np.int64), self.bits, self.table.span, base=b, out=out)
         return torch.from_numpy(out)
 
-    def aggregate(self, enc, weights, total=None, base=None, mode="div", **_):
+    def aggregate(self, enc, weights, total=None, base=None, mode="div", avg_mask=None, **_):
         total = float(sum(weights)) if total is None else float(total)
         b = None if base is None else base.detach().cpu().numpy()
         out = O.aggregate(enc.idx.numpy(), enc.vals.numpy(), enc.mn.numpy(), enc.scale.numpy(),
                           self.table.segs.astype(np.int64), self.bits, self.table.clients, weights, total,
                           {"div": O.AGG_DIV, "recip": O.AGG_RECIP, "sum": O.AGG_SUM}[mode], base=b,
-                          out_span=self.table.span_per_client)
+                          out_span=self.table.span_per_client, avg_mask=avg_mask)
         return torch.from_numpy(out)
 
 

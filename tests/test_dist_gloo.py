@@ -89,7 +89,7 @@ def test_two_rank_gloo_sharded_equals_serial():
     assert got == serial
 
 
-def _fused_sum_worker(rank, world, port, q):
+def _fused_sum_worker(rank, world, port, q, content="all"):
     """Each rank aggregates its own uploads; the fused path (one coalac_aggregate in "sum" mode, then
     reduce_models) must equal the reference's distributed branch on decoded modules (server/base.py:
     594-598: weighted_sum, then reduce_models = all_reduce + div, distributed.py:42-57)."""
@@ -104,7 +104,7 @@ def _fused_sum_worker(rank, world, port, q):
     class Conf:
         class server:
             aggregation_strategy = "FedAvg"
-            aggregation_content = "all"
+            aggregation_content = content
         is_distributed = True
         device = "cpu"
 
@@ -129,8 +129,14 @@ def _fused_sum_worker(rank, world, port, q):
     s.conf = Conf
     fused = s.aggregate(list(ups), list(weights))
     dec = [codec.decode_module(u, g, base=base) for u in ups]
-    ref, tot = weighted_sum(dec, list(weights))
-    reduce_models(ref, torch.tensor(tot))
+    if content == "parameters":  # server/base.py:588-591: the *_only_params pair (distributed.py:60-74)
+        from coala_amd.fl.distributed import reduce_models_only_params
+        from coala_amd.fl.strategies import weighted_sum_only_params
+        ref, tot = weighted_sum_only_params(dec, list(weights))
+        reduce_models_only_params(ref, torch.tensor(tot))
+    else:
+        ref, tot = weighted_sum(dec, list(weights))
+        reduce_models(ref, torch.tensor(tot))
     same = all(a.dtype == b.dtype and torch.equal(a, b)
                for a, b in zip(ref.state_dict().values(), fused.state_dict().values()))
     res = [None] * world
@@ -141,12 +147,13 @@ def _fused_sum_worker(rank, world, port, q):
 
 
 @pytest.mark.timeout(300)
-def test_two_rank_gloo_fused_weighted_sum_equals_reference_reduce():
+@pytest.mark.parametrize("content", ["all", "parameters"])
+def test_two_rank_gloo_fused_weighted_sum_equals_reference_reduce(content):
     world = 2
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_fused_sum_worker, args=(r, world, port, q)) for r in range(world)]
+    procs = [ctx.Process(target=_fused_sum_worker, args=(r, world, port, q, content)) for r in range(world)]
     [p.start() for p in procs]
     got = q.get(timeout=240)
     [p.join(timeout=60) for p in procs]

@@ -73,6 +73,63 @@ def test_aggregate_matches_torch_gpu_fedavg_on_decoded(cuda, delta):
         assert torch.equal(out[off:off + n].view(torch.int32), ref[off:off + n].view(torch.int32))
 
 
+@pytest.mark.parametrize("delta", [True, False])
+@pytest.mark.parametrize("mode,om", [("recip", O.AGG_RECIP), ("sum", O.AGG_SUM)])
+def test_aggregate_avg_mask_matches_oracle(cuda, delta, mode, om):
+    """aggregation_content "parameters": segments outside the mask (the buffers) take client 0's decoded
+    value, the others are averaged — against the oracle's restatement of federated_averaging_only_params /
+    weighted_sum_only_params (coala/server/strategies.py:32-54, 93-124)."""
+    C = 4
+    plan, one, enc, base = setup("resnet18", 0.02, 8, C, delta, seed=6)
+    rng = np.random.default_rng(3)
+    mask = (rng.random(len(plan.table.sizes)) < 0.6).tolist()
+    mask[0], mask[1] = True, False
+    weights = [5, 9, 0, 2]
+    segs = plan.table.segs.astype(np.int64)
+    h = [t.cpu().numpy() for t in (enc.idx, enc.vals, enc.mn, enc.scale)]
+    b = None if base is None else base.cpu().numpy()
+    out = plan.aggregate(enc, weights, base=base, mode=mode, avg_mask=mask)
+    torch.cuda.synchronize()
+    ref = O.aggregate(*h, segs, 8, C, weights, sum(weights), om, base=b, out_span=plan.table.span_per_client,
+                      avg_mask=mask)
+    g = out.cpu().numpy()
+    for off, n in zip(plan.table.offsets, plan.table.sizes):
+        np.testing.assert_array_equal(g[off:off + n].view(np.uint32), ref[off:off + n].view(np.uint32))
+    with pytest.raises(ValueError):
+        plan.aggregate(enc, weights, base=base, mode=mode, avg_mask=mask[:-1])
+
+
+def test_fused_params_only_server_end_to_end_on_gpu(cuda):
+    """Mixin with the HIP backend, aggregation_content "parameters": fused == decompress-each +
+    federated_averaging_only_params on the GPU (buffers from the first upload)."""
+    dev = torch.device("cuda", 0)
+
+    class Client(CompressionClientMixin, LoopbackClient):
+        codec_ratio, codec_bits, codec_mode = 0.02, 8, "delta"
+
+    class Plain(CompressionServerMixin, LoopbackServer):
+        codec_ratio, codec_bits, codec_mode = 0.02, 8, "delta"
+
+    class Fused(Plain):
+        codec_fused_aggregate = True
+
+    class Conf:
+        class server:
+            aggregation_strategy = "FedAvg"
+            aggregation_content = "parameters"
+        is_distributed = False
+
+    g0 = build_module("resnet18", seed=4, device=dev)
+    mk = lambda: [Client(f"c{i}", [11, 3, 30][i], device=dev, step_seed=i) for i in range(3)]
+    plain, fused = Plain(copy.deepcopy(g0), mk()), Fused(copy.deepcopy(g0), mk())
+    plain.conf = fused.conf = Conf
+    for r in range(2):
+        plain.round(r)
+        fused.round(r)
+        for (k, a), b in zip(plain.model.state_dict().items(), fused.model.state_dict().values()):
+            assert a.dtype == b.dtype and torch.equal(a, b), k
+
+
 def test_aggregate_single_client_equals_decode_scaled(cuda):
     plan, one, enc, base = setup("lenet", 0.05, 8, 1, True, seed=9)
     out = plan.aggregate(enc, [4], base=base, mode="div")
@@ -89,7 +146,7 @@ def test_aggregate_rejects_non_copy_layouts(cuda):
     from coala_amd.compression import _lib
     plan = CodecPlan([5000, 300, 7000], 0.01, 8, clients=1)
     # 3 segments cannot be 2 copies of one layout: refused before any launch
-    rc = plan._lib.coalac_aggregate(plan._h, 2, None, None, None, None, None, ctypes.c_float(1.0), 0, None,
+    rc = plan._lib.coalac_aggregate(plan._h, 2, None, None, None, None, None, ctypes.c_float(1.0), 0, None, None,
                                     None, None, ctypes.c_uint64(0), None)
     with pytest.raises(CodecError, match="copies"):
         _lib.check(rc, "coalac_aggregate")

@@ -224,3 +224,51 @@ def test_fused_aggregation_zero_weights_and_oracle_modes():
     assert np.array_equal(x / tot, torch.div(torch.from_numpy(x), 3).numpy())
     r = x * (np.float32(1.0) / tot)
     assert not np.array_equal(r, x / tot)  # 10 * (1/3) != 10 / 3 in fp32: the modes really differ
+
+
+def test_params_only_restatement_matches_reference_fixture():
+    """federated_averaging_only_params / weighted_sum_only_params restated (coala_amd/fl/strategies.py)
+    against the reference's own outputs (tests/golden/fedavg_params.npz, made by make_golden.py from
+    coala/server/strategies.py:32-54, 93-124): parameters averaged, buffers left as models[0]'s."""
+    from coala_amd.fl.strategies import federated_averaging_only_params, weighted_sum_only_params
+    a = np.load(os.path.join(GOLD, "fedavg_params.npz"))
+    models = [_tiny_from_npz(a, f"in{i}") for i in range(3)]
+    w = a["weights"].tolist()
+    avg = federated_averaging_only_params([copy.deepcopy(m) for m in models], w)
+    for k, v in avg.state_dict().items():
+        np.testing.assert_array_equal(v.detach().numpy(), a[f"avg/{k}"], err_msg=k)
+    for tag, ww, tot_key in (("sum", w, "total"), ("sum0", [0, 0, 0], "total0")):
+        s, tot = weighted_sum_only_params([copy.deepcopy(m) for m in models], ww)
+        assert tot == int(a[tot_key][0])
+        for k, v in s.state_dict().items():
+            np.testing.assert_array_equal(v.detach().numpy(), a[f"{tag}/{k}"], err_msg=f"{tag}/{k}")
+    assert np.array_equal(a["avg/bn.running_mean"], a["in0/bn.running_mean"])  # buffers: models[0]'s
+
+
+@pytest.mark.parametrize("mode,bits", [("delta", 8), ("weights", 32)])
+def test_fused_params_only_aggregation_matches_decode_then_fedavg_only_params(mode, bits):
+    """aggregation_content "parameters" stays fused: the server's global model after two rounds is
+    bit-identical to decompressing every upload and running federated_averaging_only_params (buffers —
+    fp32 running stats and int64 counters — from the first upload)."""
+    Client, Server = make_classes(0.05, bits, mode)
+
+    class Fused(Server):
+        codec_fused_aggregate = True
+
+    class Conf:
+        class server:
+            aggregation_strategy = "FedAvg"
+            aggregation_content = "parameters"
+        is_distributed = False
+
+    g0 = build_module("resnet18_split_cut4", seed=9)
+    mk = lambda: [Client(f"c{i}", [13, 4, 7][i], step_seed=i) for i in range(3)]
+    plain, fused = Server(copy.deepcopy(g0), mk()), Fused(copy.deepcopy(g0), mk())
+    fused.conf = plain.conf = Conf
+    for r in range(2):
+        plain.round(r)
+        fused.round(r)
+        assert all(isinstance(m, CompressedUpdate) for m in fused.uploaded.values())
+        for (k, a), (k2, b) in zip(plain.model.state_dict().items(), fused.model.state_dict().items()):
+            assert k == k2 and a.dtype == b.dtype, k
+            assert torch.equal(a, b), k

@@ -1,6 +1,7 @@
-"""cProfile of the hooks' host path on the GPU (one ResNet-50 client, delta mode): UpdateCodec.encode of
-the trained state in place (client compression()) and decode_module into a new module on w_global (server
-decompression(model)), as bench.py's 'plugin' extra runs them. Prints the top host functions by own time.
+"""Host-path breakdown of the hooks on the GPU (one ResNet-50 client, delta mode): UpdateCodec.encode_module
+of the trained module in place (client compression()) and decode_module into a new module on w_global
+(server decompression(model)), as bench.py's 'plugin' extra runs them. Prints the median per-call time of
+each host step (each call synchronised, like the bench), then cProfile's top functions by own time.
 
     python tools/plugin_profile.py [steps]
 """
@@ -15,7 +16,20 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch  # noqa: E402
 
 from coala_amd.compression import UpdateCodec  # noqa: E402
+from coala_amd.compression import codec as C  # noqa: E402
 from coala_amd.layouts import build_module  # noqa: E402
+
+
+def med(fn, n, sync=True):
+    ts = []
+    for _ in range(n):
+        t0 = time.perf_counter()
+        fn()
+        if sync:
+            torch.cuda.synchronize()
+        ts.append((time.perf_counter() - t0) * 1e3)
+    ts.sort()
+    return ts[len(ts) // 2]
 
 
 def main(steps=50):
@@ -24,27 +38,38 @@ def main(steps=50):
     g = build_module("resnet50_tv", seed=2, device=dev)
     codec = UpdateCodec(0.01, 8, "delta")
     base = codec.snapshot(g)
-    state = m.state_dict()
     for _ in range(5):
-        up = codec.encode(state, base=base)
+        up = codec.encode_module(m, base=base)
         codec.decode_module(up, g, base=base)
     torch.cuda.synchronize()
-    for name, fn in (("encode", lambda: codec.encode(state, base=base)),
-                     ("decode_module", lambda: codec.decode_module(up, g, base=base))):
-        t0 = time.perf_counter()
-        for _ in range(steps):
+    names, ts = C.module_tensors(m)
+    L, segs, raw = C.describe_tensors(names, ts)
+    st = codec.decode_state(up, base=base)
+    rows = [
+        ("compression: encode_module (total)", lambda: codec.encode_module(m, base=base), True),
+        ("  module_tensors", lambda: C.module_tensors(m), False),
+        ("  describe_tensors (layout + raw snapshot)", lambda: C.describe_tensors(names, ts), False),
+        ("  state_dict() (what round 2 walked)", lambda: m.state_dict(), False),
+        ("decompression: decode_module (total)", lambda: codec.decode_module(up, g, base=base), True),
+        ("  decode_state", lambda: codec.decode_state(up, base=base), True),
+        ("  module_with_state", lambda: C.module_with_state(g, st), False),
+        ("empty sync", lambda: None, True),
+    ]
+    for name, fn, sync in rows:
+        for _ in range(3):
             fn()
         torch.cuda.synchronize()
-        print(f"{name}: {(time.perf_counter() - t0) / steps * 1e3:.3f} ms per call", flush=True)
+        print(f"{name:48s} {med(fn, steps, sync):.4f} ms (median of {steps})", flush=True)
+    for name, fn in (("encode_module", lambda: codec.encode_module(m, base=base)),
+                     ("decode_module", lambda: codec.decode_module(up, g, base=base))):
         pr = cProfile.Profile()
         pr.enable()
         for _ in range(steps):
             fn()
         torch.cuda.synchronize()
         pr.disable()
-        st = pstats.Stats(pr)
-        st.sort_stats("tottime").print_stats(18)
-        st.sort_stats("cumulative").print_stats(18)
+        print(f"---- {name}")
+        pstats.Stats(pr).sort_stats("tottime").print_stats(14)
 
 
 if __name__ == "__main__":
