@@ -374,10 +374,10 @@ def time_workload(W, a, dev, world):
         for j, n in enumerate(W["per_slot"]):
             big = n // gk
             ops.append([graphs[gk][j]] * big + [graphs[(1, r % W["rot"])][j] for r in range(n - big * gk)])
-        for t in range(max(len(o) for o in ops)):
+        for q in range(max(len(o) for o in ops)):
             for o in ops:
-                if t < len(o):
-                    g, st = o[t]
+                if q < len(o):
+                    g, st = o[q]
                     with torch.cuda.stream(st):
                         g.replay()
     torch.cuda.synchronize()
