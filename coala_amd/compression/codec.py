@@ -17,6 +17,7 @@ import copy
 import math
 import threading
 from collections import OrderedDict
+from collections.abc import Mapping
 from itertools import repeat
 from operator import attrgetter, is_
 
@@ -114,6 +115,11 @@ class _Layout:
             self.entries.append(e)
         self.sizes = [e["n"] for e in self.entries if e["kind"] == "seg"]
         self.sizes_key = tuple(self.sizes)
+        # the passthrough entries as one group when they are all scalars of one dtype (BatchNorm counters)
+        raw_items = [items[i] for i in self.raw_idx]
+        self.raw_scalars = (None if not raw_items or any(len(sh) for _, _, sh in raw_items)
+                            or len({dt for _, dt, _ in raw_items}) != 1
+                            else [(n, (), 1) for n, _, _ in raw_items])
 
 
 _LAYOUTS = OrderedDict()
@@ -199,8 +205,17 @@ def describe_tensors(names, tensors):
     """describe_state() over (names, tensors) in state_dict order (module_tensors)."""
     L = _layout_sig(tuple(zip(names, map(_get_dtype, tensors), map(_get_shape, tensors))))
     segs = list(map(tensors.__getitem__, L.seg_idx))
-    raw = OrderedDict((n, tensors[i].detach()) for n, i in zip(L.raw_names, L.raw_idx))
-    return L, segs, _snapshot_raw(raw)
+    raw_ts = list(map(tensors.__getitem__, L.raw_idx))
+    raw = None
+    if L.raw_scalars is not None:
+        try:
+            with torch.no_grad():  # one stack of the scalar counters: no per-entry checks
+                raw = RawState([(torch.stack(raw_ts), L.raw_scalars)], L.raw_names)
+        except RuntimeError:  # (counters on several devices)
+            raw = None
+    if raw is None:
+        raw = RawState.snapshot(list(zip(L.raw_names, raw_ts)))
+    return L, segs, raw
 
 
 def describe_state(state):
@@ -213,32 +228,81 @@ def describe_state(state):
 def _describe(state):
     L = _layout(state)
     segs = [state[n] for n in L.seg_names]  # read in place by the kernels (pointer, numel, dtype, contiguity)
-    raw = OrderedDict((n, state[n].detach()) for n in L.raw_names)
-    return L, segs, _snapshot_raw(raw)
+    return L, segs, RawState.snapshot([(n, state[n]) for n in L.raw_names])
 
 
 _data_ptr, _is_contig, _get_device = torch.Tensor.data_ptr, torch.Tensor.is_contiguous, torch.Tensor.get_device
 
 
+class RawState(Mapping):
+    """The passthrough (non-fp32) entries of an update — BatchNorm's int64 num_batches_tracked and the like —
+    held as ONE flat tensor per (dtype, device) with the entries' names and shapes, in state order. Taking
+    the snapshot is one copy kernel per group (not one per entry); the per-entry tensors are views made on
+    first access (one unbind / split call per group). A read-only mapping name -> tensor."""
+
+    def __init__(self, groups, order):
+        self._groups = groups    # [(flat, [(name, shape, numel)])]
+        self._order = order      # names in state order
+        self._views = None
+
+    @classmethod
+    def snapshot(cls, items):
+        """Copies of (name, tensor) items taken now, grouped per (dtype, device)."""
+        groups, index = [], {}
+        for name, t in items:
+            key = (t.dtype, t.device)
+            g = index.get(key)
+            if g is None:
+                g = index[key] = []
+                groups.append((key, g))
+            g.append((name, t))
+        out = []
+        with torch.no_grad():
+            for _, members in groups:
+                ts = [t for _, t in members]
+                if all(t.dim() == 0 for t in ts):
+                    flat = torch.stack(ts)  # (one kernel: the usual case, scalar counters)
+                else:
+                    flat = torch.cat([t.reshape(-1) for t in ts])
+                out.append((flat, [(n, tuple(t.shape), t.numel()) for n, t in members]))
+        return cls(out, [n for n, _ in items])
+
+    def _make_views(self, groups):
+        views = {}
+        for flat, members in groups:
+            if all(len(shape) == 0 for _, shape, _ in members):
+                views.update(zip((n for n, _, _ in members), flat.unbind()))
+            else:
+                for (n, shape, _), piece in zip(members, flat.split_with_sizes([m for _, _, m in members])):
+                    views[n] = piece.view(shape)
+        return views
+
+    def __getitem__(self, name):
+        if self._views is None:
+            self._views = self._make_views(self._groups)
+        return self._views[name]
+
+    def __iter__(self):
+        return iter(self._order)
+
+    def __len__(self):
+        return len(self._order)
+
+    @property
+    def nbytes(self):
+        return sum(f.numel() * f.element_size() for f, _ in self._groups)
+
+    def fresh(self, device=None):
+        """{name: tensor} with storage of its own (one copy per group, onto `device` if given): what a
+        decode hands out, so decoded modules never alias the update or each other."""
+        groups = [(f.to(device, copy=True) if device is not None else f.clone(), m) for f, m in self._groups]
+        views = self._make_views(groups)
+        return {n: views[n] for n in self._order}
+
+
 def _snapshot_raw(raw):
-    """Copies of the passthrough entries (int64 BatchNorm counters, ...) taken now, batched per
-    (dtype, device) into one copy kernel instead of one per entry."""
-    out = OrderedDict()
-    groups = {}
-    for name, t in raw.items():
-        groups.setdefault((t.dtype, t.device), []).append(name)
-    for (dt, dev), names in groups.items():
-        ts = [raw[n] for n in names]
-        if dev.type != "cuda" or len(ts) == 1 or any(t.numel() == 0 for t in ts):  # CPU: a clone is cheaper
-            for n, t in zip(names, ts):
-                out[n] = t.clone()
-            continue
-        flat = torch.cat([t.reshape(-1) for t in ts])
-        o = 0
-        for n, t in zip(names, ts):
-            out[n] = flat[o:o + t.numel()].view(t.shape)
-            o += t.numel()
-    return OrderedDict((n, out[n]) for n in raw)
+    """Copies of the passthrough entries taken now (RawState: one copy kernel per dtype / device)."""
+    return RawState.snapshot(list(raw.items()))
 
 
 def flatten_state(state, device=None):
@@ -304,7 +368,8 @@ class CompressedUpdate:
         h = self.header
         vb = 4 if h["bits"] == RAW_BITS else 1
         ib = 0 if h["ratio"] >= 1.0 else 4  # ratio 1: indices implied, not shipped (wire.py "dense")
-        raw_b = sum(t.numel() * t.element_size() for t in self.raw.values())
+        raw_b = self.raw.nbytes if isinstance(self.raw, RawState) else \
+            sum(t.numel() * t.element_size() for t in self.raw.values())
         return 8 * h["n_segments"] + (ib + vb) * h["total_k"] + raw_b
 
     def parameters(self):
@@ -372,6 +437,7 @@ class CompressedUpdate:
                 buf = bytearray(rawb[e["off"]:e["off"] + e["nbytes"]])
                 t = torch.frombuffer(buf, dtype=dt) if buf else torch.empty(0, dtype=dt)
                 raw[e["name"]] = t.reshape(e["shape"]).clone()
+        raw = RawState.snapshot(list(raw.items()))
         enc = Encoded(torch.from_numpy(idx.copy()), torch.from_numpy(vals.copy()),
                       torch.from_numpy(mn.copy()), torch.from_numpy(scale.copy()))
         return cls(h, enc, raw, blob=bytes(blob))
@@ -388,7 +454,8 @@ class CompressedUpdate:
         """Dense fp32 (+ raw) bytes of the update / its payload bytes."""
         h = self.header
         dense = 4 * sum(e["n"] for e in h["entries"] if e["kind"] == "seg")
-        dense += sum(t.numel() * t.element_size() for t in self.raw.values())
+        dense += self.raw.nbytes if isinstance(self.raw, RawState) else \
+            sum(t.numel() * t.element_size() for t in self.raw.values())
         return dense / max(1, self.nbytes)
 
     def __repr__(self):
@@ -631,10 +698,12 @@ class UpdateCodec:
         if D.sizes:
             for pos, v in zip(D.seg_pos, _segment_views(flat, plan.table, h["entries"])):
                 vals[pos] = v
-        raw = update.raw
-        for pos, name in D.raw:
-            t = raw[name]
-            vals[pos] = t.to(device) if device is not None else t
+        if D.raw:
+            raw = update.raw
+            raw = raw.fresh(device) if isinstance(raw, RawState) else \
+                {n: (t.to(device) if device is not None else t).clone() for n, t in raw.items()}
+            for pos, name in D.raw:
+                vals[pos] = raw[name]
         return OrderedDict(zip(D.names, vals))
 
     def decode_module(self, update, template, base=None):
