@@ -234,6 +234,26 @@ def _describe(state):
 _data_ptr, _is_contig, _get_device = torch.Tensor.data_ptr, torch.Tensor.is_contiguous, torch.Tensor.get_device
 
 
+_PACKED_HEADERS = OrderedDict()  # (layout entries id, fields, raw sizes) -> (entries, header JSON bytes)
+
+
+def _to_host(*ts):
+    """numpy copies of tensors, with ONE device-to-host transfer when they live on a GPU."""
+    if not ts or ts[0].device.type == "cpu":
+        return [t.numpy() for t in ts]
+    parts = [t.contiguous().view(torch.uint8).reshape(-1) for t in ts]
+    host = torch.cat(parts).cpu().numpy()
+    out, o = [], 0
+    for t, p in zip(ts, parts):
+        n = p.numel()
+        out.append(host[o:o + n].view(_NP_DTYPES[t.dtype]))
+        o += n
+    return out
+
+
+_NP_DTYPES = {torch.float32: np.float32, torch.int32: np.int32, torch.uint8: np.uint8, torch.int64: np.int64}
+
+
 class RawState(Mapping):
     """The passthrough (non-fp32) entries of an update — BatchNorm's int64 num_batches_tracked and the like —
     held as ONE flat tensor per (dtype, device) with the entries' names and shapes, in state order. Taking
@@ -291,6 +311,43 @@ class RawState(Mapping):
     @property
     def nbytes(self):
         return sum(f.numel() * f.element_size() for f, _ in self._groups)
+
+    @classmethod
+    def from_entries(cls, entries, rawb):
+        """From a blob's raw section: entries with "dtype", "shape", "off", "nbytes" (in state order). Runs of
+        same-dtype entries stored back to back become one tensor (one copy of the bytes)."""
+        groups, order, run = [], [], []
+
+        def flush():
+            if run:
+                dt = getattr(torch, run[0]["dtype"])
+                lo, hi = run[0]["off"], run[-1]["off"] + run[-1]["nbytes"]
+                buf = bytearray(rawb[lo:hi])
+                flat = torch.frombuffer(buf, dtype=dt) if buf else torch.empty(0, dtype=dt)
+                members = [(e["name"], tuple(e["shape"]), int(np.prod(e["shape"], dtype=np.int64))) for e in run]
+                if sum(m for _, _, m in members) != flat.numel():
+                    raise ValueError("COALAQ1: raw entry sizes inconsistent with their shapes")
+                groups.append((flat, members))
+                run.clear()
+        for e in entries:
+            if run and (e["dtype"] != run[-1]["dtype"] or e["off"] != run[-1]["off"] + run[-1]["nbytes"]):
+                flush()
+            run.append(e)
+            order.append(e["name"])
+        flush()
+        return cls(groups, order)
+
+    def entry_bytes(self):
+        """{name: little-endian bytes} with one device-to-host copy per group."""
+        out = {}
+        for flat, members in self._groups:
+            b = flat.detach().cpu().contiguous().view(torch.uint8).numpy().tobytes()
+            per = flat.element_size()
+            o = 0
+            for n, _, m in members:
+                out[n] = b[o:o + m * per]
+                o += m * per
+        return {n: out[n] for n in self._order}
 
     def fresh(self, device=None):
         """{name: tensor} with storage of its own (one copy per group, onto `device` if given): what a
@@ -355,7 +412,7 @@ class CompressedUpdate:
         # The encoded payload is immutable after encode: a deep copy shares it (and the packed blob)
         # instead of a D2H + pack + unpack round trip through __getstate__/__setstate__.
         other = CompressedUpdate.__new__(CompressedUpdate)
-        other.header = copy.deepcopy(self.header, memo)
+        other.header = dict(self.header)  # (its "entries" list is shared and never mutated)
         other.encoded = self.encoded
         other.raw = self.raw
         other._blob = self._blob
@@ -385,21 +442,36 @@ class CompressedUpdate:
 
     def _pack(self):
         h = dict(self.header)
-        raw_entries, chunks, pos = [], [], 0
-        for e in h["entries"]:
-            if e["kind"] == "raw":
-                b = self.raw[e["name"]].cpu().contiguous().reshape(-1).view(torch.uint8).numpy().tobytes() \
-                    if self.raw[e["name"]].numel() else b""
-                e = dict(e, off=pos, nbytes=len(b))
-                chunks.append(b)
-                pos += len(b)
-            raw_entries.append(e)
-        h["entries"] = raw_entries
-        if h["ratio"] >= 1.0:
-            h["dense"] = True
+        raw = self.raw
+        rawb = raw.entry_bytes() if isinstance(raw, RawState) else {
+            n: (t.cpu().contiguous().reshape(-1).view(torch.uint8).numpy().tobytes() if t.numel() else b"")
+            for n, t in raw.items()}
+        # the header (with each raw entry's blob offset) depends on the layout and the raw byte counts only
+        sizes = tuple(len(rawb[n]) for n in rawb)
+        key = (id(h["entries"]), h["ratio"], h["bits"], h["mode"], h["n_segments"], h.get("total_k"), sizes)
+        hit = _PACKED_HEADERS.get(key)
+        if hit is not None and hit[0] is h["entries"]:
+            hjson = hit[1]
+        else:
+            raw_entries, pos = [], 0
+            for e in h["entries"]:
+                if e["kind"] == "raw":
+                    nb = len(rawb[e["name"]])
+                    e = dict(e, off=pos, nbytes=nb)
+                    pos += nb
+                raw_entries.append(e)
+            h["entries"] = raw_entries
+            if h["ratio"] >= 1.0:
+                h["dense"] = True
+            hjson = wire.encode_header(h)
+            with _LAYOUTS_LOCK:
+                _PACKED_HEADERS[key] = (self.header["entries"], hjson)
+                while len(_PACKED_HEADERS) > 16:
+                    _PACKED_HEADERS.popitem(last=False)
         enc = self.encoded
-        return wire.pack(h, enc.mn.cpu().numpy(), enc.scale.cpu().numpy(), enc.idx.cpu().numpy(),
-                         enc.vals.cpu().numpy(), b"".join(chunks))
+        arrs = _to_host(enc.mn, enc.scale, enc.idx, enc.vals)
+        return wire.pack({"dense": h["ratio"] >= 1.0}, *arrs, b"".join(rawb[e["name"]] for e in h["entries"]
+                                                                        if e["kind"] == "raw"), header_json=hjson)
 
     def encoded_to(self, device, staging=None):
         """The encoded buffers on `device`. An unpickled update (the server side of a remote upload,
@@ -411,7 +483,7 @@ class CompressedUpdate:
         if (staging is None or device.type != "cuda" or blob is None or self.header.get("dense")
                 or self.encoded.idx.device == device):
             return self.encoded.to(device, non_blocking=True)
-        _, sec = wire.sections(blob)
+        _, sec = wire.sections(blob, self.header)
         lo = sec["mn"][0]
         hi = sec["vals"][0] + sec["vals"][1]
         stage = staging(hi - lo)
@@ -430,14 +502,7 @@ class CompressedUpdate:
     def from_bytes(cls, blob):
         h, mn, scale, idx, vals, rawb = wire.unpack(blob)
         validate(h, idx)
-        raw = OrderedDict()
-        for e in h["entries"]:
-            if e["kind"] == "raw":
-                dt = getattr(torch, e["dtype"])
-                buf = bytearray(rawb[e["off"]:e["off"] + e["nbytes"]])
-                t = torch.frombuffer(buf, dtype=dt) if buf else torch.empty(0, dtype=dt)
-                raw[e["name"]] = t.reshape(e["shape"]).clone()
-        raw = RawState.snapshot(list(raw.items()))
+        raw = RawState.from_entries([e for e in h["entries"] if e["kind"] == "raw"], rawb)
         enc = Encoded(torch.from_numpy(idx.copy()), torch.from_numpy(vals.copy()),
                       torch.from_numpy(mn.copy()), torch.from_numpy(scale.copy()))
         return cls(h, enc, raw, blob=bytes(blob))
@@ -464,12 +529,38 @@ class CompressedUpdate:
                 f"segments={h['n_segments']}, kept={h['total_k']}, bytes={self.nbytes})")
 
 
+_VALIDATED = OrderedDict()  # (id(entries), ratio, n_segments, total_k) -> (entries, ns_rep, first) of a checked layout
+
+
 def validate(header, idx):
     """Check an (untrusted) blob's index lists: per fp32 segment, k = k_for(n, ratio) entries, strictly
     increasing, inside [0, n). The decode kernels are bounds-safe anyway; this turns a corrupt upload
-    into an error instead of a silently wrong model."""
+    into an error instead of a silently wrong model. The header's structure is checked once per layout
+    (headers of one layout share their entries list: wire._parse_header); the indices every call."""
     if header.get("bits") not in VALID_BITS or header.get("mode") not in MODES:
         raise ValueError("COALAQ1: bad bits/mode")
+    entries = header["entries"]
+    key = (id(entries), float(header["ratio"]), int(header["n_segments"]), int(header["total_k"]))
+    hit = _VALIDATED.get(key)
+    if hit is None or hit[0] is not entries:
+        hit = (entries,) + _validate_layout(header)
+        with _LAYOUTS_LOCK:
+            _VALIDATED[key] = hit
+            while len(_VALIDATED) > 32:
+                _VALIDATED.popitem(last=False)
+    _, ns_rep, first = hit
+    if idx.size != int(header["total_k"]):
+        raise ValueError("COALAQ1: kept-entry count mismatch")
+    if ns_rep is None:
+        return
+    if idx.size and (int(idx.min()) < 0 or np.any(idx >= ns_rep)):
+        raise ValueError("COALAQ1: index out of range")
+    d = np.diff(idx, prepend=np.int32(-1))
+    if np.any((d <= 0) & ~first):
+        raise ValueError("COALAQ1: indices not strictly increasing")
+
+
+def _validate_layout(header):
     segs = [e for e in header["entries"] if e["kind"] == "seg"]
     if len(segs) != int(header["n_segments"]):
         raise ValueError("COALAQ1: segment count mismatch")
@@ -481,21 +572,16 @@ def validate(header, idx):
                 int(e["off"]) != table.offsets[i]:
             raise ValueError(f"COALAQ1: segment entry {e.get('name')!r} has inconsistent seg/n/off/shape")
     ks = np.array([k_for(e["n"], header["ratio"]) for e in segs], dtype=np.int64)
-    if int(ks.sum()) != int(header["total_k"]) or idx.size != int(header["total_k"]):
+    if int(ks.sum()) != int(header["total_k"]):
         raise ValueError("COALAQ1: kept-entry count mismatch")
     if not ks.size:
-        return
-    ns = np.array([e["n"] for e in segs], dtype=np.int64)
-    seg_of = np.repeat(np.arange(ks.size), ks)
-    i64 = idx.astype(np.int64)
-    if np.any(i64 < 0) or np.any(i64 >= ns[seg_of]):
-        raise ValueError("COALAQ1: index out of range")
-    first = np.zeros(idx.size, dtype=bool)
+        return None, None
+    ns = np.array([e["n"] for e in segs], dtype=np.int32)
+    ns_rep = np.repeat(ns, ks)  # each entry's segment size
+    first = np.zeros(int(ks.sum()), dtype=bool)  # each segment's first entry (no predecessor to compare)
     first[np.cumsum(ks)[:-1][ks[1:] > 0] if ks.size > 1 else []] = True
     first[0] = True
-    d = np.diff(i64, prepend=-1)
-    if np.any((d <= 0) & ~first):
-        raise ValueError("COALAQ1: indices not strictly increasing")
+    return ns_rep, first
 
 
 class UpdateCodec:

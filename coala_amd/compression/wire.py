@@ -20,6 +20,8 @@ Layout (little-endian):
 """
 import json
 import struct
+import threading
+from collections import OrderedDict
 
 import numpy as np
 
@@ -39,11 +41,12 @@ def dense_idx(header):
     return np.concatenate([np.arange(n, dtype=np.int32) for n in ns])
 
 
-def pack(header, mn, scale, idx, vals, raw):
-    """numpy arrays + raw bytes -> blob (bytes). A "dense" header drops idx (it is implied)."""
+def pack(header, mn, scale, idx, vals, raw, header_json=None):
+    """numpy arrays + raw bytes -> blob (bytes). A "dense" header drops idx (it is implied). header_json: the
+    header's JSON encoding, if the caller has it already."""
     if header.get("dense"):
         idx = np.zeros(0, dtype=np.int32)
-    h = json.dumps(header, separators=(",", ":"), sort_keys=True).encode()
+    h = header_json if header_json is not None else encode_header(header)
     parts = [MAGIC, struct.pack("<II", VERSION, len(h)), h]
     size = 16 + len(h)
     for arr in (np.ascontiguousarray(mn, "<f4"), np.ascontiguousarray(scale, "<f4"),
@@ -59,14 +62,40 @@ def pack(header, mn, scale, idx, vals, raw):
     return b"".join(parts)
 
 
-def sections(blob):
+_HEADERS = OrderedDict()  # header JSON bytes -> parsed header (the same layout arrives round after round)
+_HEADERS_LOCK = threading.Lock()
+
+
+def _parse_header(mv, hl):
+    """The blob's JSON header, parsed once per distinct header text (LRU of 32): a SHALLOW copy of the
+    cached dict is returned — its "entries" list is shared and must never be mutated (nothing does)."""
+    key = bytes(mv[16:16 + hl])
+    with _HEADERS_LOCK:
+        h = _HEADERS.get(key)
+        if h is not None:
+            _HEADERS.move_to_end(key)
+    if h is None:
+        h = json.loads(key.decode())
+        with _HEADERS_LOCK:
+            _HEADERS[key] = h
+            while len(_HEADERS) > 32:
+                _HEADERS.popitem(last=False)
+    return dict(h)
+
+
+def encode_header(header):
+    return json.dumps(header, separators=(",", ":"), sort_keys=True).encode()
+
+
+def sections(blob, header=None):
     """(header, {name: (byte offset, byte count)}) of the mn / scale / idx / vals sections in `blob`, which
     lie back to back (each 16-byte aligned) — one host-to-device copy moves all of them."""
     mv = memoryview(blob)
     if bytes(mv[:8]) != MAGIC:
         raise ValueError("not a COALAQ1 blob (bad magic)")
     ver, hl = struct.unpack_from("<II", mv, 8)
-    header = json.loads(bytes(mv[16:16 + hl]).decode())
+    if header is None:
+        header = _parse_header(mv, hl)
     T, K = int(header["n_segments"]), int(header["total_k"])
     vsz = 4 if int(header["bits"]) == 32 else 1
     pos = 16 + hl
@@ -86,7 +115,7 @@ def unpack(blob):
     ver, hl = struct.unpack_from("<II", mv, 8)
     if ver != VERSION:
         raise ValueError(f"unsupported COALAQ1 version {ver}")
-    header = json.loads(bytes(mv[16:16 + hl]).decode())
+    header = _parse_header(mv, hl)
     T, K = int(header["n_segments"]), int(header["total_k"])
     vdt = np.dtype("<f4") if int(header["bits"]) == 32 else np.dtype("u1")
     pos = 16 + hl

@@ -7,6 +7,9 @@ all on one stream, timed with the host clock around K steps after warmup. Report
 update (4N per client per step), next to the device-resident rate of the same batch.
 
     python tools/host_rate.py [--clients 1 16] [--steps 10]
+
+Then the hooks' own bytes-to-bytes path (run_hooks): compression() -> pickle -> unpickle -> decompression()
+-> D2H of the decoded state.
 """
 import argparse
 import json
@@ -71,6 +74,66 @@ def run(clients, steps, warmup, layout, ratio, bits):
     return res
 
 
+def run_hooks(steps, warmup, layout, ratio, bits, mode="delta"):
+    """The hooks' own path, bytes to bytes: client compression() of the trained module on the
+    GPU (UpdateCodec.encode_module, in place) -> pickle.dumps of the carrier (the D2H of the payload + the
+    COALAQ1 pack, what codec.marshal does at coala/client/base.py:363) -> pickle.loads on the server
+    (coala/server/service.py:83) -> decompression(model) (UpdateCodec.decode_module: one pinned H2D of the
+    payload + decode into a new module on w_global) -> D2H of the decoded dense state (one copy of its flat
+    storage). Per client, serial, wall clock."""
+    import pickle
+
+    import torch
+
+    from coala_amd.compression import UpdateCodec
+    from coala_amd.layouts import build_module
+
+    dev = torch.device("cuda", 0)
+    m = build_module(layout, seed=1, device=dev)
+    g = build_module(layout, seed=2, device=dev)
+    codec = UpdateCodec(ratio, bits, mode)
+    base = codec.snapshot(g) if mode == "delta" else None
+    N = sum(p.numel() for p in m.state_dict().values() if p.dtype == torch.float32)
+    host = None
+    parts = {"encode_module": 0.0, "pickle_dumps": 0.0, "pickle_loads": 0.0, "decode_module": 0.0, "d2h_state": 0.0}
+
+    def step(acc):
+        nonlocal host
+        t = [time.perf_counter()]
+        up = codec.encode_module(m, base=base)
+        t.append(time.perf_counter())
+        blob = pickle.dumps(up)
+        t.append(time.perf_counter())
+        up2 = pickle.loads(blob)
+        t.append(time.perf_counter())
+        mod = codec.decode_module(up2, g, base=base)
+        torch.cuda.synchronize()
+        t.append(time.perf_counter())
+        w = next(iter(mod.parameters()))
+        st = w.untyped_storage()
+        if host is None or host.numel() < st.nbytes():
+            host = torch.empty(st.nbytes(), dtype=torch.uint8, pin_memory=True)
+        src = torch.empty(0, dtype=torch.uint8, device=dev).set_(st)
+        host[:st.nbytes()].copy_(src)
+        t.append(time.perf_counter())
+        if acc:
+            for k, a, b in zip(parts, t[:-1], t[1:]):
+                parts[k] += b - a
+        return len(blob)
+
+    for _ in range(warmup):
+        step(False)
+    nb = 0
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        nb = step(True)
+    el = time.perf_counter() - t0
+    return {"path": "hooks, bytes to bytes", "layout": layout, "mode": mode, "ratio": ratio, "bits": bits,
+            "GBps": round(4.0 * N * steps / el / 1e9, 2), "ms_per_client": round(el / steps * 1e3, 4),
+            "blob_bytes": nb, "update_bytes": 4 * N,
+            "ms_parts": {k: round(v / steps * 1e3, 4) for k, v in parts.items()}}
+
+
 def main():
     p = argparse.ArgumentParser()
     p.add_argument("--clients", type=int, nargs="+", default=[1, 16])
@@ -82,6 +145,8 @@ def main():
     a = p.parse_args()
     for c in a.clients:
         print(json.dumps(run(c, a.steps, a.warmup, a.layout, a.ratio, a.bits)), flush=True)
+    for mode in ("delta", "weights"):
+        print(json.dumps(run_hooks(max(a.steps, 20), a.warmup, a.layout, a.ratio, a.bits, mode)), flush=True)
 
 
 if __name__ == "__main__":

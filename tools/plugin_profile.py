@@ -60,8 +60,32 @@ def main(steps=50):
             fn()
         torch.cuda.synchronize()
         print(f"{name:48s} {med(fn, steps, sync):.4f} ms (median of {steps})", flush=True)
+    import gc
+    import pickle
+    blob = pickle.dumps(up)
+    up_r = pickle.loads(blob)
+    for name, fn in (("pickle.dumps (fresh pack)", lambda: pickle.dumps(C.CompressedUpdate(up.header, up.encoded, up.raw))),
+                     ("pickle.loads", lambda: pickle.loads(blob)),
+                     ("decode_module of the unpickled update", lambda: codec.decode_module(up_r, g, base=base))):
+        for _ in range(3):
+            fn()
+        torch.cuda.synchronize()
+        print(f"{name:48s} {med(fn, steps):.4f} ms (median of {steps})", flush=True)
+    for gc_on in (True, False):  # the mean vs the median: Python's cyclic GC passes triggered by allocations
+        (gc.enable if gc_on else gc.disable)()
+        ts = []
+        for _ in range(200):
+            t0 = time.perf_counter()
+            codec.decode_module(up, g, base=base)
+            torch.cuda.synchronize()
+            ts.append((time.perf_counter() - t0) * 1e3)
+        ts.sort()
+        print(f"decode_module x200, gc {'on ' if gc_on else 'off'}: median {ts[100]:.3f} mean {sum(ts) / 200:.3f} "
+              f"max {ts[-1]:.3f} ms", flush=True)
+    gc.enable()
     for name, fn in (("encode_module", lambda: codec.encode_module(m, base=base)),
-                     ("decode_module", lambda: codec.decode_module(up, g, base=base))):
+                     ("decode_module", lambda: codec.decode_module(up, g, base=base)),
+                     ("decode_module (unpickled)", lambda: codec.decode_module(up_r, g, base=base))):
         pr = cProfile.Profile()
         pr.enable()
         for _ in range(steps):
