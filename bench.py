@@ -90,6 +90,9 @@ def parse():
                    help="at most this many timed steps captured in one graph (--graph; whole input rotations, the "
                         "count that needs the fewest launches): 1 / 4 / 10 steps per launch measured 0.0845 / 0.0803 / "
                         "0.0796 ms per single step (eager 0.080-0.083)")
+    p.add_argument("--fill-ahead", choices=["auto", "on", "off"], default="auto",
+                   help="one-update configs: write the decode's background on a side stream beside the encode's "
+                        "select chain (SplitPipeline.roundtrip fill_ahead); auto = in captured graphs")
     p.add_argument("--cpu-seconds", type=float, default=8.0, help="CPU baseline time budget per leg")
     p.add_argument("--no-cpu-baseline", action="store_true")
     return p.parse_args()
@@ -278,16 +281,18 @@ def setup_workload(cfg, a, dev, rank, headline):
         slots.append((p, [(p.empty_encoded(), p.empty_flat()) for _ in range(rot)]))
     torch.cuda.synchronize()
     return {"cfg": cfg, "headline": headline, "table": t, "desc": desc, "flats": flats, "base": base, "rot": rot,
-            "slots": slots, "split": slots[0][0].n_parts, "graphs": None, "graph_error": None}
+            "slots": slots, "split": slots[0][0].n_parts, "graphs": None, "graph_error": None,
+            "fill_ahead": a.fill_ahead == "on" or (a.fill_ahead == "auto" and use_graph(cfg, a))}
 
 
 def _step(W, i, joined, enc_events=None, dec_events=None):
-    """Step i: slot i % inflight, buffer set (i // inflight) % rot."""
+    """Step i: slot i % inflight, buffer set (i // inflight) % rot. (Steps carrying timing events take the
+    plain roundtrip: its kernel boundaries are the ones the events bracket.)"""
     p, bufs = W["slots"][i % len(W["slots"])]
     r = (i // len(W["slots"])) % W["rot"]
     enc, out = bufs[r]
     p.roundtrip(W["flats"][r], base=W["base"], enc=enc, out=out, enc_events=enc_events, dec_events=dec_events,
-                joined=joined)
+                joined=joined, fill_ahead=W["fill_ahead"] and enc_events is None)
 
 
 def warm_workload(W, a):
@@ -444,6 +449,7 @@ def time_workload(W, a, dev, world):
         "stages_ms": {k: round(v, 4) for k, v in stages.items()},
         "sample_fallbacks": W.get("fallbacks", 0),
         "graph": W["graph_error"] or (graphs is not None and f"{W['gk']} step(s) per graph launch"),
+        "fill_ahead": W["fill_ahead"] and all(p.n_parts == 1 for p in pipes),
     }
     if headline:
         traffic, src = pmc_traffic(dom, W["cfg"], a, split)
@@ -628,7 +634,7 @@ def main():
             "graph": head["graph"],
             "configs": {k: {f: v[f] for f in ("value", "ms_per_step", "step_roofline", "roofline", "stages_ms", "desc",
                                               "elements_per_gpu", "segments_per_gpu", "split", "inflight", "rotation",
-                                              "graph", "sample_fallbacks")}
+                                              "graph", "fill_ahead", "sample_fallbacks")}
                         for k, v in results.items()},
         }
         if plugin is not None:

@@ -75,7 +75,8 @@ _lib = None
 
 
 def lib_path():
-    return _build.LIB
+    """The in-tree library; COALAC_LIB names another build of the same source (A/B variants under tools/)."""
+    return os.environ.get("COALAC_LIB") or _build.LIB
 
 
 def load(build_if_missing=True):
@@ -87,7 +88,8 @@ def load(build_if_missing=True):
         if _lib is not None:
             return _lib
         path = lib_path()
-        if not os.path.exists(path) or (build_if_missing and _build.stale() and _can_build()):
+        if not os.environ.get("COALAC_LIB") and (
+                not os.path.exists(path) or (build_if_missing and _build.stale() and _can_build())):
             if not build_if_missing:
                 raise CodecError(f"HIP codec library not found at {path}; run __graft_entry__.build()")
             _build.build()

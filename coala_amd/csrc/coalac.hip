@@ -2120,6 +2120,107 @@ __global__ __launch_bounds__(BLOCK, DECODE_WPE) void k_decode(Params P) {
   }
 }
 
+// k_decode_lds (batches, DECODE_LDS): the same output as k_decode, with the kept values placed through a
+// per-wave LDS tile instead of the register merge (a wave-uniform walk over every kept entry: ~10 VALU per
+// entry, ~450 per unit, as much issue time per unit as its 16 stores). A unit is written as 4 quarters of 4
+// rows (1,024 elements): the quarter's kept values are scattered into the zeroed 4 KiB tile (one ds_write per
+// 64 entries), its 4 rows read back (ds_read_b128, + base in delta mode) and stored, and the same slots zeroed
+// again. Entries outside the unit (an untrusted list) never match a quarter and are dropped.
+#ifndef DECODE_LDS
+#define DECODE_LDS 1
+#endif
+#ifndef DECODE_LDS_DPW
+#define DECODE_LDS_DPW 2u
+#endif
+#ifndef DECODE_LDS_WPE
+#define DECODE_LDS_WPE 5
+#endif
+constexpr uint32_t QROWS = 4;  // rows per tile quarter
+
+template <bool RAW, bool HASBASE>
+__global__ __launch_bounds__(BLOCK, DECODE_LDS_WPE) void k_decode_lds(Params P) {
+  constexpr uint32_t DPW = DECODE_LDS_DPW;
+  __shared__ float4 qtile[WAVES][QROWS * 64];
+  const uint32_t lane = lane_id(), wv = threadIdx.x >> 6;
+  const uint32_t u0 = ((DECODE_XCD ? xcd_block(blockIdx.x) : blockIdx.x) * WAVES + wv) * DPW;
+  if (u0 >= P.n_units) return;
+  float4* tile = qtile[wv];
+  float* tf = reinterpret_cast<float*>(tile);
+#pragma unroll
+  for (uint32_t it = 0; it < QROWS; ++it) tile[it * 64 + lane] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+  UnitDev U[DPW];
+  uint32_t lo[DPW], hi[DPW];
+#pragma unroll
+  for (uint32_t r = 0; r < DPW; ++r) {
+    const uint32_t uu = min(u0 + r, P.n_units - 1);
+    U[r] = P.units[uu];
+    lo[r] = P.ustart[uu];
+    hi[r] = P.ustart[uu + 1];  // ustart has n_units + 1 entries
+  }
+  uint32_t pos[DPW];
+  float val[DPW];
+#pragma unroll
+  for (uint32_t r = 0; r < DPW; ++r) {
+    // clamp: the bounds come from a possibly untrusted idx list (k >= 1 for every unit)
+    lo[r] = min(lo[r], U[r].k);
+    hi[r] = max(lo[r], min(U[r].last ? U[r].k : hi[r], U[r].k));
+    const uint64_t e = U[r].out_off + min(lo[r] + lane, U[r].k - 1);
+    const uint32_t q = load_code<RAW>(P, e);
+    pos[r] = (uint32_t)P.cidx[e] - U[r].start;
+    val[r] = code_value<RAW>(q, RAW ? 0.0f : P.cmn[U[r].seg], RAW ? 0.0f : P.cscale[U[r].seg]);
+  }
+  wave_fence();
+#pragma unroll
+  for (uint32_t r = 0; r < DPW; ++r) {
+    if (u0 + r >= P.n_units) break;
+    const uint32_t len = U[r].len, cnt = hi[r] - lo[r];
+    const __amdgpu_buffer_rsrc_t rout = unit_rsrc(P.out + U[r].off, len);
+    const __amdgpu_buffer_rsrc_t rb = unit_rsrc(HASBASE ? P.base + U[r].off : P.out + U[r].off, len);
+    const float mn = RAW ? 0.0f : P.cmn[U[r].seg], sc = RAW ? 0.0f : P.cscale[U[r].seg];
+    constexpr int SAUX = STORE_AUX;
+#pragma unroll
+    for (uint32_t qq = 0; qq < UNIT_IT / QROWS; ++qq) {
+      float4 bq[QROWS];
+      if (HASBASE) {  // issue the quarter's base loads before the LDS round trip
+#pragma unroll
+        for (uint32_t it = 0; it < QROWS; ++it)
+          bq[it] = unit_load_x4<false>(rb, rb, ((qq * QROWS + it) * 64 + lane) * 16);
+      }
+      // scatter: the first 64 entries are in registers; more (ratio >~ 1.5 %) are loaded chunk by chunk
+      if (lane < min(cnt, 64u) && (pos[r] >> 10) == qq) tf[pos[r] & 1023u] = val[r];
+      for (uint32_t e0 = lo[r] + 64; e0 < hi[r]; e0 += 64) {
+        const uint64_t e = U[r].out_off + min(e0 + lane, hi[r] - 1);
+        const uint32_t p2 = (uint32_t)P.cidx[e] - U[r].start;
+        if (e0 + lane < hi[r] && (p2 >> 10) == qq) tf[p2 & 1023u] = code_value<RAW>(load_code<RAW>(P, e), mn, sc);
+      }
+      wave_fence();
+      float4 o[QROWS];
+#pragma unroll
+      for (uint32_t it = 0; it < QROWS; ++it) {
+        const float4 d = tile[it * 64 + lane];
+        o[it] = HASBASE ? make_float4(bq[it].x + d.x, bq[it].y + d.y, bq[it].z + d.z, bq[it].w + d.w) : d;
+      }
+      wave_fence();
+      // zero what was written (the same slots), for the next quarter / unit
+      if (lane < min(cnt, 64u) && (pos[r] >> 10) == qq) tf[pos[r] & 1023u] = 0.0f;
+      for (uint32_t e0 = lo[r] + 64; e0 < hi[r]; e0 += 64) {
+        const uint64_t e = U[r].out_off + min(e0 + lane, hi[r] - 1);
+        const uint32_t p2 = (uint32_t)P.cidx[e] - U[r].start;
+        if (e0 + lane < hi[r] && (p2 >> 10) == qq) tf[p2 & 1023u] = 0.0f;
+      }
+      if ((len & 3u) == 0) {  // wave-uniform: one float4 buffer store per slot
+#pragma unroll
+        for (uint32_t it = 0; it < QROWS; ++it) unit_store_x4<SAUX>(rout, ((qq * QROWS + it) * 64 + lane) * 16, o[it]);
+      } else {  // a segment's last unit with n % 4 != 0: dword stores (range-checked per dword)
+#pragma unroll
+        for (uint32_t it = 0; it < QROWS; ++it)
+          unit_store_x1x4<SAUX>(rout, ((qq * QROWS + it) * 64 + lane) * 16, o[it]);
+      }
+      wave_fence();
+    }
+  }
+}
+
 // Latency-bound plans, DECODE_SCATTER: the background first (k_fill: every unit's 0 / base + 0.0f, no entry
 // lookup, so the write stream starts at once), then the kept values on top (k_scatter: one thread per entry,
 // per k_bounds chunk; bounds-checked like k_decode). Stream order puts every kept value after the fill.
@@ -2612,12 +2713,14 @@ int launch_encode(const Params& P, coalac_plan_t plan, hipStream_t st, const coa
   const unsigned all = COALAC_STAGE_SAMPLE | COALAC_STAGE_SCAN | COALAC_STAGE_SELECT | COALAC_STAGE_SMALL;
   const unsigned stages = (sc && (sc->stages & all)) ? (sc->stages & all) : all;
   // whole encode: small segments forked beside k_sample / k_scan (big batches) or inside k_scan;
-  // split encode: only in stage SMALL (k_small)
+  // a call holding SAMPLE + SCAN + SMALL (the encode's front, SELECT maybe in a later call) places them the
+  // same way; any other split: k_small in stage SMALL
   const bool split = stages != all;
+  const unsigned front = COALAC_STAGE_SAMPLE | COALAC_STAGE_SCAN | COALAC_STAGE_SMALL;
   const bool fork = plan->n_small && !split && plan->n_lunits >= FORK_MIN_LUNITS && !(P.flags & COALAC_FLAG_NO_FORK);
-  // otherwise (whole encode) the small segments run beside the samplers in k_presel, or (latency-bound
-  // plans, SCAN_SMALL_LAT) in k_scan's first blocks, beside the streaming waves: k_sample alone ahead of it
-  const bool presel = !split && !fork && plan->n_small;
+  // otherwise the small segments run beside the samplers in k_presel, or (latency-bound plans,
+  // SCAN_SMALL_LAT) in k_scan's first blocks, beside the streaming waves: k_sample alone ahead of it
+  const bool presel = (stages & front) == front && !fork && plan->n_small;
   const bool small_in_scan = presel && SCAN_SMALL_LAT && plan->n_lunits <= LATENCY_PLAN_UNITS;
   Params Q = P;
   Q.scan_small = 0u;
@@ -2649,7 +2752,7 @@ int launch_encode(const Params& P, coalac_plan_t plan, hipStream_t st, const coa
     hipLaunchKernelGGL((k_presel<DELTA, RAW>), dim3(plan->n_large + plan->n_small), dim3(BLOCK), 0, st, P);
   else if ((stages & COALAC_STAGE_SAMPLE) && plan->n_large)
     hipLaunchKernelGGL((k_sample<DELTA, RAW>), dim3(plan->n_large), dim3(BLOCK), 0, st, P);
-  if (split && (stages & COALAC_STAGE_SMALL) && plan->n_small)
+  if ((stages & COALAC_STAGE_SMALL) && plan->n_small && !presel && !fork)
     hipLaunchKernelGGL((k_small<DELTA, RAW>), dim3(plan->n_small), dim3(BLOCK), 0, st, P);
   ENC_BOUNDARY(1);
   if (small_in_scan) {
@@ -3019,6 +3122,7 @@ int coalac_decode_sched(coalac_plan_t plan, const int32_t* d_idx, const void* d_
   const uint32_t upb = WAVES * (hb ? decode_dpw<true, false>()
                                    : search ? decode_dpw<false, true>() : decode_dpw<false, false>());  // units per block
   const uint32_t g = (plan->n_units + upb - 1) / upb;
+  const uint32_t glds = (plan->n_units + WAVES * DECODE_LDS_DPW - 1) / (WAVES * DECODE_LDS_DPW);
   const coalac_sched_t* sc = sched;
   auto B = [&](int i) { return at_boundary(stages, DEC_SPAN, 2, i) ? boundary(sc, i, st) : COALAC_OK; };
 #define DEC_BOUNDARY(i)       \
@@ -3035,6 +3139,8 @@ int coalac_decode_sched(coalac_plan_t plan, const int32_t* d_idx, const void* d_
   do {                                                                                     \
     if (search)                                                                            \
       hipLaunchKernelGGL((k_decode<R, H, true>), dim3(g), dim3(BLOCK), 0, st, P);          \
+    else if (DECODE_LDS)                                                                   \
+      hipLaunchKernelGGL((k_decode_lds<R, H>), dim3(glds), dim3(BLOCK), 0, st, P);         \
     else                                                                                   \
       hipLaunchKernelGGL((k_decode<R, H, false>), dim3(g), dim3(BLOCK), 0, st, P);         \
   } while (0)

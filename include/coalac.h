@@ -145,7 +145,7 @@ int coalac_decode_ev(coalac_plan_t plan, const int32_t* d_idx, const void* d_val
  * an earlier call enqueued BOUNDS for the same arrays on the same workspace, ordered before this one;
  * without it the call returns COALAC_EINVAL (stale bounds would mis-decode silently). The caller orders them, e.g. with the events below.
  * (A whole encode places the small segments itself: beside k_scan on the plan's side stream for big
- * batches, inside k_scan otherwise.) At every boundary an enqueued stage starts or ends at, the call first makes
+ * batches, inside k_scan otherwise; so does a call holding SAMPLE + SCAN + SMALL, the encode's front.) At every boundary an enqueued stage starts or ends at, the call first makes
  * `stream` wait for wait[i] (hipStreamWaitEvent; an event another stream recorded) and then records
  * record[i] (hipEventRecord). Boundaries are those of the _ev variants (encode 0..4, decode 0..2).
  * This lets a host pipeline independent batches over two streams: the HBM-streaming kernels (k_scan,

@@ -328,3 +328,41 @@ def test_split_pipeline_graph_capture_records_every_part(cuda, split):
     torch.cuda.synchronize()
     assert torch.equal(e.idx, enc.idx) and torch.equal(e.vals, enc.vals)
     assert torch.equal(d.view(torch.int32), out.view(torch.int32))
+
+
+@pytest.mark.parametrize("delta", [False, True])
+def test_fill_ahead_roundtrip_eager_and_captured(cuda, delta):
+    """fill_ahead: the decode background on a side stream beside the select chain (encode front / select as
+    separate stage calls, decode FILL then SCATTER) — eager and as a captured graph replayed on new data, the
+    result is the plain roundtrip's, bit for bit (and so the oracle's, via the plain path's tests)."""
+    t = SegmentTable(fp32_sizes("resnet50_tv"), 0.01, 1)
+    flat = synth_batch(t, cuda, client_ids=[51])
+    base = synth_batch(t, cuda, client_ids=[52]) if delta else None
+    pipe = SplitPipeline(t, 8, split=1, device=cuda)
+    enc, out = pipe.empty_encoded(), pipe.empty_flat().zero_()
+    pipe.roundtrip(flat, base=base, enc=enc, out=out, fill_ahead=True)
+    torch.cuda.synchronize()
+    plan = CodecPlan(fp32_sizes("resnet50_tv"), 0.01, 8, clients=1, device=cuda)
+
+    def ref():
+        e = plan.encode(flat, base=base)
+        d = plan.decode(e, base=base, out=torch.zeros_like(flat))
+        torch.cuda.synchronize()
+        return e, d
+    e, d = ref()
+    assert torch.equal(e.idx, enc.idx) and torch.equal(e.vals, enc.vals)
+    assert torch.equal(d.view(torch.int32), out.view(torch.int32))
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, stream=pipe.streams[0]):
+        for _ in range(2):
+            pipe.roundtrip(flat, base=base, enc=enc, out=out, joined=False, fill_ahead=True)
+    torch.cuda.synchronize()
+    flat.copy_(synth_batch(t, cuda, client_ids=[53]))
+    out.zero_()
+    torch.cuda.synchronize()
+    with torch.cuda.stream(pipe.streams[0]):
+        g.replay()
+    torch.cuda.synchronize()
+    e, d = ref()
+    assert torch.equal(e.idx, enc.idx) and torch.equal(e.vals, enc.vals)
+    assert torch.equal(d.view(torch.int32), out.view(torch.int32))
