@@ -505,6 +505,7 @@ DEV float4 load_x4(const Params& P, uint64_t off) {
 }
 
 typedef float f4v __attribute__((ext_vector_type(4)));
+typedef float f2v __attribute__((ext_vector_type(2)));
 
 // histogram shift of the sampled band [tlo, thi]: HIST_BINS bins of 2^shift keys cover it. k_scan
 // (band histogram) and k_select (bin -> key window) must agree, so both use this.
@@ -2472,20 +2473,29 @@ __global__ __launch_bounds__(BLOCK, AGG_WPE) void k_aggregate(Params P, AggArgs 
         if (p2 < hlen) tf[p2] = v2;
       }
       wave_fence();
-      const bool first = c0 + j == 0;
+      // x = base + d; acc = x * w (first client) or acc + x * w: IEEE fp32 ops in this order, on float2 pairs
+      // (v_pk_add_f32 / v_pk_mul_f32: half the VALU issue of scalar fp32); the first-client test is
+      // wave-uniform (a branch, no per-element select)
+      const f2v w2 = {w, w};
+      if (c0 + j == 0) {
 #pragma unroll
-      for (uint32_t it = 0; it < RI; ++it) {
-        const float4 d = tile[it * 64 + lane];
-        float4 x;
-        x.x = HASBASE ? b[it].x + d.x : d.x;
-        x.y = HASBASE ? b[it].y + d.y : d.y;
-        x.z = HASBASE ? b[it].z + d.z : d.z;
-        x.w = HASBASE ? b[it].w + d.w : d.w;
-        const float4 t = make_float4(x.x * w, x.y * w, x.z * w, x.w * w);
-        acc[it].x = first ? t.x : acc[it].x + t.x;
-        acc[it].y = first ? t.y : acc[it].y + t.y;
-        acc[it].z = first ? t.z : acc[it].z + t.z;
-        acc[it].w = first ? t.w : acc[it].w + t.w;
+        for (uint32_t it = 0; it < RI; ++it) {
+          const float4 d = tile[it * 64 + lane];
+          const f2v dl = {d.x, d.y}, dh = {d.z, d.w};
+          const f2v bl = {b[it].x, b[it].y}, bh = {b[it].z, b[it].w};
+          const f2v tl = (HASBASE ? bl + dl : dl) * w2, th = (HASBASE ? bh + dh : dh) * w2;
+          acc[it] = make_float4(tl.x, tl.y, th.x, th.y);
+        }
+      } else {
+#pragma unroll
+        for (uint32_t it = 0; it < RI; ++it) {
+          const float4 d = tile[it * 64 + lane];
+          const f2v dl = {d.x, d.y}, dh = {d.z, d.w};
+          const f2v bl = {b[it].x, b[it].y}, bh = {b[it].z, b[it].w};
+          const f2v al = {acc[it].x, acc[it].y}, ah = {acc[it].z, acc[it].w};
+          const f2v sl = al + (HASBASE ? bl + dl : dl) * w2, sh = ah + (HASBASE ? bh + dh : dh) * w2;
+          acc[it] = make_float4(sl.x, sl.y, sh.x, sh.y);
+        }
       }
       wave_fence();
       if (ne > 64) {

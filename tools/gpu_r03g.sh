@@ -16,3 +16,4 @@ timeout -k 10 120 python bench.py $B --config single > $O/single_fa.json
 timeout -k 10 120 python bench.py $B --config single --fill-ahead off > $O/single_nofa.json
 timeout -k 10 200 python tools/plugin_profile.py 100 > $O/plugin_profile.txt 2>&1
 timeout -k 10 200 python tools/host_rate.py --clients 1 > $O/host_rate.jsonl 2> $O/host_rate.err
+timeout -k 10 120 python tools/bench_aggregate.py > $O/aggregate.json 2>&1
