@@ -90,9 +90,10 @@ def parse():
                    help="at most this many timed steps captured in one graph (--graph; whole input rotations, the "
                         "count that needs the fewest launches): 1 / 4 / 10 steps per launch measured 0.0845 / 0.0803 / "
                         "0.0796 ms per single step (eager 0.080-0.083)")
-    p.add_argument("--fill-ahead", choices=["auto", "on", "off"], default="auto",
+    p.add_argument("--fill-ahead", choices=["on", "off"], default="off",
                    help="one-update configs: write the decode's background on a side stream beside the encode's "
-                        "select chain (SplitPipeline.roundtrip fill_ahead); auto = in captured graphs")
+                        "select chain (SplitPipeline.roundtrip fill_ahead). Off: in a captured graph it measured "
+                        "0.0922 vs 0.0786 ms per single step (the cross-stream edges cost more than the fill)")
     p.add_argument("--cpu-seconds", type=float, default=8.0, help="CPU baseline time budget per leg")
     p.add_argument("--no-cpu-baseline", action="store_true")
     return p.parse_args()
@@ -202,9 +203,11 @@ def pmc_traffic(kernel, cfg, a, split):
         return None, None
     with open(files[-1]) as f:
         d = json.load(f)
-    for name, e in sorted(d.items()):
-        if name.split("<")[0] == kernel and "FETCH_SIZE_x2_bytes" in e and "WRITE_SIZE_bytes" in e:
-            return e["FETCH_SIZE_x2_bytes"] + e["WRITE_SIZE_bytes"], os.path.relpath(files[-1], ROOT)
+    names = {"k_decode": ("k_decode_lds", "k_decode")}.get(kernel, (kernel,))  # (the batch decode kernel)
+    for want in names:
+        for name, e in sorted(d.items()):
+            if name.split("<")[0] == want and "FETCH_SIZE_x2_bytes" in e and "WRITE_SIZE_bytes" in e:
+                return e["FETCH_SIZE_x2_bytes"] + e["WRITE_SIZE_bytes"], os.path.relpath(files[-1], ROOT)
     return None, None
 
 
@@ -270,7 +273,7 @@ def setup_workload(cfg, a, dev, rank, headline):
     from coala_amd.workload import synth_batch
 
     t, ids, split, desc = build_table(cfg, a, rank, headline)
-    rot = ROTATE if cfg in ROTATE_CONFIGS and not headline else 1
+    rot = ROTATE if cfg in ROTATE_CONFIGS else 1
     flats = [synth_batch(t, dev, client_ids=[1000 * r + i for i in ids]) for r in range(rot)]
     base = synth_batch(t, dev, client_ids=[10_000 + i for i in ids]) if a.mode == "delta" else None
     split = max(1, split)
@@ -282,7 +285,7 @@ def setup_workload(cfg, a, dev, rank, headline):
     torch.cuda.synchronize()
     return {"cfg": cfg, "headline": headline, "table": t, "desc": desc, "flats": flats, "base": base, "rot": rot,
             "slots": slots, "split": slots[0][0].n_parts, "graphs": None, "graph_error": None,
-            "fill_ahead": a.fill_ahead == "on" or (a.fill_ahead == "auto" and use_graph(cfg, a))}
+            "fill_ahead": a.fill_ahead == "on"}
 
 
 def _step(W, i, joined, enc_events=None, dec_events=None):

@@ -24,9 +24,9 @@ def rows(pattern):
 
 
 def short(name):
-    if name.startswith("_Z"):  # mangled: keep the kernel's base name
-        m = re.search(r"\d(k_[a-z]+)", name)
-        return m.group(1) if m else name
+    if name.startswith("_Z"):  # mangled (<length><name>): keep the kernel's base name
+        m = re.search(r"N_\d(\d+)(k_\w+)", name)
+        return m.group(2)[:int(m.group(1))] if m else name
     for tok in ("(anonymous namespace)::", "void ", "__global__ "):
         name = name.replace(tok, "")
     return name.split("(")[0].strip()

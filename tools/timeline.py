@@ -15,8 +15,8 @@ import os
 import sys
 
 CODEC = ("k_sample", "k_presel", "k_scan", "k_small", "k_ghist", "k_pick", "k_gwin", "k_select", "k_emit", "k_bounds",
-         "k_decode", "k_aggregate", "k_fused")
-STREAMING = ("k_scan", "k_decode")
+         "k_decode", "k_decode_lds", "k_fill", "k_fillscatter", "k_scatter", "k_aggregate")
+STREAMING = ("k_scan", "k_decode", "k_decode_lds")
 
 
 def base_name(n):
