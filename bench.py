@@ -519,8 +519,23 @@ def run_plugin(a, dev, steps):
     K, T = up.header["total_k"], up.header["n_segments"]
     alg = 16 * N + 10 * K + 16 * T
     ms = res["compression_in_place_ms"] + dec_ms
+    # the fused server (codec_fused_aggregate): decompression(model) keeps the carrier, aggregate() decodes and
+    # averages a round's uploads in one coalac_aggregate — per client, compression + 1/C of that call
+    C = 16
+    ups = [codec.encode_module(m, base=base) for _ in range(C)]
+    wts = [10 + i for i in range(C)]
+    for _ in range(3):
+        codec.aggregate(ups, wts, g, base=base, mode="recip")
+    torch.cuda.synchronize()
+    agg_ms, _ = per_call(lambda: codec.aggregate(ups, wts, g, base=base, mode="recip"), max(steps, 20))
+    fused_ms = res["compression_in_place_ms"] + agg_ms / C
     return {"value": round(4.0 * N / (ms * 1e-3) / 1e9, 2), "ms_per_client": round(ms, 4),
             **res, "decompression_ms": round(dec_ms, 4), "decompression_mean_ms": round(dec_mean, 4),
+            "fused_server": {"value": round(4.0 * N / (fused_ms * 1e-3) / 1e9, 2), "ms_per_client": round(fused_ms, 4),
+                             "aggregate_ms_per_round": round(agg_ms, 4), "clients_per_round": C,
+                             "desc": "compression() + 1/C of the server's fused aggregate() of C uploads "
+                                     "(UpdateCodec.aggregate: decode + FedAvg in one kernel, new module built once "
+                                     "per round); decompression(model) passes the carrier through"},
             "timing": "median of per-call times (each call synchronised); means alongside",
             "alg_bytes_per_client": alg,
             "step_roofline": {"achieved_GBs": round(alg / (ms * 1e-3) / 1e9, 1),
