@@ -856,10 +856,14 @@ class UpdateCodec:
                 avg_mask = [e["name"] in pnames for e in h0["entries"] if e["kind"] == "seg"]
             flat = plan.aggregate(batched, weights, total=total, base=base_flat, mode=mode, avg_mask=avg_mask)
             offs = plan.table.offsets
+        raw_avg = _aggregate_raw(updates, weights, total, mode, device,
+                                 keep=(lambda n: n not in pnames) if params_only else None)
         for e in h0["entries"]:
             if e["kind"] == "seg":
                 o = offs[e["seg"]]
                 state[e["name"]] = flat[o:o + e["n"]].view(e["shape"])
+            elif raw_avg is not None:
+                state[e["name"]] = raw_avg[e["name"]]
             elif params_only and e["name"] not in pnames:  # a buffer: update 0's (deepcopy(models[0]))
                 state[e["name"]] = updates[0].raw[e["name"]].to(device).clone()
             else:  # restated weighted_sum (+ torch.div) on the raw entries
@@ -869,6 +873,35 @@ class UpdateCodec:
                     acc += updates[i].raw[e["name"]].to(device) * weights[i]
                 state[e["name"]] = acc if mode == "sum" else torch.div(acc, total).to(acc.dtype)
         return module_with_state(template, state)
+
+
+def _aggregate_raw(updates, weights, total, mode, device, keep=None):
+    """The passthrough entries of several updates combined as the per-entry loop in UpdateCodec.aggregate
+    does — acc = x_0 * w_0; acc += x_i * w_i in update order; then torch.div(acc, total) cast back (not in
+    mode "sum"); entries for which keep(name) is true take update 0's value — but with the same elementwise
+    ops on each dtype group's flat tensor at once (a BatchNorm model's 53 counters: 2 ops per update instead
+    of 2 per update and counter). None when the updates' RawStates are not grouped alike."""
+    raws = [u.raw for u in updates]
+    if not all(isinstance(r, RawState) for r in raws):
+        return None
+    g0 = raws[0]._groups
+    sig = [(f.dtype, f.numel(), tuple(m)) for f, m in g0]
+    if any([(f.dtype, f.numel(), tuple(m)) for f, m in r._groups] != sig for r in raws[1:]):
+        return None
+    out = {}
+    for gi, (f0, members) in enumerate(g0):
+        acc = f0.to(device, copy=True)
+        acc *= weights[0]
+        for i in range(1, len(raws)):
+            acc += raws[i]._groups[gi][0].to(device) * weights[i]
+        if mode != "sum":
+            acc = torch.div(acc, total).to(acc.dtype)
+        first = f0.to(device, copy=True) if keep is not None else None
+        views = raws[0]._make_views([(acc, members)])
+        firsts = raws[0]._make_views([(first, members)]) if first is not None else None
+        for n, _, _ in members:
+            out[n] = firsts[n] if keep is not None and keep(n) else views[n]
+    return out
 
 
 def _segment_views(flat, table, entries):
