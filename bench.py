@@ -559,7 +559,19 @@ def launch_ranks(a):
     for r in range(a.gpus):
         env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(a.gpus), LOCAL_WORLD_SIZE=str(a.gpus),
                    MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+        # rank 0's stdout through a pipe: only its JSON line reaches ours (the communication libraries print
+        # status lines to stdout); everything else goes to stderr
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env,
+                                      stdout=subprocess.PIPE if r == 0 else sys.stderr, text=True))
+    import threading
+
+    def forward(pipe):
+        for line in pipe:
+            (sys.stdout if line.startswith('{"metric"') else sys.stderr).write(line)
+            sys.stdout.flush()
+    fwd = threading.Thread(target=forward, args=(procs[0].stdout,), daemon=True) if procs[0].stdout else None
+    if fwd is not None:
+        fwd.start()
     rc = 0
     try:
         pending = list(procs)
@@ -579,6 +591,8 @@ def launch_ranks(a):
             if p.poll() is None:
                 p.kill()
                 p.wait()
+        if fwd is not None:
+            fwd.join(timeout=10)
     return rc
 
 

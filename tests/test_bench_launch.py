@@ -42,8 +42,10 @@ class FakeProc:
 def _run(monkeypatch, argv, codes):
     log, procs = [], []
 
-    def popen(args, env=None, **kw):
+    def popen(args, env=None, stdout=None, **kw):
         p = FakeProc(args, env, codes, log)
+        p.stdout = None if stdout is not subprocess.PIPE else iter(
+            ['[Gloo] Rank 0 is connected to 1 peer ranks\n', '{"metric": "m", "value": 1}\n'])
         procs.append(p)
         return p
     monkeypatch.setattr(subprocess, "Popen", popen)
@@ -89,3 +91,11 @@ def test_rank_rejects_mismatched_world(monkeypatch):
     monkeypatch.setattr(sys, "argv", ["bench.py", "--gpus", "4"])
     with pytest.raises(SystemExit, match="WORLD_SIZE=2"):
         bench.main()
+
+
+def test_launcher_forwards_only_rank0_json_line(monkeypatch, capsys):
+    rc, procs, _ = _run(monkeypatch, ["--gpus", "2"], {})
+    out, err = capsys.readouterr()
+    assert rc == 0
+    assert out == '{"metric": "m", "value": 1}\n'  # the library's status line went to stderr
+    assert "[Gloo]" in err
