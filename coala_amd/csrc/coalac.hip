@@ -94,6 +94,9 @@ constexpr int SEL_NT_LAT = 512;           // ... in latency-bound plans, where n
 #ifndef SCAN_XCD
 #define SCAN_XCD 0    // k_scan: XCD-aware unit order
 #endif
+#ifndef SCAN_LEAN
+#define SCAN_LEAN 1  // k_scan: no per-element length test on units that cannot need it (scan_unit CHECK)
+#endif
 #ifndef SCAN_SMALL_LAT
 #define SCAN_SMALL_LAT 1  // latency-bound plans: small segments in k_scan's first blocks (k_sample alone ahead;
                           // batches measured the same either way and keep k_presel)
@@ -274,6 +277,14 @@ DEV uint32_t wave_max_u32(uint32_t v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v = max(v, (uint32_t)__shfl_xor((int)v, o, 64));
   return v;
+}
+
+// Order one wave's own LDS accesses (a scatter, then reads of the same tile by other lanes): the LDS executes a
+// wave's DS instructions in issue order, so only the compiler must not move them across this point. Unlike
+// wave_fence (a wavefront-scope seq_cst fence), it emits no s_waitcnt: loads in flight stay in flight.
+DEV void lds_order() {
+  __builtin_amdgcn_wave_barrier();
+  asm volatile("" ::: "memory");
 }
 
 DEV void wave_fence() {
@@ -634,7 +645,9 @@ struct Band {
 // The unit is loaded in NB batches of UNIT_IT/NB float4 per lane: NB = 1 for the streaming pass (all
 // loads in flight at once), more for the register-lean fallback inside k_select.
 // ------------------------------------------------------------------------------------------------
-template <bool DELTA, int NB>
+// CHECK: test each element against the unit's length. A full unit never needs it, nor does a partial one when
+// tlo > 0 (its loads past len return 0, key 0 < tlo): k_scan picks the lean form then (wave-uniform).
+template <bool DELTA, int NB, bool CHECK = true>
 DEV void scan_unit(const Params& P, uint32_t lu, const UnitDev& L, const uint32_t tlo, const uint32_t thi,
                    uint2* stage) {
   constexpr uint32_t IT = UNIT_IT / NB;
@@ -667,8 +680,8 @@ DEV void scan_unit(const Params& P, uint32_t lu, const UnitDev& L, const uint32_
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const uint32_t key = fkey(xs[j]);
-        fc[j] = e0 + j < len && key >= tlo;
-        fa[j] = fc[j] && key > thi;
+        fc[j] = (!CHECK || e0 + j < len) && key >= tlo;
+        fa[j] = CHECK ? fc[j] && key > thi : key > thi;  // (thi >= tlo: key > thi implies a candidate)
         any = any || fc[j];
       }
       const uint32_t c = (uint32_t)fc[0] + (uint32_t)fc[1] + (uint32_t)fc[2] + (uint32_t)fc[3];
@@ -1067,7 +1080,11 @@ __global__ __launch_bounds__(BLOCK, WPE) void k_scan(Params P) {
   if (lu >= P.n_lunits) return;
   const UnitDev L = P.lunits[lu];
   // delta: 4 load batches (32 float4 in flight spill)
-  scan_unit<DELTA, DELTA ? 4 : NB>(P, lu, L, P.tlo[lu], P.thi[lu], stage + wv * STAGE_CAP);
+  const uint32_t tlo = P.tlo[lu], thi = P.thi[lu];
+  if (SCAN_LEAN && (L.len == UNIT || tlo > 0))
+    scan_unit<DELTA, DELTA ? 4 : NB, false>(P, lu, L, tlo, thi, stage + wv * STAGE_CAP);
+  else
+    scan_unit<DELTA, DELTA ? 4 : NB, true>(P, lu, L, tlo, thi, stage + wv * STAGE_CAP);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -2170,7 +2187,7 @@ __global__ __launch_bounds__(BLOCK, DECODE_LDS_WPE) void k_decode_lds(Params P) 
     pos[r] = (uint32_t)P.cidx[e] - U[r].start;
     val[r] = code_value<RAW>(q, RAW ? 0.0f : P.cmn[U[r].seg], RAW ? 0.0f : P.cscale[U[r].seg]);
   }
-  wave_fence();
+  lds_order();
 #pragma unroll
   for (uint32_t r = 0; r < DPW; ++r) {
     if (u0 + r >= P.n_units) break;
@@ -2194,14 +2211,14 @@ __global__ __launch_bounds__(BLOCK, DECODE_LDS_WPE) void k_decode_lds(Params P) 
         const uint32_t p2 = (uint32_t)P.cidx[e] - U[r].start;
         if (e0 + lane < hi[r] && (p2 >> 10) == qq) tf[p2 & 1023u] = code_value<RAW>(load_code<RAW>(P, e), mn, sc);
       }
-      wave_fence();
+      lds_order();
       float4 o[QROWS];
 #pragma unroll
       for (uint32_t it = 0; it < QROWS; ++it) {
         const float4 d = tile[it * 64 + lane];
         o[it] = HASBASE ? make_float4(bq[it].x + d.x, bq[it].y + d.y, bq[it].z + d.z, bq[it].w + d.w) : d;
       }
-      wave_fence();
+      lds_order();
       // zero what was written (the same slots), for the next quarter / unit
       if (lane < min(cnt, 64u) && (pos[r] >> 10) == qq) tf[pos[r] & 1023u] = 0.0f;
       for (uint32_t e0 = lo[r] + 64; e0 < hi[r]; e0 += 64) {
@@ -2217,7 +2234,7 @@ __global__ __launch_bounds__(BLOCK, DECODE_LDS_WPE) void k_decode_lds(Params P) 
         for (uint32_t it = 0; it < QROWS; ++it)
           unit_store_x1x4<SAUX>(rout, ((qq * QROWS + it) * 64 + lane) * 16, o[it]);
       }
-      wave_fence();
+      lds_order();
     }
   }
 }
@@ -2341,7 +2358,7 @@ __global__ __launch_bounds__(BLOCK) void k_bounds(Params P, const BChunk* chunks
 #define AGG_SPLIT 2u  // waves per 4096-element unit in k_aggregate (each owns UNIT_IT / AGG_SPLIT rows)
 #endif
 #ifndef AGG_DEPTH
-#define AGG_DEPTH 8u  // clients whose entries k_aggregate keeps in flight (16 ResNet-50: 2 -> 92.5 us, 8 -> 73.7 us, 16 -> 93.5 us)
+#define AGG_DEPTH 16u  // clients whose entries k_aggregate loads together (16 ResNet-50 clients: 4 -> 73.5 us, 8 -> 70.9 us, 16 -> 69.1 us)
 #endif
 
 // k_scatter's work list: one chunk of <= BCHUNK entries of one segment, with the segment's offsets and
@@ -2398,8 +2415,9 @@ struct AggArgs {
 // d_i goes through a per-wave LDS tile: the client's kept values are scattered into the zeroed tile,
 // every lane reads its 64 elements back with ds_read_b128, then the same positions are re-zeroed.
 // Latency: every client's range / mn / scale / weight is fetched lane-parallel in one round (lane j =
-// client j of a 64-client chunk); the first 64 kept entries of the next AGG_DEPTH clients are in flight
-// while client j is accumulated (rotating register slots). Clients are identical copies of one layout, so
+// client j of a 64-client chunk); the first 64 kept entries of AGG_DEPTH clients are then loaded in one
+// batch and accumulated in client order (a unit where some client keeps more than 64 entries takes the
+// unbatched path, one client at a time). Clients are identical copies of one layout, so
 // client c's unit / segment / entry offsets are u + c*U0, seg + c*T, out_off + c*Kc (host-validated).
 template <bool RAW, bool HASBASE, int MODE>
 __global__ __launch_bounds__(BLOCK, AGG_WPE) void k_aggregate(Params P, AggArgs A) {
@@ -2451,31 +2469,21 @@ __global__ __launch_bounds__(BLOCK, AGG_WPE) void k_aggregate(Params P, AggArgs 
     const float m_sc = RAW ? 0.0f : P.cscale[sl];
     const float m_w = avg ? A.weights[cl] : 1.0f;  // (x_0 * 1.0f == x_0)
     auto entries = [&](uint32_t j) -> uint64_t { return U.out_off + (uint64_t)(c0 + j) * A.Kc; };
-    auto fetch = [&](uint32_t j, uint32_t& pos, uint32_t& q) {
+    // fetch: the raw loaded words only — any arithmetic on them here would make the wave wait for the loads
+    // right away (in-order vmcnt), turning the AGG_DEPTH-deep prefetch into one exposed latency per client
+    auto fetch = [&](uint32_t j, uint32_t& idx, uint32_t& q) {
       const uint32_t jj = min(j, cn - 1);
       const uint32_t lo = __builtin_amdgcn_readlane(m_lo, jj), hi = __builtin_amdgcn_readlane(m_hi, jj);
       const uint64_t oo = entries(jj);
       const uint32_t e = min(lo + lane, hi > lo ? hi - 1 : lo);  // kseg >= 1: entry lo always exists
-      pos = (uint32_t)P.cidx[oo + min(e, kseg - 1)] - U.start - e_lo;  // wraps (>= hlen) outside this wave's rows
+      idx = (uint32_t)P.cidx[oo + min(e, kseg - 1)];
       q = load_code<RAW>(P, oo + min(e, kseg - 1));
     };
-    auto process = [&](uint32_t j, uint32_t pos, uint32_t q) {
-      const uint32_t lo = __builtin_amdgcn_readlane(m_lo, j), hi = __builtin_amdgcn_readlane(m_hi, j);
-      const float mn = __uint_as_float(__builtin_amdgcn_readlane(__float_as_uint(m_mn), j));
-      const float sc = __uint_as_float(__builtin_amdgcn_readlane(__float_as_uint(m_sc), j));
+    // x = base + d; acc = x * w (first client) or acc + x * w: IEEE fp32 ops in this order, on float2 pairs
+    // (v_pk_add_f32 / v_pk_mul_f32: half the VALU issue of scalar fp32); the first-client test is
+    // wave-uniform (a branch, no per-element select)
+    auto accumulate = [&](uint32_t j) {
       const float w = __uint_as_float(__builtin_amdgcn_readlane(__float_as_uint(m_w), j));
-      const uint32_t ne = hi - lo;
-      const uint64_t oo = entries(j);
-      if (lane < ne && pos < hlen) tf[pos] = code_value<RAW>(q, mn, sc);
-      for (uint32_t e = lo + 64 + lane; e < hi; e += 64) {  // more than 64 kept entries in this unit
-        const uint32_t p2 = (uint32_t)P.cidx[oo + e] - U.start - e_lo;
-        const float v2 = load_val<RAW>(P, oo + e, mn, sc);
-        if (p2 < hlen) tf[p2] = v2;
-      }
-      wave_fence();
-      // x = base + d; acc = x * w (first client) or acc + x * w: IEEE fp32 ops in this order, on float2 pairs
-      // (v_pk_add_f32 / v_pk_mul_f32: half the VALU issue of scalar fp32); the first-client test is
-      // wave-uniform (a branch, no per-element select)
       const f2v w2 = {w, w};
       if (c0 + j == 0) {
 #pragma unroll
@@ -2497,26 +2505,55 @@ __global__ __launch_bounds__(BLOCK, AGG_WPE) void k_aggregate(Params P, AggArgs 
           acc[it] = make_float4(sl.x, sl.y, sh.x, sh.y);
         }
       }
-      wave_fence();
-      if (ne > 64) {
-#pragma unroll
-        for (uint32_t it = 0; it < RI; ++it) tile[it * 64 + lane] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-      } else if (lane < ne && pos < hlen) {
-        tf[pos] = 0.0f;
-      }
-      wave_fence();
     };
-    // AGG_DEPTH clients' first 64 entries in flight: slot t holds client j0 + t and is refilled with client
-    // j0 + t + AGG_DEPTH right after it is accumulated
-    uint32_t pa[AGG_DEPTH], qa[AGG_DEPTH];
-#pragma unroll
-    for (uint32_t t = 0; t < AGG_DEPTH; ++t) fetch(t, pa[t], qa[t]);
-    for (uint32_t j0 = 0; j0 < cn; j0 += AGG_DEPTH) {
-#pragma unroll
-      for (uint32_t t = 0; t < AGG_DEPTH; ++t) {
-        if (j0 + t < cn) process(j0 + t, pa[t], qa[t]);
-        if (j0 + t + AGG_DEPTH < cn) fetch(j0 + t + AGG_DEPTH, pa[t], qa[t]);
+    // client j with <= 64 kept entries in this unit (the prefetched ones): scatter, accumulate, re-zero
+    auto process = [&](uint32_t j, uint32_t idx, uint32_t q) {
+      const uint32_t pos = idx - U.start - e_lo;  // wraps (>= hlen) outside this wave's rows
+      const uint32_t ne = __builtin_amdgcn_readlane(m_hi, j) - __builtin_amdgcn_readlane(m_lo, j);
+      const float mn = __uint_as_float(__builtin_amdgcn_readlane(__float_as_uint(m_mn), j));
+      const float sc = __uint_as_float(__builtin_amdgcn_readlane(__float_as_uint(m_sc), j));
+      const bool mine = lane < ne && pos < hlen;
+      if (mine) tf[pos] = code_value<RAW>(q, mn, sc);
+      lds_order();
+      accumulate(j);
+      lds_order();
+      if (mine) tf[pos] = 0.0f;
+      lds_order();
+    };
+    // any client with more than 64 kept entries in this unit (ratio >~ 1.5 %): every client in turn, its
+    // entries loaded chunk by chunk, no prefetch (the fast path below has no load loop inside: with one, the
+    // compiler's wait counting falls back to draining every load in flight)
+    auto process_all = [&](uint32_t j) {
+      const uint32_t lo = __builtin_amdgcn_readlane(m_lo, j), hi = __builtin_amdgcn_readlane(m_hi, j);
+      const float mn = __uint_as_float(__builtin_amdgcn_readlane(__float_as_uint(m_mn), j));
+      const float sc = __uint_as_float(__builtin_amdgcn_readlane(__float_as_uint(m_sc), j));
+      const uint64_t oo = entries(j);
+      for (uint32_t e = lo + lane; e < hi; e += 64) {
+        const uint32_t p2 = (uint32_t)P.cidx[oo + e] - U.start - e_lo;
+        const float v2 = load_val<RAW>(P, oo + e, mn, sc);
+        if (p2 < hlen) tf[p2] = v2;
       }
+      lds_order();
+      accumulate(j);
+      lds_order();
+#pragma unroll
+      for (uint32_t it = 0; it < RI; ++it) tile[it * 64 + lane] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+      lds_order();
+    };
+    if (__ballot(lane < cn && m_hi - m_lo > 64) != 0) {
+      for (uint32_t j = 0; j < cn; ++j) process_all(j);
+      continue;
+    }
+    // AGG_DEPTH clients' entries loaded together (unconditionally: past cn the clamped client's words are
+    // read again), then accumulated in client order. No load stays in flight across the loop's back edge:
+    // with one, the compiler's wait counting merges the two paths into the loop header and drains them all
+    for (uint32_t j0 = 0; j0 < cn; j0 += AGG_DEPTH) {
+      uint32_t pa[AGG_DEPTH], qa[AGG_DEPTH];
+#pragma unroll
+      for (uint32_t t = 0; t < AGG_DEPTH; ++t) fetch(j0 + t, pa[t], qa[t]);
+#pragma unroll
+      for (uint32_t t = 0; t < AGG_DEPTH; ++t)
+        if (j0 + t < cn) process(j0 + t, pa[t], qa[t]);
     }
   }
   float* out = P.out + U.off + e_lo;
