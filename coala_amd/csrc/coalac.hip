@@ -2153,10 +2153,16 @@ __global__ __launch_bounds__(BLOCK, DECODE_WPE) void k_decode(Params P) {
 #ifndef DECODE_LDS_WPE
 #define DECODE_LDS_WPE 5
 #endif
+#ifndef DECODE_BASE_PF
+#define DECODE_BASE_PF 1  // k_decode_lds delta mode: the next quarter's base rows in flight (0: loaded per quarter)
+#endif
+#ifndef DECODE_LDS_WPE_BASE
+#define DECODE_LDS_WPE_BASE 4  // delta mode: two quarters of base rows in registers (5 per CU spilled)
+#endif
 constexpr uint32_t QROWS = 4;  // rows per tile quarter
 
 template <bool RAW, bool HASBASE>
-__global__ __launch_bounds__(BLOCK, DECODE_LDS_WPE) void k_decode_lds(Params P) {
+__global__ __launch_bounds__(BLOCK, HASBASE ? DECODE_LDS_WPE_BASE : DECODE_LDS_WPE) void k_decode_lds(Params P) {
   constexpr uint32_t DPW = DECODE_LDS_DPW;
   __shared__ float4 qtile[WAVES][QROWS * 64];
   const uint32_t lane = lane_id(), wv = threadIdx.x >> 6;
@@ -2196,13 +2202,27 @@ __global__ __launch_bounds__(BLOCK, DECODE_LDS_WPE) void k_decode_lds(Params P) 
     const __amdgpu_buffer_rsrc_t rb = unit_rsrc(HASBASE ? P.base + U[r].off : P.out + U[r].off, len);
     const float mn = RAW ? 0.0f : P.cmn[U[r].seg], sc = RAW ? 0.0f : P.cscale[U[r].seg];
     constexpr int SAUX = STORE_AUX;
+    // delta mode: the base rows of quarter qq + 1 are loaded while quarter qq goes through the LDS round trip
+    // (loads and stores share vmcnt in issue order: the wait for them leaves quarter qq's stores in flight)
+    float4 bq[QROWS], bn[QROWS];
+    if (HASBASE && DECODE_BASE_PF) {
+#pragma unroll
+      for (uint32_t it = 0; it < QROWS; ++it) bn[it] = unit_load_x4<false>(rb, rb, (it * 64 + lane) * 16);
+    }
 #pragma unroll
     for (uint32_t qq = 0; qq < UNIT_IT / QROWS; ++qq) {
-      float4 bq[QROWS];
-      if (HASBASE) {  // issue the quarter's base loads before the LDS round trip
+      if (HASBASE) {
 #pragma unroll
-        for (uint32_t it = 0; it < QROWS; ++it)
-          bq[it] = unit_load_x4<false>(rb, rb, ((qq * QROWS + it) * 64 + lane) * 16);
+        for (uint32_t it = 0; it < QROWS; ++it) bq[it] = bn[it];
+        if (!DECODE_BASE_PF) {
+#pragma unroll
+          for (uint32_t it = 0; it < QROWS; ++it)
+            bq[it] = unit_load_x4<false>(rb, rb, ((qq * QROWS + it) * 64 + lane) * 16);
+        } else if (qq + 1 < UNIT_IT / QROWS) {
+#pragma unroll
+          for (uint32_t it = 0; it < QROWS; ++it)
+            bn[it] = unit_load_x4<false>(rb, rb, (((qq + 1) * QROWS + it) * 64 + lane) * 16);
+        }
       }
       // scatter: the first 64 entries are in registers; more (ratio >~ 1.5 %) are loaded chunk by chunk
       if (lane < min(cnt, 64u) && (pos[r] >> 10) == qq) tf[pos[r] & 1023u] = val[r];
@@ -2354,6 +2374,9 @@ __global__ __launch_bounds__(BLOCK) void k_bounds(Params P, const BChunk* chunks
 #ifndef AGG_WPE
 #define AGG_WPE 1  // k_aggregate launch-bounds blocks per CU (register budget)
 #endif
+#ifndef AGG_PROBE
+#define AGG_PROBE 0  // A/B probe builds only (tools/build_variant.sh): 1 = no client loop, 2 = no scatter
+#endif
 #ifndef AGG_SPLIT
 #define AGG_SPLIT 2u  // waves per 4096-element unit in k_aggregate (each owns UNIT_IT / AGG_SPLIT rows)
 #endif
@@ -2438,14 +2461,12 @@ __global__ __launch_bounds__(BLOCK, AGG_WPE) void k_aggregate(Params P, AggArgs 
   const uint32_t hlen = min(len - e_lo, HE);
   float4* tile = tiles[wv];
   float* tf = reinterpret_cast<float*>(tile);
-#pragma unroll
-  for (uint32_t it = 0; it < RI; ++it) tile[it * 64 + lane] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
   float4 b[RI], acc[RI];
   const float* bs = HASBASE ? P.base + U.off + e_lo : nullptr;
+  auto load_base = [&]() {
 #pragma unroll
-  for (uint32_t it = 0; it < RI; ++it) {
-    const uint32_t e = (it * 64 + lane) * 4;
-    if (HASBASE) {
+    for (uint32_t it = 0; it < RI; ++it) {
+      const uint32_t e = (it * 64 + lane) * 4;
       if (hlen == HE) {
         b[it] = *reinterpret_cast<const float4*>(bs + e);
       } else {
@@ -2455,9 +2476,21 @@ __global__ __launch_bounds__(BLOCK, AGG_WPE) void k_aggregate(Params P, AggArgs 
         b[it].w = e + 3 < hlen ? bs[e + 3] : 0.0f;
       }
     }
-    acc[it] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-  }
-  for (uint32_t c0 = 0; c0 < nclients; c0 += 64) {
+  };
+  auto tile_zero = [&]() {
+#pragma unroll
+    for (uint32_t it = 0; it < RI; ++it) tile[it * 64 + lane] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+  };
+  if (HASBASE) load_base();
+  tile_zero();
+#pragma unroll
+  for (uint32_t it = 0; it < RI; ++it) acc[it] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+#if AGG_PROBE == 1
+  const uint32_t nclients_run = 0;  // probe build: the base read and output write alone
+#else
+  const uint32_t nclients_run = nclients;
+#endif
+  for (uint32_t c0 = 0; c0 < nclients_run; c0 += 64) {
     const uint32_t cn = min(64u, nclients - c0);
     // lane j: metadata of client c0 + j (unconditional loads at a clamped client index)
     const uint32_t cl = c0 + min(lane, cn - 1);
@@ -2512,7 +2545,11 @@ __global__ __launch_bounds__(BLOCK, AGG_WPE) void k_aggregate(Params P, AggArgs 
       const uint32_t ne = __builtin_amdgcn_readlane(m_hi, j) - __builtin_amdgcn_readlane(m_lo, j);
       const float mn = __uint_as_float(__builtin_amdgcn_readlane(__float_as_uint(m_mn), j));
       const float sc = __uint_as_float(__builtin_amdgcn_readlane(__float_as_uint(m_sc), j));
+#if AGG_PROBE == 2
+      const bool mine = false;  // probe build: no scatter (loads and accumulation only)
+#else
       const bool mine = lane < ne && pos < hlen;
+#endif
       if (mine) tf[pos] = code_value<RAW>(q, mn, sc);
       lds_order();
       accumulate(j);
@@ -2536,8 +2573,7 @@ __global__ __launch_bounds__(BLOCK, AGG_WPE) void k_aggregate(Params P, AggArgs 
       lds_order();
       accumulate(j);
       lds_order();
-#pragma unroll
-      for (uint32_t it = 0; it < RI; ++it) tile[it * 64 + lane] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+      tile_zero();
       lds_order();
     };
     if (__ballot(lane < cn && m_hi - m_lo > 64) != 0) {

@@ -144,6 +144,248 @@ __global__ __launch_bounds__(256) void scan(const float* __restrict__ in, const 
   if (lane == 0) { cnt[2 * u] = cA; cnt[2 * u + 1] = cB + sink; }
 }
 
+
+__device__ __forceinline__ void load_unit(const float* in, uint32_t u, uint32_t lane, float4 (&v)[16]) {
+  const float4* p = reinterpret_cast<const float4*>(in + (uint64_t)u * UNIT);
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    const f4v t = __builtin_nontemporal_load(reinterpret_cast<const f4v*>(p + i * 64 + lane));
+    v[i] = make_float4(t.x, t.y, t.z, t.w);
+  }
+}
+
+template <bool WORK>
+__device__ __forceinline__ void process_unit(const float4 (&v)[16], uint32_t u, uint32_t lane, uint32_t tlo,
+                                             uint32_t thi, uint2* stR, uint2* Rall, uint32_t* cnt) {
+  if (!WORK) {
+    float s = 0.f;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) s += v[i].x + v[i].y + v[i].z + v[i].w;
+    if (s == 1234.5f) cnt[0] = 1;
+    return;
+  }
+  const uint64_t reg = (uint64_t)u * UNIT;
+  uint32_t cA = 0, cB = 0;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    const uint32_t e0 = (i * 64 + lane) * 4;
+    const float xs[4] = {v[i].x, v[i].y, v[i].z, v[i].w};
+    bool fa[4], fb[4], any = false;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const uint32_t key = __float_as_uint(xs[j]) & 0x7FFFFFFFu;
+      fa[j] = key > thi;
+      fb[j] = !fa[j] && key >= tlo;
+      any = any || fa[j] || fb[j];
+    }
+    if (!__any(any)) continue;
+    uint64_t bc[4];
+    uint32_t pc = cA;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      bc[j] = __ballot(fa[j] || fb[j]);
+      pc += mbcnt(bc[j]);
+      cB += (uint32_t)__popcll(__ballot(fa[j]));
+    }
+    uint2* R = Rall + reg;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      if (fa[j] || fb[j]) {
+        const uint2 rec = make_uint2((e0 + j) | (fa[j] ? 0x80000000u : 0u), __float_as_uint(xs[j]));
+        if (pc < 512) stR[pc] = rec;
+        else R[pc] = rec;
+        ++pc;
+      }
+      cA += (uint32_t)__popcll(bc[j]);
+    }
+  }
+  __builtin_amdgcn_wave_barrier(); asm volatile("" ::: "memory");
+  uint2* R = Rall + reg;
+  for (uint32_t i = lane; i < cA && i < 512; i += 64) R[i] = stR[i];
+  __builtin_amdgcn_wave_barrier(); asm volatile("" ::: "memory");
+  if (lane == 0) { cnt[2 * u] = cA; cnt[2 * u + 1] = cB; }
+}
+
+template <bool WORK, int PER>
+__global__ __launch_bounds__(256, 2) void scan_p(const float* __restrict__ in, uint32_t nunits, uint32_t per,
+                                                 uint32_t tlo, uint32_t thi, int32_t* aI, uint32_t* cnt) {
+  __shared__ uint2 stR[4][512];
+  const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const uint32_t u0 = (blockIdx.x * 4 + wv) * per;
+  if (u0 >= nunits) return;
+  const uint32_t u1 = min(u0 + per, nunits);
+  uint2* R = reinterpret_cast<uint2*>(aI);
+  float4 A[16], B[16];
+  if (PER == 0) {
+    load_unit(in, u0, lane, A);
+    for (uint32_t u = u0; u < u1; u += 2) {
+      load_unit(in, min(u + 1, u1 - 1), lane, B);
+      process_unit<WORK>(A, u, lane, tlo, thi, stR[wv], R, cnt);
+      load_unit(in, min(u + 2, u1 - 1), lane, A);
+      if (u + 1 < u1) process_unit<WORK>(B, u + 1, lane, tlo, thi, stR[wv], R, cnt);
+    }
+  } else {
+    // straight-line: PER units, no loop edge for a load to stay in flight across
+    load_unit(in, u0, lane, A);
+#pragma unroll
+    for (uint32_t k = 0; k < (uint32_t)PER; k += 2) {
+      load_unit(in, min(u0 + k + 1, u1 - 1), lane, B);
+      if (u0 + k < u1) process_unit<WORK>(A, u0 + k, lane, tlo, thi, stR[wv], R, cnt);
+      if (k + 2 < (uint32_t)PER) load_unit(in, min(u0 + k + 2, u1 - 1), lane, A);
+      if (u0 + k + 1 < u1) process_unit<WORK>(B, u0 + k + 1, lane, tlo, thi, stR[wv], R, cnt);
+    }
+  }
+}
+
+// 14: straight-line PER units per wave with the next unit in flight, and NO global store until every unit is
+// classified (a store pending beside prefetched loads makes the compiler wait for everything: vmcnt counts
+// loads and stores together on gfx9, out of order): records staged per unit in LDS (512 each; more are only
+// counted — the real kernel would re-scan such a unit), counts kept in lanes, all flushed at the end.
+template <int PER>
+__device__ __forceinline__ void classify_unit(const float4 (&v)[16], uint32_t lane, uint32_t tlo, uint32_t thi,
+                                              uint2* st, uint32_t& cA, uint32_t& cB) {
+  cA = 0;
+  cB = 0;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    const uint32_t e0 = (i * 64 + lane) * 4;
+    const float xs[4] = {v[i].x, v[i].y, v[i].z, v[i].w};
+    bool fa[4], fb[4], any = false;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const uint32_t key = __float_as_uint(xs[j]) & 0x7FFFFFFFu;
+      fa[j] = key > thi;
+      fb[j] = !fa[j] && key >= tlo;
+      any = any || fa[j] || fb[j];
+    }
+    if (!__any(any)) continue;
+    uint64_t bc[4];
+    uint32_t pc = cA;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      bc[j] = __ballot(fa[j] || fb[j]);
+      pc += mbcnt(bc[j]);
+      cB += (uint32_t)__popcll(__ballot(fa[j]));
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      if ((fa[j] || fb[j]) && pc < 512)
+        st[pc] = make_uint2((e0 + j) | (fa[j] ? 0x80000000u : 0u), __float_as_uint(xs[j]));
+      pc += (fa[j] || fb[j]) ? 1u : 0u;
+      cA += (uint32_t)__popcll(bc[j]);
+    }
+  }
+}
+
+template <int PER>
+__global__ __launch_bounds__(256, 2) void scan_d(const float* __restrict__ in, uint32_t nunits, uint32_t tlo,
+                                                 uint32_t thi, int32_t* aI, uint32_t* cnt) {
+  __shared__ uint2 stR[4][PER][512];
+  const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const uint32_t u0 = (blockIdx.x * 4 + wv) * PER;
+  if (u0 >= nunits) return;
+  const uint32_t u1 = min(u0 + PER, nunits);
+  uint2* R = reinterpret_cast<uint2*>(aI);
+  float4 A[16], B[16];
+  uint32_t ca[PER], cb[PER];
+  load_unit(in, u0, lane, A);
+#pragma unroll
+  for (uint32_t k = 0; k < (uint32_t)PER; k += 2) {
+    load_unit(in, min(u0 + k + 1, u1 - 1), lane, B);
+    classify_unit<PER>(A, lane, tlo, thi, stR[wv][k], ca[k], cb[k]);
+    if (k + 2 < (uint32_t)PER) load_unit(in, min(u0 + k + 2, u1 - 1), lane, A);
+    classify_unit<PER>(B, lane, tlo, thi, stR[wv][k + 1], ca[k + 1], cb[k + 1]);
+  }
+  __builtin_amdgcn_wave_barrier();
+  asm volatile("" ::: "memory");
+#pragma unroll
+  for (uint32_t k = 0; k < (uint32_t)PER; ++k) {
+    if (u0 + k >= u1) break;
+    uint2* Ru = R + (uint64_t)(u0 + k) * UNIT;
+    for (uint32_t i = lane; i < ca[k] && i < 512; i += 64) Ru[i] = stR[wv][k][i];
+    if (lane == 0) { cnt[2 * (u0 + k)] = ca[k]; cnt[2 * (u0 + k) + 1] = cb[k]; }
+  }
+}
+
+// 15: half-unit pipeline: PER units per wave as 2*PER halves of 8 float4 per lane, the next half in flight while
+// the current one is classified; records staged in LDS (SC per unit; more only counted), stores deferred to
+// the end (as 14). Fewer registers than 14: ~5 waves per SIMD.
+template <int SC>
+__device__ __forceinline__ void classify_half(const float4 (&v)[8], uint32_t hbase, uint32_t lane, uint32_t tlo,
+                                              uint32_t thi, uint2* st, uint32_t& cA, uint32_t& cB) {
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const uint32_t e0 = hbase + (i * 64 + lane) * 4;
+    const float xs[4] = {v[i].x, v[i].y, v[i].z, v[i].w};
+    bool fa[4], fb[4], any = false;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const uint32_t key = __float_as_uint(xs[j]) & 0x7FFFFFFFu;
+      fa[j] = key > thi;
+      fb[j] = !fa[j] && key >= tlo;
+      any = any || fa[j] || fb[j];
+    }
+    if (!__any(any)) continue;
+    uint64_t bc[4];
+    uint32_t pc = cA;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      bc[j] = __ballot(fa[j] || fb[j]);
+      pc += mbcnt(bc[j]);
+      cB += (uint32_t)__popcll(__ballot(fa[j]));
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      if ((fa[j] || fb[j]) && pc < SC)
+        st[pc] = make_uint2((e0 + j) | (fa[j] ? 0x80000000u : 0u), __float_as_uint(xs[j]));
+      pc += (fa[j] || fb[j]) ? 1u : 0u;
+      cA += (uint32_t)__popcll(bc[j]);
+    }
+  }
+}
+
+__device__ __forceinline__ void load_half(const float* in, uint32_t u, uint32_t half, uint32_t lane, float4 (&v)[8]) {
+  const float4* p = reinterpret_cast<const float4*>(in + (uint64_t)u * UNIT + half * (UNIT / 2));
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const f4v t = __builtin_nontemporal_load(reinterpret_cast<const f4v*>(p + i * 64 + lane));
+    v[i] = make_float4(t.x, t.y, t.z, t.w);
+  }
+}
+
+template <int PER, int SC, int OCC>
+__global__ __launch_bounds__(256, OCC) void scan_h(const float* __restrict__ in, uint32_t nunits, uint32_t tlo,
+                                                   uint32_t thi, int32_t* aI, uint32_t* cnt) {
+  __shared__ uint2 stR[4][PER][SC];
+  const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const uint32_t u0 = (blockIdx.x * 4 + wv) * PER;
+  if (u0 >= nunits) return;
+  const uint32_t u1 = min(u0 + PER, nunits);
+  uint2* R = reinterpret_cast<uint2*>(aI);
+  float4 A[8], B[8];
+  uint32_t ca[PER], cb[PER];
+#pragma unroll
+  for (int k = 0; k < PER; ++k) ca[k] = cb[k] = 0;
+  load_half(in, u0, 0, lane, A);
+#pragma unroll
+  for (uint32_t k = 0; k < (uint32_t)PER; ++k) {
+    const uint32_t uk = min(u0 + k, u1 - 1);
+    load_half(in, uk, 1, lane, B);
+    classify_half<SC>(A, 0, lane, tlo, thi, stR[wv][k], ca[k], cb[k]);
+    if (k + 1 < (uint32_t)PER) load_half(in, min(u0 + k + 1, u1 - 1), 0, lane, A);
+    classify_half<SC>(B, UNIT / 2, lane, tlo, thi, stR[wv][k], ca[k], cb[k]);
+  }
+  __builtin_amdgcn_wave_barrier();
+  asm volatile("" ::: "memory");
+#pragma unroll
+  for (uint32_t k = 0; k < (uint32_t)PER; ++k) {
+    if (u0 + k >= u1) break;
+    uint2* Ru = R + (uint64_t)(u0 + k) * UNIT;
+    for (uint32_t i = lane; i < ca[k] && i < SC; i += 64) Ru[i] = stR[wv][k][i];
+    if (lane == 0) { cnt[2 * (u0 + k)] = ca[k]; cnt[2 * (u0 + k) + 1] = cb[k]; }
+  }
+}
+
 int main() {
   const uint32_t nunits = 16u * 6252u;  // ~ 16 ResNet-50 clients of large units
   const size_t n = (size_t)nunits * UNIT;
@@ -201,5 +443,23 @@ int main() {
   RUN(8, "8_combined_lds_staged");
   RUN(9, "9_combined_lds_staged_nt");
   RUN(0, "0_load_only_again");
+  for (uint32_t bpc : {2u, 3u}) {
+    const uint32_t waves = 256u * bpc * 4u, per = (nunits + waves - 1) / waves, gp = (nunits + per * 4 - 1) / (per * 4);
+    char nm[64];
+    snprintf(nm, sizeof nm, "11_persistent_load_only_b%u", bpc);
+    run(nm, [&] { hipLaunchKernelGGL((scan_p<false, 0>), dim3(gp), dim3(256), 0, 0, in, nunits, per, tlo, thi, aI, cnt); });
+    snprintf(nm, sizeof nm, "10_persistent_prefetch_b%u", bpc);
+    run(nm, [&] { hipLaunchKernelGGL((scan_p<true, 0>), dim3(gp), dim3(256), 0, 0, in, nunits, per, tlo, thi, aI, cnt); });
+  }
+#define RUNS(PER) { const uint32_t gp = (nunits + PER * 4 - 1) / (PER * 4); \
+    run("12_straight_prefetch_per" #PER, [&] { hipLaunchKernelGGL((scan_p<true, PER>), dim3(gp), dim3(256), 0, 0, in, nunits, PER, tlo, thi, aI, cnt); }); \
+    run("13_straight_load_only_per" #PER, [&] { hipLaunchKernelGGL((scan_p<false, PER>), dim3(gp), dim3(256), 0, 0, in, nunits, PER, tlo, thi, aI, cnt); }); }
+#define RUND(PER) { const uint32_t gp = (nunits + PER * 4 - 1) / (PER * 4); \
+    run("14_deferred_stores_per" #PER, [&] { hipLaunchKernelGGL((scan_d<PER>), dim3(gp), dim3(256), 0, 0, in, nunits, tlo, thi, aI, cnt); }); }
+  RUND(2)
+#define RUNH(PER, SC, OCC) { const uint32_t gp = (nunits + PER * 4 - 1) / (PER * 4); \
+    run("15_half_pipeline_per" #PER "_sc" #SC "_occ" #OCC, [&] { hipLaunchKernelGGL((scan_h<PER, SC, OCC>), dim3(gp), dim3(256), 0, 0, in, nunits, tlo, thi, aI, cnt); }); }
+  RUNH(1, 512, 5) RUNH(2, 256, 5) RUNH(2, 256, 6) RUNH(4, 256, 4) RUNH(4, 128, 5) RUNH(8, 128, 4)
+  RUN(9, "9_combined_lds_staged_nt_again");
   return 0;
 }
