@@ -286,3 +286,24 @@ def test_workspace_is_capped(cuda):
     plan = CodecPlan(sizes, 0.01, 8, clients=16)
     n = plan.table.n_elements
     assert plan.ws_bytes < 1.5 * n, plan.ws_bytes / n
+
+
+@pytest.mark.parametrize("delta", [False, True])
+def test_scan_stage_overflow_in_a_batch(cuda, delta):
+    """k_scan stages a unit's first 512 candidate records per wave in LDS and stores the rest directly
+    (coalac.hip scan_unit). One unit of a 2-client ResNet-50 batch plan (> 8192 units: the staged scan) gets
+    450 large values on top of its ~300 ordinary candidates at ratio 0.05 (> 512, inside the plan's 896
+    record slots, so no raw-path fallback): bit-exact against the oracle."""
+    rng = np.random.default_rng(5 + delta)
+    sizes = fp32_sizes("resnet50_tv")
+    xs = [gauss(rng, sizes) for _ in range(2)]
+    big = int(np.argmax(sizes))
+    x = xs[0][big]
+    lo = 5 * 4096
+    pick = rng.choice(4096, 450, replace=False) + lo
+    x[pick] = (rng.standard_normal(450) * 100.0 + 500.0).astype(np.float32)
+    bases = [gauss(rng, sizes, -2, -1) for _ in range(2)] if delta else None
+    plan, g, r = run_both(sizes, 0.05, 8, xs, bases, clients=2)
+    assert plan.n_units > 8192  # a batch plan
+    assert_same(plan, g, r)
+    assert g["fallbacks"] == 0
