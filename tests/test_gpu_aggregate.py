@@ -176,3 +176,33 @@ def test_fused_server_end_to_end_on_gpu(cuda):
         for (k, a), b in zip(plain.model.state_dict().items(), fused.model.state_dict().values()):
             assert a.dtype == b.dtype and torch.equal(a, b), k
     assert federated_averaging is not None
+
+
+@pytest.mark.parametrize("ratio", [0.01, 0.3])
+@pytest.mark.parametrize("delta", [True, False])
+@pytest.mark.parametrize("mode,om", [("recip", O.AGG_RECIP), ("div", O.AGG_DIV), ("sum", O.AGG_SUM)])
+def test_aggregate_many_clients_matches_oracle(cuda, ratio, delta, mode, om):
+    """More clients than one 16-client chunk of the aggregate kernel (37: two full chunks and a ragged one),
+    ragged units (partial last units, a segment under one unit, n = 1), light (<= 64 kept entries per unit)
+    and heavy (ratio 0.3: the one-client-at-a-time path) chunks, every division mode."""
+    sizes = [1, 300, 5000, 8192, 12289, 70001]
+    C = 37
+    plan = CodecPlan(sizes, ratio, 8, clients=C)
+    one = CodecPlan(sizes, ratio, 8, clients=1)
+    dev = torch.device("cuda", 0)
+    flat = synth_batch(plan.table, dev, client_ids=[500 + i for i in range(C)])
+    base = synth_batch(one.table, dev, client_ids=[777]) if delta else None
+    enc = plan.encode(flat, base=None if base is None else base.repeat(C))
+    weights = [(7 * i) % 23 for i in range(C)]
+    mask = [True, False, True, True, False, True]
+    segs = plan.table.segs.astype(np.int64)
+    h = [t.cpu().numpy() for t in (enc.idx, enc.vals, enc.mn, enc.scale)]
+    b = None if base is None else base.cpu().numpy()
+    for am in (None, mask):
+        out = plan.aggregate(enc, weights, base=base, mode=mode, avg_mask=am)
+        torch.cuda.synchronize()
+        ref = O.aggregate(*h, segs, 8, C, weights, sum(weights), om, base=b, out_span=plan.table.span_per_client,
+                          avg_mask=am)
+        g = out.cpu().numpy()
+        for off, n in zip(plan.table.offsets, plan.table.sizes):
+            np.testing.assert_array_equal(g[off:off + n].view(np.uint32), ref[off:off + n].view(np.uint32))
