@@ -28,6 +28,9 @@ What it pins, and from where (SURVEY.md §8(c) "What reference imports pin"):
    pickled carrier: codec.marshal(copy.deepcopy(self.model)), base.py:363), data_size / type, the
    tracked upload size, and the reference's strategies.federated_averaging (server/strategies.py:6-29)
    of the decoded uploads. tests/test_reference_fixture.py reproduces all of it with the HIP backend.
+6. splitFL feature uploads through the REAL reference BaseSFLClient.marshal_data
+   (/root/reference/application/splitFL/client/base_sfl.py:248-257), plain and with the mixin
+   (splitfl_features.npz); tests/test_splitfl_features.py reproduces both.
 
 The reference is imported read-only with a namespace stub for `coala` (its __init__ needs omegaconf,
 which is not installed). No reference source is copied; only data is written.
@@ -310,12 +313,65 @@ def make_plugin_fixture():
           [int(arrays[f"upload_bytes/{i}"].size) for i in range(len(PLUGIN_SIZES))])
 
 
+SFL_FEATURE_SHAPE, SFL_SEED, SFL_RATIO, SFL_BITS = (3, 8, 6, 6), 11, 0.05, 8
+
+
+def sfl_feature():
+    """The fixture's cut-layer activation (also restated by tests/test_splitfl_features.py)."""
+    g = torch.Generator().manual_seed(SFL_SEED)
+    return torch.relu(torch.randn(SFL_FEATURE_SHAPE, generator=g)), torch.tensor([4, 0, 9])
+
+
+def make_splitfl_fixture():
+    """splitFL feature upload through the REAL reference client (splitfl_features.npz): the reference's own
+    BaseSFLClient.marshal_data("feature_label") (application/splitFL/client/base_sfl.py:248-257), plain and with
+    CompressionClientMixin mixed in (oracle backend). base_sfl.py imports coala.datasets.dataset_util for its
+    training data wrapper only; that module (torchvision) is absent here, so a placeholder module stands in for
+    it — marshal_data does not touch it. Pinned: the plain upload's dict layout (names, feature, label) and data
+    type, and the mixin's upload: its dict layout and the exact bytes of the encoded feature (the carrier's
+    COALAQ1 blob); tests/test_splitfl_features.py reproduces both."""
+    import importlib.util
+    import pickle
+
+    sys.path.insert(0, REPO)
+    ds = types.ModuleType("coala.datasets")
+    ds.__path__ = []
+    du = types.ModuleType("coala.datasets.dataset_util")
+    du.TransformDataset = object
+    sys.modules.setdefault("coala.datasets", ds)
+    sys.modules.setdefault("coala.datasets.dataset_util", du)
+    spec = importlib.util.spec_from_file_location(
+        "_ref_base_sfl", os.path.join(REF, "application", "splitFL", "client", "base_sfl.py"))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    from coala_amd.compression import CompressionClientMixin
+    from tests.oracle_backend import OracleBackend
+
+    class Mixed(CompressionClientMixin, mod.BaseSFLClient):
+        codec_features, codec_ratio, codec_bits, codec_backend = True, SFL_RATIO, SFL_BITS, OracleBackend()
+
+    x, lab = sfl_feature()
+    arrays = {"feature": x.numpy(), "label": lab.numpy()}
+    for key, cls in (("plain", mod.BaseSFLClient), ("mixed", Mixed)):
+        c = cls.__new__(cls)  # marshal_data reads feature / label only (no dataset, no config)
+        c.feature, c.label, c.model = x.clone(), lab.clone(), None
+        data, typ = c.marshal_data("feature_label")
+        arrays[f"{key}/type"] = np.array([int(typ)], np.int64)
+        d = pickle.loads(data)  # (bytes this script just wrote)
+        arrays[f"{key}/names"] = np.array(d["name"])
+        assert torch.equal(d["content"][1], lab)
+        if key == "mixed":  # the carrier's COALAQ1 blob (the label's pickle embeds a storage address)
+            arrays["mixed/carrier"] = np.frombuffer(d["content"][0].to_bytes(), dtype=np.uint8).copy()
+    np.savez_compressed(os.path.join(HERE, "splitfl_features.npz"), **arrays)
+    print("splitfl_features.npz:", {k: v.shape for k, v in arrays.items()})
+
+
 if __name__ == "__main__":
     if not os.environ.get("PYTHONDONTWRITEBYTECODE"):
         sys.exit("run with PYTHONDONTWRITEBYTECODE=1 so nothing is written into /root/reference")
     sys.dont_write_bytecode = True
     _stub_coala()
     parts = {"layouts": make_layouts, "fedavg": make_fedavg, "fedavg_params": make_fedavg_params,
-             "hooks": make_hooks, "plugin": make_plugin_fixture}
+             "hooks": make_hooks, "plugin": make_plugin_fixture, "splitfl": make_splitfl_fixture}
     for name in (sys.argv[1:] or list(parts)):  # e.g. `make_golden.py fedavg_params`: that fixture only
         parts[name]()

@@ -3,11 +3,14 @@
 The reference's splitFL client serialises `{"content": [feature.detach().cpu(), label], "name": [...]}`
 in marshal_data("feature_label") (application/splitFL/client/base_sfl.py:248-257) and its server reads
 it back with decompression(codec.unmarshal(data)) (application/splitFL/server/base_sfl.py:207-209). The
-reference splitFL client does not import here (coala.datasets is missing), so `SFLClient` below restates
-that marshal_data as the mixin's parent. Bar: the server-side decoded feature equals the oracle's decode
-of the same tensor bit for bit (CPU: oracle backend; GPU: the HIP codec), labels unchanged, model
-uploads and uncompressed runs untouched.
+reference splitFL client cannot be imported on the GPU box (no /root/reference there), so `SFLClient` below
+restates that marshal_data as the mixin's parent; tests/golden/splitfl_features.npz, written in the build
+container by the REAL BaseSFLClient.marshal_data (plain, and with the mixin: tests/golden/make_golden.py
+make_splitfl_fixture), pins the restatement's dict layout and the mixin's exact upload bytes. Bar: the
+server-side decoded feature equals the oracle's decode of the same tensor bit for bit (CPU: oracle backend;
+GPU: the HIP codec), labels unchanged, model uploads and uncompressed runs untouched.
 """
+import os
 import copy
 import pickle
 
@@ -122,3 +125,52 @@ def test_feature_upload_gpu(cuda, shape):
     np.testing.assert_array_equal(f.cpu().numpy().view(np.uint32), oracle_dense(x, 0.01, 8).view(np.uint32))
     dense, _ = SFLClient(x, lab).marshal_data("feature_label")
     assert len(data) * 30 < len(dense)
+
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "splitfl_features.npz")
+SFL_RATIO, SFL_BITS = 0.05, 8  # make_golden.py make_splitfl_fixture
+
+
+def _fixture():
+    z = np.load(GOLDEN)  # data arrays only (allow_pickle stays False)
+    return {k: z[k] for k in z.files}
+
+
+def test_restated_marshal_data_matches_reference_client():
+    """The restated SFLClient.marshal_data builds what the reference's BaseSFLClient.marshal_data built for
+    the fixture's feature: the same data type, the same name list, the same feature and label tensors."""
+    z = _fixture()
+    x, lab = torch.from_numpy(z["feature"]), torch.from_numpy(z["label"])
+    data, typ = SFLClient(x, lab).marshal_data("feature_label")
+    d = pickle.loads(data)  # (our own bytes)
+    assert typ == int(z["plain/type"][0]) == DATA_TYPE_FEATURE
+    assert d["name"] == [str(v) for v in z["plain/names"]]
+    assert torch.equal(d["content"][0], x) and torch.equal(d["content"][1], lab)
+
+
+def _mixin_upload(backend, device):
+    z = _fixture()
+    Client, _ = classes(backend, ratio=SFL_RATIO, bits=SFL_BITS)
+    x, lab = torch.from_numpy(z["feature"]).to(device), torch.from_numpy(z["label"])
+    data, typ = Client(x, lab).marshal_data("feature_label")
+    d = pickle.loads(data)  # (our own bytes)
+    assert typ == int(z["mixed/type"][0])
+    assert d["name"] == [str(v) for v in z["mixed/names"]] and torch.equal(d["content"][1], lab)
+    assert isinstance(d["content"][0], CompressedUpdate)
+    return z, d["content"][0].to_bytes()
+
+
+def test_mixin_feature_upload_bytes_match_reference_client_cpu():
+    """CompressionClientMixin on the restated client (oracle backend) writes the upload the mixin wrote on top
+    of the REAL reference BaseSFLClient for the fixture: same type and dict layout, the encoded feature byte
+    for byte (the whole pickle differs only in the label storage's address key)."""
+    z, blob = _mixin_upload(OracleBackend(), "cpu")
+    assert blob == z["mixed/carrier"].tobytes()
+
+
+@pytest.mark.gpu
+def test_mixin_feature_upload_bytes_match_reference_client_gpu(cuda):
+    """The same upload encoded on the GPU by the HIP codec: the identical bytes."""
+    from coala_amd.compression.codec import HipBackend
+    z, blob = _mixin_upload(HipBackend(), cuda)
+    assert blob == z["mixed/carrier"].tobytes()
