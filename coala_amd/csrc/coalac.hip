@@ -2148,7 +2148,7 @@ __global__ __launch_bounds__(BLOCK, DECODE_WPE) void k_decode(Params P) {
 #define DECODE_LDS 1
 #endif
 #ifndef DECODE_LDS_DPW
-#define DECODE_LDS_DPW 2u
+#define DECODE_LDS_DPW 1u  // units per wave (2: C3 0.672 vs 0.622 ms per step with 8-row passes, profiles/r03_decode_ab.txt)
 #endif
 #ifndef DECODE_LDS_WPE
 #define DECODE_LDS_WPE 5
@@ -2159,14 +2159,26 @@ __global__ __launch_bounds__(BLOCK, DECODE_WPE) void k_decode(Params P) {
 #ifndef DECODE_LDS_WPE_BASE
 #define DECODE_LDS_WPE_BASE 4  // delta mode: two quarters of base rows in registers (5 per CU spilled)
 #endif
-constexpr uint32_t QROWS = 4;  // rows per tile quarter
+#ifndef DECODE_QROWS
+#define DECODE_QROWS 8u  // weights mode: rows per tile pass (8: half a unit, 8 KiB of LDS per wave; 4 rows: C3
+                         // 0.671-0.674 ms per step, 8 rows: 0.621-0.623, profiles/r03_decode_ab.txt)
+#endif
+#ifndef DECODE_NT
+#define DECODE_NT 256  // k_decode_lds block size (its per-wave LDS tile is QROWS KiB)
+#endif
+#ifndef DECODE_QROWS_BASE
+#define DECODE_QROWS_BASE 4u  // delta mode: rows per tile pass
+#endif
 
 template <bool RAW, bool HASBASE>
-__global__ __launch_bounds__(BLOCK, HASBASE ? DECODE_LDS_WPE_BASE : DECODE_LDS_WPE) void k_decode_lds(Params P) {
-  constexpr uint32_t DPW = DECODE_LDS_DPW;
-  __shared__ float4 qtile[WAVES][QROWS * 64];
+__global__ __launch_bounds__(DECODE_NT, HASBASE ? DECODE_LDS_WPE_BASE : DECODE_LDS_WPE) void k_decode_lds(Params P) {
+  constexpr uint32_t DPW = DECODE_LDS_DPW, DW = DECODE_NT / 64;
+  constexpr uint32_t QROWS = HASBASE ? DECODE_QROWS_BASE : DECODE_QROWS;  // rows per tile pass
+  constexpr uint32_t QSH = QROWS == 2u ? 9u : QROWS == 4u ? 10u : QROWS == 8u ? 11u : 12u, QM = (1u << QSH) - 1u;
+  static_assert((QROWS << 8) == (1u << QSH), "tile pass geometry");
+  __shared__ float4 qtile[DW][QROWS * 64];
   const uint32_t lane = lane_id(), wv = threadIdx.x >> 6;
-  const uint32_t u0 = ((DECODE_XCD ? xcd_block(blockIdx.x) : blockIdx.x) * WAVES + wv) * DPW;
+  const uint32_t u0 = ((DECODE_XCD ? xcd_block(blockIdx.x) : blockIdx.x) * DW + wv) * DPW;
   if (u0 >= P.n_units) return;
   float4* tile = qtile[wv];
   float* tf = reinterpret_cast<float*>(tile);
@@ -2225,11 +2237,11 @@ __global__ __launch_bounds__(BLOCK, HASBASE ? DECODE_LDS_WPE_BASE : DECODE_LDS_W
         }
       }
       // scatter: the first 64 entries are in registers; more (ratio >~ 1.5 %) are loaded chunk by chunk
-      if (lane < min(cnt, 64u) && (pos[r] >> 10) == qq) tf[pos[r] & 1023u] = val[r];
+      if (lane < min(cnt, 64u) && (pos[r] >> QSH) == qq) tf[pos[r] & QM] = val[r];
       for (uint32_t e0 = lo[r] + 64; e0 < hi[r]; e0 += 64) {
         const uint64_t e = U[r].out_off + min(e0 + lane, hi[r] - 1);
         const uint32_t p2 = (uint32_t)P.cidx[e] - U[r].start;
-        if (e0 + lane < hi[r] && (p2 >> 10) == qq) tf[p2 & 1023u] = code_value<RAW>(load_code<RAW>(P, e), mn, sc);
+        if (e0 + lane < hi[r] && (p2 >> QSH) == qq) tf[p2 & QM] = code_value<RAW>(load_code<RAW>(P, e), mn, sc);
       }
       lds_order();
       float4 o[QROWS];
@@ -2240,11 +2252,11 @@ __global__ __launch_bounds__(BLOCK, HASBASE ? DECODE_LDS_WPE_BASE : DECODE_LDS_W
       }
       lds_order();
       // zero what was written (the same slots), for the next quarter / unit
-      if (lane < min(cnt, 64u) && (pos[r] >> 10) == qq) tf[pos[r] & 1023u] = 0.0f;
+      if (lane < min(cnt, 64u) && (pos[r] >> QSH) == qq) tf[pos[r] & QM] = 0.0f;
       for (uint32_t e0 = lo[r] + 64; e0 < hi[r]; e0 += 64) {
         const uint64_t e = U[r].out_off + min(e0 + lane, hi[r] - 1);
         const uint32_t p2 = (uint32_t)P.cidx[e] - U[r].start;
-        if (e0 + lane < hi[r] && (p2 >> 10) == qq) tf[p2 & 1023u] = 0.0f;
+        if (e0 + lane < hi[r] && (p2 >> QSH) == qq) tf[p2 & QM] = 0.0f;
       }
       if ((len & 3u) == 0) {  // wave-uniform: one float4 buffer store per slot
 #pragma unroll
@@ -3205,7 +3217,8 @@ int coalac_decode_sched(coalac_plan_t plan, const int32_t* d_idx, const void* d_
   const uint32_t upb = WAVES * (hb ? decode_dpw<true, false>()
                                    : search ? decode_dpw<false, true>() : decode_dpw<false, false>());  // units per block
   const uint32_t g = (plan->n_units + upb - 1) / upb;
-  const uint32_t glds = (plan->n_units + WAVES * DECODE_LDS_DPW - 1) / (WAVES * DECODE_LDS_DPW);
+  constexpr uint32_t DW = DECODE_NT / 64;
+  const uint32_t glds = (plan->n_units + DW * DECODE_LDS_DPW - 1) / (DW * DECODE_LDS_DPW);
   const coalac_sched_t* sc = sched;
   auto B = [&](int i) { return at_boundary(stages, DEC_SPAN, 2, i) ? boundary(sc, i, st) : COALAC_OK; };
 #define DEC_BOUNDARY(i)       \
@@ -3223,7 +3236,7 @@ int coalac_decode_sched(coalac_plan_t plan, const int32_t* d_idx, const void* d_
     if (search)                                                                            \
       hipLaunchKernelGGL((k_decode<R, H, true>), dim3(g), dim3(BLOCK), 0, st, P);          \
     else if (DECODE_LDS)                                                                   \
-      hipLaunchKernelGGL((k_decode_lds<R, H>), dim3(glds), dim3(BLOCK), 0, st, P);         \
+      hipLaunchKernelGGL((k_decode_lds<R, H>), dim3(glds), dim3(DECODE_NT), 0, st, P);     \
     else                                                                                   \
       hipLaunchKernelGGL((k_decode<R, H, false>), dim3(g), dim3(BLOCK), 0, st, P);         \
   } while (0)
