@@ -2787,6 +2787,10 @@ bool at_boundary(unsigned stages, const int (*span)[2], int nst, int i) {
 // decode plans of up to this many 4096-element units (~1.3 ResNet-50 updates) search their entry ranges
 // in k_decode; bigger ones run k_bounds first
 constexpr uint32_t DECODE_SEARCH_MAX_UNITS = 8192;
+#ifndef DECODE_LAT_LDS
+#define DECODE_LAT_LDS 0  // 1: latency-bound plans decode like batches (k_bounds + k_decode_lds)
+#endif
+constexpr uint32_t DECODE_SEARCH_UNITS = DECODE_LAT_LDS ? 0u : DECODE_SEARCH_MAX_UNITS;
 
 constexpr int ENC_SPAN[4][2] = {{0, 1}, {1, 2}, {2, 4}, {0, 1}};  // SAMPLE, SCAN, SELECT, SMALL
 constexpr int DEC_SPAN[2][2] = {{0, 1}, {1, 2}};                  // BOUNDS, DECODE
@@ -3181,7 +3185,7 @@ int coalac_decode_sched(coalac_plan_t plan, const int32_t* d_idx, const void* d_
   // plans of > DECODE_SEARCH_MAX_UNITS units read the per-unit entry bounds k_bounds leaves in the workspace:
   // the kept values need BOUNDS in this call, or the caller's word (BOUNDS_DONE) that an earlier call
   // enqueued it on this workspace for these arrays, ordered before this one (else stale bounds mis-decode)
-  if (plan->n_units > DECODE_SEARCH_MAX_UNITS && (stages & COALAC_STAGE_SCATTER) && !(stages & COALAC_STAGE_BOUNDS) &&
+  if (plan->n_units > DECODE_SEARCH_UNITS && (stages & COALAC_STAGE_SCATTER) && !(stages & COALAC_STAGE_BOUNDS) &&
       !(sched && (sched->stages & COALAC_STAGE_BOUNDS_DONE)))
     return fail(COALAC_EINVAL, "coalac_decode: a plan of %u units decodes its kept values from the bounds of "
                 "COALAC_STAGE_BOUNDS: pass BOUNDS in the same call, or BOUNDS_DONE after a BOUNDS call on this "
@@ -3212,7 +3216,7 @@ int coalac_decode_sched(coalac_plan_t plan, const int32_t* d_idx, const void* d_
   const bool raw = plan->bits == 32, hb = d_base != nullptr;
   // small plans: k_decode finds its units' entry ranges itself (one launch), or (DECODE_SCATTER) the
   // background and then the kept values; batches: k_bounds first
-  const bool search = plan->n_units <= DECODE_SEARCH_MAX_UNITS;
+  const bool search = plan->n_units <= DECODE_SEARCH_UNITS;
   const bool scatter = (search || DECODE_SCATTER_ALL) && DECODE_SCATTER;
   const uint32_t upb = WAVES * (hb ? decode_dpw<true, false>()
                                    : search ? decode_dpw<false, true>() : decode_dpw<false, false>());  // units per block
