@@ -2140,10 +2140,12 @@ __global__ __launch_bounds__(BLOCK, DECODE_WPE) void k_decode(Params P) {
 
 // k_decode_lds (batches, DECODE_LDS): the same output as k_decode, with the kept values placed through a
 // per-wave LDS tile instead of the register merge (a wave-uniform walk over every kept entry: ~10 VALU per
-// entry, ~450 per unit, as much issue time per unit as its 16 stores). A unit is written as 4 quarters of 4
-// rows (1,024 elements): the quarter's kept values are scattered into the zeroed 4 KiB tile (one ds_write per
-// 64 entries), its 4 rows read back (ds_read_b128, + base in delta mode) and stored, and the same slots zeroed
-// again. Entries outside the unit (an untrusted list) never match a quarter and are dropped.
+// entry, ~450 per unit, as much issue time per unit as its 16 stores). A unit is written in passes of QROWS rows
+// (8 in weights mode, 4 in delta mode): the pass's kept values are scattered into the zeroed per-wave tile (one
+// ds_write per 64 entries), its rows read back (ds_read_b128, + base in delta mode) and stored, and the same
+// slots zeroed again; one unit per wave. Fewer, larger passes and one unit per wave measured faster than 4-row
+// passes over 2 units (C3 0.672 -> 0.622 ms per step, profiles/r03_decode_ab.txt). Entries outside the unit (an
+// untrusted list) never match a pass and are dropped.
 #ifndef DECODE_LDS
 #define DECODE_LDS 1
 #endif
