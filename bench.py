@@ -201,13 +201,14 @@ def pmc_traffic(kernel, cfg, a, split):
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_summary.json")))
     if not default or not files:
         return None, None
-    with open(files[-1]) as f:
-        d = json.load(f)
     names = {"k_decode": ("k_decode_lds", "k_decode")}.get(kernel, (kernel,))  # (the batch decode kernel)
-    for want in names:
-        for name, e in sorted(d.items()):
-            if name.split("<")[0] == want and "FETCH_SIZE_x2_bytes" in e and "WRITE_SIZE_bytes" in e:
-                return e["FETCH_SIZE_x2_bytes"] + e["WRITE_SIZE_bytes"], os.path.relpath(files[-1], ROOT)
+    for path in reversed(files):  # the newest summary that holds the kernel
+        with open(path) as f:
+            d = json.load(f)
+        for want in names:
+            for name, e in sorted(d.items()):
+                if name.split("<")[0] == want and "FETCH_SIZE_x2_bytes" in e and "WRITE_SIZE_bytes" in e:
+                    return e["FETCH_SIZE_x2_bytes"] + e["WRITE_SIZE_bytes"], os.path.relpath(path, ROOT)
     return None, None
 
 
