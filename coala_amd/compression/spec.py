@@ -12,8 +12,9 @@ import numpy as np
 
 ALIGN = 32          # elements; 128-byte aligned segment starts (float4 loads need >= 4)
 RAW_BITS = 32       # bits == 32: values stored as raw fp32 (lossless at ratio 1)
-SMALL_MAX = 4096    # mirrors coalac.hip: segments up to this size are encoded by one block, no sampling
-SMALL_MAX_LATENCY = 1024   # ... in plans of <= LATENCY_PLAN_UNITS units (mirrors coalac.hip)
+SMALL_MAX = 4096    # mirrors coalac.hip: the largest small-segment limit (one block, no sampling; COALAC_SMALL_MAX)
+SMALL_MAX_BATCH = 1024     # mirrors coalac.hip: the default limit of batch plans
+SMALL_MAX_LATENCY = 1024   # ... and of plans of <= LATENCY_PLAN_UNITS units (mirrors coalac.hip)
 LATENCY_PLAN_UNITS = 8192
 UNIT = 4096         # mirrors coalac.hip: elements per wave work unit
 VALID_BITS = tuple(range(1, 9)) + (RAW_BITS,)
@@ -22,9 +23,9 @@ VALID_BITS = tuple(range(1, 9)) + (RAW_BITS,)
 def small_limit(sizes):
     """The largest segment a plan over these segment sizes encodes whole in one block (coalac.hip
     coalac_plan_create): SMALL_MAX_LATENCY for latency-bound plans of <= LATENCY_PLAN_UNITS units, else
-    SMALL_MAX (COALAC_SMALL_MAX overrides, clamped to [1024, SMALL_MAX])."""
+    SMALL_MAX_BATCH (COALAC_SMALL_MAX overrides, clamped to [1024, SMALL_MAX])."""
     units = sum((min(int(n), 1 << 31) + UNIT - 1) // UNIT for n in sizes)
-    lim = SMALL_MAX_LATENCY if units <= LATENCY_PLAN_UNITS else SMALL_MAX
+    lim = SMALL_MAX_LATENCY if units <= LATENCY_PLAN_UNITS else SMALL_MAX_BATCH
     env = os.environ.get("COALAC_SMALL_MAX")
     if env:
         lim = min(max(int(env), 1024), SMALL_MAX)

@@ -62,7 +62,11 @@ constexpr int WAVES = BLOCK / 64;
 constexpr uint32_t UNIT = 4096;           // elements per wave work unit
 constexpr uint32_t UNIT_SHIFT = 12;
 constexpr uint32_t UNIT_IT = UNIT / 256;  // float4 loads per lane per unit
-constexpr uint32_t SMALL_MAX = 4096;      // segments up to this size are encoded whole in one block
+constexpr uint32_t SMALL_MAX = 4096;      // segments up to this size can be encoded whole in one block (the
+                                          // small-segment LDS arena; COALAC_SMALL_MAX may raise the limit to it)
+constexpr uint32_t SMALL_MAX_BATCH = 1024;  // ... and are, by default, in batch plans (4096 until round 3: C2
+                                            // 0.296-0.314 -> 0.280-0.285 ms per step, C3 / C4 equal or faster;
+                                            // a 4096-element block select takes 14 us, the sampled path streams it)
 constexpr uint32_t SMALL_MAX_LATENCY = 1024;  // ... in latency-bound plans (<= LATENCY_PLAN_UNITS units): a
                                               // block's radix select grows with n (64: 5 us, 2048: 9 us,
                                               // 4096: 14 us, alone on a CU) and the slowest small segment set
@@ -2909,7 +2913,7 @@ int coalac_plan_create(const coalac_seg_t* h_segs, int nseg, int bits, coalac_pl
   std::vector<std::pair<uint64_t, uint64_t>> in_r, out_r;
   uint64_t est_units = 0;
   for (int s = 0; s < nseg; ++s) est_units += (std::min<uint64_t>(h_segs[s].n, 1ull << 31) + UNIT - 1) / UNIT;
-  uint32_t small_max = est_units <= LATENCY_PLAN_UNITS ? SMALL_MAX_LATENCY : SMALL_MAX;
+  uint32_t small_max = est_units <= LATENCY_PLAN_UNITS ? SMALL_MAX_LATENCY : SMALL_MAX_BATCH;
   if (const char* e = getenv("COALAC_SMALL_MAX")) small_max = std::min<uint32_t>(std::max(atoi(e), 1024), SMALL_MAX);
   for (int s = 0; s < nseg; ++s) {
     const coalac_seg_t& g = h_segs[s];

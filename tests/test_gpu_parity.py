@@ -134,7 +134,7 @@ def test_forked_small_segments_resnet50_x3(cuda, delta):
     xs = [gauss(rng, sizes) for _ in range(3)]
     bases = [gauss(rng, sizes) for _ in range(3)] if delta else None
     plan, g, r = run_both(sizes, 0.01, 8, xs, bases=bases, clients=3)
-    assert plan.n_units - sum(1 for n in sizes if 0 < n <= SMALL_MAX) * 3 >= 16384
+    assert plan.n_units - sum(1 for n in sizes if 0 < n <= small_limit(sizes * 3)) * 3 >= 16384
     assert_same(plan, g, r)
 
 

@@ -63,6 +63,7 @@ def test_constants_mirror_kernel():
     src = open(__import__("coala_amd._build", fromlist=["SRC"]).SRC).read()
     assert f"constexpr uint32_t SMALL_MAX = {spec.SMALL_MAX};" in src
     assert f"constexpr uint32_t SMALL_MAX_LATENCY = {spec.SMALL_MAX_LATENCY};" in src
+    assert f"constexpr uint32_t SMALL_MAX_BATCH = {spec.SMALL_MAX_BATCH};" in src
     assert f"constexpr uint32_t LATENCY_PLAN_UNITS = {spec.LATENCY_PLAN_UNITS};" in src
     assert f"constexpr uint32_t UNIT = {spec.UNIT};" in src
 
@@ -97,15 +98,15 @@ def test_subtable_extents():
 
 def test_small_limit_follows_plan_size(monkeypatch):
     """spec.small_limit mirrors coalac_plan_create: latency-bound plans (<= LATENCY_PLAN_UNITS units)
-    encode segments of up to SMALL_MAX_LATENCY elements whole, bigger plans up to SMALL_MAX; the
+    encode segments of up to SMALL_MAX_LATENCY elements whole, bigger plans up to SMALL_MAX_BATCH; the
     COALAC_SMALL_MAX override is clamped to [1024, SMALL_MAX]."""
     monkeypatch.delenv("COALAC_SMALL_MAX", raising=False)
     one = fp32_sizes("resnet50_tv")
     assert spec.small_limit(one) == spec.SMALL_MAX_LATENCY
-    assert spec.small_limit(one * 2) == spec.SMALL_MAX
+    assert spec.small_limit(one * 2) == spec.SMALL_MAX_BATCH
     units = spec.LATENCY_PLAN_UNITS
     assert spec.small_limit([spec.UNIT] * units) == spec.SMALL_MAX_LATENCY
-    assert spec.small_limit([spec.UNIT] * (units + 1)) == spec.SMALL_MAX
+    assert spec.small_limit([spec.UNIT] * (units + 1)) == spec.SMALL_MAX_BATCH
     monkeypatch.setenv("COALAC_SMALL_MAX", "4096")
     assert spec.small_limit(one) == 4096
     monkeypatch.setenv("COALAC_SMALL_MAX", "10")
