@@ -124,7 +124,7 @@ int coalac_decode_ev(coalac_plan_t plan, const int32_t* d_idx, const void* d_val
 /* Scheduled variants: identical work, split into stages that may be enqueued by separate calls on
  * separate streams. Stages (sched->stages bit mask; 0 = all):
  *   encode  COALAC_STAGE_SAMPLE  k_sample (large segments: sampled bracket)    boundaries 0 .. 1
- *           COALAC_STAGE_SMALL   k_small  (segments of <= 4096 elements, whole) 0 .. 1
+ *           COALAC_STAGE_SMALL   k_small  (segments of <= 1024 elements, whole) 0 .. 1
  *           COALAC_STAGE_SCAN    k_scan   (the one HBM read of the large segments) 1 .. 2
  *           COALAC_STAGE_SELECT  k_ghist k_gwin k_select k_emit                  2 .. 4
  *   decode  COALAC_STAGE_BOUNDS  k_bounds (plans of > 8192 units; smaller    boundaries 0 .. 1
