@@ -96,6 +96,12 @@ def parse():
                         "0.0922 vs 0.0786 ms per single step (the cross-stream edges cost more than the fill)")
     p.add_argument("--cpu-seconds", type=float, default=8.0, help="CPU baseline time budget per leg")
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--launch-check", action="store_true",
+                   help="test hook (CPU, no GPU): every rank joins a gloo group from the launcher's environment and "
+                        "rank 0 prints the ranks' (RANK, LOCAL_RANK, WORLD_SIZE); tests/test_bench_launch.py")
+    p.add_argument("--launch-check-fail", type=int, default=-1,
+                   help="with --launch-check: this rank exits with code 3 before joining (the others block in the "
+                        "rendezvous until the launcher stops them)")
     return p.parse_args()
 
 
@@ -190,13 +196,14 @@ def cpu_baseline(layout, ratio, bits, budget_s):
 # ----------------------------------------------------------------------------------------------------
 # GPU workloads
 # ----------------------------------------------------------------------------------------------------
-def pmc_traffic(kernel, cfg, a, split):
+def pmc_traffic(kernel, cfg, a, split, world=1):
     """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC summary of the default workload
     (profiles/rNN_pmc_summary.json, written by tools/profile_round.sh + tools/pmc_summary.py): FETCH_SIZE
     doubled (gfx950 reports half the bytes of wide coalesced streaming reads, MI355X_MICROARCH.md §HBM)
-    + WRITE_SIZE. Only reported for the default configuration the summary was collected on."""
+    + WRITE_SIZE. Only reported for the configuration the summary was collected on: the default workload on
+    ONE GPU (a multi-rank line gets null — its ranks were never profiled)."""
     import glob
-    default = (cfg, a.layout, a.clients, a.ratio, a.bits, a.mode, a.inflight, split) == \
+    default = world == 1 and (cfg, a.layout, a.clients, a.ratio, a.bits, a.mode, a.inflight, split) == \
         ("C3", None, None, 0.01, 8, "weights", 1, SPLIT)
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_summary.json")))
     if not default or not files:
@@ -393,10 +400,8 @@ def time_workload(W, a, dev, world):
     if world > 1:
         dist.barrier()
     el = time.perf_counter() - t0
-    if world > 1:
-        x = torch.tensor([el], dtype=torch.float64, device=dev)
-        dist.all_reduce(x, op=dist.ReduceOp.MAX)
-        el = x.item()
+    rank_el = gather_elapsed(el, world, dev)
+    el = max(rank_el)  # the job's time: the slowest rank
 
     # Roofline steps (after the timed region, not part of `value`): per sub-batch, HIP events [1] / [2]
     # recorded on its own stream around its streaming kernels, each step joined with the caller's stream
@@ -454,15 +459,39 @@ def time_workload(W, a, dev, world):
         "sample_fallbacks": W.get("fallbacks", 0),
         "graph": W["graph_error"] or (graphs is not None and f"{W['gk']} step(s) per graph launch"),
         "fill_ahead": W["fill_ahead"] and all(p.n_parts == 1 for p in pipes),
+        "rank_ms_per_step": rank_spread(rank_el, a.steps),
     }
     if headline:
-        traffic, src = pmc_traffic(dom, W["cfg"], a, split)
+        traffic, src = pmc_traffic(dom, W["cfg"], a, split, world)
         res["roofline"]["traffic"] = traffic * split if traffic is not None else None
         res["roofline"]["traffic_source"] = src
         res["stage_timing"] = (f"HIP events on each sub-batch stream around k_scan / k_decode, union over the "
                                f"{split} concurrent launches, mean of {len(timed_steps)} joined steps run after the "
                                f"timed region")
     return res
+
+
+def gather_elapsed(el, world, device):
+    """Every rank's elapsed seconds of the timed region, in rank order, on every rank (one all_gather; RCCL
+    needs device tensors, gloo host ones). world == 1: [el]."""
+    if world == 1:
+        return [el]
+    import torch
+    import torch.distributed as dist
+    if dist.get_backend() != "nccl":
+        device = "cpu"
+    x = torch.tensor([el], dtype=torch.float64, device=device)
+    out = [torch.zeros_like(x) for _ in range(world)]
+    dist.all_gather(out, x)
+    return [float(t.item()) for t in out]
+
+
+def rank_spread(rank_el, steps):
+    """Per-rank ms per step of a multi-rank run (load imbalance shows as max / min > 1); None for one rank."""
+    if len(rank_el) == 1:
+        return None
+    ms = [e / steps * 1e3 for e in rank_el]
+    return {"min": round(min(ms), 4), "max": round(max(ms), 4), "per_rank": [round(m, 4) for m in ms]}
 
 
 def release_workload(W):
@@ -597,6 +626,26 @@ def launch_ranks(a):
     return rc
 
 
+def launch_check(a, world, rank, local):
+    """--launch-check: the launcher's plumbing without a GPU — rendezvous over gloo on MASTER_ADDR / MASTER_PORT
+    from the environment, gather every rank's (RANK, LOCAL_RANK, WORLD_SIZE) and print them from rank 0."""
+    if rank == a.launch_check_fail:
+        return 3
+    import torch
+    import torch.distributed as dist
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    mine = torch.tensor([rank, local, world], dtype=torch.int64)
+    allr = [torch.zeros_like(mine) for _ in range(world)]
+    dist.all_gather(allr, mine)
+    times = gather_elapsed(0.01 * (rank + 1), world, "cpu")  # the timed region's per-rank gather, fake times
+    if rank == 0:
+        print(json.dumps({"metric": "launch-check", "ranks": [t.tolist() for t in allr],
+                          "rank_ms_per_step": rank_spread(times, 1),
+                          "master": [os.environ.get("MASTER_ADDR"), os.environ.get("MASTER_PORT")]}), flush=True)
+    dist.destroy_process_group()
+    return 0
+
+
 def main():
     a = parse()
     if a.gpus > 1 and "WORLD_SIZE" not in os.environ:
@@ -606,6 +655,8 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != a.gpus:
         raise SystemExit(f"--gpus {a.gpus} but WORLD_SIZE={world}")
+    if a.launch_check:
+        sys.exit(launch_check(a, world, rank, local))
     cpu = None
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         layout = a.layout or CONFIGS[a.config][0]
@@ -664,10 +715,10 @@ def main():
                        "parallelism": f"replicas{world}"},
             "roofline": head["roofline"], "step_roofline": head["step_roofline"], "stages_ms": head["stages_ms"],
             "stage_timing": head["stage_timing"], "sample_fallbacks": head["sample_fallbacks"],
-            "graph": head["graph"],
+            "graph": head["graph"], "rank_ms_per_step": head["rank_ms_per_step"],
             "configs": {k: {f: v[f] for f in ("value", "ms_per_step", "step_roofline", "roofline", "stages_ms", "desc",
                                               "elements_per_gpu", "segments_per_gpu", "split", "inflight", "rotation",
-                                              "graph", "fill_ahead", "sample_fallbacks")}
+                                              "graph", "fill_ahead", "sample_fallbacks", "rank_ms_per_step")}
                         for k, v in results.items()},
         }
         if plugin is not None:

@@ -144,7 +144,9 @@ class _StateWalk:
     """The tensors of a module's state_dict, in state_dict order, without building the state_dict: the
     module tree walked once (pre-order, as Module.state_dict recurses), then per call each module's
     parameter and persistent-buffer tables read in place (no per-entry detach, no prefix strings, no
-    state-dict hooks: the reference's models register none). Re-walked when a table's size changes."""
+    state-dict hooks: the reference's models register none). Re-walked when a table's size changes, when a
+    submodule is replaced or added (each module's children are compared by identity: a client that keeps one
+    root module across rounds may swap `model.head`), or when the non-persistent buffer set changes."""
 
     def __init__(self, module):
         self.mods, names = [], []
@@ -154,17 +156,19 @@ class _StateWalk:
             self.hooked = self.hooked or bool(m._state_dict_hooks or m._state_dict_pre_hooks)
             pn = tuple(k for k, v in m._parameters.items() if v is not None)
             bn = tuple(k for k, v in m._buffers.items() if v is not None and k not in m._non_persistent_buffers_set)
-            self.mods.append((m, pn, bn))
-            self.sizes.append((len(m._parameters), len(m._buffers)))
+            self.mods.append((m, pn, bn, tuple(m._modules.values()), frozenset(m._non_persistent_buffers_set)))
+            self.sizes.append((len(m._parameters), len(m._buffers), len(m._modules)))
             p = prefix + "." if prefix else ""
             names.extend(p + k for k in pn + bn)
         self.names = tuple(names)
 
     def tensors(self):
         out = []
-        for (m, pn, bn), (np_, nb) in zip(self.mods, self.sizes):
-            P, B = m._parameters, m._buffers
-            if len(P) != np_ or len(B) != nb:
+        for (m, pn, bn, kids, npb), (np_, nb, nk) in zip(self.mods, self.sizes):
+            P, B, C = m._parameters, m._buffers, m._modules
+            if len(P) != np_ or len(B) != nb or len(C) != nk or not all(map(is_, C.values(), kids)):
+                return None
+            if npb != m._non_persistent_buffers_set:
                 return None
             out.extend(map(P.__getitem__, pn))
             out.extend(map(B.__getitem__, bn))
@@ -252,6 +256,11 @@ def _to_host(*ts):
 
 
 _NP_DTYPES = {torch.float32: np.float32, torch.int32: np.int32, torch.uint8: np.uint8, torch.int64: np.int64}
+# the dtypes a passthrough entry of a blob may name (a state_dict's non-fp32 or empty entries); a blob naming
+# anything else is rejected rather than handed to getattr(torch, ...)
+_RAW_DTYPES = {_dtype_name(d): d for d in (torch.float32, torch.float64, torch.float16, torch.bfloat16, torch.int64,
+                                          torch.int32, torch.int16, torch.int8, torch.uint8, torch.bool,
+                                          torch.complex64, torch.complex128)}
 
 
 class RawState(Mapping):
@@ -320,13 +329,22 @@ class RawState(Mapping):
 
         def flush():
             if run:
-                dt = getattr(torch, run[0]["dtype"])
+                dt = _RAW_DTYPES.get(run[0]["dtype"])
+                if dt is None:
+                    raise ValueError(f"COALAQ1: unsupported raw entry dtype {run[0]['dtype']!r}")
+                size = torch.empty(0, dtype=dt).element_size()
+                members = []
+                for e in run:  # every entry's byte count must match its own shape (not only the run's total)
+                    m = int(np.prod(e["shape"], dtype=np.int64))
+                    if m < 0 or int(e["nbytes"]) != m * size:
+                        raise ValueError(f"COALAQ1: raw entry {e['name']!r}: {e['nbytes']} bytes for shape "
+                                         f"{e['shape']} of {e['dtype']}")
+                    members.append((e["name"], tuple(e["shape"]), m))
                 lo, hi = run[0]["off"], run[-1]["off"] + run[-1]["nbytes"]
+                if lo < 0 or hi > len(rawb):
+                    raise ValueError("COALAQ1: raw entries past the end of the blob")
                 buf = bytearray(rawb[lo:hi])
                 flat = torch.frombuffer(buf, dtype=dt) if buf else torch.empty(0, dtype=dt)
-                members = [(e["name"], tuple(e["shape"]), int(np.prod(e["shape"], dtype=np.int64))) for e in run]
-                if sum(m for _, _, m in members) != flat.numel():
-                    raise ValueError("COALAQ1: raw entry sizes inconsistent with their shapes")
                 groups.append((flat, members))
                 run.clear()
         for e in entries:
@@ -713,13 +731,16 @@ class UpdateCodec:
     WS_CACHE = 16  # encode workspaces kept per codec (one per plan and launch stream in use)
 
     def _workspace(self, plan):
-        """The encode workspace of `plan` for the current stream, reused across calls (kernels on one stream
-        run in order, so consecutive encodes can share it). A bounded LRU: an evicted workspace was allocated
-        on its stream, whose later allocations are the only ones that can reuse it (stream-ordered)."""
+        """The encode workspace of `plan` for the current thread and stream, reused across calls (kernels on
+        one stream run in order, so consecutive encodes of one thread can share it). Keyed by thread too: two
+        threads encoding on one stream (e.g. both on the default stream) interleave their launches, since the
+        ctypes call releases the GIL, and one encode's select would read the other's scan results. A bounded
+        LRU: an evicted workspace was allocated on its stream, whose later allocations are the only ones that
+        can reuse it (stream-ordered)."""
         if not hasattr(plan, "empty_workspace"):
             return None
         stream = torch.cuda.current_stream(plan.device) if plan.device.type == "cuda" else None
-        key = (id(plan), None if stream is None else stream.cuda_stream)
+        key = (id(plan), threading.get_ident(), None if stream is None else stream.cuda_stream)
         with self._lock:
             hit = self._ws.get(key)
             if hit is not None and hit[0] is plan:

@@ -99,3 +99,50 @@ def test_launcher_forwards_only_rank0_json_line(monkeypatch, capsys):
     assert rc == 0
     assert out == '{"metric": "m", "value": 1}\n'  # the library's status line went to stderr
     assert "[Gloo]" in err
+
+
+def _launch_real(argv, timeout):
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "MASTER_PORT")}
+    env["MASTER_ADDR"] = "127.0.0.1"
+    return subprocess.run([sys.executable, os.path.join(ROOT, "bench.py")] + argv, env=env, capture_output=True,
+                          text=True, timeout=timeout, cwd=ROOT)
+
+
+def test_real_launch_of_four_ranks_plumbs_the_environment():
+    """A real `bench.py --gpus 4` launch (rank processes, not fakes) on the CPU: the 4 ranks rendezvous over gloo
+    with the launcher's MASTER_ADDR / MASTER_PORT and report RANK / LOCAL_RANK / WORLD_SIZE 0..3 / 4."""
+    import json
+    r = _launch_real(["--gpus", "4", "--launch-check"], timeout=240)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.strip()]
+    assert len(lines) == 1, r.stdout
+    d = json.loads(lines[0])
+    assert d["ranks"] == [[i, i, 4] for i in range(4)]
+    assert d["rank_ms_per_step"] == {"min": 10.0, "max": 40.0, "per_rank": [10.0, 20.0, 30.0, 40.0]}
+    assert d["master"][0] == "127.0.0.1" and int(d["master"][1]) > 0
+
+
+def test_real_launch_fails_fast_when_one_rank_fails():
+    """Rank 2 exits with code 3 before the rendezvous; ranks 0, 1, 3 would wait in init_process_group forever.
+    The launcher returns rank 2's code and stops the others well before the rendezvous timeout."""
+    import time
+    t0 = time.perf_counter()
+    r = _launch_real(["--gpus", "4", "--launch-check", "--launch-check-fail", "2"], timeout=240)
+    assert r.returncode == 3, r.stderr[-2000:]
+    assert time.perf_counter() - t0 < 120
+
+
+def test_rank_spread_and_gather_single_rank():
+    assert bench.gather_elapsed(1.5, 1, None) == [1.5]
+    assert bench.rank_spread([1.5], 10) is None
+    s = bench.rank_spread([0.02, 0.03, 0.025], 10)
+    assert s["min"] == 2.0 and s["max"] == 3.0 and s["per_rank"] == [2.0, 3.0, 2.5]
+
+
+def test_pmc_traffic_only_for_one_gpu(monkeypatch):
+    monkeypatch.setattr(sys, "argv", ["bench.py"])
+    a = bench.parse()
+    traffic1, _ = bench.pmc_traffic("k_scan", "C3", a, bench.SPLIT, world=1)
+    traffic8, src8 = bench.pmc_traffic("k_scan", "C3", a, bench.SPLIT, world=8)
+    assert traffic8 is None and src8 is None
+    assert traffic1 is not None  # the committed one-GPU summary

@@ -98,3 +98,15 @@ def test_module_tensors_matches_state_dict_and_follows_changes():
     m.b1.conv.weight = nn.Parameter(torch.zeros(3, 2, 3, 3))  # replaced parameter: same table size
     _, ts3 = module_tensors(m)
     assert any(t is m.b1.conv.weight for t in ts3)
+    # a replaced submodule (same table sizes everywhere): the walk must return the NEW module's tensors
+    m.shared = nn.Linear(4, 4)
+    names4, ts4 = module_tensors(m)
+    st4 = m.state_dict()
+    assert names4 == tuple(st4) and [t.data_ptr() for t in ts4] == [v.data_ptr() for v in st4.values()]
+    # a replaced grandchild, and a buffer turned non-persistent
+    m.b1.bn = nn.BatchNorm2d(3)
+    names5, ts5 = module_tensors(m)
+    assert [t.data_ptr() for t in ts5] == [v.data_ptr() for v in m.state_dict().values()]
+    m.b1._non_persistent_buffers_set.add("extra_buf")
+    names6, _ = module_tensors(m)
+    assert names6 == tuple(m.state_dict()) and "b1.extra_buf" not in names6

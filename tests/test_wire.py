@@ -88,3 +88,21 @@ def test_sections_locate_the_unpacked_arrays():
         o, n = sec[name]
         assert o % 16 == 0 and n == arr.nbytes
         assert blob[o:o + n] == arr.tobytes()
+
+
+def test_raw_entries_checked_one_by_one():
+    """Raw (passthrough) entries of an untrusted blob: each entry's byte count must match its own shape, even
+    when the run's total does, and the dtype must be one a state_dict holds."""
+    from coala_amd.compression.codec import RawState
+    rawb = np.arange(4, dtype=np.int64).tobytes()
+    good = [{"name": "a", "dtype": "int64", "shape": [1], "off": 0, "nbytes": 8},
+            {"name": "b", "dtype": "int64", "shape": [3], "off": 8, "nbytes": 24}]
+    r = RawState.from_entries(good, rawb)
+    assert r["b"].tolist() == [1, 2, 3]
+    swapped = [dict(good[0], nbytes=24), dict(good[1], off=24, nbytes=8)]  # same total, wrong split
+    with pytest.raises(ValueError):
+        RawState.from_entries(swapped, rawb)
+    with pytest.raises(ValueError):
+        RawState.from_entries([dict(good[0], dtype="Tensor")], rawb)
+    with pytest.raises(ValueError):
+        RawState.from_entries([dict(good[1], off=16)], rawb)  # past the end of the raw section
