@@ -41,20 +41,23 @@ SIGNATURES = [
     ("coalac_plan_destroy", _I, [_P]),
     ("coalac_plan_query", _I, [_P, ctypes.POINTER(_U64), ctypes.POINTER(_U64), ctypes.POINTER(_U64),
                                ctypes.POINTER(_U64), ctypes.POINTER(_U64)]),
-    ("coalac_encode", _I, [_P, _P, _P, _P, _P, _P, _P, _P, _U64, ctypes.c_uint, _P]),
-    ("coalac_encode_segptr", _I, [_P, _P, _P, _P, _P, _P, _P, _P, _U64, ctypes.c_uint, _P]),
-    ("coalac_decode", _I, [_P, _P, _P, _P, _P, _P, _P, _P, _U64, _P]),
-    ("coalac_encode_ev", _I, [_P, _P, _P, _P, _P, _P, _P, _P, _U64, ctypes.c_uint, _P, _P]),
-    ("coalac_decode_ev", _I, [_P, _P, _P, _P, _P, _P, _P, _P, _U64, _P, _P]),
-    ("coalac_encode_sched", _I, [_P, _P, _P, _P, _P, _P, _P, _P, _U64, ctypes.c_uint, _P, _P]),
-    ("coalac_decode_sched", _I, [_P, _P, _P, _P, _P, _P, _P, _P, _U64, _P, _P]),
-    ("coalac_aggregate", _I, [_P, _I, _P, _P, _P, _P, _P, ctypes.c_float, _I, _P, _P, _P, _P, _U64, _P]),
-    ("coalac_aggregate_ev", _I, [_P, _I, _P, _P, _P, _P, _P, ctypes.c_float, _I, _P, _P, _P, _P, _U64, _P, _P]),
+    # encode: plan, in / seg pointers, base, idx, vals, mn, scale, ustart, ws, ws_bytes, flags, stream (+ events / sched)
+    ("coalac_encode", _I, [_P, _P, _P, _P, _P, _P, _P, _P, _P, _U64, ctypes.c_uint, _P]),
+    ("coalac_encode_segptr", _I, [_P, _P, _P, _P, _P, _P, _P, _P, _P, _U64, ctypes.c_uint, _P]),
+    # decode: plan, idx, vals, mn, scale, ustart, base, out, ws, ws_bytes, stream (+ events / sched)
+    ("coalac_decode", _I, [_P, _P, _P, _P, _P, _P, _P, _P, _P, _U64, _P]),
+    ("coalac_encode_ev", _I, [_P, _P, _P, _P, _P, _P, _P, _P, _P, _U64, ctypes.c_uint, _P, _P]),
+    ("coalac_decode_ev", _I, [_P, _P, _P, _P, _P, _P, _P, _P, _P, _U64, _P, _P]),
+    ("coalac_encode_sched", _I, [_P, _P, _P, _P, _P, _P, _P, _P, _P, _U64, ctypes.c_uint, _P, _P]),
+    ("coalac_decode_sched", _I, [_P, _P, _P, _P, _P, _P, _P, _P, _P, _U64, _P, _P]),
+    # aggregate: plan, clients, idx, vals, mn, scale, ustart, weights, total, mode, mask, base, out, ws, ws_bytes, stream
+    ("coalac_aggregate", _I, [_P, _I, _P, _P, _P, _P, _P, _P, ctypes.c_float, _I, _P, _P, _P, _P, _U64, _P]),
+    ("coalac_aggregate_ev", _I, [_P, _I, _P, _P, _P, _P, _P, _P, ctypes.c_float, _I, _P, _P, _P, _P, _U64, _P, _P]),
     ("coalac_workspace_fallbacks", _I, [_P, _P, _P, ctypes.POINTER(_I)]),
     ("coalac_debug_stamps", _I, [_P, _P, _P, ctypes.POINTER(ctypes.c_uint64), _I]),
 ]
 
-ABI_VERSION = 3
+ABI_VERSION = 4
 
 
 class CodecError(RuntimeError):

@@ -27,7 +27,7 @@ from torch import nn
 
 from . import wire
 from .plan import CodecPlan, Encoded
-from .spec import ALIGN, RAW_BITS, VALID_BITS, SegmentTable, align_up, k_for
+from .spec import ALIGN, RAW_BITS, UNIT, VALID_BITS, SegmentTable, align_up, k_for
 
 MODES = ("delta", "weights")
 
@@ -445,7 +445,7 @@ class CompressedUpdate:
         ib = 0 if h["ratio"] >= 1.0 else 4  # ratio 1: indices implied, not shipped (wire.py "dense")
         raw_b = self.raw.nbytes if isinstance(self.raw, RawState) else \
             sum(t.numel() * t.element_size() for t in self.raw.values())
-        return 8 * h["n_segments"] + (ib + vb) * h["total_k"] + raw_b
+        return 8 * h["n_segments"] + (ib + vb) * h["total_k"] + 4 * h.get("n_units", 0) + raw_b
 
     def parameters(self):
         """One meta tensor whose numel * 32 bit equals the payload size, so the reference's
@@ -466,7 +466,8 @@ class CompressedUpdate:
             for n, t in raw.items()}
         # the header (with each raw entry's blob offset) depends on the layout and the raw byte counts only
         sizes = tuple(len(rawb[n]) for n in rawb)
-        key = (id(h["entries"]), h["ratio"], h["bits"], h["mode"], h["n_segments"], h.get("total_k"), sizes)
+        key = (id(h["entries"]), h["ratio"], h["bits"], h["mode"], h["n_segments"], h.get("total_k"),
+               h.get("n_units"), sizes)
         hit = _PACKED_HEADERS.get(key)
         if hit is not None and hit[0] is h["entries"]:
             hjson = hit[1]
@@ -487,9 +488,13 @@ class CompressedUpdate:
                 while len(_PACKED_HEADERS) > 16:
                     _PACKED_HEADERS.popitem(last=False)
         enc = self.encoded
-        arrs = _to_host(enc.mn, enc.scale, enc.idx, enc.vals)
-        return wire.pack({"dense": h["ratio"] >= 1.0}, *arrs, b"".join(rawb[e["name"]] for e in h["entries"]
-                                                                        if e["kind"] == "raw"), header_json=hjson)
+        v2 = "n_units" in h  # wire v2: the per-unit starts ride along
+        arrs = _to_host(enc.mn, enc.scale, enc.idx, enc.vals, *((enc.ustart,) if v2 else ()))
+        pack_h = {"dense": h["ratio"] >= 1.0}
+        if v2:
+            pack_h["n_units"] = h["n_units"]
+        return wire.pack(pack_h, *arrs[:4], b"".join(rawb[e["name"]] for e in h["entries"] if e["kind"] == "raw"),
+                         header_json=hjson, ustart=arrs[4] if v2 else None)
 
     def encoded_to(self, device, staging=None):
         """The encoded buffers on `device`. An unpickled update (the server side of a remote upload,
@@ -503,7 +508,8 @@ class CompressedUpdate:
             return self.encoded.to(device, non_blocking=True)
         _, sec = wire.sections(blob, self.header)
         lo = sec["mn"][0]
-        hi = sec["vals"][0] + sec["vals"][1]
+        last = sec["ustart"] if "ustart" in sec else sec["vals"]
+        hi = last[0] + last[1]
         stage = staging(hi - lo)
         stage[:hi - lo].numpy()[:] = np.frombuffer(blob, dtype=np.uint8, count=hi - lo, offset=lo)
         dev = torch.empty(hi - lo, dtype=torch.uint8, device=device)
@@ -514,15 +520,16 @@ class CompressedUpdate:
             o, n = sec[name]
             return dev[o - lo:o - lo + n].view(dt)
         return Encoded(view("idx", torch.int32), view("vals", vdt), view("mn", torch.float32),
-                       view("scale", torch.float32))
+                       view("scale", torch.float32), view("ustart", torch.int32) if "ustart" in sec else None)
 
     @classmethod
     def from_bytes(cls, blob):
-        h, mn, scale, idx, vals, rawb = wire.unpack(blob)
-        validate(h, idx)
+        h, mn, scale, idx, vals, rawb, ustart = wire.unpack(blob)
+        validate(h, idx, ustart)
         raw = RawState.from_entries([e for e in h["entries"] if e["kind"] == "raw"], rawb)
         enc = Encoded(torch.from_numpy(idx.copy()), torch.from_numpy(vals.copy()),
-                      torch.from_numpy(mn.copy()), torch.from_numpy(scale.copy()))
+                      torch.from_numpy(mn.copy()), torch.from_numpy(scale.copy()),
+                      None if ustart is None else torch.from_numpy(ustart.copy()))
         return cls(h, enc, raw, blob=bytes(blob))
 
     def __getstate__(self):
@@ -547,13 +554,14 @@ class CompressedUpdate:
                 f"segments={h['n_segments']}, kept={h['total_k']}, bytes={self.nbytes})")
 
 
-_VALIDATED = OrderedDict()  # (id(entries), ratio, n_segments, total_k) -> (entries, ns_rep, first) of a checked layout
+_VALIDATED = OrderedDict()  # (id(entries), ratio, n_segments, total_k) -> (entries, ns_rep, first, units) of a layout
 
 
-def validate(header, idx):
+def validate(header, idx, ustart=None):
     """Check an (untrusted) blob's index lists: per fp32 segment, k = k_for(n, ratio) entries, strictly
-    increasing, inside [0, n). The decode kernels are bounds-safe anyway; this turns a corrupt upload
-    into an error instead of a silently wrong model. The header's structure is checked once per layout
+    increasing, inside [0, n); and (wire v2) the per-unit starts: exactly the lower bounds of every unit's
+    first element in its segment's list. The decode kernels are bounds-safe anyway; this turns a corrupt
+    upload into an error instead of a silently wrong model. The header's structure is checked once per layout
     (headers of one layout share their entries list: wire._parse_header); the indices every call."""
     if header.get("bits") not in VALID_BITS or header.get("mode") not in MODES:
         raise ValueError("COALAQ1: bad bits/mode")
@@ -566,9 +574,12 @@ def validate(header, idx):
             _VALIDATED[key] = hit
             while len(_VALIDATED) > 32:
                 _VALIDATED.popitem(last=False)
-    _, ns_rep, first = hit
+    _, ns_rep, first, units = hit
     if idx.size != int(header["total_k"]):
         raise ValueError("COALAQ1: kept-entry count mismatch")
+    if ustart is not None and (units is None or int(header.get("n_units", -1)) != units[0].size
+                               or ustart.size != units[0].size):
+        raise ValueError("COALAQ1: per-unit start count mismatch")
     if ns_rep is None:
         return
     if idx.size and (int(idx.min()) < 0 or np.any(idx >= ns_rep)):
@@ -576,6 +587,13 @@ def validate(header, idx):
     d = np.diff(idx, prepend=np.int32(-1))
     if np.any((d <= 0) & ~first):
         raise ValueError("COALAQ1: indices not strictly increasing")
+    if ustart is not None:
+        # every entry's global unit (non-decreasing, the indices being sorted per segment): a unit starts where
+        # the first entry of that unit or a later one sits, relative to its segment's first entry
+        unit_seg_out, unit_base_rep, arange_u = units
+        gu = unit_base_rep + (idx >> 12)
+        if not np.array_equal(np.searchsorted(gu, arange_u) - unit_seg_out, ustart):
+            raise ValueError("COALAQ1: per-unit starts inconsistent with the indices")
 
 
 def _validate_layout(header):
@@ -593,13 +611,18 @@ def _validate_layout(header):
     if int(ks.sum()) != int(header["total_k"]):
         raise ValueError("COALAQ1: kept-entry count mismatch")
     if not ks.size:
-        return None, None
+        return None, None, None
     ns = np.array([e["n"] for e in segs], dtype=np.int32)
     ns_rep = np.repeat(ns, ks)  # each entry's segment size
     first = np.zeros(int(ks.sum()), dtype=bool)  # each segment's first entry (no predecessor to compare)
     first[np.cumsum(ks)[:-1][ks[1:] > 0] if ks.size > 1 else []] = True
     first[0] = True
-    return ns_rep, first
+    # wire v2: per unit its segment's first entry; per entry its segment's first global unit
+    nu = (ns.astype(np.int64) + UNIT - 1) // UNIT
+    seg_out = np.concatenate([[0], np.cumsum(ks)[:-1]]).astype(np.int64)
+    unit_base = np.concatenate([[0], np.cumsum(nu)[:-1]]).astype(np.int32)
+    units = (np.repeat(seg_out, nu), np.repeat(unit_base, ks), np.arange(int(nu.sum()), dtype=np.int32))
+    return ns_rep, first, units
 
 
 class UpdateCodec:
@@ -691,6 +714,8 @@ class UpdateCodec:
             fs = flatten_state(state_fn(), device=device)
             enc = plan.encode(fs.flat, base=base_flat, workspace=ws)
         header["total_k"] = int(plan.table.total_k)
+        if enc.ustart is not None and self.ratio < 1.0:  # wire v2 (a dense download implies its starts)
+            header["n_units"] = int(plan.table.n_units)
         return CompressedUpdate(header, enc, raw)
 
     def _thread_stream(self, device):
@@ -870,7 +895,8 @@ class UpdateCodec:
             C = len(updates)
             plan = self.plan_for(sizes, device, ratio=h0["ratio"], bits=h0["bits"], clients=C)
             encs = [u.encoded.to(device, non_blocking=True) for u in updates]
-            batched = Encoded(*(torch.cat([getattr(e, f) for e in encs]) for f in ("idx", "vals", "mn", "scale")))
+            batched = Encoded(*(torch.cat([getattr(e, f) for e in encs]) for f in ("idx", "vals", "mn", "scale")),
+                              torch.cat([e.ustart for e in encs]) if all(e.ustart is not None for e in encs) else None)
             avg_mask = None
             if params_only:
                 pnames = {n for n, _ in template.named_parameters(remove_duplicate=False)}

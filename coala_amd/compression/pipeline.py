@@ -12,7 +12,7 @@ import torch
 
 from . import _lib
 from .plan import CodecPlan, Encoded
-from .spec import LATENCY_PLAN_UNITS, SegmentTable
+from .spec import LATENCY_PLAN_UNITS, SegmentTable, units_of
 
 _STREAM_POOL = {}  # device index -> streams shared by every SplitPipeline of the process
 
@@ -109,24 +109,27 @@ class SplitPipeline:
         with torch.cuda.device(self.device):
             if S <= C:  # client ranges: ordinary plans over views of the batch buffers
                 cuts = balanced_cuts(table.client_elements(), S)
-                so, ko, to = table.client_span_off, table.client_k_off, table.client_seg_off
+                so, ko, to, uo = table.client_span_off, table.client_k_off, table.client_seg_off, table.client_unit_off
                 # stream_base: pipelines meant to run side by side (several batches in flight) take
                 # disjoint pool ranges; by default every pipeline starts at pooled stream 0
                 streams = pooled_streams(self.device, stream_base + len(cuts) - 1)[stream_base:]
                 for c0, c1, st in zip(cuts[:-1], cuts[1:], streams):
                     plan = CodecPlan(None, table.ratio, self.bits, device=self.device, table=table.sub_table(c0, c1))
                     self.parts.append(dict(x=slice(so[c0], so[c1]), k=slice(ko[c0], ko[c1]), t=slice(to[c0], to[c1]),
-                                           plan=plan, ws=plan.empty_workspace(), dws=plan.empty_decode_workspace(),
-                                           stream=st))
+                                           u=slice(uo[c0], uo[c1]), plan=plan, ws=plan.empty_workspace(),
+                                           dws=plan.empty_decode_workspace(), stream=st))
             else:
                 # fewer clients than sub-batches (e.g. ONE update): contiguous SEGMENT ranges balanced by
                 # element count, each a plan over absolute segment rows that reads / writes the whole
                 # buffers in place (its own segments only) — the ranges' latency-bound phases overlap
                 ranges = split_lanes(table.segs[:, 1].tolist(), S)
+                uo = [0]
+                for n in table.segs[:, 1].tolist():
+                    uo.append(uo[-1] + units_of(n))
                 for (s0, s1), st in zip(ranges, pooled_streams(self.device, stream_base + len(ranges))[stream_base:]):
                     plan = CodecPlan.from_segments(table.segs[s0:s1], self.bits, device=self.device)
-                    self.parts.append(dict(x=slice(None), k=slice(None), t=slice(s0, s1), plan=plan,
-                                           ws=plan.empty_workspace(), dws=plan.empty_decode_workspace(),
+                    self.parts.append(dict(x=slice(None), k=slice(None), t=slice(s0, s1), u=slice(uo[s0], uo[s1]),
+                                           plan=plan, ws=plan.empty_workspace(), dws=plan.empty_decode_workspace(),
                                            stream=st))
 
     @property
@@ -142,13 +145,15 @@ class SplitPipeline:
 
     def empty_encoded(self):
         d, vt = self.device, torch.float32 if self.bits == 32 else torch.uint8
-        T, K = self.table.n_segments, self.table.total_k
+        T, K, U = self.table.n_segments, self.table.total_k, self.table.n_units
         return Encoded(torch.empty(K, dtype=torch.int32, device=d), torch.empty(K, dtype=vt, device=d),
-                       torch.empty(T, dtype=torch.float32, device=d), torch.empty(T, dtype=torch.float32, device=d))
+                       torch.empty(T, dtype=torch.float32, device=d), torch.empty(T, dtype=torch.float32, device=d),
+                       torch.empty(U, dtype=torch.int32, device=d))
 
     @staticmethod
     def _enc(enc, P):
-        return Encoded(enc.idx[P["k"]], enc.vals[P["k"]], enc.mn[P["t"]], enc.scale[P["t"]])
+        return Encoded(enc.idx[P["k"]], enc.vals[P["k"]], enc.mn[P["t"]], enc.scale[P["t"]],
+                       None if enc.ustart is None else enc.ustart[P["u"]])
 
 
     @staticmethod

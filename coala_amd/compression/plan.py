@@ -18,14 +18,19 @@ from .spec import RAW_BITS, VALID_BITS, SegmentTable, SubTable
 @dataclass
 class Encoded:
     """Device buffers of one encode: idx int32[K], vals uint8[K] (fp32[K] when bits == 32),
-    mn fp32[T], scale fp32[T]."""
+    mn fp32[T], scale fp32[T], and (wire v2) ustart int32[U]: per 4096-element unit, the segment-relative
+    index of its first kept entry — a decoder then needs no search of the idx lists (None: not available)."""
     idx: torch.Tensor
     vals: torch.Tensor
     mn: torch.Tensor
     scale: torch.Tensor
+    ustart: torch.Tensor = None
+
+    FIELDS = ("idx", "vals", "mn", "scale", "ustart")
 
     def to(self, device, non_blocking=False):
-        return Encoded(*(t.to(device, non_blocking=non_blocking) for t in (self.idx, self.vals, self.mn, self.scale)))
+        return Encoded(*(None if t is None else t.to(device, non_blocking=non_blocking)
+                         for t in (self.idx, self.vals, self.mn, self.scale, self.ustart)))
 
 
 def _ptr(t):
@@ -78,6 +83,8 @@ class CodecPlan:
         self.total_k, self.span, self.n_units = tk.value, span.value, nu.value
         if self.total_k != self.table.total_k:
             raise _lib.CodecError(f"plan total_k {self.total_k} != table {self.table.total_k}")
+        if self.n_units != self.table.n_units:
+            raise _lib.CodecError(f"plan n_units {self.n_units} != table {self.table.n_units}")
 
     @classmethod
     def from_segments(cls, segs, bits=8, device=None):
@@ -117,7 +124,8 @@ class CodecPlan:
         return Encoded(torch.empty(self.total_k, dtype=torch.int32, device=d),
                        torch.empty(self.total_k, dtype=self.vals_dtype, device=d),
                        torch.empty(self.n_segments, dtype=torch.float32, device=d),
-                       torch.empty(self.n_segments, dtype=torch.float32, device=d))
+                       torch.empty(self.n_segments, dtype=torch.float32, device=d),
+                       torch.empty(self.n_units, dtype=torch.int32, device=d))
 
     def empty_workspace(self):
         return torch.empty(self.ws_bytes, dtype=torch.uint8, device=self.device)
@@ -139,12 +147,19 @@ class CodecPlan:
             raise ValueError(f"{name}: storage must be 16-byte aligned")
 
     def _check_encoded(self, e):
+        """Dtype, device, contiguity and length of every encoded buffer; returns the ustart pointer to pass (its
+        length must be exactly the plan's unit count: a buffer of another layout is an error, not a hint)."""
         want = ((e.idx, torch.int32, self.total_k), (e.vals, self.vals_dtype, self.total_k),
                 (e.mn, torch.float32, self.n_segments), (e.scale, torch.float32, self.n_segments))
+        if e.ustart is not None:
+            want += ((e.ustart, torch.int32, self.n_units),)
+            if e.ustart.numel() != self.n_units:
+                raise ValueError(f"encoded ustart: {e.ustart.numel()} entries, the plan has {self.n_units} units")
         for t, dt, n in want:
             if t.device != self.device or t.dtype != dt or not t.is_contiguous() or t.numel() < n:
                 raise ValueError(f"encoded buffer mismatch: need {dt}[{n}] on {self.device}, got "
                                  f"{t.dtype}[{t.numel()}] on {t.device}")
+        return _ptr(e.ustart)
 
     # -- codec ------------------------------------------------------------------------------------
     def encode(self, flat, base=None, out=None, workspace=None, flags=0, stream=None, events=None, sched=None):
@@ -157,11 +172,11 @@ class CodecPlan:
         with _on(stream):
             out = self.empty_encoded() if out is None else out
             ws = self.empty_workspace() if workspace is None else workspace
-        self._check_encoded(out)
+        ust = self._check_encoded(out)
         if ws.device != self.device or ws.numel() * ws.element_size() < self.ws_bytes:
             raise ValueError(f"workspace: need {self.ws_bytes} bytes on {self.device}")
         args = (self._h, _ptr(flat), _ptr(base), _ptr(out.idx), _ptr(out.vals), _ptr(out.mn),
-                _ptr(out.scale), _ptr(ws), ctypes.c_uint64(self.ws_bytes), ctypes.c_uint(flags),
+                _ptr(out.scale), ust, _ptr(ws), ctypes.c_uint64(self.ws_bytes), ctypes.c_uint(flags),
                 _stream_handle(stream))
         with torch.cuda.device(self.device):
             if sched is not None:
@@ -214,21 +229,23 @@ class CodecPlan:
         with _on(stream):
             out = self.empty_encoded() if out is None else out
             ws = self.empty_workspace() if workspace is None else workspace
-        self._check_encoded(out)
+        ust = self._check_encoded(out)
         if ws.device != self.device or ws.numel() * ws.element_size() < self.ws_bytes:
             raise ValueError(f"workspace: need {self.ws_bytes} bytes on {self.device}")
         with torch.cuda.device(self.device):
             rc = self._lib.coalac_encode_segptr(self._h, _ptr(ptrs), _ptr(base), _ptr(out.idx), _ptr(out.vals),
-                                                _ptr(out.mn), _ptr(out.scale), _ptr(ws), ctypes.c_uint64(self.ws_bytes),
-                                                ctypes.c_uint(flags), _stream_handle(stream))
+                                                _ptr(out.mn), _ptr(out.scale), ust, _ptr(ws),
+                                                ctypes.c_uint64(self.ws_bytes), ctypes.c_uint(flags),
+                                                _stream_handle(stream))
         _lib.check(rc, "coalac_encode_segptr")
         return out
 
     def decode(self, enc, base=None, out=None, workspace=None, stream=None, events=None, sched=None):
         """Decode Encoded -> dense flat fp32[span] (+ base, fused). Asynchronous on `stream`.
 
+        enc.ustart (wire v2 per-unit starts), when present, saves the decode its search of the idx lists.
         events / sched: as encode(), 3 boundaries (coalac_decode_ev / coalac_decode_sched)."""
-        self._check_encoded(enc)
+        ust = self._check_encoded(enc)
         self._check_flat(base, "base")
         with _on(stream):
             if out is None:
@@ -237,7 +254,7 @@ class CodecPlan:
         self._check_flat(out, "output")
         if ws.device != self.device or ws.numel() * ws.element_size() < self.dec_ws_bytes:
             raise ValueError(f"decode workspace: need {self.dec_ws_bytes} bytes on {self.device}")
-        args = (self._h, _ptr(enc.idx), _ptr(enc.vals), _ptr(enc.mn), _ptr(enc.scale), _ptr(base), _ptr(out),
+        args = (self._h, _ptr(enc.idx), _ptr(enc.vals), _ptr(enc.mn), _ptr(enc.scale), ust, _ptr(base), _ptr(out),
                 _ptr(ws), ctypes.c_uint64(self.dec_ws_bytes), _stream_handle(stream))
         with torch.cuda.device(self.device):
             if sched is not None:
@@ -262,8 +279,9 @@ class CodecPlan:
         strategies.py:57-90: what a multi-GPU server hands to reduce_models, distributed.py:42-57).
         avg_mask: one bool per segment of a client (None: all True); a False segment is not averaged but
         takes client 0's decoded value — aggregation_content "parameters" (strategies.py:32-54, 93-124).
+        enc.ustart (the clients' per-unit starts, concatenated) replaces the k_bounds pass when present.
         """
-        self._check_encoded(enc)
+        ust = self._check_encoded(enc)
         if not getattr(self.table, "uniform", False):
             raise ValueError("fused aggregation needs a plan over copies of one layout (a SegmentTable)")
         C = self.table.clients
@@ -288,7 +306,7 @@ class CodecPlan:
         if ws.device != self.device or ws.numel() * ws.element_size() < self.dec_ws_bytes:
             raise ValueError(f"aggregate workspace: need {self.dec_ws_bytes} bytes on {self.device}")
         total = float(sum(weights)) if total is None else float(total)
-        args = (self._h, C, _ptr(enc.idx), _ptr(enc.vals), _ptr(enc.mn), _ptr(enc.scale), _ptr(w),
+        args = (self._h, C, _ptr(enc.idx), _ptr(enc.vals), _ptr(enc.mn), _ptr(enc.scale), ust, _ptr(w),
                 ctypes.c_float(total), modes[mode], _ptr(m),
                 _ptr(base), _ptr(out), _ptr(ws), ctypes.c_uint64(self.dec_ws_bytes), _stream_handle(stream))
         with torch.cuda.device(self.device):

@@ -49,6 +49,12 @@ def align_up(x, a=ALIGN):
     return (int(x) + a - 1) // a * a
 
 
+def units_of(n):
+    """4096-element work units of a segment of n elements (0 for an empty one): the length of its stretch of the
+    per-unit starts array (wire v2), in segment order (coalac.hip coalac_plan_create)."""
+    return (int(n) + UNIT - 1) // UNIT
+
+
 class SegmentTable:
     """Segment table of `clients` copies of one layout (list of fp32 segment sizes).
 
@@ -76,6 +82,7 @@ class SegmentTable:
         self.out_offsets = oofs
         self.span_per_client = max(off, align)
         self.total_k_per_client = oo
+        self.units_per_client = sum(units_of(n) for n in self.sizes)
         T = len(self.sizes)
         segs = np.zeros((self.clients * T, 4), dtype=np.uint64)
         for c in range(self.clients):
@@ -99,6 +106,10 @@ class SegmentTable:
         return self.clients * self.total_k_per_client
 
     @property
+    def n_units(self):
+        return self.clients * self.units_per_client
+
+    @property
     def n_elements(self):
         return self.clients * sum(self.sizes)
 
@@ -115,6 +126,10 @@ class SegmentTable:
     def client_seg_off(self):
         T = len(self.sizes)
         return [c * T for c in range(self.clients + 1)]
+
+    @property
+    def client_unit_off(self):
+        return [c * self.units_per_client for c in range(self.clients + 1)]
 
     def client_sizes(self, c):
         return self.sizes
@@ -161,8 +176,8 @@ class MixedTable:
         if self.clients < 1:
             raise ValueError("a MixedTable needs at least one client")
         rows = []
-        span_off, k_off, seg_off = [0], [0], [0]
-        off = oo = 0
+        span_off, k_off, seg_off, unit_off = [0], [0], [0], [0]
+        off = oo = uo = 0
         for sizes in self.layouts:
             c0 = off
             for n in sizes:
@@ -170,12 +185,15 @@ class MixedTable:
                 rows.append((off, n, k, oo))
                 off = align_up(off + n, align)
                 oo += k
+                uo += units_of(n)
             off = max(off, c0 + align)  # a client with no fp32 element still owns one aligned slot
             span_off.append(off)
             k_off.append(oo)
             seg_off.append(len(rows))
+            unit_off.append(uo)
         self.segs = np.array(rows, dtype=np.uint64).reshape(-1, 4)
         self.client_span_off, self.client_k_off, self.client_seg_off = span_off, k_off, seg_off
+        self.client_unit_off = unit_off
 
     @property
     def n_segments(self):
@@ -188,6 +206,10 @@ class MixedTable:
     @property
     def total_k(self):
         return self.client_k_off[-1]
+
+    @property
+    def n_units(self):
+        return self.client_unit_off[-1]
 
     @property
     def n_elements(self):
@@ -228,6 +250,10 @@ class SubTable:
     @property
     def span(self):
         return int((self.segs[:, 0] + self.segs[:, 1]).max()) if len(self.segs) else 0
+
+    @property
+    def n_units(self):
+        return sum(units_of(n) for n in self.segs[:, 1].tolist())
 
     @property
     def n_elements(self):

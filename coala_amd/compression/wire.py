@@ -7,13 +7,16 @@ self-describing because remote clients never receive new config keys (OperateCon
 
 Layout (little-endian):
     0   8B   magic b"COALAQ1\\0"
-    8   u32  format version (1)
+    8   u32  format version (2 when the header has "n_units", else 1)
     12  u32  header length H
-    16  H    UTF-8 JSON header: ratio, bits, mode, n_segments, total_k, entries[]
+    16  H    UTF-8 JSON header: ratio, bits, mode, n_segments, total_k, [n_units], entries[]
              entry = {"name", "dtype", "shape", "kind": "seg", "seg": i, "n", "k", "out_off"}
                    | {"name", "dtype", "shape", "kind": "raw", "off", "nbytes"}
     then, each section starting at a 16-byte boundary:
-         mn f32[T] | scale f32[T] | idx i32[K] | vals (u8[K], or f32[K] if bits == 32) | raw bytes
+         mn f32[T] | scale f32[T] | idx i32[K] | vals (u8[K], or f32[K] if bits == 32) | [ustart i32[U]] | raw bytes
+    ustart (version 2): per 4096-element unit of every fp32 segment, in segment order, the segment-relative
+    index of the unit's first kept entry — what the encoder's k_select computed anyway, so the decoder (and the
+    server's fused aggregate) finds each unit's entries without searching the idx lists. U = "n_units".
     A header with "dense": true (ratio 1: every segment keeps all n elements, idx = 0..n-1 per segment)
     carries an empty idx section; unpack regenerates it. This is the download-direction default
     (dense 8-bit weights, ~4x smaller than fp32 instead of 5 B per element with explicit indices).
@@ -26,7 +29,8 @@ from collections import OrderedDict
 import numpy as np
 
 MAGIC = b"COALAQ1\0"
-VERSION = 1
+VERSION = 1     # mn | scale | idx | vals | raw
+VERSION_2 = 2   # ... | vals | ustart | raw
 
 
 def _pad16(n):
@@ -41,16 +45,22 @@ def dense_idx(header):
     return np.concatenate([np.arange(n, dtype=np.int32) for n in ns])
 
 
-def pack(header, mn, scale, idx, vals, raw, header_json=None):
+def pack(header, mn, scale, idx, vals, raw, header_json=None, ustart=None):
     """numpy arrays + raw bytes -> blob (bytes). A "dense" header drops idx (it is implied). header_json: the
-    header's JSON encoding, if the caller has it already."""
+    header's JSON encoding, if the caller has it already. ustart: the per-unit starts (version 2; the header
+    must then carry "n_units" = len(ustart))."""
     if header.get("dense"):
         idx = np.zeros(0, dtype=np.int32)
+    if (ustart is not None) != ("n_units" in header) or (ustart is not None and len(ustart) != header["n_units"]):
+        raise ValueError("COALAQ1: ustart section and header n_units disagree")
     h = header_json if header_json is not None else encode_header(header)
-    parts = [MAGIC, struct.pack("<II", VERSION, len(h)), h]
+    parts = [MAGIC, struct.pack("<II", VERSION if ustart is None else VERSION_2, len(h)), h]
     size = 16 + len(h)
-    for arr in (np.ascontiguousarray(mn, "<f4"), np.ascontiguousarray(scale, "<f4"),
-                np.ascontiguousarray(idx, "<i4"), np.ascontiguousarray(vals)):
+    arrays = [np.ascontiguousarray(mn, "<f4"), np.ascontiguousarray(scale, "<f4"),
+              np.ascontiguousarray(idx, "<i4"), np.ascontiguousarray(vals)]
+    if ustart is not None:
+        arrays.append(np.ascontiguousarray(ustart, "<i4"))
+    for arr in arrays:
         p = _pad16(size)
         parts.append(b"\0" * p)
         b = arr.tobytes()
@@ -88,8 +98,8 @@ def encode_header(header):
 
 
 def sections(blob, header=None):
-    """(header, {name: (byte offset, byte count)}) of the mn / scale / idx / vals sections in `blob`, which
-    lie back to back (each 16-byte aligned) — one host-to-device copy moves all of them."""
+    """(header, {name: (byte offset, byte count)}) of the mn / scale / idx / vals (/ ustart) sections in `blob`,
+    which lie back to back (each 16-byte aligned) — one host-to-device copy moves all of them."""
     mv = memoryview(blob)
     if bytes(mv[:8]) != MAGIC:
         raise ValueError("not a COALAQ1 blob (bad magic)")
@@ -100,7 +110,10 @@ def sections(blob, header=None):
     vsz = 4 if int(header["bits"]) == 32 else 1
     pos = 16 + hl
     out = {}
-    for name, n in (("mn", 4 * T), ("scale", 4 * T), ("idx", 0 if header.get("dense") else 4 * K), ("vals", vsz * K)):
+    names = [("mn", 4 * T), ("scale", 4 * T), ("idx", 0 if header.get("dense") else 4 * K), ("vals", vsz * K)]
+    if "n_units" in header:
+        names.append(("ustart", 4 * int(header["n_units"])))
+    for name, n in names:
         pos += _pad16(pos)
         out[name] = (pos, n)
         pos += n
@@ -108,21 +121,29 @@ def sections(blob, header=None):
 
 
 def unpack(blob):
-    """blob -> (header dict, mn, scale, idx, vals, raw bytes). Arrays are read-only views of blob."""
+    """blob -> (header dict, mn, scale, idx, vals, raw bytes, ustart or None). Arrays are read-only views of
+    blob."""
     mv = memoryview(blob)
     if bytes(mv[:8]) != MAGIC:
         raise ValueError("not a COALAQ1 blob (bad magic)")
     ver, hl = struct.unpack_from("<II", mv, 8)
-    if ver != VERSION:
+    if ver not in (VERSION, VERSION_2):
         raise ValueError(f"unsupported COALAQ1 version {ver}")
     header = _parse_header(mv, hl)
+    if (ver == VERSION_2) != ("n_units" in header):
+        raise ValueError("COALAQ1: version and header n_units disagree")
     T, K = int(header["n_segments"]), int(header["total_k"])
     vdt = np.dtype("<f4") if int(header["bits"]) == 32 else np.dtype("u1")
     pos = 16 + hl
     out = []
     dense = bool(header.get("dense"))
-    for dt, n in ((np.dtype("<f4"), T), (np.dtype("<f4"), T), (np.dtype("<i4"), 0 if dense else K), (vdt, K)):
+    layout = [(np.dtype("<f4"), T), (np.dtype("<f4"), T), (np.dtype("<i4"), 0 if dense else K), (vdt, K)]
+    if ver == VERSION_2:
+        layout.append((np.dtype("<i4"), int(header["n_units"])))
+    for dt, n in layout:
         pos += _pad16(pos)
+        if n < 0 or pos + n * dt.itemsize > len(mv):
+            raise ValueError("COALAQ1: truncated blob")
         out.append(np.frombuffer(mv, dtype=dt, count=n, offset=pos))
         pos += n * dt.itemsize
     pos += _pad16(pos)
@@ -131,4 +152,5 @@ def unpack(blob):
         out[2] = dense_idx(header)
         if out[2].size != K:
             raise ValueError("COALAQ1: dense header with k != n")
-    return (header, *out, raw)
+    ustart = out[4] if ver == VERSION_2 else None
+    return (header, *out[:4], raw, ustart)

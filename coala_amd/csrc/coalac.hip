@@ -18,24 +18,26 @@
 //
 //   Work unit = 4096 contiguous elements of one segment, owned by ONE wave64: ordered compaction is
 //   done with wave ballots + mbcnt (records staged in the wave's LDS slice, flushed coalesced), so the
-//   streaming pass has no block barriers. Segments of <= 4096 elements ("small") are encoded whole by
-//   one block in LDS.
+//   streaming pass has no block barriers. Segments of <= 1024 elements ("small"; COALAC_SMALL_MAX raises the
+//   limit up to 4096) are encoded whole by one block in LDS.
 //
 //   Encode kernels, in stream order:
-//     k_sample  one block per large segment: stratified sample -> [T_lo, T_hi]; then one block per
-//               small segment: the whole segment in LDS (latency-bound work placed where CUs idle)
+//     k_presel  the samplers (one block per large segment: stratified sample -> [T_lo, T_hi]) and the small
+//               segments side by side (batches; latency-bound plans run k_sample alone and the small
+//               segments in k_scan's first blocks)
 //     k_scan    one wave per large unit: single HBM read, classify A / B, 8-byte records in index order
 //     k_ghist   one block per 32-unit group: band histogram of the group's B records
 //     k_gwin    one block per group: sum the segment's group histograms -> key window of the k-th key
 //               (every group block of the segment, redundantly); per-unit counts above the window + the
 //               group's in-window entries
-//     k_select  one 512-thread block per large segment: exact k-th key + tie quota from the window
-//               lists (generic multi-pass select / exact re-select on a bracket miss), per-unit output
-//               offsets, min / max -> scale
-//     k_emit    one wave per 8 large units: kept records -> ascending idx + codes
-//   Decode: k_bounds (first kept entry of every unit) and k_decode (two units per wave, hoisted loads,
-//   kept values merged in registers, one non-temporal write per output line).
-//   Aggregate (fused decode + FedAvg, server side): k_bounds + k_aggregate.
+//     k_select  one block per large segment: exact k-th key + tie quota from the window lists (generic
+//               multi-pass select / exact re-select on a bracket miss), per-unit output offsets (= the
+//               payload's per-unit starts, wire v2), min / max -> scale
+//     k_emit    one wave per 8 large units (1 in latency-bound plans): kept records -> ascending idx + codes
+//   Decode: k_decode_lds — every output line written once, the unit's kept values placed through a per-wave
+//   LDS tile; entry ranges from the payload's per-unit starts, or from k_bounds (batches) / an in-kernel
+//   search (k_fillscatter, latency-bound plans) for a payload without them.
+//   Aggregate (fused decode + FedAvg, server side): k_aggregate (+ k_bounds without per-unit starts).
 //
 // Numerics: built with -ffp-contract=off; fp32 sub/div/mul/add are separate IEEE ops, rintf is
 // round-half-even — the same op sequence as the oracle, so decoded values are bit-identical.
@@ -86,14 +88,11 @@ constexpr int SEL_NT_LAT = 512;           // ... in latency-bound plans, where n
 #ifndef SCAN_WPE
 #define SCAN_WPE 5
 #endif
-#ifndef DECODE_WPE
-#define DECODE_WPE 5
-#endif
 #ifndef SCAN_NB
 #define SCAN_NB 1  // load batches per k_scan unit (weights mode): 1 = all 16 float4 per lane in flight
 #endif
 #ifndef DECODE_XCD
-#define DECODE_XCD 1  // batch k_decode: XCD-aware unit order (xcd_block)
+#define DECODE_XCD 1  // batch k_decode_lds: XCD-aware unit order (xcd_block)
 #endif
 #ifndef SCAN_XCD
 #define SCAN_XCD 0    // k_scan: XCD-aware unit order
@@ -104,9 +103,6 @@ constexpr int SEL_NT_LAT = 512;           // ... in latency-bound plans, where n
 #ifndef SCAN_SMALL_LAT
 #define SCAN_SMALL_LAT 1  // latency-bound plans: small segments in k_scan's first blocks (k_sample alone ahead;
                           // batches measured the same either way and keep k_presel)
-#endif
-#ifndef DECODE_FS
-#define DECODE_FS 1  // latency-bound plans: the whole decode as k_fillscatter (else k_fill + k_scatter)
 #endif
 #ifndef SCAN_WPE_LAT
 #define SCAN_WPE_LAT 6  // latency-bound plans' k_scan: blocks per CU (5 / 1 batch: 24.5 us, 6 / 2: 23.0, 6 / 1
@@ -173,6 +169,7 @@ struct Params {
   void* vals;
   float* mn;
   float* scale;
+  uint32_t* ustart_out;  // encode: per-unit start of the unit's kept entries (segment-relative), or null
   const int32_t* cidx;
   const void* cvals;
   const float* cmn;
@@ -206,8 +203,8 @@ struct Params {
   uint4* sstate;           // [n_large] {wlo, whi, rank inside the window, path: 0 fast / 1 generic}
   uint32_t* shhi;          // [n_large] histogram upper bound: min(T_hi, largest sampled key)
 
-  // decode workspace
-  const uint32_t* ustart;  // [n_units + 1] first kept entry of every unit (k_bounds; aggregate only)
+  // decode: first kept entry (segment-relative) of every unit — the payload's (wire v2) or k_bounds'
+  const uint32_t* ustart;
   // diagnostics: per-block phase timestamps (COALAC_FLAG_STAMPS), NSTAMP per block, 100 MHz ticks
   uint64_t* stamps;
 };
@@ -910,6 +907,7 @@ DEV void small_encode(const Params& P, uint32_t s, float* vals, uint32_t* hist, 
   if (t == 0) {
     P.mn[s] = mn;
     P.scale[s] = scale;
+    if (P.ustart_out != nullptr) P.ustart_out[sd.unit_begin] = 0u;  // (n <= SMALL_MAX < UNIT: one unit)
   }
   uint64_t o = sd.out_off + opre;
   uint32_t eqseen = 0;
@@ -1758,6 +1756,7 @@ DEV void segment_select(const Params& P, uint32_t li, SelSmem& S) {
     if (valid) {
       pst(P, P.eqpre + lb + i, ex);
       pst(P, P.outoff + lb + i, so);
+      if (P.ustart_out != nullptr) pst(P, P.ustart_out + sd.unit_begin + i, so);  // wire v2: the unit's start
     }
   }
   STAMP(P, li, 11);
@@ -1947,38 +1946,6 @@ __global__ __launch_bounds__(BLOCK) void k_emit(Params P) {
 // ------------------------------------------------------------------------------------------------
 // decode
 // ------------------------------------------------------------------------------------------------
-// k_decode: DPW = 2 units per wave (1 in delta mode), all loads issued up front. Partial units (a
-// segment's last, len < 4096) take the same register path with masked stores. Under a saturated write stream every load
-// round trip a wave waits on keeps its slot from issuing stores (tools/decode_ablate.hip: one unit per
-// wave with a dependent load = 4.6 TB/s, two units with hoisted loads + non-temporal stores = 5.7 TB/s,
-// above the 5.5 TB/s of plain zero stores). Round 1: both units' metadata and [lo, hi) bounds (k_bounds);
-// round 2: their first 64 kept entries (+ the base of the unit in delta mode). The kept values are merged
-// into the unit's registers (wave-uniform walk over the sorted entries, rows visited in order), so every
-// output line is written exactly once, with non-temporal float4 stores.
-// Values: out = base + v where kept, base + 0.0f elsewhere (delta), or v / 0.0f without a base: the
-// kept-mask (bit 4*row + component, per lane) tells the two apart.
-template <bool HASBASE>
-DEV void merge_entries(float4 (&b)[UNIT_IT], uint64_t& kept, uint32_t pos0, float v0, uint32_t cnt, uint32_t lane) {
-  uint32_t j = 0;
-#pragma unroll
-  for (uint32_t i = 0; i < UNIT_IT; ++i) {
-    while (j < cnt) {
-      const uint32_t pos = __builtin_amdgcn_readlane(pos0, j);
-      if ((pos >> 8) != i) break;  // sorted entries: the next row (or an out-of-unit / corrupt entry)
-      const float v = __uint_as_float(__builtin_amdgcn_readlane(__float_as_uint(v0), j));
-      if (((pos >> 2) & 63u) == lane) {
-        const uint32_t c = pos & 3u;
-        b[i].x = c == 0 ? (HASBASE ? b[i].x + v : v) : b[i].x;
-        b[i].y = c == 1 ? (HASBASE ? b[i].y + v : v) : b[i].y;
-        b[i].z = c == 2 ? (HASBASE ? b[i].z + v : v) : b[i].z;
-        b[i].w = c == 3 ? (HASBASE ? b[i].w + v : v) : b[i].w;
-        kept |= 1ull << (i * 4 + c);
-      }
-      ++j;
-    }
-  }
-}
-
 // First entry e of each list L_m[0, k_m) with (uint32)L_m[e] >= target_m (k_m if none), for M lists at once,
 // by one wave: each round probes 64 evenly spaced entries of every remaining interval (all M probe loads
 // in flight together) and keeps the 1/64 of it the answer lies in; ceil(log64 k) rounds (3 for k <= 262k).
@@ -2025,262 +1992,130 @@ DEV void wave_lower_bound(const int32_t* const (&L)[M], const uint32_t (&k)[M], 
   for (int m = 0; m < M; ++m) res[m] = a[m];
 }
 
-// units per wave of k_decode: 1 with a base (its 16 float4 of base per unit would double the registers) or
-// in the in-kernel search variant (latency-bound plans: twice the waves, each with half the serial merge)
-#ifndef DECODE_SCATTER
-#define DECODE_SCATTER 1  // latency-bound plans decode as k_fill + k_scatter (else k_decode with the search)
-#endif
-#ifndef DECODE_SCATTER_ALL
-#define DECODE_SCATTER_ALL 0  // experiment: batches decode as k_fill + k_scatter too
-#endif
-#ifndef FILL_AUX
-#define FILL_AUX 0  // k_fill store cache policy (0 plain, 2 non-temporal)
-#endif
-#ifndef DECODE_SEARCH_DPW
-#define DECODE_SEARCH_DPW 1u
-#endif
-template <bool HASBASE, bool SEARCH>
-constexpr uint32_t decode_dpw() { return HASBASE ? 1u : SEARCH ? DECODE_SEARCH_DPW : 2u; }
-
-// SEARCH: the units' entry ranges are found in-kernel (wave_lower_bound) instead of read from k_bounds'
-// ustart: one launch less, three more dependent load rounds per wave — worth it when the plan is small
-// and latency-bound (one update), not for a batch (the rounds then cost write-stream slots).
-template <bool RAW, bool HASBASE, bool SEARCH>
-__global__ __launch_bounds__(BLOCK, DECODE_WPE) void k_decode(Params P) {
-  constexpr uint32_t DPW = decode_dpw<HASBASE, SEARCH>();
-  const uint32_t lane = lane_id(), wv = threadIdx.x >> 6;
-  const uint32_t u0 = ((DECODE_XCD && !SEARCH ? xcd_block(blockIdx.x) : blockIdx.x) * WAVES + wv) * DPW;
-  if (u0 >= P.n_units) return;
-  UnitDev U[DPW];
-  uint32_t lo[DPW], hi[DPW];
-#pragma unroll
-  for (uint32_t r = 0; r < DPW; ++r) U[r] = P.units[min(u0 + r, P.n_units - 1)];
-  if (!SEARCH) {
-#pragma unroll
-    for (uint32_t r = 0; r < DPW; ++r) {
-      const uint32_t uu = min(u0 + r, P.n_units - 1);
-      lo[r] = P.ustart[uu];
-      hi[r] = P.ustart[uu + 1];  // ustart has n_units + 1 entries
-    }
-  } else {
-    // the unit's kept entries [lo, hi) in its segment's sorted idx list, found in-kernel (no k_bounds
-    // launch): lower bounds of the unit's first and one-past-last element index
-    const int32_t* L[2 * DPW];
-    uint32_t kk[2 * DPW], tg[2 * DPW], res[2 * DPW];
-#pragma unroll
-    for (uint32_t r = 0; r < DPW; ++r) {
-      L[2 * r] = L[2 * r + 1] = P.cidx + U[r].out_off;
-      kk[2 * r] = U[r].k;
-      kk[2 * r + 1] = U[r].last ? 0u : U[r].k;  // a segment's last unit ends at k: no search
-      tg[2 * r] = U[r].start;
-      tg[2 * r + 1] = U[r].last ? 0xFFFFFFFFu : U[r].start + U[r].len;
-    }
-    wave_lower_bound<2 * DPW>(L, kk, tg, res);
-#pragma unroll
-    for (uint32_t r = 0; r < DPW; ++r) {
-      lo[r] = res[2 * r];
-      hi[r] = res[2 * r + 1];
-    }
-  }
-  uint32_t pos[DPW], q[DPW];
-  float mn[DPW], sc[DPW];
-#pragma unroll
-  for (uint32_t r = 0; r < DPW; ++r) {
-    // clamp: the bounds come from a possibly untrusted idx list (k >= 1 for every unit)
-    lo[r] = min(lo[r], U[r].k);
-    hi[r] = max(lo[r], min(U[r].last ? U[r].k : hi[r], U[r].k));
-    const uint64_t e = U[r].out_off + min(lo[r] + lane, U[r].k - 1);
-    pos[r] = (uint32_t)P.cidx[e] - U[r].start;
-    q[r] = load_code<RAW>(P, e);
-    mn[r] = RAW ? 0.0f : P.cmn[U[r].seg];
-    sc[r] = RAW ? 0.0f : P.cscale[U[r].seg];
-  }
-#pragma unroll
-  for (uint32_t r = 0; r < DPW; ++r) {
-    if (u0 + r >= P.n_units) break;
-    const uint32_t len = U[r].len;
-    // buffer resources over exactly this unit: base loads past len return 0, stores past len are
-    // dropped, so partial units take the same straight-line path
-    const __amdgpu_buffer_rsrc_t rout = unit_rsrc(P.out + U[r].off, len);
-    // kept values are merged into zeros first; with a base, the base is read afterwards and added one
-    // float4 at a time (out = base + v where kept, base + 0.0f elsewhere: -0 -> +0, as the oracle's
-    // base + dense). Loading the base before the merge held 2 x 64 VGPRs live and spilled to scratch.
-    float4 b[UNIT_IT];
-#pragma unroll
-    for (uint32_t it = 0; it < UNIT_IT; ++it) b[it] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-    uint64_t kept = 0;
-    const uint32_t cnt = hi[r] - lo[r];
-    merge_entries<false>(b, kept, pos[r], code_value<RAW>(q[r], mn[r], sc[r]), min(cnt, 64u), lane);
-    for (uint32_t e0 = lo[r] + 64; e0 < hi[r]; e0 += 64) {  // more than 64 kept entries in the unit
-      const uint64_t e = U[r].out_off + min(e0 + lane, hi[r] - 1);
-      const uint32_t p2 = (uint32_t)P.cidx[e] - U[r].start;
-      const float v2 = code_value<RAW>(load_code<RAW>(P, e), mn[r], sc[r]);
-      merge_entries<false>(b, kept, p2, v2, min(hi[r] - e0, 64u), lane);
-    }
-    if (HASBASE) {
-      const __amdgpu_buffer_rsrc_t rb = unit_rsrc(P.base + U[r].off, len);
-#pragma unroll
-      for (uint32_t it = 0; it < UNIT_IT; ++it) {
-        const float4 a = unit_load_x4<false>(rb, rb, (it * 64 + lane) * 16);
-        const uint32_t m = (uint32_t)(kept >> (it * 4)) & 15u;
-        b[it].x = a.x + ((m & 1u) ? b[it].x : 0.0f);
-        b[it].y = a.y + ((m & 2u) ? b[it].y : 0.0f);
-        b[it].z = a.z + ((m & 4u) ? b[it].z : 0.0f);
-        b[it].w = a.w + ((m & 8u) ? b[it].w : 0.0f);
-      }
-    }
-    // non-temporal stores for batches; a latency-bound plan's output (~100 MB) stores plainly (measured
-    // 33.8 -> 30.8 us on one ResNet-50 update; a batch streams 15 % slower that way)
-    constexpr int SAUX = SEARCH ? 0 : STORE_AUX;
-    if ((len & 3u) == 0) {  // wave-uniform: one float4 buffer store per slot
-#pragma unroll
-      for (uint32_t it = 0; it < UNIT_IT; ++it) unit_store_x4<SAUX>(rout, (it * 64 + lane) * 16, b[it]);
-    } else {  // a segment's last unit with n % 4 != 0: dword stores (range-checked per dword)
-#pragma unroll
-      for (uint32_t it = 0; it < UNIT_IT; ++it) unit_store_x1x4<SAUX>(rout, (it * 64 + lane) * 16, b[it]);
-    }
-  }
-}
-
-// k_decode_lds (batches, DECODE_LDS): the same output as k_decode, with the kept values placed through a
-// per-wave LDS tile instead of the register merge (a wave-uniform walk over every kept entry: ~10 VALU per
-// entry, ~450 per unit, as much issue time per unit as its 16 stores). A unit is written in passes of QROWS rows
-// (8 in weights mode, 4 in delta mode): the pass's kept values are scattered into the zeroed per-wave tile (one
-// ds_write per 64 entries), its rows read back (ds_read_b128, + base in delta mode) and stored, and the same
-// slots zeroed again; one unit per wave. Fewer, larger passes and one unit per wave measured faster than 4-row
-// passes over 2 units (C3 0.672 -> 0.622 ms per step, profiles/r03_decode_ab.txt). Entries outside the unit (an
-// untrusted list) never match a pass and are dropped.
-#ifndef DECODE_LDS
-#define DECODE_LDS 1
-#endif
-#ifndef DECODE_LDS_DPW
-#define DECODE_LDS_DPW 1u  // units per wave (2: C3 0.672 vs 0.622 ms per step with 8-row passes, profiles/r03_decode_ab.txt)
-#endif
+// k_decode_lds: every output line written ONCE (non-temporal float4 stores for batches). WPU waves per unit, each
+// owning RPW = 16 / WPU of its 16 rows, in passes of QROWS rows through a per-wave LDS tile: the pass's kept
+// values are scattered into the zeroed tile (one ds_write per 64 entries), its rows read back (ds_read_b128, + the
+// base in delta mode, whose next pass's rows load while the current one goes through LDS) and stored, and the same
+// slots zeroed again. The unit's entry range [lo, hi) comes from the per-unit starts: the payload's own (wire v2,
+// written by the encoder) or k_bounds'. Round 2 merged the kept values in registers instead (a wave-uniform walk
+// over every entry, ~10 VALU each: as much issue time per unit as its stores); round 3 measured one unit per wave in
+// two 8-row passes fastest for batches (C3 0.672 -> 0.622 ms per step, profiles/r03_decode_ab.txt). Entries outside
+// the wave's rows (an untrusted list) never match a pass and are dropped.
 #ifndef DECODE_LDS_WPE
 #define DECODE_LDS_WPE 5
 #endif
-#ifndef DECODE_BASE_PF
-#define DECODE_BASE_PF 1  // k_decode_lds delta mode: the next quarter's base rows in flight (0: loaded per quarter)
-#endif
 #ifndef DECODE_LDS_WPE_BASE
-#define DECODE_LDS_WPE_BASE 4  // delta mode: two quarters of base rows in registers (5 per CU spilled)
+#define DECODE_LDS_WPE_BASE 4  // delta mode: two passes of base rows in registers (5 per SIMD spilled)
 #endif
 #ifndef DECODE_QROWS
-#define DECODE_QROWS 8u  // weights mode: rows per tile pass (8: half a unit, 8 KiB of LDS per wave; 4 rows: C3
+#define DECODE_QROWS 8u  // batches, weights mode: rows per tile pass (8: half a unit, 8 KiB of LDS per wave; 4 rows: C3
                          // 0.671-0.674 ms per step, 8 rows: 0.621-0.623, profiles/r03_decode_ab.txt)
-#endif
-#ifndef DECODE_NT
-#define DECODE_NT 256  // k_decode_lds block size (its per-wave LDS tile is QROWS KiB)
 #endif
 #ifndef DECODE_QROWS_BASE
 #define DECODE_QROWS_BASE 4u  // delta mode: rows per tile pass
 #endif
+#ifndef DECODE_NT
+#define DECODE_NT 256  // k_decode_lds block size (its per-wave LDS tile is QROWS KiB)
+#endif
+#ifndef DECODE_WPU_LAT
+#define DECODE_WPU_LAT 2u  // latency-bound plans: waves per unit (one update: every wave one 8-row pass)
+#endif
+#ifndef DECODE_SAUX_LAT
+#define DECODE_SAUX_LAT 0  // latency-bound plans: store cache policy (a ~100 MB output: plain stores)
+#endif
 
-template <bool RAW, bool HASBASE>
+template <bool RAW, bool HASBASE, uint32_t WPU, uint32_t QROWS, int SAUX, bool XCD>
 __global__ __launch_bounds__(DECODE_NT, HASBASE ? DECODE_LDS_WPE_BASE : DECODE_LDS_WPE) void k_decode_lds(Params P) {
-  constexpr uint32_t DPW = DECODE_LDS_DPW, DW = DECODE_NT / 64;
-  constexpr uint32_t QROWS = HASBASE ? DECODE_QROWS_BASE : DECODE_QROWS;  // rows per tile pass
+  constexpr uint32_t DW = DECODE_NT / 64, RPW = UNIT_IT / WPU, NPASS = RPW / QROWS;
   constexpr uint32_t QSH = QROWS == 2u ? 9u : QROWS == 4u ? 10u : QROWS == 8u ? 11u : 12u, QM = (1u << QSH) - 1u;
-  static_assert((QROWS << 8) == (1u << QSH), "tile pass geometry");
+  static_assert((QROWS << 8) == (1u << QSH) && RPW % QROWS == 0 && NPASS >= 1, "tile pass geometry");
   __shared__ float4 qtile[DW][QROWS * 64];
   const uint32_t lane = lane_id(), wv = threadIdx.x >> 6;
-  const uint32_t u0 = ((DECODE_XCD ? xcd_block(blockIdx.x) : blockIdx.x) * DW + wv) * DPW;
-  if (u0 >= P.n_units) return;
+  const uint32_t wid = (XCD ? xcd_block(blockIdx.x) : blockIdx.x) * DW + wv;
+  const uint32_t u = wid / WPU, pass0 = (wid % WPU) * NPASS;  // this wave's unit and first pass (QROWS rows each)
+  if (u >= P.n_units) return;
   float4* tile = qtile[wv];
   float* tf = reinterpret_cast<float*>(tile);
 #pragma unroll
   for (uint32_t it = 0; it < QROWS; ++it) tile[it * 64 + lane] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-  UnitDev U[DPW];
-  uint32_t lo[DPW], hi[DPW];
+  // round 1: the unit and its entry range (the next unit's start is the end of this one's: a non-last unit is
+  // followed by its segment's next unit; the index is clamped for the plan's final unit, which is a last unit)
+  const UnitDev U = P.units[u];
+  uint32_t lo = P.ustart[u];
+  uint32_t hi = P.ustart[min(u + 1, P.n_units - 1)];
+  const float mn = RAW ? 0.0f : P.cmn[U.seg], sc = RAW ? 0.0f : P.cscale[U.seg];
+  // clamp: the bounds may come from an untrusted payload (k >= 1 for every unit); a valid unit holds at most len
+  // kept entries (distinct positions), which also bounds the entry loops below for any corrupt range
+  lo = min(lo, U.k);
+  hi = max(lo, min(min(U.last ? U.k : hi, U.k), lo + U.len));
+  const uint32_t cnt = hi - lo;
+  // round 2: the first 64 entries (+ the base rows of the first pass)
+  const uint64_t e1 = U.out_off + min(lo + lane, U.k - 1);
+  const uint32_t q1 = load_code<RAW>(P, e1);
+  const uint32_t pos = (uint32_t)P.cidx[e1] - U.start;
+  const uint32_t len = U.len;
+  const __amdgpu_buffer_rsrc_t rout = unit_rsrc(P.out + U.off, len);
+  const __amdgpu_buffer_rsrc_t rb = unit_rsrc(HASBASE ? P.base + U.off : P.out + U.off, len);
+  float4 bq[QROWS], bn[QROWS];
+  if (HASBASE) {
 #pragma unroll
-  for (uint32_t r = 0; r < DPW; ++r) {
-    const uint32_t uu = min(u0 + r, P.n_units - 1);
-    U[r] = P.units[uu];
-    lo[r] = P.ustart[uu];
-    hi[r] = P.ustart[uu + 1];  // ustart has n_units + 1 entries
+    for (uint32_t it = 0; it < QROWS; ++it) bn[it] = unit_load_x4<false>(rb, rb, ((pass0 * QROWS + it) * 64 + lane) * 16);
   }
-  uint32_t pos[DPW];
-  float val[DPW];
-#pragma unroll
-  for (uint32_t r = 0; r < DPW; ++r) {
-    // clamp: the bounds come from a possibly untrusted idx list (k >= 1 for every unit)
-    lo[r] = min(lo[r], U[r].k);
-    hi[r] = max(lo[r], min(U[r].last ? U[r].k : hi[r], U[r].k));
-    const uint64_t e = U[r].out_off + min(lo[r] + lane, U[r].k - 1);
-    const uint32_t q = load_code<RAW>(P, e);
-    pos[r] = (uint32_t)P.cidx[e] - U[r].start;
-    val[r] = code_value<RAW>(q, RAW ? 0.0f : P.cmn[U[r].seg], RAW ? 0.0f : P.cscale[U[r].seg]);
-  }
+  const float val = code_value<RAW>(q1, mn, sc);
   lds_order();
 #pragma unroll
-  for (uint32_t r = 0; r < DPW; ++r) {
-    if (u0 + r >= P.n_units) break;
-    const uint32_t len = U[r].len, cnt = hi[r] - lo[r];
-    const __amdgpu_buffer_rsrc_t rout = unit_rsrc(P.out + U[r].off, len);
-    const __amdgpu_buffer_rsrc_t rb = unit_rsrc(HASBASE ? P.base + U[r].off : P.out + U[r].off, len);
-    const float mn = RAW ? 0.0f : P.cmn[U[r].seg], sc = RAW ? 0.0f : P.cscale[U[r].seg];
-    constexpr int SAUX = STORE_AUX;
-    // delta mode: the base rows of quarter qq + 1 are loaded while quarter qq goes through the LDS round trip
-    // (loads and stores share vmcnt in issue order: the wait for them leaves quarter qq's stores in flight)
-    float4 bq[QROWS], bn[QROWS];
-    if (HASBASE && DECODE_BASE_PF) {
+  for (uint32_t qi = 0; qi < NPASS; ++qi) {
+    const uint32_t qq = pass0 + qi;
+    if (HASBASE) {
 #pragma unroll
-      for (uint32_t it = 0; it < QROWS; ++it) bn[it] = unit_load_x4<false>(rb, rb, (it * 64 + lane) * 16);
-    }
-#pragma unroll
-    for (uint32_t qq = 0; qq < UNIT_IT / QROWS; ++qq) {
-      if (HASBASE) {
-#pragma unroll
-        for (uint32_t it = 0; it < QROWS; ++it) bq[it] = bn[it];
-        if (!DECODE_BASE_PF) {
-#pragma unroll
-          for (uint32_t it = 0; it < QROWS; ++it)
-            bq[it] = unit_load_x4<false>(rb, rb, ((qq * QROWS + it) * 64 + lane) * 16);
-        } else if (qq + 1 < UNIT_IT / QROWS) {
-#pragma unroll
-          for (uint32_t it = 0; it < QROWS; ++it)
-            bn[it] = unit_load_x4<false>(rb, rb, (((qq + 1) * QROWS + it) * 64 + lane) * 16);
-        }
-      }
-      // scatter: the first 64 entries are in registers; more (ratio >~ 1.5 %) are loaded chunk by chunk
-      if (lane < min(cnt, 64u) && (pos[r] >> QSH) == qq) tf[pos[r] & QM] = val[r];
-      for (uint32_t e0 = lo[r] + 64; e0 < hi[r]; e0 += 64) {
-        const uint64_t e = U[r].out_off + min(e0 + lane, hi[r] - 1);
-        const uint32_t p2 = (uint32_t)P.cidx[e] - U[r].start;
-        if (e0 + lane < hi[r] && (p2 >> QSH) == qq) tf[p2 & QM] = code_value<RAW>(load_code<RAW>(P, e), mn, sc);
-      }
-      lds_order();
-      float4 o[QROWS];
-#pragma unroll
-      for (uint32_t it = 0; it < QROWS; ++it) {
-        const float4 d = tile[it * 64 + lane];
-        o[it] = HASBASE ? make_float4(bq[it].x + d.x, bq[it].y + d.y, bq[it].z + d.z, bq[it].w + d.w) : d;
-      }
-      lds_order();
-      // zero what was written (the same slots), for the next quarter / unit
-      if (lane < min(cnt, 64u) && (pos[r] >> QSH) == qq) tf[pos[r] & QM] = 0.0f;
-      for (uint32_t e0 = lo[r] + 64; e0 < hi[r]; e0 += 64) {
-        const uint64_t e = U[r].out_off + min(e0 + lane, hi[r] - 1);
-        const uint32_t p2 = (uint32_t)P.cidx[e] - U[r].start;
-        if (e0 + lane < hi[r] && (p2 >> QSH) == qq) tf[p2 & QM] = 0.0f;
-      }
-      if ((len & 3u) == 0) {  // wave-uniform: one float4 buffer store per slot
-#pragma unroll
-        for (uint32_t it = 0; it < QROWS; ++it) unit_store_x4<SAUX>(rout, ((qq * QROWS + it) * 64 + lane) * 16, o[it]);
-      } else {  // a segment's last unit with n % 4 != 0: dword stores (range-checked per dword)
+      for (uint32_t it = 0; it < QROWS; ++it) bq[it] = bn[it];
+      if (qi + 1 < NPASS) {
 #pragma unroll
         for (uint32_t it = 0; it < QROWS; ++it)
-          unit_store_x1x4<SAUX>(rout, ((qq * QROWS + it) * 64 + lane) * 16, o[it]);
+          bn[it] = unit_load_x4<false>(rb, rb, (((qq + 1) * QROWS + it) * 64 + lane) * 16);
       }
-      lds_order();
     }
+    // scatter: the first 64 entries are in registers; more (ratio >~ 1.5 %) are loaded chunk by chunk
+    if (lane < min(cnt, 64u) && (pos >> QSH) == qq) tf[pos & QM] = val;
+    for (uint32_t e0 = lo + 64; e0 < hi; e0 += 64) {
+      const uint64_t e = U.out_off + min(e0 + lane, hi - 1);
+      const uint32_t p2 = (uint32_t)P.cidx[e] - U.start;
+      if (e0 + lane < hi && (p2 >> QSH) == qq) tf[p2 & QM] = code_value<RAW>(load_code<RAW>(P, e), mn, sc);
+    }
+    lds_order();
+    float4 o[QROWS];
+#pragma unroll
+    for (uint32_t it = 0; it < QROWS; ++it) {
+      const float4 d = tile[it * 64 + lane];
+      o[it] = HASBASE ? make_float4(bq[it].x + d.x, bq[it].y + d.y, bq[it].z + d.z, bq[it].w + d.w) : d;
+    }
+    lds_order();
+    if (qi + 1 < NPASS) {  // zero what was written (the same slots), for the next pass
+      if (lane < min(cnt, 64u) && (pos >> QSH) == qq) tf[pos & QM] = 0.0f;
+      for (uint32_t e0 = lo + 64; e0 < hi; e0 += 64) {
+        const uint64_t e = U.out_off + min(e0 + lane, hi - 1);
+        const uint32_t p2 = (uint32_t)P.cidx[e] - U.start;
+        if (e0 + lane < hi && (p2 >> QSH) == qq) tf[p2 & QM] = 0.0f;
+      }
+    }
+    if ((len & 3u) == 0) {  // wave-uniform: one float4 buffer store per slot
+#pragma unroll
+      for (uint32_t it = 0; it < QROWS; ++it) unit_store_x4<SAUX>(rout, ((qq * QROWS + it) * 64 + lane) * 16, o[it]);
+    } else {  // a segment's last unit with n % 4 != 0: dword stores (range-checked per dword)
+#pragma unroll
+      for (uint32_t it = 0; it < QROWS; ++it) unit_store_x1x4<SAUX>(rout, ((qq * QROWS + it) * 64 + lane) * 16, o[it]);
+    }
+    lds_order();
   }
 }
 
-// Latency-bound plans, DECODE_SCATTER: the background first (k_fill: every unit's 0 / base + 0.0f, no entry
+// Latency-bound plans without per-unit starts (a wire v1 payload): the background first (k_fill: every unit's 0 / base + 0.0f, no entry
 // lookup, so the write stream starts at once), then the kept values on top (k_scatter: one thread per entry,
 // per k_bounds chunk; bounds-checked like k_decode). Stream order puts every kept value after the fill.
 // one wave writes unit U's background: 0, or base + 0.0f (-0 -> +0, as the oracle's base + dense)
+#ifndef FILL_AUX
+#define FILL_AUX 0  // k_fill store cache policy (0 plain, 2 non-temporal)
+#endif
 template <bool HASBASE>
 DEV void fill_unit(const Params& P, const UnitDev& U, uint32_t lane) {
   const __amdgpu_buffer_rsrc_t rout = unit_rsrc(P.out + U.off, U.len);
@@ -2312,7 +2147,7 @@ __global__ __launch_bounds__(BLOCK) void k_fill(Params P) {
   fill_unit<HASBASE>(P, P.units[u], lane_id());
 }
 
-// k_fillscatter (latency-bound plans, DECODE_FS): k_fill and k_scatter as one launch, one wave per unit. The
+// k_fillscatter (latency-bound plans decoding a payload without per-unit starts): k_fill and k_scatter as one launch, one wave per unit. The
 // wave stores its unit's background first (nothing to wait for), finds the unit's kept entries [lo, hi) in
 // its segment's sorted idx list in-kernel (wave_lower_bound, while the stores drain), waits until its own
 // stores have completed, and then writes the kept values on top: every output element is written by the
@@ -2331,7 +2166,7 @@ __global__ __launch_bounds__(BLOCK) void k_fillscatter(Params P) {
   const uint32_t tg[2] = {U.start, U.last ? 0xFFFFFFFFu : U.start + U.len};
   uint32_t res[2];
   wave_lower_bound<2>(L, kk, tg, res);
-  const uint32_t lo = min(res[0], U.k), hi = max(lo, min(U.last ? U.k : res[1], U.k));
+  const uint32_t lo = min(res[0], U.k), hi = max(lo, min(min(U.last ? U.k : res[1], U.k), lo + U.len));
   const float mn = RAW ? 0.0f : P.cmn[U.seg];
   const float sc = RAW ? 0.0f : P.cscale[U.seg];
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the background stores have completed
@@ -2391,9 +2226,6 @@ __global__ __launch_bounds__(BLOCK) void k_bounds(Params P, const BChunk* chunks
 
 #ifndef AGG_WPE
 #define AGG_WPE 1  // k_aggregate launch-bounds blocks per CU (register budget)
-#endif
-#ifndef AGG_PROBE
-#define AGG_PROBE 0  // A/B probe builds only (tools/build_variant.sh): 1 = no client loop, 2 = no scatter
 #endif
 #ifndef AGG_SPLIT
 #define AGG_SPLIT 2u  // waves per 4096-element unit in k_aggregate (each owns UNIT_IT / AGG_SPLIT rows)
@@ -2503,18 +2335,13 @@ __global__ __launch_bounds__(BLOCK, AGG_WPE) void k_aggregate(Params P, AggArgs 
   tile_zero();
 #pragma unroll
   for (uint32_t it = 0; it < RI; ++it) acc[it] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-#if AGG_PROBE == 1
-  const uint32_t nclients_run = 0;  // probe build: the base read and output write alone
-#else
-  const uint32_t nclients_run = nclients;
-#endif
-  for (uint32_t c0 = 0; c0 < nclients_run; c0 += 64) {
+  for (uint32_t c0 = 0; c0 < nclients; c0 += 64) {
     const uint32_t cn = min(64u, nclients - c0);
     // lane j: metadata of client c0 + j (unconditional loads at a clamped client index)
     const uint32_t cl = c0 + min(lane, cn - 1);
     const uint32_t ucl = u + cl * A.U0;
     const uint32_t m_lo = min(A.ustart[ucl], kseg);
-    const uint32_t m_hi = max(m_lo, min(U.last ? kseg : A.ustart[min(ucl + 1, P.n_units - 1)], kseg));
+    const uint32_t m_hi = max(m_lo, min(min(U.last ? kseg : A.ustart[min(ucl + 1, P.n_units - 1)], kseg), m_lo + len));
     const uint32_t sl = U.seg + cl * A.T;
     const float m_mn = RAW ? 0.0f : P.cmn[sl];
     const float m_sc = RAW ? 0.0f : P.cscale[sl];
@@ -2563,11 +2390,7 @@ __global__ __launch_bounds__(BLOCK, AGG_WPE) void k_aggregate(Params P, AggArgs 
       const uint32_t ne = __builtin_amdgcn_readlane(m_hi, j) - __builtin_amdgcn_readlane(m_lo, j);
       const float mn = __uint_as_float(__builtin_amdgcn_readlane(__float_as_uint(m_mn), j));
       const float sc = __uint_as_float(__builtin_amdgcn_readlane(__float_as_uint(m_sc), j));
-#if AGG_PROBE == 2
-      const bool mine = false;  // probe build: no scatter (loads and accumulation only)
-#else
       const bool mine = lane < ne && pos < hlen;
-#endif
       if (mine) tf[pos] = code_value<RAW>(q, mn, sc);
       lds_order();
       accumulate(j);
@@ -2789,14 +2612,6 @@ bool at_boundary(unsigned stages, const int (*span)[2], int nst, int i) {
       if (span[k][0] <= i && i <= span[k][1]) return true;
   return false;
 }
-
-// decode plans of up to this many 4096-element units (~1.3 ResNet-50 updates) search their entry ranges
-// in k_decode; bigger ones run k_bounds first
-constexpr uint32_t DECODE_SEARCH_MAX_UNITS = 8192;
-#ifndef DECODE_LAT_LDS
-#define DECODE_LAT_LDS 0  // 1: latency-bound plans decode like batches (k_bounds + k_decode_lds)
-#endif
-constexpr uint32_t DECODE_SEARCH_UNITS = DECODE_LAT_LDS ? 0u : DECODE_SEARCH_MAX_UNITS;
 
 constexpr int ENC_SPAN[4][2] = {{0, 1}, {1, 2}, {2, 4}, {0, 1}};  // SAMPLE, SCAN, SELECT, SMALL
 constexpr int DEC_SPAN[2][2] = {{0, 1}, {1, 2}};                  // BOUNDS, DECODE
@@ -3074,19 +2889,19 @@ int coalac_plan_query(coalac_plan_t plan, uint64_t* ws_bytes, uint64_t* dec_ws_b
 }
 
 int coalac_encode_ev(coalac_plan_t plan, const float* d_in, const float* d_base, int32_t* d_idx,
-                     void* d_vals, float* d_mn, float* d_scale, void* d_ws, uint64_t ws_bytes,
+                     void* d_vals, float* d_mn, float* d_scale, uint32_t* d_ustart, void* d_ws, uint64_t ws_bytes,
                      unsigned flags, void* stream, void* const* events) {
   const coalac_sched_t s = record_only(events, 5);
-  return coalac_encode_sched(plan, d_in, d_base, d_idx, d_vals, d_mn, d_scale, d_ws, ws_bytes, flags, stream,
-                             events ? &s : nullptr);
+  return coalac_encode_sched(plan, d_in, d_base, d_idx, d_vals, d_mn, d_scale, d_ustart, d_ws, ws_bytes, flags,
+                             stream, events ? &s : nullptr);
 }
 
 }  // extern "C"
 
 namespace {
 int encode_impl(coalac_plan_t plan, const float* d_in, const float* const* d_inptr, const float* d_base,
-                int32_t* d_idx, void* d_vals, float* d_mn, float* d_scale, void* d_ws, uint64_t ws_bytes,
-                unsigned flags, void* stream, const coalac_sched_t* sched) {
+                int32_t* d_idx, void* d_vals, float* d_mn, float* d_scale, uint32_t* d_ustart, void* d_ws,
+                uint64_t ws_bytes, unsigned flags, void* stream, const coalac_sched_t* sched) {
   if (!plan) return fail(COALAC_EINVAL, "coalac_encode: plan is NULL");
   if (plan->nseg == 0) return COALAC_OK;
   if (!d_mn || !d_scale) return fail(COALAC_EINVAL, "coalac_encode: mn/scale pointers are NULL");
@@ -3094,6 +2909,7 @@ int encode_impl(coalac_plan_t plan, const float* d_in, const float* const* d_inp
   if (plan->total_k && (!d_idx || !d_vals)) return fail(COALAC_EINVAL, "coalac_encode: idx/vals pointers are NULL");
   if ((reinterpret_cast<uintptr_t>(d_in) | reinterpret_cast<uintptr_t>(d_base)) & 15)
     return fail(COALAC_EINVAL, "coalac_encode: input/base must be 16-byte aligned");
+  if (reinterpret_cast<uintptr_t>(d_ustart) & 3) return fail(COALAC_EINVAL, "coalac_encode: ustart must be 4-byte aligned");
   if (!d_ws || ws_bytes < plan->ws.total)
     return fail(COALAC_EWORKSPACE, "coalac_encode: workspace %llu < required %llu", (unsigned long long)ws_bytes,
                 (unsigned long long)plan->ws.total);
@@ -3108,6 +2924,7 @@ int encode_impl(coalac_plan_t plan, const float* d_in, const float* const* d_inp
   P.vals = d_vals;
   P.mn = d_mn;
   P.scale = d_scale;
+  P.ustart_out = d_ustart;
   P.flags = flags;
   uint8_t* w = static_cast<uint8_t*>(d_ws);
   const WsLayout& L = plan->ws;
@@ -3149,53 +2966,90 @@ int encode_impl(coalac_plan_t plan, const float* d_in, const float* const* d_inp
 extern "C" {
 
 int coalac_encode_sched(coalac_plan_t plan, const float* d_in, const float* d_base, int32_t* d_idx,
-                        void* d_vals, float* d_mn, float* d_scale, void* d_ws, uint64_t ws_bytes,
+                        void* d_vals, float* d_mn, float* d_scale, uint32_t* d_ustart, void* d_ws, uint64_t ws_bytes,
                         unsigned flags, void* stream, const coalac_sched_t* sched) {
-  return encode_impl(plan, d_in, nullptr, d_base, d_idx, d_vals, d_mn, d_scale, d_ws, ws_bytes, flags, stream, sched);
+  return encode_impl(plan, d_in, nullptr, d_base, d_idx, d_vals, d_mn, d_scale, d_ustart, d_ws, ws_bytes, flags,
+                     stream, sched);
 }
 
 int coalac_encode_segptr(coalac_plan_t plan, const float* const* d_seg_in, const float* d_base, int32_t* d_idx,
-                         void* d_vals, float* d_mn, float* d_scale, void* d_ws, uint64_t ws_bytes, unsigned flags,
-                         void* stream) {
+                         void* d_vals, float* d_mn, float* d_scale, uint32_t* d_ustart, void* d_ws, uint64_t ws_bytes,
+                         unsigned flags, void* stream) {
   if (plan && plan->nseg && !d_seg_in) return fail(COALAC_EINVAL, "coalac_encode_segptr: d_seg_in is NULL");
-  return encode_impl(plan, nullptr, d_seg_in, d_base, d_idx, d_vals, d_mn, d_scale, d_ws, ws_bytes, flags, stream,
-                     nullptr);
+  return encode_impl(plan, nullptr, d_seg_in, d_base, d_idx, d_vals, d_mn, d_scale, d_ustart, d_ws, ws_bytes, flags,
+                     stream, nullptr);
 }
 
 int coalac_encode(coalac_plan_t plan, const float* d_in, const float* d_base, int32_t* d_idx, void* d_vals,
-                  float* d_mn, float* d_scale, void* d_ws, uint64_t ws_bytes, unsigned flags, void* stream) {
-  return coalac_encode_ev(plan, d_in, d_base, d_idx, d_vals, d_mn, d_scale, d_ws, ws_bytes, flags, stream,
+                  float* d_mn, float* d_scale, uint32_t* d_ustart, void* d_ws, uint64_t ws_bytes, unsigned flags,
+                  void* stream) {
+  return coalac_encode_ev(plan, d_in, d_base, d_idx, d_vals, d_mn, d_scale, d_ustart, d_ws, ws_bytes, flags, stream,
                           nullptr);
 }
 
 int coalac_decode_ev(coalac_plan_t plan, const int32_t* d_idx, const void* d_vals, const float* d_mn,
-                     const float* d_scale, const float* d_base, float* d_out, void* d_ws, uint64_t ws_bytes,
-                     void* stream, void* const* events) {
+                     const float* d_scale, const uint32_t* d_ustart, const float* d_base, float* d_out, void* d_ws,
+                     uint64_t ws_bytes, void* stream, void* const* events) {
   const coalac_sched_t s = record_only(events, 3);
-  return coalac_decode_sched(plan, d_idx, d_vals, d_mn, d_scale, d_base, d_out, d_ws, ws_bytes, stream,
+  return coalac_decode_sched(plan, d_idx, d_vals, d_mn, d_scale, d_ustart, d_base, d_out, d_ws, ws_bytes, stream,
                              events ? &s : nullptr);
 }
 
+}  // extern "C"
+
+namespace {
+// The write-once decode (k_decode_lds) of a whole plan: batches one wave per unit in two 8-row passes (4-row in
+// delta mode) with non-temporal stores and the XCD-aware order; latency-bound plans DECODE_WPU_LAT waves per unit
+// (one pass each: twice the waves, each with half the work, for a launch of one update's ~6.5 k units).
+template <bool RAW, bool HB>
+void launch_decode_lds(const Params& P, coalac_plan_t plan, hipStream_t st) {
+  constexpr uint32_t DW = DECODE_NT / 64;
+  if (plan->n_units <= LATENCY_PLAN_UNITS) {
+    constexpr uint32_t W = DECODE_WPU_LAT, Q = HB ? DECODE_QROWS_BASE : UNIT_IT / DECODE_WPU_LAT;
+    hipLaunchKernelGGL((k_decode_lds<RAW, HB, W, (Q < 8u ? Q : 8u), DECODE_SAUX_LAT, false>),
+                       dim3((plan->n_units * W + DW - 1) / DW), dim3(DECODE_NT), 0, st, P);
+  } else {
+    hipLaunchKernelGGL((k_decode_lds<RAW, HB, 1u, HB ? DECODE_QROWS_BASE : DECODE_QROWS, STORE_AUX, DECODE_XCD != 0>),
+                       dim3((plan->n_units + DW - 1) / DW), dim3(DECODE_NT), 0, st, P);
+  }
+}
+
+template <bool RAW, bool HB>
+void launch_fillscatter(const Params& P, coalac_plan_t plan, hipStream_t st, unsigned stages) {
+  const dim3 gf((plan->n_units + WAVES - 1) / WAVES);
+  if ((stages & COALAC_STAGE_FILL) && (stages & COALAC_STAGE_SCATTER)) {
+    hipLaunchKernelGGL((k_fillscatter<RAW, HB>), gf, dim3(BLOCK), 0, st, P);
+    return;
+  }
+  if (stages & COALAC_STAGE_FILL) hipLaunchKernelGGL((k_fill<HB>), gf, dim3(BLOCK), 0, st, P);
+  if ((stages & COALAC_STAGE_SCATTER) && plan->n_bchunks)
+    hipLaunchKernelGGL((k_scatter<RAW, HB>), dim3(plan->n_bchunks), dim3(BLOCK), 0, st, P, plan->schunks);
+}
+}  // namespace
+
+extern "C" {
+
 int coalac_decode_sched(coalac_plan_t plan, const int32_t* d_idx, const void* d_vals, const float* d_mn,
-                        const float* d_scale, const float* d_base, float* d_out, void* d_ws, uint64_t ws_bytes,
-                        void* stream, const coalac_sched_t* sched) {
+                        const float* d_scale, const uint32_t* d_ustart, const float* d_base, float* d_out, void* d_ws,
+                        uint64_t ws_bytes, void* stream, const coalac_sched_t* sched) {
   const unsigned all = COALAC_STAGE_BOUNDS | COALAC_STAGE_DECODE;
   const unsigned known = all | COALAC_STAGE_FILL | COALAC_STAGE_SCATTER;
   unsigned stages = (sched && (sched->stages & known)) ? (sched->stages & known) : all;
-  // DECODE = FILL + SCATTER: the background (k_fill) and the kept values (k_scatter, or k_decode for plans
-  // that merge the background in registers) as separately enqueued parts
+  // DECODE = FILL + SCATTER: the background and the kept values as separately enqueued parts
   if (stages & COALAC_STAGE_DECODE) stages |= COALAC_STAGE_FILL | COALAC_STAGE_SCATTER;
   if (stages & (COALAC_STAGE_FILL | COALAC_STAGE_SCATTER)) stages |= COALAC_STAGE_DECODE;
   if (!plan) return fail(COALAC_EINVAL, "coalac_decode: plan is NULL");
   if (plan->n_units == 0) return COALAC_OK;
-  // plans of > DECODE_SEARCH_MAX_UNITS units read the per-unit entry bounds k_bounds leaves in the workspace:
-  // the kept values need BOUNDS in this call, or the caller's word (BOUNDS_DONE) that an earlier call
-  // enqueued it on this workspace for these arrays, ordered before this one (else stale bounds mis-decode)
-  if (plan->n_units > DECODE_SEARCH_UNITS && (stages & COALAC_STAGE_SCATTER) && !(stages & COALAC_STAGE_BOUNDS) &&
+  const bool lat = plan->n_units <= LATENCY_PLAN_UNITS;
+  // Entry ranges per unit: the payload's starts (d_ustart, wire v2), else — batches — the ones k_bounds leaves in the
+  // workspace: the kept values then need BOUNDS in this call, or the caller's word (BOUNDS_DONE) that an earlier call
+  // enqueued it on this workspace for these arrays, ordered before this one (stale bounds would mis-decode
+  // silently); latency-bound plans without starts search their ranges in-kernel (k_fillscatter).
+  if (!d_ustart && !lat && (stages & COALAC_STAGE_SCATTER) && !(stages & COALAC_STAGE_BOUNDS) &&
       !(sched && (sched->stages & COALAC_STAGE_BOUNDS_DONE)))
-    return fail(COALAC_EINVAL, "coalac_decode: a plan of %u units decodes its kept values from the bounds of "
-                "COALAC_STAGE_BOUNDS: pass BOUNDS in the same call, or BOUNDS_DONE after a BOUNDS call on this "
-                "workspace", plan->n_units);
+    return fail(COALAC_EINVAL, "coalac_decode: a plan of %u units without per-unit starts decodes its kept values "
+                "from the bounds of COALAC_STAGE_BOUNDS: pass BOUNDS in the same call, or BOUNDS_DONE after a BOUNDS "
+                "call on this workspace", plan->n_units);
   if (!d_out) return fail(COALAC_EINVAL, "coalac_decode: output pointer is NULL");
   const bool payload = (stages & (COALAC_STAGE_BOUNDS | COALAC_STAGE_SCATTER)) != 0;  // reads the encoded arrays
   if (payload && plan->total_k && (!d_idx || !d_vals))
@@ -3204,6 +3058,7 @@ int coalac_decode_sched(coalac_plan_t plan, const int32_t* d_idx, const void* d_
     return fail(COALAC_EINVAL, "coalac_decode: mn/scale pointers are NULL");
   if ((reinterpret_cast<uintptr_t>(d_out) | reinterpret_cast<uintptr_t>(d_base)) & 15)
     return fail(COALAC_EINVAL, "coalac_decode: output/base must be 16-byte aligned");
+  if (reinterpret_cast<uintptr_t>(d_ustart) & 3) return fail(COALAC_EINVAL, "coalac_decode: ustart must be 4-byte aligned");
   if (!d_ws || ws_bytes < plan->dec_ws)
     return fail(COALAC_EWORKSPACE, "coalac_decode: workspace %llu < required %llu", (unsigned long long)ws_bytes,
                 (unsigned long long)plan->dec_ws);
@@ -3217,18 +3072,9 @@ int coalac_decode_sched(coalac_plan_t plan, const int32_t* d_idx, const void* d_
   P.cscale = d_scale;
   P.base = d_base;
   P.out = d_out;
-  P.ustart = static_cast<const uint32_t*>(d_ws);
+  P.ustart = d_ustart ? d_ustart : static_cast<const uint32_t*>(d_ws);
   hipStream_t st = static_cast<hipStream_t>(stream);
   const bool raw = plan->bits == 32, hb = d_base != nullptr;
-  // small plans: k_decode finds its units' entry ranges itself (one launch), or (DECODE_SCATTER) the
-  // background and then the kept values; batches: k_bounds first
-  const bool search = plan->n_units <= DECODE_SEARCH_UNITS;
-  const bool scatter = (search || DECODE_SCATTER_ALL) && DECODE_SCATTER;
-  const uint32_t upb = WAVES * (hb ? decode_dpw<true, false>()
-                                   : search ? decode_dpw<false, true>() : decode_dpw<false, false>());  // units per block
-  const uint32_t g = (plan->n_units + upb - 1) / upb;
-  constexpr uint32_t DW = DECODE_NT / 64;
-  const uint32_t glds = (plan->n_units + DW * DECODE_LDS_DPW - 1) / (DW * DECODE_LDS_DPW);
   const coalac_sched_t* sc = sched;
   auto B = [&](int i) { return at_boundary(stages, DEC_SPAN, 2, i) ? boundary(sc, i, st) : COALAC_OK; };
 #define DEC_BOUNDARY(i)       \
@@ -3237,61 +3083,27 @@ int coalac_decode_sched(coalac_plan_t plan, const int32_t* d_idx, const void* d_
     if (rc_) return rc_;      \
   } while (0)
   DEC_BOUNDARY(0);
-  if ((stages & COALAC_STAGE_BOUNDS) && plan->n_bchunks && !search)
+  if ((stages & COALAC_STAGE_BOUNDS) && plan->n_bchunks && !lat && !d_ustart)
     hipLaunchKernelGGL(k_bounds, dim3(plan->n_bchunks), dim3(BLOCK), 0, st, P, plan->bchunks,
                        static_cast<uint32_t*>(d_ws));
   DEC_BOUNDARY(1);
-#define DEC(R, H)                                                                          \
-  do {                                                                                     \
-    if (search)                                                                            \
-      hipLaunchKernelGGL((k_decode<R, H, true>), dim3(g), dim3(BLOCK), 0, st, P);          \
-    else if (DECODE_LDS)                                                                   \
-      hipLaunchKernelGGL((k_decode_lds<R, H>), dim3(glds), dim3(DECODE_NT), 0, st, P);     \
-    else                                                                                   \
-      hipLaunchKernelGGL((k_decode<R, H, false>), dim3(g), dim3(BLOCK), 0, st, P);         \
+  const bool whole = (stages & COALAC_STAGE_FILL) && (stages & COALAC_STAGE_SCATTER);
+#define DISPATCH(F, ...)                                   \
+  do {                                                     \
+    if (raw && hb) F<true, true>(__VA_ARGS__);             \
+    else if (raw) F<true, false>(__VA_ARGS__);             \
+    else if (hb) F<false, true>(__VA_ARGS__);              \
+    else F<false, false>(__VA_ARGS__);                     \
   } while (0)
-  if (!(stages & COALAC_STAGE_DECODE))
-    ;
-  else if (scatter && DECODE_FS && (stages & COALAC_STAGE_FILL) && (stages & COALAC_STAGE_SCATTER)) {
-    const dim3 gf((plan->n_units + WAVES - 1) / WAVES);
-    if (raw && hb)
-      hipLaunchKernelGGL((k_fillscatter<true, true>), gf, dim3(BLOCK), 0, st, P);
-    else if (raw)
-      hipLaunchKernelGGL((k_fillscatter<true, false>), gf, dim3(BLOCK), 0, st, P);
-    else if (hb)
-      hipLaunchKernelGGL((k_fillscatter<false, true>), gf, dim3(BLOCK), 0, st, P);
-    else
-      hipLaunchKernelGGL((k_fillscatter<false, false>), gf, dim3(BLOCK), 0, st, P);
-  } else if (scatter) {
-    const uint32_t gf = (plan->n_units + WAVES - 1) / WAVES;
-    if (!(stages & COALAC_STAGE_FILL))
-      ;
-    else if (hb)
-      hipLaunchKernelGGL((k_fill<true>), dim3(gf), dim3(BLOCK), 0, st, P);
-    else
-      hipLaunchKernelGGL((k_fill<false>), dim3(gf), dim3(BLOCK), 0, st, P);
-    if (plan->n_bchunks && (stages & COALAC_STAGE_SCATTER)) {
-      const dim3 gs(plan->n_bchunks);
-      if (raw && hb)
-        hipLaunchKernelGGL((k_scatter<true, true>), gs, dim3(BLOCK), 0, st, P, plan->schunks);
-      else if (raw)
-        hipLaunchKernelGGL((k_scatter<true, false>), gs, dim3(BLOCK), 0, st, P, plan->schunks);
-      else if (hb)
-        hipLaunchKernelGGL((k_scatter<false, true>), gs, dim3(BLOCK), 0, st, P, plan->schunks);
-      else
-        hipLaunchKernelGGL((k_scatter<false, false>), gs, dim3(BLOCK), 0, st, P, plan->schunks);
-    }
-  } else if (!(stages & COALAC_STAGE_SCATTER))
-    ;  // FILL alone: k_decode writes the background itself
-  else if (raw && hb)
-    DEC(true, true);
-  else if (raw)
-    DEC(true, false);
-  else if (hb)
-    DEC(false, true);
+  if (lat && (!whole || !d_ustart))
+    // a separately enqueued FILL / SCATTER (the background may go out before the payload exists), or no starts:
+    // k_fill / k_scatter, or k_fillscatter (background, in-kernel range search, kept values on top)
+    DISPATCH(launch_fillscatter, P, plan, st, stages);
+  else if (!lat && !(stages & COALAC_STAGE_SCATTER))
+    ;  // FILL alone on a batch plan: k_decode_lds writes the background itself, with the kept values
   else
-    DEC(false, false);
-#undef DEC
+    DISPATCH(launch_decode_lds, P, plan, st);
+#undef DISPATCH
   DEC_BOUNDARY(2);
 #undef DEC_BOUNDARY
   HIP_CHECK(hipGetLastError());
@@ -3299,13 +3111,15 @@ int coalac_decode_sched(coalac_plan_t plan, const int32_t* d_idx, const void* d_
 }
 
 int coalac_decode(coalac_plan_t plan, const int32_t* d_idx, const void* d_vals, const float* d_mn,
-                  const float* d_scale, const float* d_base, float* d_out, void* d_ws, uint64_t ws_bytes,
-                  void* stream) {
-  return coalac_decode_ev(plan, d_idx, d_vals, d_mn, d_scale, d_base, d_out, d_ws, ws_bytes, stream, nullptr);
+                  const float* d_scale, const uint32_t* d_ustart, const float* d_base, float* d_out, void* d_ws,
+                  uint64_t ws_bytes, void* stream) {
+  return coalac_decode_ev(plan, d_idx, d_vals, d_mn, d_scale, d_ustart, d_base, d_out, d_ws, ws_bytes, stream,
+                          nullptr);
 }
 
 int coalac_aggregate_ev(coalac_plan_t plan, int clients, const int32_t* d_idx, const void* d_vals,
-                        const float* d_mn, const float* d_scale, const float* d_weights, float total, int mode,
+                        const float* d_mn, const float* d_scale, const uint32_t* d_ustart, const float* d_weights,
+                        float total, int mode,
                         const uint8_t* d_avg_mask, const float* d_base, float* d_out, void* d_ws,
                         uint64_t ws_bytes, void* stream, void* const* events) {
   if (!plan) return fail(COALAC_EINVAL, "coalac_aggregate: plan is NULL");
@@ -3319,6 +3133,8 @@ int coalac_aggregate_ev(coalac_plan_t plan, int clients, const int32_t* d_idx, c
   if (plan->bits != 32 && (!d_mn || !d_scale)) return fail(COALAC_EINVAL, "coalac_aggregate: mn/scale pointers are NULL");
   if ((reinterpret_cast<uintptr_t>(d_out) | reinterpret_cast<uintptr_t>(d_base)) & 15)
     return fail(COALAC_EINVAL, "coalac_aggregate: output/base must be 16-byte aligned");
+  if (reinterpret_cast<uintptr_t>(d_ustart) & 3)
+    return fail(COALAC_EINVAL, "coalac_aggregate: ustart must be 4-byte aligned");
   if (!d_ws || ws_bytes < plan->dec_ws)
     return fail(COALAC_EWORKSPACE, "coalac_aggregate: workspace %llu < required %llu", (unsigned long long)ws_bytes,
                 (unsigned long long)plan->dec_ws);
@@ -3347,7 +3163,7 @@ int coalac_aggregate_ev(coalac_plan_t plan, int clients, const int32_t* d_idx, c
   P.base = d_base;
   P.out = d_out;
   AggArgs A{};
-  A.ustart = static_cast<const uint32_t*>(d_ws);
+  A.ustart = d_ustart ? d_ustart : static_cast<const uint32_t*>(d_ws);  // the payloads' starts, or k_bounds'
   A.weights = d_weights;
   A.clients = (uint32_t)clients;
   A.T = T;
@@ -3360,7 +3176,7 @@ int coalac_aggregate_ev(coalac_plan_t plan, int clients, const int32_t* d_idx, c
   const coalac_sched_t s = record_only(events, 3);
   const coalac_sched_t* sc = events ? &s : nullptr;
   BOUNDARY(0);
-  if (plan->n_bchunks)
+  if (plan->n_bchunks && !d_ustart)
     hipLaunchKernelGGL(k_bounds, dim3(plan->n_bchunks), dim3(BLOCK), 0, st, P, plan->bchunks,
                        static_cast<uint32_t*>(d_ws));
   BOUNDARY(1);
@@ -3389,10 +3205,11 @@ int coalac_aggregate_ev(coalac_plan_t plan, int clients, const int32_t* d_idx, c
 }
 
 int coalac_aggregate(coalac_plan_t plan, int clients, const int32_t* d_idx, const void* d_vals, const float* d_mn,
-                     const float* d_scale, const float* d_weights, float total, int mode, const uint8_t* d_avg_mask,
-                     const float* d_base, float* d_out, void* d_ws, uint64_t ws_bytes, void* stream) {
-  return coalac_aggregate_ev(plan, clients, d_idx, d_vals, d_mn, d_scale, d_weights, total, mode, d_avg_mask, d_base,
-                             d_out, d_ws, ws_bytes, stream, nullptr);
+                     const float* d_scale, const uint32_t* d_ustart, const float* d_weights, float total, int mode,
+                     const uint8_t* d_avg_mask, const float* d_base, float* d_out, void* d_ws, uint64_t ws_bytes,
+                     void* stream) {
+  return coalac_aggregate_ev(plan, clients, d_idx, d_vals, d_mn, d_scale, d_ustart, d_weights, total, mode, d_avg_mask,
+                             d_base, d_out, d_ws, ws_bytes, stream, nullptr);
 }
 
 int coalac_workspace_fallbacks(coalac_plan_t plan, const void* d_ws, void* stream, int* out) {

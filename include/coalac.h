@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define COALAC_ABI_VERSION 3
+#define COALAC_ABI_VERSION 4
 
 enum {
   COALAC_OK = 0,
@@ -53,7 +53,8 @@ enum {
                                      (for callers that run several plans concurrently themselves) */
 };
 /* (ABI 3 dropped ABI 2's COALAC_FLAG_ONE_LAUNCH / FRONT_LAUNCH / ITEM_STAMPS: the one-launch encode variants
- * measured slower than the kernel sequence) */
+ * measured slower than the kernel sequence, DESIGN.md §6c. ABI 4 added the per-unit starts d_ustart to encode,
+ * decode and aggregate: wire v2) */
 
 /* One fp32 segment (= one flattened tensor of the state_dict). Offsets are in ELEMENTS.
  *   in_off : start of the segment in the flat input / dense output buffer; must be a multiple of 4
@@ -80,15 +81,19 @@ int coalac_plan_destroy(coalac_plan_t plan);
 /* ws_bytes / dec_ws_bytes: workspace coalac_encode / coalac_decode (and coalac_aggregate) need;
  * total_k: length of idx/vals;
  * span: max(in_off + n) = the minimum length (elements) of the input/output flat buffers;
- * n_units: 4096-element work units. Any output pointer may be NULL. */
+ * n_units: 4096-element work units (segment by segment: ceil(n / 4096) each) = the length of the per-unit
+ * starts array (ustart). Any output pointer may be NULL. */
 int coalac_plan_query(coalac_plan_t plan, uint64_t* ws_bytes, uint64_t* dec_ws_bytes, uint64_t* total_k,
                       uint64_t* span, uint64_t* n_units);
 
 /* Encode d_in (fp32[span]) into idx (int32[total_k], segment-relative, ascending per segment),
  * vals (uint8[total_k] codes or fp32[total_k]), mn (fp32[nseg]) and scale (fp32[nseg]).
+ * d_ustart (uint32[n_units], or NULL = not written): per 4096-element unit, the index (segment-relative, into
+ * the segment's idx list) of its first kept entry — the wire v2 section that lets a decoder find every unit's
+ * entries without searching the idx lists (coalac_decode / coalac_aggregate d_ustart).
  * d_base != NULL selects delta mode: the codec encodes (d_in - d_base). */
 int coalac_encode(coalac_plan_t plan, const float* d_in, const float* d_base, int32_t* d_idx,
-                  void* d_vals, float* d_mn, float* d_scale, void* d_ws, uint64_t ws_bytes,
+                  void* d_vals, float* d_mn, float* d_scale, uint32_t* d_ustart, void* d_ws, uint64_t ws_bytes,
                   unsigned flags, void* stream);
 
 /* Encode with every segment read from its OWN device pointer: d_seg_in is a DEVICE array of nseg
@@ -97,28 +102,30 @@ int coalac_encode(coalac_plan_t plan, const float* d_in, const float* d_base, in
  * coala/client/base.py:330-332). d_base (delta mode) stays a flat buffer indexed by in_off. Outputs,
  * workspace, flags and stream as coalac_encode. */
 int coalac_encode_segptr(coalac_plan_t plan, const float* const* d_seg_in, const float* d_base, int32_t* d_idx,
-                         void* d_vals, float* d_mn, float* d_scale, void* d_ws, uint64_t ws_bytes, unsigned flags,
-                         void* stream);
+                         void* d_vals, float* d_mn, float* d_scale, uint32_t* d_ustart, void* d_ws, uint64_t ws_bytes,
+                         unsigned flags, void* stream);
 
 /* Decode into the dense d_out (fp32[span]); only positions inside segments are written.
- * d_base != NULL: d_out = d_base + decoded (fused; d_out may alias d_base). The encoded arrays may come
- * from an untrusted blob: out-of-range or unsorted indices can mis-decode but never write outside the
- * segment (still, validate blobs on the host; coala_amd/compression/wire.py does). */
+ * d_ustart: the encoder's per-unit starts (wire v2), or NULL (a v1 payload: batches compute them with k_bounds,
+ * latency-bound plans search them in-kernel). d_base != NULL: d_out = d_base + decoded (fused; d_out may alias
+ * d_base). The encoded arrays may come from an untrusted blob: out-of-range or unsorted indices, or wrong
+ * starts, can mis-decode but never write outside the unit (still, validate blobs on the host; coala_amd/
+ * compression/codec.py validate() does). */
 int coalac_decode(coalac_plan_t plan, const int32_t* d_idx, const void* d_vals, const float* d_mn,
-                  const float* d_scale, const float* d_base, float* d_out, void* d_ws, uint64_t ws_bytes,
-                  void* stream);
+                  const float* d_scale, const uint32_t* d_ustart, const float* d_base, float* d_out, void* d_ws,
+                  uint64_t ws_bytes, void* stream);
 
 /* Profiling variants: identical work, plus hipEventRecord(events[i], stream) between kernels.
  * encode: [0] before k_sample, [1] after k_sample, [2] after k_scan, [3] after the select kernels
  *         (k_ghist, k_gwin, k_select), [4] after k_emit (recorded even if the plan has no large segment);
- * decode: [0] before k_bounds (plans of > 8192 units only), [1] before k_decode (plans of <= 8192 units:
- *         before k_fill), [2] after it (after k_scatter). NULL
+ * decode: [0] before k_bounds (batches decoding a payload without per-unit starts), [1] before the decode
+ *         kernel (k_decode_lds, or k_fillscatter / k_fill), [2] after it (after k_scatter). NULL
  *         array or NULL entries are skipped. */
 int coalac_encode_ev(coalac_plan_t plan, const float* d_in, const float* d_base, int32_t* d_idx,
-                     void* d_vals, float* d_mn, float* d_scale, void* d_ws, uint64_t ws_bytes,
+                     void* d_vals, float* d_mn, float* d_scale, uint32_t* d_ustart, void* d_ws, uint64_t ws_bytes,
                      unsigned flags, void* stream, void* const* events);
 int coalac_decode_ev(coalac_plan_t plan, const int32_t* d_idx, const void* d_vals, const float* d_mn,
-                     const float* d_scale, const float* d_base, float* d_out, void* d_ws,
+                     const float* d_scale, const uint32_t* d_ustart, const float* d_base, float* d_out, void* d_ws,
                      uint64_t ws_bytes, void* stream, void* const* events);
 
 /* Scheduled variants: identical work, split into stages that may be enqueued by separate calls on
@@ -127,23 +134,25 @@ int coalac_decode_ev(coalac_plan_t plan, const int32_t* d_idx, const void* d_val
  *           COALAC_STAGE_SMALL   k_small  (segments of <= 1024 elements, whole) 0 .. 1
  *           COALAC_STAGE_SCAN    k_scan   (the one HBM read of the large segments) 1 .. 2
  *           COALAC_STAGE_SELECT  k_ghist k_gwin k_select k_emit                  2 .. 4
- *   decode  COALAC_STAGE_BOUNDS  k_bounds (plans of > 8192 units; smaller    boundaries 0 .. 1
- *                                 plans need no bounds)
- *           COALAC_STAGE_DECODE  k_decode (plans of <= 8192 units: k_fill     1 .. 2
- *                                 writes the background, then k_scatter the
- *                                 kept values)
+ *   decode  COALAC_STAGE_BOUNDS  k_bounds (plans of > 8192 units decoding a   boundaries 0 .. 1
+ *                                 payload without per-unit starts; others
+ *                                 need no bounds)
+ *           COALAC_STAGE_DECODE  the whole decode: k_decode_lds (every line    1 .. 2
+ *                                 written once), or — a plan of <= 8192 units
+ *                                 without per-unit starts — k_fillscatter
  *           COALAC_STAGE_FILL    the background only (k_fill: 0, or the base)  1 .. 2
  *                                 of a plan of <= 8192 units; it reads no
  *                                 encoded array, so it may run before the
  *                                 payload exists. Other plans: nothing.
  *           COALAC_STAGE_SCATTER the kept values only (k_scatter), after a     1 .. 2
  *                                 FILL of the same d_out / d_base; other plans:
- *                                 the whole k_decode. FILL + SCATTER = DECODE.
+ *                                 the whole k_decode_lds. FILL + SCATTER = DECODE.
  * SAMPLE, SCAN, SELECT of one encode (and BOUNDS, DECODE of one decode) must run in this order on the
- * same workspace; SMALL is independent of them. A decode call of a plan of > 8192 units that enqueues the
- * kept values (DECODE or SCATTER) without BOUNDS must set COALAC_STAGE_BOUNDS_DONE: the caller states that
- * an earlier call enqueued BOUNDS for the same arrays on the same workspace, ordered before this one;
- * without it the call returns COALAC_EINVAL (stale bounds would mis-decode silently). The caller orders them, e.g. with the events below.
+ * same workspace; SMALL is independent of them. A decode call of a plan of > 8192 units without per-unit
+ * starts that enqueues the kept values (DECODE or SCATTER) without BOUNDS must set COALAC_STAGE_BOUNDS_DONE:
+ * the caller states that an earlier call enqueued BOUNDS for the same arrays on the same workspace, ordered
+ * before this one; without it the call returns COALAC_EINVAL (stale bounds would mis-decode silently). The
+ * caller orders them, e.g. with the events below.
  * (A whole encode places the small segments itself: beside k_scan on the plan's side stream for big
  * batches, inside k_scan otherwise; so does a call holding SAMPLE + SCAN + SMALL, the encode's front.) At every boundary an enqueued stage starts or ends at, the call first makes
  * `stream` wait for wait[i] (hipStreamWaitEvent; an event another stream recorded) and then records
@@ -168,10 +177,10 @@ typedef struct coalac_sched {
   unsigned stages;
 } coalac_sched_t;
 int coalac_encode_sched(coalac_plan_t plan, const float* d_in, const float* d_base, int32_t* d_idx,
-                        void* d_vals, float* d_mn, float* d_scale, void* d_ws, uint64_t ws_bytes,
+                        void* d_vals, float* d_mn, float* d_scale, uint32_t* d_ustart, void* d_ws, uint64_t ws_bytes,
                         unsigned flags, void* stream, const coalac_sched_t* sched);
 int coalac_decode_sched(coalac_plan_t plan, const int32_t* d_idx, const void* d_vals, const float* d_mn,
-                        const float* d_scale, const float* d_base, float* d_out, void* d_ws,
+                        const float* d_scale, const uint32_t* d_ustart, const float* d_base, float* d_out, void* d_ws,
                         uint64_t ws_bytes, void* stream, const coalac_sched_t* sched);
 
 /* Fused server-side decode + FedAvg of the `clients` updates the plan batches.
@@ -192,17 +201,18 @@ int coalac_decode_sched(coalac_plan_t plan, const int32_t* d_idx, const void* d_
  * (coala/server/base.py:588-591), where strategies.weighted_sum_only_params / federated_averaging_only_params
  * average the parameters only and keep models[0]'s buffers (coala/server/strategies.py:32-54, 93-124).
  * d_weights: DEVICE fp32[clients] = float(w_i); total: float(sum of the weights). d_out / d_base are
- * indexed like client 0's segments. Workspace: dec_ws_bytes of coalac_plan_query. Events (the _ev
- * variant): [0] before the unit-bounds pass, [1] before k_aggregate, [2] after. */
+ * indexed like client 0's segments. d_ustart: the clients' per-unit starts, concatenated in client order
+ * (uint32[n_units]), or NULL (then a k_bounds pass computes them). Workspace: dec_ws_bytes of
+ * coalac_plan_query. Events (the _ev variant): [0] before the unit-bounds pass, [1] before k_aggregate, [2] after. */
 enum { COALAC_AGG_DIV = 0, COALAC_AGG_RECIP = 1, COALAC_AGG_SUM = 2 };
 int coalac_aggregate(coalac_plan_t plan, int clients, const int32_t* d_idx, const void* d_vals,
-                     const float* d_mn, const float* d_scale, const float* d_weights, float total, int mode,
-                     const uint8_t* d_avg_mask, const float* d_base, float* d_out, void* d_ws, uint64_t ws_bytes,
-                     void* stream);
+                     const float* d_mn, const float* d_scale, const uint32_t* d_ustart, const float* d_weights,
+                     float total, int mode, const uint8_t* d_avg_mask, const float* d_base, float* d_out, void* d_ws,
+                     uint64_t ws_bytes, void* stream);
 int coalac_aggregate_ev(coalac_plan_t plan, int clients, const int32_t* d_idx, const void* d_vals,
-                        const float* d_mn, const float* d_scale, const float* d_weights, float total, int mode,
-                        const uint8_t* d_avg_mask, const float* d_base, float* d_out, void* d_ws,
-                        uint64_t ws_bytes, void* stream, void* const* events);
+                        const float* d_mn, const float* d_scale, const uint32_t* d_ustart, const float* d_weights,
+                        float total, int mode, const uint8_t* d_avg_mask, const float* d_base, float* d_out,
+                        void* d_ws, uint64_t ws_bytes, void* stream, void* const* events);
 
 /* Diagnostics: number of segments whose sampled thresholds were rejected and re-selected exactly in
  * the last encode that used workspace d_ws (synchronises `stream`). */

@@ -28,6 +28,9 @@ CodecSpec v1 (per fp32 segment = one flattened tensor of n elements):
   decode: xhat = mn + float(q) * scale  (fp32 multiply then fp32 add; never fused)
           dense out = 0 everywhere, xhat at idx; fused delta mode: out = base + dense (fp32 add, every
           element, so base -0.0 becomes +0.0 where nothing was selected).
+  ustart (wire v2): per 4096-element unit of every segment (ceil(n / 4096) of them, in segment order), the
+          index into the segment's idx list of the first kept entry at or after the unit's first element,
+          i.e. the number of the segment's kept indices below unit * 4096 (a sorted-list lower bound).
 """
 import math
 
@@ -165,6 +168,20 @@ def decode(idx, vals, mn, scale, segs, bits, span, base=None, out=None):
         b = None if base is None else base[off:off + n]
         out[off:off + n] = decode_segment(idx[oo:oo + k], vals[oo:oo + k], mn[s], scale[s], int(n), bits, b)
     return out
+
+
+UNIT = 4096
+
+
+def unit_starts(idx, segs):
+    """The wire v2 per-unit starts of an encode (idx of encode(), same segs): int32[sum ceil(n / UNIT)]."""
+    segs = np.asarray(segs, dtype=np.int64).reshape(-1, 4)
+    parts = []
+    for off, n, k, oo in segs:
+        nu = (int(n) + UNIT - 1) // UNIT
+        if nu:
+            parts.append(np.searchsorted(idx[oo:oo + k], np.arange(nu, dtype=np.int64) * UNIT, side="left"))
+    return np.concatenate(parts).astype(np.int32) if parts else np.zeros(0, dtype=np.int32)
 
 
 AGG_DIV, AGG_RECIP, AGG_SUM = 0, 1, 2

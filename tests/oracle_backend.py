@@ -19,8 +19,10 @@ class OraclePlan:
     def encode(self, flat, base=None, **_):
         x = flat.detach().cpu().numpy()
         b = None if base is None else base.detach().cpu().numpy()
-        idx, vals, mn, sc = O.encode(x, self.table.segs.astype(np.int64), self.bits, base=b)
-        return Encoded(torch.from_numpy(idx), torch.from_numpy(vals), torch.from_numpy(mn), torch.from_numpy(sc))
+        segs = self.table.segs.astype(np.int64)
+        idx, vals, mn, sc = O.encode(x, segs, self.bits, base=b)
+        return Encoded(torch.from_numpy(idx), torch.from_numpy(vals), torch.from_numpy(mn), torch.from_numpy(sc),
+                       torch.from_numpy(O.unit_starts(idx, segs)))
 
     def decode(self, enc, base=None, **_):
         b = None if base is None else base.detach().cpu().numpy()

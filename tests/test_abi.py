@@ -54,8 +54,19 @@ def test_null_arguments():
     lib = _lib.load()
     assert lib.coalac_plan_create(None, 1, 8, None) == -1
     assert lib.coalac_plan_destroy(None) == 0
-    assert lib.coalac_encode(None, None, None, None, None, None, None, None, 0, 0, None) == -1
-    assert lib.coalac_decode(None, None, None, None, None, None, None, None, 0, None) == -1
+    assert lib.coalac_encode(None, None, None, None, None, None, None, None, None, 0, 0, None) == -1
+    assert lib.coalac_decode(None, None, None, None, None, None, None, None, None, 0, None) == -1
+
+
+def test_binding_argument_counts_match_header():
+    """Every declaration's parameter count equals the ctypes binding's (an ABI change that misses one side would
+    shift every argument after it)."""
+    hdr = re.sub(r"/\*.*?\*/", "", open(_build.HDR).read(), flags=re.S)
+    decls = dict(re.findall(r"(coalac_\w+)\s*\(([^;{]*?)\)\s*;", hdr))
+    for name, _, args in _lib.SIGNATURES:
+        params = decls[name].strip()
+        n = 0 if params in ("", "void") else params.count(",") + 1
+        assert n == len(args), (name, n, len(args))
 
 
 def test_enum_constants_match_header():

@@ -85,10 +85,10 @@ def test_deepcopy_shares_payload_and_packs_once():
 def _blob_with(header_edit):
     codec = UpdateCodec(0.05, 8, "weights", OracleBackend())
     up = codec.encode(build_module("lenet", seed=6).state_dict())
-    h, mn, sc, idx, vals, raw = wire.unpack(up.to_bytes())
+    h, mn, sc, idx, vals, raw, ust = wire.unpack(up.to_bytes())
     h = copy.deepcopy(h)
     header_edit(h)
-    return wire.pack(h, mn, sc, idx, vals, raw)
+    return wire.pack(h, mn, sc, idx, vals, raw, ustart=ust if "n_units" in h else None)
 
 
 @pytest.mark.parametrize("edit", ["off", "n", "seg"])
@@ -108,8 +108,26 @@ def test_validate_rejects_inconsistent_segment_entries(edit):
 def test_validate_accepts_encoder_output():
     codec = UpdateCodec(0.05, 8, "weights", OracleBackend())
     up = codec.encode(build_module("resnet18_split_cut4", seed=8).state_dict())
-    h, mn, sc, idx, vals, raw = wire.unpack(up.to_bytes())
-    validate(h, idx)
+    h, mn, sc, idx, vals, raw, ust = wire.unpack(up.to_bytes())
+    assert ust is not None and h["n_units"] == ust.size  # wire v2
+    validate(h, idx, ust)
+
+
+def test_validate_rejects_inconsistent_unit_starts():
+    """Wire v2: the per-unit starts must be exactly the lower bounds of the units in the idx lists (a lying
+    start would make the decode drop or misplace a unit's entries)."""
+    codec = UpdateCodec(0.05, 8, "weights", OracleBackend())
+    up = codec.encode(build_module("resnet18_split_cut4", seed=8).state_dict())
+    h, mn, sc, idx, vals, raw, ust = wire.unpack(up.to_bytes())
+    big = int(np.argmax(np.diff(ust)))  # a unit with kept entries: move its start by one
+    for bad in (ust + np.int32(1), np.concatenate([ust[:big + 1], ust[big + 1:] - 1])):
+        with pytest.raises(ValueError):
+            CompressedUpdate.from_bytes(wire.pack(h, mn, sc, idx, vals, raw, ustart=bad.astype(np.int32)))
+    h2 = dict(h, n_units=h["n_units"] - 1)
+    with pytest.raises(ValueError):
+        CompressedUpdate.from_bytes(wire.pack(h2, mn, sc, idx, vals, raw, ustart=ust[:-1]))
+    back = CompressedUpdate.from_bytes(wire.pack(h, mn, sc, idx, vals, raw, ustart=ust))
+    assert torch.equal(back.encoded.ustart, torch.from_numpy(ust.copy()))
 
 
 def test_snapshot_follows_codec_device_and_moves_once():

@@ -11,7 +11,7 @@ import numpy as np
 import pytest
 import torch
 
-from coala_amd.compression import CodecPlan, CompressionClientMixin, CompressionServerMixin, UpdateCodec
+from coala_amd.compression import CodecPlan, CompressionClientMixin, CompressionServerMixin, Encoded, UpdateCodec
 from coala_amd.compression._lib import CodecError
 from coala_amd.fl import LoopbackClient, LoopbackServer, federated_averaging
 from coala_amd.layouts import build_module, fp32_sizes
@@ -44,13 +44,15 @@ def test_aggregate_matches_oracle_both_modes(cuda, bits, ratio, delta):
     segs = plan.table.segs.astype(np.int64)
     h = [t.cpu().numpy() for t in (enc.idx, enc.vals, enc.mn, enc.scale)]
     b = None if base is None else base.cpu().numpy()
+    v1 = Encoded(enc.idx, enc.vals, enc.mn, enc.scale)  # without the per-unit starts: k_bounds computes them
     for mode, om in (("recip", O.AGG_RECIP), ("div", O.AGG_DIV)):
-        out = plan.aggregate(enc, weights, base=base, mode=mode)
-        torch.cuda.synchronize()
         ref = O.aggregate(*h, segs, bits, C, weights, sum(weights), om, base=b, out_span=plan.table.span_per_client)
-        g = out.cpu().numpy()
-        for off, n in zip(plan.table.offsets, plan.table.sizes):
-            np.testing.assert_array_equal(g[off:off + n].view(np.uint32), ref[off:off + n].view(np.uint32))
+        for e in (enc, v1):
+            out = plan.aggregate(e, weights, base=base, mode=mode)
+            torch.cuda.synchronize()
+            g = out.cpu().numpy()
+            for off, n in zip(plan.table.offsets, plan.table.sizes):
+                np.testing.assert_array_equal(g[off:off + n].view(np.uint32), ref[off:off + n].view(np.uint32))
 
 
 @pytest.mark.parametrize("delta", [True, False])
@@ -146,8 +148,8 @@ def test_aggregate_rejects_non_copy_layouts(cuda):
     from coala_amd.compression import _lib
     plan = CodecPlan([5000, 300, 7000], 0.01, 8, clients=1)
     # 3 segments cannot be 2 copies of one layout: refused before any launch
-    rc = plan._lib.coalac_aggregate(plan._h, 2, None, None, None, None, None, ctypes.c_float(1.0), 0, None, None,
-                                    None, None, ctypes.c_uint64(0), None)
+    rc = plan._lib.coalac_aggregate(plan._h, 2, None, None, None, None, None, None, ctypes.c_float(1.0), 0, None,
+                                    None, None, None, ctypes.c_uint64(0), None)
     with pytest.raises(CodecError, match="copies"):
         _lib.check(rc, "coalac_aggregate")
     with pytest.raises(ValueError):

@@ -8,7 +8,8 @@ batch is synthesised on the GPU exactly as bench.py does (coala_amd/workload.py)
 with the SplitPipeline the bench times, and compared client by client with oracle/codec_oracle.py run
 over a spawned process pool (tests/oracle_pool.py) on a shared-memory copy of the same batch.
 
-Tolerance (the bar of test_gpu_parity.py): idx, codes, mn, scale BIT-IDENTICAL; the dense output
+Tolerance (the bar of test_gpu_parity.py): idx, codes, mn, scale and the per-unit starts (wire v2)
+BIT-IDENTICAL; the dense output
 bit-identical to the oracle's decode at every kept position and +0.0 (weights mode) / base + 0.0f (delta
 mode) everywhere else inside the segments.
 """
@@ -20,6 +21,7 @@ from coala_amd.compression import SplitPipeline
 from coala_amd.compression.spec import SegmentTable
 from coala_amd.layouts import fp32_sizes
 from coala_amd.workload import c5_share, mixed_table, synth_batch
+from oracle import codec_oracle as O
 from tests.oracle_pool import SharedBatch, oracle_clients
 
 pytestmark = pytest.mark.gpu
@@ -67,8 +69,9 @@ def test_fullsize_share_bit_exact_vs_oracle(cuda, case):
         assert pipe.fallbacks() == 0
         g_idx, g_vals = enc.idx.cpu().numpy(), enc.vals.cpu().numpy()
         g_mn, g_sc = enc.mn.cpu().numpy().view(np.uint32), enc.scale.cpu().numpy().view(np.uint32)
+        g_us = enc.ustart.cpu().numpy()
 
-        so, ko, to = table.client_span_off, table.client_k_off, table.client_seg_off
+        so, ko, to, uo = table.client_span_off, table.client_k_off, table.client_seg_off, table.client_unit_off
         segs = table.segs.astype(np.int64)
         spans, csegs = [], []
         for c in range(table.clients):
@@ -84,6 +87,8 @@ def test_fullsize_share_bit_exact_vs_oracle(cuda, case):
             np.testing.assert_array_equal(g_vals[k0:k1], vals, err_msg=f"{case} client {c}: codes")
             np.testing.assert_array_equal(g_mn[to[c]:to[c + 1]], mn.view(np.uint32), err_msg=f"{case} client {c}: mn")
             np.testing.assert_array_equal(g_sc[to[c]:to[c + 1]], sc.view(np.uint32), err_msg=f"{case} client {c}: scale")
+            np.testing.assert_array_equal(g_us[uo[c]:uo[c + 1]], O.unit_starts(idx, csegs[c]),
+                                          err_msg=f"{case} client {c}: per-unit starts")
             p = torch.from_numpy(pos + so[c]).to(cuda)
             got = out[p].view(torch.int32)
             want = torch.from_numpy(xhat).to(cuda).view(torch.int32)

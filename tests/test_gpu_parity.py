@@ -1,15 +1,16 @@
 """GPU parity: HIP kernels (through the C ABI) vs the CPU oracle, bit-exact.
 
-Tolerance (written here as the bar): indices, codes, mn, scale and decoded values must be BIT-IDENTICAL
-to oracle/codec_oracle.py (both follow the same fp32 op order with no FMA). The spec's guaranteed bound,
-if a rounding-boundary case ever differed, would be one quantisation step; we do not
-use it — any difference fails.
+Tolerance (written here as the bar): indices, codes, mn, scale, the wire v2 per-unit starts and decoded values
+must be BIT-IDENTICAL to oracle/codec_oracle.py (both follow the same fp32 op order with no FMA). The spec's
+guaranteed bound, if a rounding-boundary case ever differed, would be one quantisation step;
+we do not use it — any difference fails. Every decode runs twice: from the encoder's per-unit starts (wire v2)
+and without them (a v1 payload: k_bounds / the in-kernel search).
 """
 import numpy as np
 import pytest
 import torch
 
-from coala_amd.compression import CodecPlan, SegmentTable
+from coala_amd.compression import CodecPlan, Encoded, SegmentTable
 from coala_amd.compression._lib import COALAC_FLAG_FORCE_EXACT, COALAC_FLAG_GENERIC_SELECT
 from coala_amd.compression.spec import SMALL_MAX, SMALL_MAX_LATENCY, small_limit
 from coala_amd.layouts import fp32_sizes
@@ -38,13 +39,15 @@ def run_both(sizes, ratio, bits, xs, bases=None, flags=0, clients=1):
     ws = plan.empty_workspace()
     enc = plan.encode(d_flat, base=d_base, workspace=ws, flags=flags)
     dec = plan.decode(enc, base=d_base)
+    dec_v1 = plan.decode(Encoded(enc.idx, enc.vals, enc.mn, enc.scale), base=d_base)  # no per-unit starts
     torch.cuda.synchronize()
     g = dict(idx=enc.idx.cpu().numpy(), vals=enc.vals.cpu().numpy(), mn=enc.mn.cpu().numpy(),
-             scale=enc.scale.cpu().numpy(), dec=dec.cpu().numpy(), fallbacks=plan.fallbacks(ws))
+             scale=enc.scale.cpu().numpy(), ustart=enc.ustart.cpu().numpy(), dec=dec.cpu().numpy(),
+             dec_v1=dec_v1.cpu().numpy(), fallbacks=plan.fallbacks(ws))
     segs = table.segs.astype(np.int64)
     idx, vals, mn, sc = O.encode(flat, segs, bits, base=base)
     ref_dec = O.decode(idx, vals, mn, sc, segs, bits, table.span, base=base)
-    r = dict(idx=idx, vals=vals, mn=mn, scale=sc, dec=ref_dec)
+    r = dict(idx=idx, vals=vals, mn=mn, scale=sc, ustart=O.unit_starts(idx, segs), dec=ref_dec)
     return plan, g, r
 
 
@@ -54,8 +57,10 @@ def assert_same(plan, g, r):
     np.testing.assert_array_equal(g["vals"].view(np.uint8), r["vals"].view(np.uint8))
     np.testing.assert_array_equal(g["mn"].view(np.uint32), r["mn"].view(np.uint32))
     np.testing.assert_array_equal(g["scale"].view(np.uint32), r["scale"].view(np.uint32))
+    np.testing.assert_array_equal(g["ustart"], r["ustart"])
     for (off, n, k, oo) in t.segs.astype(np.int64):
         np.testing.assert_array_equal(g["dec"][off:off + n].view(np.uint32), r["dec"][off:off + n].view(np.uint32))
+        np.testing.assert_array_equal(g["dec_v1"][off:off + n].view(np.uint32), r["dec"][off:off + n].view(np.uint32))
 
 
 def gauss(rng, sizes, lo=-4, hi=-2):
@@ -196,13 +201,16 @@ def test_raw_bits_idempotent(cuda):
     assert torch.equal(e1.idx, e2.idx) and torch.equal(e1.vals, e2.vals)
 
 
+@pytest.mark.parametrize("starts", ["none", "garbage"])
+@pytest.mark.parametrize("clients", [1, 3])
 @pytest.mark.parametrize("kind", ["random", "reversed", "out_of_range", "duplicates"])
-def test_decode_untrusted_idx_stays_in_bounds(cuda, kind):
-    """A corrupt idx list (the blob may be untrusted) can mis-decode but never write outside its
-    segment: the decode kernel's unit-range search and scatter are bounds-checked. Sentinels after the
-    span and in the alignment pads between segments must survive."""
-    sizes = [5000, 70, 9000, 4096 * 3 + 5]
-    plan = CodecPlan(sizes, 0.1, 8)
+def test_decode_untrusted_idx_stays_in_bounds(cuda, kind, clients, starts):
+    """A corrupt idx list or corrupt per-unit starts (the blob may be untrusted) can mis-decode but never write
+    outside its segment: the decode kernels' unit ranges are clamped and every kept entry is bounds-checked
+    against its unit. Sentinels after the span and in the alignment pads between segments must survive. clients
+    3 makes a plan of > 8192 units (the batch decode), 1 a latency-bound one."""
+    sizes = [5000, 70, 9000, 4096 * 3 + 5] + ([4096 * 4000] if clients == 3 else [])
+    plan = CodecPlan(sizes, 0.1, 8, clients=clients)
     t = plan.table
     rng = np.random.default_rng(11)
     enc = plan.empty_encoded()
@@ -219,6 +227,11 @@ def test_decode_untrusted_idx_stays_in_bounds(cuda, kind):
     enc.vals.copy_(torch.from_numpy(rng.integers(0, 256, K, dtype=np.uint8)))
     enc.mn.fill_(1.0)
     enc.scale.fill_(0.5)
+    if starts == "none":
+        enc.ustart = None
+    else:
+        enc.ustart.copy_(torch.from_numpy(rng.integers(-(2 ** 31), 2 ** 31 - 1, plan.n_units, dtype=np.int64)
+                                          .astype(np.int32)))
     sentinel = 12345.0
     out = torch.full((t.span + 1024,), sentinel, dtype=torch.float32, device="cuda")
     plan.decode(enc, out=out)
@@ -254,6 +267,7 @@ def test_golden_vectors_bit_exact(cuda, ratio, bits):
     dec = plan.decode(enc).cpu().numpy()
     idx, vals = enc.idx.cpu().numpy(), enc.vals.cpu().numpy()
     mn, sc = enc.mn.cpu().numpy(), enc.scale.cpu().numpy()
+    np.testing.assert_array_equal(enc.ustart.cpu().numpy(), O.unit_starts(idx, t.segs.astype(np.int64)))
     for s, (n, (off, _, k, oo)) in enumerate(zip(names, t.segs.astype(np.int64))):
         tag = f"{n}/r{ratio}/b{bits}"
         assert int(gold[f"{tag}/k"][0]) == k, tag

@@ -212,16 +212,23 @@ def test_decode_fill_scatter_stages(cuda):
 
 
 def test_decode_scatter_without_bounds_is_refused(cuda):
-    """A batch plan (> 8192 units) decodes its kept values from the per-unit bounds k_bounds leaves in the
-    workspace. SCATTER alone on a fresh workspace would read stale bounds: the ABI refuses it (EINVAL)
-    unless the caller sets BOUNDS_DONE after its own BOUNDS call — which then decodes exactly."""
-    from coala_amd.compression import _lib
+    """A batch plan (> 8192 units) decoding a payload WITHOUT per-unit starts (wire v1) reads the bounds k_bounds
+    leaves in the workspace. SCATTER alone on a fresh workspace would read stale bounds: the ABI refuses it
+    (EINVAL) unless the caller sets BOUNDS_DONE after its own BOUNDS call — which then decodes exactly. With the
+    payload's starts (wire v2) nothing is read from the workspace: SCATTER alone decodes exactly."""
+    from coala_amd.compression import Encoded, _lib
     t = SegmentTable(fp32_sizes("resnet50_tv"), 0.01, 4)
     assert CodecPlan(None, 0.01, 8, table=t, device=cuda).n_units > 8192
     flat = synth_batch(t, cuda, client_ids=range(4))
     plan = CodecPlan(None, 0.01, 8, table=t, device=cuda)
-    e = plan.encode(flat)
+    e2 = plan.encode(flat)
+    e = Encoded(e2.idx, e2.vals, e2.mn, e2.scale)  # the same payload without its starts
     ref = plan.decode(e, out=torch.zeros_like(flat))
+    o2 = torch.zeros_like(flat)
+    garbage = torch.full((plan.dec_ws_bytes,), 0xAB, dtype=torch.uint8, device=cuda)
+    plan.decode(e2, out=o2, workspace=garbage, sched=(None, None, _lib.COALAC_STAGE_SCATTER))
+    torch.cuda.synchronize()
+    assert torch.equal(o2.view(torch.int32), ref.view(torch.int32))
     ws = torch.full((plan.dec_ws_bytes,), 0xAB, dtype=torch.uint8, device=cuda)  # garbage bounds
     out = torch.zeros_like(flat)
     for stages in (_lib.COALAC_STAGE_SCATTER, _lib.COALAC_STAGE_DECODE):
@@ -236,6 +243,7 @@ def test_decode_scatter_without_bounds_is_refused(cuda):
     p1 = CodecPlan(None, 0.01, 8, table=t1, device=cuda)
     f1 = flat[:t1.span]
     e1 = p1.encode(f1)
+    e1 = Encoded(e1.idx, e1.vals, e1.mn, e1.scale)
     r1 = p1.decode(e1, out=torch.zeros_like(f1))
     o1 = torch.zeros_like(f1)
     p1.decode(e1, out=o1, sched=(None, None, _lib.COALAC_STAGE_FILL))

@@ -24,7 +24,7 @@ def test_pack_unpack_roundtrip():
     h = {"bits": 8, "n_segments": 2, "total_k": 3, "x": [1, 2]}
     blob = wire.pack(h, np.array([1, 2], np.float32), np.array([3, 4], np.float32), np.array([5, 6, 7], np.int32),
                      np.array([8, 9, 10], np.uint8), b"raw!")
-    h2, mn, sc, idx, vals, raw = wire.unpack(blob)
+    h2, mn, sc, idx, vals, raw, _ = wire.unpack(blob)
     assert h2 == h and raw == b"raw!"
     assert mn.tolist() == [1, 2] and sc.tolist() == [3, 4] and idx.tolist() == [5, 6, 7] and vals.tolist() == [8, 9, 10]
 
@@ -66,7 +66,7 @@ def test_bad_magic_and_version():
 def test_validate_rejects_corrupt_indices():
     u = _update()
     blob = u.to_bytes()
-    h, mn, sc, idx, vals, raw = wire.unpack(blob)
+    h, mn, sc, idx, vals, raw, _ = wire.unpack(blob)
     bad = idx.copy()
     bad[0] = 99  # out of range for a 6-element segment
     blob2 = wire.pack(h, mn, sc, bad, vals, raw)
