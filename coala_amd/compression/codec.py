@@ -15,6 +15,7 @@ honours:
 """
 import copy
 import math
+import sys
 import threading
 from collections import OrderedDict
 from collections.abc import Mapping
@@ -370,9 +371,17 @@ class RawState(Mapping):
     def fresh(self, device=None):
         """{name: tensor} with storage of its own (one copy per group, onto `device` if given): what a
         decode hands out, so decoded modules never alias the update or each other."""
+        return self.fresh_groups(device)[1]
+
+    def fresh_groups(self, device=None):
+        """(the per-group flat copies, fresh()'s {name: view of them})."""
         groups = [(f.to(device, copy=True) if device is not None else f.clone(), m) for f, m in self._groups]
         views = self._make_views(groups)
-        return {n: views[n] for n in self._order}
+        return [f for f, _ in groups], {n: views[n] for n in self._order}
+
+    def signature(self):
+        """What a copy into another RawState's group buffers needs to match: dtype, size and members per group."""
+        return tuple((f.dtype, f.numel(), tuple(m)) for f, m in self._groups)
 
 
 def _snapshot_raw(raw):
@@ -800,9 +809,16 @@ class UpdateCodec:
         upload, coala/server/service.py:74), after a pinned H2D of a received payload; the caller's current
         stream waits for it (no host synchronisation), so the returned tensors are ready for any work the
         caller enqueues next."""
+        return self._decode(update, base, device)[0]
+
+    def _decode(self, update, base=None, device=None, into=None):
+        """decode_state's work: (state, flat buffer, raw group buffers). `into` (a recycled skeleton, see
+        decode_module): decode into its flat buffer and copy the passthrough entries into its raw buffers
+        instead of allocating — state is then None."""
         h = update.header  # self-describing: decode with the blob's own ratio/bits/mode
         D = _decode_layout(h["entries"])
         flat = plan = None
+        raw = update.raw
         if D.sizes:
             if device is None:
                 device = self.backend.default_device()
@@ -817,36 +833,64 @@ class UpdateCodec:
                 cur = torch.cuda.current_stream(device)
                 side = self._thread_stream(device)
                 side.wait_stream(cur)
-                out = torch.empty(plan.span, dtype=torch.float32, device=device)  # (the caller's stream's pool)
+                # (the caller's stream's pool; a recycled skeleton's buffer is only reused once its consumers,
+                # ordered on that stream, are done: the side stream waits for it above)
+                out = into.flat if into is not None else torch.empty(plan.span, dtype=torch.float32, device=device)
                 with torch.cuda.stream(side):
                     enc = update.encoded_to(device, staging=self._staging)
                     self._staged(side)
                     flat = plan.decode(enc, base=base_flat, out=out, stream=side)
+                    if into is not None:
+                        for dst, (src, _) in zip(into.raws, raw._groups):
+                            dst.copy_(src, non_blocking=True)
                 cur.wait_stream(side)
             else:
                 enc = update.encoded.to(device, non_blocking=True)
-                flat = plan.decode(enc, base=base_flat)
+                flat = plan.decode(enc, base=base_flat, out=None if into is None else into.flat)
+                if into is not None:
+                    for dst, (src, _) in zip(into.raws, raw._groups):
+                        dst.copy_(src)
+        elif into is not None:
+            for dst, (src, _) in zip(into.raws, raw._groups):
+                dst.copy_(src)
+        if into is not None:
+            return None, flat, into.raws
         vals = [None] * len(D.names)
         if D.sizes:
             for pos, v in zip(D.seg_pos, _segment_views(flat, plan.table, h["entries"])):
                 vals[pos] = v
+        raws = None
         if D.raw:
-            raw = update.raw
-            raw = raw.fresh(device) if isinstance(raw, RawState) else \
-                {n: (t.to(device) if device is not None else t).clone() for n, t in raw.items()}
+            if isinstance(raw, RawState):
+                raws, raw = raw.fresh_groups(device)
+            else:
+                raw = {n: (t.to(device) if device is not None else t).clone() for n, t in raw.items()}
             for pos, name in D.raw:
                 vals[pos] = raw[name]
-        return OrderedDict(zip(D.names, vals))
+        return OrderedDict(zip(D.names, vals)), flat, raws
 
     def decode_module(self, update, template, base=None):
         """CompressedUpdate -> new nn.Module shaped like `template` holding the decoded state.
 
         No parameter data is copied: the new module's parameters/buffers are views into the decode
-        output (deepcopy with a memo that pre-binds every tensor). `template` is never aliased.
-        """
-        state = self.decode_state(update, base=base)
-        return module_with_state(template, state)
-
+        output. `template` is never aliased. Decoded modules are RECYCLED: once nothing outside this codec
+        references a module it returned — none of its submodules, parameters or buffers (the reference server
+        drops a round's uploads when the next round's replace them in client_uploads, coala/server/base.py:
+        377-381, 562-571) — a later call of the same layout decodes straight into that module's storage and
+        returns it, instead of building a module tree again (the Python of ~130 modules and ~160 Parameters
+        for a ResNet-50 was most of a decompression(model) call)."""
+        D = _decode_layout(update.header["entries"])
+        recipe = _recipe(template)
+        device = self.backend.default_device() if D.sizes else None
+        sk = recipe.idle_skeleton(D, update.raw, device)
+        if sk is not None:
+            root = sk.root  # (a reference of this frame: the skeleton is no longer idle for other threads)
+            self._decode(update, base, device, into=sk)
+            recipe.refresh(sk)
+            return root
+        box = [None]
+        box[0], flat, raws = self._decode(update, base, device)  # (the state lives in `box` only)
+        return recipe.build_and_adopt(box, D, flat, raws, update.raw, device)
 
     # -- fused server-side aggregation ------------------------------------------------------------
     def aggregate(self, updates, weights, template, base=None, mode="recip", device=None, params_only=False):
@@ -1003,6 +1047,7 @@ class _TreeRecipe:
     set, table sizes or special attribute types changed since is re-classified."""
 
     def __init__(self, template):
+        self.pool, self.pool_lock = [], threading.Lock()
         self.mods, self.prefixes, self.index = [], [], {}
         stack = [(template, "")]
         while stack:
@@ -1056,7 +1101,10 @@ class _TreeRecipe:
             self.getters.append(None if not keys else itemgetter(*keys) if len(keys) > 1 else
                                 (lambda d, k=keys[0]: (d[k],)))
 
-    def build(self, state):
+    def _current(self):
+        """Re-classify the template modules that changed since (attribute / table sizes, hooks registered, the
+        types of special attributes); returns the per-module fast tables. A change also retires every pooled
+        skeleton (they were built from the old classification)."""
         mods, info = self.mods, self.info
         if not hasattr(self, "getters"):
             self._getters()
@@ -1065,9 +1113,22 @@ class _TreeRecipe:
             for i in stale:
                 info[i] = self.classify(mods[i], self.prefixes[i])
             self._getters()
+            with self.pool_lock:
+                self.pool.clear()
         fast = self.__dict__.get("fast")
         if fast is None or stale:
             fast = self.fast = [self._fast(x) for x in info]
+            self.plain = [tuple(k for k in m.__dict__ if k not in _MODULE_TABLES and k not in set(f[5] + f[9] + f[10]))
+                          for m, f in zip(mods, fast)]
+        return fast
+
+    def build(self, state):
+        return self._build(state)[0]
+
+    def _build(self, state):
+        """The new module tree: the list of new module objects in recipe order (root first)."""
+        mods = self.mods
+        fast = self._current()
         new = [m.__class__.__new__(m.__class__) for m in mods]
         get = state.get
         deep_todo = []
@@ -1102,7 +1163,72 @@ class _TreeRecipe:
                 nd = new[i].__dict__
                 for k in deep:
                     nd[k] = copy.deepcopy(nd[k], memo)
-        return new[0]
+        return new
+
+    # -- recycling of decoded modules (UpdateCodec.decode_module) ------------------------------------------
+    POOL_MAX = 64            # skeletons kept per template (a server needs two rounds' uploads: 2 x clients)
+    POOL_BYTES = 16 << 30    # ... and at most this many bytes of decoded storage
+
+    def build_and_adopt(self, box, D, flat, raws, raw, device):
+        """Build the module tree for the decoded state in box (a one-element list, emptied here: the caller
+        keeps no reference to the state) and keep it in the pool as a skeleton for later decodes of the same
+        layout. Returns the root module."""
+        state = box.pop()
+        new = self._build(state)
+        del state
+        root = new[0]
+        if (flat is None and not raws) or not isinstance(raw, RawState) or len(self.pool) >= self.POOL_MAX:
+            return root
+        nbytes = (flat.numel() * 4 if flat is not None else 0) + sum(r.numel() * r.element_size() for r in raws or ())
+        with self.pool_lock:
+            if sum(sk.nbytes for sk in self.pool) + nbytes > self.POOL_BYTES or len(self.pool) >= self.POOL_MAX:
+                return root
+            sk = _Skeleton(root, new, flat, list(raws or ()), D, raw.signature(), device, nbytes)
+            del new
+            sk.base = sk.counts()
+            sk.base[0][0] -= 1  # the root: this frame's `root` is the only transient reference
+            self.pool.append(sk)
+        return root
+
+    def idle_skeleton(self, D, raw, device):
+        """A pooled skeleton of this layout that nothing outside the pool references any more (every module,
+        parameter and buffer object at its idle reference count, the decoded storage at its idle use count,
+        every module's tables unchanged), or None."""
+        if not self.pool or not isinstance(raw, RawState):
+            return None
+        self._current()
+        sig = raw.signature()
+        with self.pool_lock:
+            for sk in self.pool:
+                if sk.D is D and sk.device == device and sk.raw_sig == sig and sk.counts() == sk.base:
+                    sk.generation += 1  # (the caller takes `sk.root` before releasing the lock's protection)
+                    return sk
+        return None
+
+    def refresh(self, sk):
+        """Bring a recycled tree's attributes in line with the template's CURRENT ones, as a fresh build would:
+        plain attributes copied, hook containers emptied if a previous holder registered hooks, special
+        attributes re-copied unless still equal."""
+        memo = None
+        for i, (m, c) in enumerate(zip(self.mods, sk.mods)):
+            d, nd = m.__dict__, c.__dict__
+            f = self.fast[i]
+            for k in self.plain[i]:
+                nd[k] = d[k]
+            for k, tv in zip(f[5], f[6]):
+                if nd.get(k):
+                    nd[k] = tv()
+            for k in f[9]:
+                nd[k] = d[k].clone()
+            for k in f[10]:
+                try:
+                    same = bool(nd.get(k) == d[k])
+                except Exception:
+                    same = False
+                if not same:
+                    if memo is None:
+                        memo = self._memo(sk.mods, {})
+                    nd[k] = copy.deepcopy(d[k], memo)
 
     @staticmethod
     def _fast(x):
@@ -1113,7 +1239,7 @@ class _TreeRecipe:
                 tuple(n for n, _ in children), tuple(j for _, j in children),
                 tuple(k for k, _ in tens), tuple(k for k, _ in deep))
 
-    def _memo(self, new, state):
+    def _memo(self, new, state=None):
         """deepcopy memo: template module / parameter / buffer -> its counterpart in the clone."""
         memo = {}
         for m, c in zip(self.mods, new):
@@ -1128,18 +1254,38 @@ class _TreeRecipe:
         return memo
 
 
+class _Skeleton:
+    """A decoded module tree kept for reuse: its objects (modules, then their parameter / buffer tensors), the
+    decoded storage they view (the flat fp32 decode output and the passthrough groups) and their idle
+    reference counts."""
+
+    __slots__ = ("root", "mods", "objs", "sizes", "flat", "raws", "D", "raw_sig", "device", "nbytes", "base",
+                 "generation")
+
+    def __init__(self, root, mods, flat, raws, D, raw_sig, device, nbytes):
+        self.root, self.mods = root, mods
+        self.objs = list(mods)
+        for c in mods:
+            self.objs.extend(t for t in c._parameters.values() if t is not None)
+            self.objs.extend(t for t in c._buffers.values() if t is not None)
+        self.sizes = [(len(c._parameters), len(c._buffers), len(c._modules)) for c in mods]
+        self.flat, self.raws, self.D, self.raw_sig, self.device, self.nbytes = flat, raws, D, raw_sig, device, nbytes
+        self.generation = 0
+
+    def counts(self):
+        refs = list(map(sys.getrefcount, self.objs))
+        store = [torch._C._storage_Use_Count(t.untyped_storage()._cdata) for t in [self.flat] + self.raws
+                 if t is not None]
+        sizes = [(len(c._parameters), len(c._buffers), len(c._modules)) for c in self.mods]
+        return [refs, store, sizes == self.sizes]
+
+
 _RECIPES = {}  # id(template) -> (weakref to it, recipe)
 _RECIPES_LOCK = threading.Lock()
 
 
-def module_with_state(template, state):
-    """A new nn.Module shaped like `template` whose parameters / buffers ARE the tensors of `state`
-    (views into the decode output: no parameter data is copied; `template` is never aliased).
-
-    The module tree is rebuilt from a per-template recipe (_TreeRecipe) — new objects of the same classes,
-    their __dict__ copied one level deep with fresh tables and hook dicts, other attributes deep-copied —
-    instead of copy.deepcopy, whose generic recursion cost ~8 ms per ResNet-50 on the server's per-upload
-    path. Tensors outside the state (non-persistent buffers, unregistered tensors) are cloned."""
+def _recipe(template):
+    """The template's _TreeRecipe (one per template object: the server's global model, for a whole task)."""
     key = id(template)
     with _RECIPES_LOCK:
         hit = _RECIPES.get(key)
@@ -1150,7 +1296,18 @@ def module_with_state(template, state):
             if len(_RECIPES) > 32:
                 for k in [k for k, (r, _) in _RECIPES.items() if r() is None]:
                     del _RECIPES[k]
-    return hit[1].build(state)
+    return hit[1]
+
+
+def module_with_state(template, state):
+    """A new nn.Module shaped like `template` whose parameters / buffers ARE the tensors of `state`
+    (views into the decode output: no parameter data is copied; `template` is never aliased).
+
+    The module tree is rebuilt from a per-template recipe (_TreeRecipe) — new objects of the same classes,
+    their __dict__ copied one level deep with fresh tables and hook dicts, other attributes deep-copied —
+    instead of copy.deepcopy, whose generic recursion cost ~8 ms per ResNet-50 on the server's per-upload
+    path. Tensors outside the state (non-persistent buffers, unregistered tensors) are cloned."""
+    return _recipe(template).build(state)
 
 
 _SAME_LAYOUT = OrderedDict()  # (id(a), id(b)) -> (a, b): pairs of entry lists already found equal

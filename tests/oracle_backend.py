@@ -24,12 +24,15 @@ class OraclePlan:
         return Encoded(torch.from_numpy(idx), torch.from_numpy(vals), torch.from_numpy(mn), torch.from_numpy(sc),
                        torch.from_numpy(O.unit_starts(idx, segs)))
 
-    def decode(self, enc, base=None, **_):
+    def decode(self, enc, base=None, out=None, **_):
         b = None if base is None else base.detach().cpu().numpy()
-        out = np.zeros(self.table.span, dtype=np.float32) if b is None else b.copy()
+        res = np.zeros(self.table.span, dtype=np.float32) if b is None else b.copy()
         O.decode(enc.idx.numpy(), enc.vals.numpy(), enc.mn.numpy(), enc.scale.numpy(),
-                 self.table.segs.astype(np.int64), self.bits, self.table.span, base=b, out=out)
-        return torch.from_numpy(out)
+                 self.table.segs.astype(np.int64), self.bits, self.table.span, base=b, out=res)
+        if out is not None:  # (a recycled decoded module's storage: written in place, as the HIP plan does)
+            out[:res.size].copy_(torch.from_numpy(res))
+            return out
+        return torch.from_numpy(res)
 
     def aggregate(self, enc, weights, total=None, base=None, mode="div", avg_mask=None, **_):
         total = float(sum(weights)) if total is None else float(total)

@@ -218,7 +218,7 @@ def test_decode_untrusted_idx_stays_in_bounds(cuda, kind, clients, starts):
     if kind == "random":
         idx = rng.integers(0, 20000, K, dtype=np.int64)
     elif kind == "reversed":
-        idx = np.concatenate([np.arange(k)[::-1] for k in t.ks])
+        idx = np.concatenate([np.arange(k)[::-1] for k in t.ks] * clients)
     elif kind == "out_of_range":
         idx = rng.integers(-(2 ** 31), 2 ** 31 - 1, K, dtype=np.int64)
     else:
