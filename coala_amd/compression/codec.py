@@ -150,29 +150,48 @@ class _StateWalk:
     root module across rounds may swap `model.head`), or when the non-persistent buffer set changes."""
 
     def __init__(self, module):
-        self.mods, names = [], []
-        self.sizes = []
+        self.mods, self.rows, names = [], [], []
+        self.parents, self.npbs = [], []  # (module, children) of the modules with children; (module, set) likewise
         self.hooked = False
         for prefix, m in module.named_modules(remove_duplicate=False):
             self.hooked = self.hooked or bool(m._state_dict_hooks or m._state_dict_pre_hooks)
             pn = tuple(k for k, v in m._parameters.items() if v is not None)
             bn = tuple(k for k, v in m._buffers.items() if v is not None and k not in m._non_persistent_buffers_set)
-            self.mods.append((m, pn, bn, tuple(m._modules.values()), frozenset(m._non_persistent_buffers_set)))
-            self.sizes.append((len(m._parameters), len(m._buffers), len(m._modules)))
+            self.mods.append(m)
+            if pn or bn:
+                self.rows.append((m, pn, bn))
+            if m._modules:
+                self.parents.append((m, tuple(m._modules.values())))
+            if m._non_persistent_buffers_set:
+                self.npbs.append((m, frozenset(m._non_persistent_buffers_set)))
             p = prefix + "." if prefix else ""
             names.extend(p + k for k in pn + bn)
+        self.sizes = self._sizes()
         self.names = tuple(names)
+        self.last = None  # (dtypes, shapes, layout) of the last describe_tensors
+
+    def _sizes(self):
+        return [(len(m._parameters), len(m._buffers), len(m._modules), len(m._non_persistent_buffers_set))
+                for m in self.mods]
 
     def tensors(self):
+        """The tensors, or None when the tree changed since the walk (a table's size, a replaced or added
+        submodule, the non-persistent buffer set): the caller walks again."""
+        if self._sizes() != self.sizes:
+            return None
+        for m, kids in self.parents:  # (tuple equality: identity first, so a replaced child compares unequal)
+            if tuple(m._modules.values()) != kids:
+                return None
+        for m, npb in self.npbs:
+            if m._non_persistent_buffers_set != npb:
+                return None
         out = []
-        for (m, pn, bn, kids, npb), (np_, nb, nk) in zip(self.mods, self.sizes):
-            P, B, C = m._parameters, m._buffers, m._modules
-            if len(P) != np_ or len(B) != nb or len(C) != nk or not all(map(is_, C.values(), kids)):
-                return None
-            if npb != m._non_persistent_buffers_set:
-                return None
-            out.extend(map(P.__getitem__, pn))
-            out.extend(map(B.__getitem__, bn))
+        ext = out.extend
+        for m, pn, bn in self.rows:
+            if pn:
+                ext(map(m._parameters.__getitem__, pn))
+            if bn:
+                ext(map(m._buffers.__getitem__, bn))
         return out
 
 
@@ -182,9 +201,14 @@ _WALKS = {}  # id(module) -> (weakref, _StateWalk)
 def module_tensors(module):
     """(names, tensors) of module.state_dict() — the same names and tensor storage, in the same order — via a
     cached _StateWalk. A module tree with state-dict hooks takes state_dict() itself."""
+    return _module_walk(module)[:2]
+
+
+def _module_walk(module):
+    """module_tensors' (names, tensors) and the walk (None when state_dict() was taken)."""
     if module._state_dict_hooks or module._state_dict_pre_hooks:
         st = module.state_dict()
-        return tuple(st), list(st.values())
+        return tuple(st), list(st.values()), None
     hit = _WALKS.get(id(module))
     w = hit[1] if hit is not None and hit[0]() is module else None
     ts = w.tensors() if w is not None else None
@@ -199,16 +223,25 @@ def module_tensors(module):
         ts = w.tensors()
     if w.hooked:
         st = module.state_dict()
-        return tuple(st), list(st.values())
-    return w.names, ts
+        return tuple(st), list(st.values()), None
+    return w.names, ts, w
 
 
 _get_dtype, _get_shape = attrgetter("dtype"), attrgetter("shape")
 
 
-def describe_tensors(names, tensors):
-    """describe_state() over (names, tensors) in state_dict order (module_tensors)."""
-    L = _layout_sig(tuple(zip(names, map(_get_dtype, tensors), map(_get_shape, tensors))))
+def describe_tensors(names, tensors, walk=None):
+    """describe_state() over (names, tensors) in state_dict order (module_tensors). walk: the _StateWalk the
+    tensors came from — the layout is then looked up again only when a dtype or shape changed since its last
+    call (list comparisons, instead of hashing the whole (name, dtype, shape) signature every call)."""
+    dts, shs = list(map(_get_dtype, tensors)), list(map(_get_shape, tensors))
+    last = walk.last if walk is not None else None
+    if last is not None and last[0] == dts and last[1] == shs:
+        L = last[2]
+    else:
+        L = _layout_sig(tuple(zip(names, dts, shs)))
+        if walk is not None:
+            walk.last = (dts, shs, L)
     segs = list(map(tensors.__getitem__, L.seg_idx))
     raw_ts = list(map(tensors.__getitem__, L.raw_idx))
     raw = None
@@ -552,7 +585,7 @@ class CompressedUpdate:
     def compression_ratio(self):
         """Dense fp32 (+ raw) bytes of the update / its payload bytes."""
         h = self.header
-        dense = 4 * sum(e["n"] for e in h["entries"] if e["kind"] == "seg")
+        dense = 4 * _dense_elements(h["entries"])
         dense += self.raw.nbytes if isinstance(self.raw, RawState) else \
             sum(t.numel() * t.element_size() for t in self.raw.values())
         return dense / max(1, self.nbytes)
@@ -561,6 +594,20 @@ class CompressedUpdate:
         h = self.header
         return (f"CompressedUpdate(mode={h['mode']}, ratio={h['ratio']}, bits={h['bits']}, "
                 f"segments={h['n_segments']}, kept={h['total_k']}, bytes={self.nbytes})")
+
+
+_DENSE = OrderedDict()  # id(entries) -> (entries, fp32 elements)
+
+
+def _dense_elements(entries):
+    hit = _DENSE.get(id(entries))
+    if hit is None or hit[0] is not entries:
+        hit = (entries, sum(e["n"] for e in entries if e["kind"] == "seg"))
+        with _LAYOUTS_LOCK:
+            _DENSE[id(entries)] = hit
+            while len(_DENSE) > 32:
+                _DENSE.popitem(last=False)
+    return hit[1]
 
 
 _VALIDATED = OrderedDict()  # (id(entries), ratio, n_segments, total_k) -> (entries, ns_rep, first, units) of a layout
@@ -655,6 +702,7 @@ class UpdateCodec:
         self.ratio, self.bits, self.mode = float(ratio), int(bits), mode
         self.backend = backend if backend is not None else HipBackend()
         self._plans = {}
+        self._checked_ptrs = {}  # id(plan) -> the segment pointers of the last in-place encode that passed the checks
         self._ws = OrderedDict()
         self._lock = threading.Lock()
         self._tls = threading.local()
@@ -684,10 +732,10 @@ class UpdateCodec:
         """module -> CompressedUpdate of its state_dict (what CompressionClientMixin.compression() runs): the
         same result as encode(module.state_dict(), ...), with the state read through a cached walk of the
         module tree (module_tensors) instead of building the state_dict."""
-        names, tensors = module_tensors(module)
+        names, tensors, walk = _module_walk(module)
         if device is None:
             device = self._device_for(tensors)
-        L, segs, raw = describe_tensors(names, tensors)
+        L, segs, raw = describe_tensors(names, tensors, walk)
         return self._encode(L, segs, raw, base, device, lambda: OrderedDict(zip(names, tensors)))
 
     def _encode(self, L, segs, raw, base, device, state_fn):
@@ -714,8 +762,13 @@ class UpdateCodec:
         in_place = getattr(plan, "encode_segments", None) is not None
         if in_place:  # every segment on the plan's device, contiguous, 16-B aligned (one pass per property)
             ptrs = tuple(map(_data_ptr, segs))
-            in_place = (all(map(_is_contig, segs)) and all(d == dev_index for d in map(_get_device, segs))
-                        and not any(p & 15 for p in ptrs))
+            # (the same storage as an encode that passed the checks: a model's parameters do not move between
+            # rounds; a strides-only change of a parameter in place is not looked for)
+            if self._checked_ptrs.get(id(plan)) != ptrs:
+                in_place = (all(map(_is_contig, segs)) and list(map(_get_device, segs)) == [dev_index] * len(segs)
+                            and not any(p & 15 for p in ptrs))
+                if in_place:
+                    self._checked_ptrs[id(plan)] = ptrs
         if in_place:  # read the parameters where they live: no flattening copy (+8 B/element of traffic)
             # (dtype and sizes hold by construction: the plan was made from this layout's segments)
             enc = plan.encode_segments(segs, base=base_flat, workspace=ws, checked=True, ptrs=ptrs)

@@ -2285,8 +2285,12 @@ struct AggArgs {
 //   division by a host scalar)                       — coala/server/strategies.py:6-29, 57-90
 //   or out = acc (mode SUM: weighted_sum, strategies.py:57-90, whose result the distributed server hands
 //   to reduce_models, coala/distributed/distributed.py:42-57)
-// d_i goes through a per-wave LDS tile: the client's kept values are scattered into the zeroed tile,
-// every lane reads its 64 elements back with ds_read_b128, then the same positions are re-zeroed.
+// d_i goes through a per-wave LDS tile: the client's kept values are scattered into the zeroed tile and each
+// marks its row in a per-lane row-flag byte of the lane owning it; every lane then reads its rows back with
+// ds_read_b128 — a row no kept value fell into reads the tile's zero slot instead, the same address for every
+// such lane, so the read moves only the marked rows' bytes (a client keeps ~20 of a wave's 2048 elements: the
+// full read-back of every row for every client was most of the kernel's LDS traffic) — and the same positions
+// and flags are re-zeroed.
 // Latency: every client's range / mn / scale / weight is fetched lane-parallel in one round (lane j =
 // client j of a 64-client chunk); the first 64 kept entries of AGG_DEPTH clients are then loaded in one
 // batch and accumulated in client order (a unit where some client keeps more than 64 entries takes the
@@ -2297,7 +2301,10 @@ __global__ __launch_bounds__(BLOCK, AGG_WPE) void k_aggregate(Params P, AggArgs 
   // AGG_SPLIT waves per unit, each owning RI of its UNIT_IT rows: a smaller LDS tile and half the registers
   // per wave, so twice the waves are resident
   constexpr uint32_t RI = UNIT_IT / AGG_SPLIT, HE = UNIT / AGG_SPLIT;  // rows / elements per wave
-  __shared__ float4 tiles[WAVES][HE / 4];
+  constexpr uint32_t ZS = HE / 4;  // the tile's zero slot (float4 index), never written
+  static_assert(RI == 8, "one row-flag byte per row: 8 rows in a uint2");
+  __shared__ float4 tiles[WAVES][HE / 4 + 1];
+  __shared__ uint2 rflags[WAVES][64];  // per owner lane: byte r != 0 = a kept value landed in its row r
   const uint32_t lane = lane_id(), wv = threadIdx.x >> 6;
   const uint32_t wid = blockIdx.x * WAVES + wv;
   const uint32_t u = wid / AGG_SPLIT, h = wid % AGG_SPLIT;
@@ -2311,6 +2318,7 @@ __global__ __launch_bounds__(BLOCK, AGG_WPE) void k_aggregate(Params P, AggArgs 
   const uint32_t hlen = min(len - e_lo, HE);
   float4* tile = tiles[wv];
   float* tf = reinterpret_cast<float*>(tile);
+  uint8_t* rf = reinterpret_cast<uint8_t*>(rflags[wv]);
   float4 b[RI], acc[RI];
   const float* bs = HASBASE ? P.base + U.off + e_lo : nullptr;
   auto load_base = [&]() {
@@ -2330,9 +2338,16 @@ __global__ __launch_bounds__(BLOCK, AGG_WPE) void k_aggregate(Params P, AggArgs 
   auto tile_zero = [&]() {
 #pragma unroll
     for (uint32_t it = 0; it < RI; ++it) tile[it * 64 + lane] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    rflags[wv][lane] = make_uint2(0u, 0u);
+  };
+  // a kept value at wave-relative position p: tile slot p, owner lane (p >> 2) & 63, row p >> 8
+  auto mark = [&](uint32_t p, float v) {
+    tf[p] = v;
+    rf[((p >> 2) & 63u) * 8u + (p >> 8)] = 1;
   };
   if (HASBASE) load_base();
   tile_zero();
+  if (lane == 0) tile[ZS] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
 #pragma unroll
   for (uint32_t it = 0; it < RI; ++it) acc[it] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
   for (uint32_t c0 = 0; c0 < nclients; c0 += 64) {
@@ -2363,10 +2378,15 @@ __global__ __launch_bounds__(BLOCK, AGG_WPE) void k_aggregate(Params P, AggArgs 
     auto accumulate = [&](uint32_t j) {
       const float w = __uint_as_float(__builtin_amdgcn_readlane(__float_as_uint(m_w), j));
       const f2v w2 = {w, w};
+      const uint2 fl = rflags[wv][lane];
+      auto row = [&](uint32_t it) {  // (unmarked rows read the zero slot: +0.0f, as the zeroed tile holds)
+        const uint32_t f = ((it < 4 ? fl.x : fl.y) >> (8u * (it & 3u))) & 0xFFu;
+        return tile[f ? it * 64 + lane : ZS];
+      };
       if (c0 + j == 0) {
 #pragma unroll
         for (uint32_t it = 0; it < RI; ++it) {
-          const float4 d = tile[it * 64 + lane];
+          const float4 d = row(it);
           const f2v dl = {d.x, d.y}, dh = {d.z, d.w};
           const f2v bl = {b[it].x, b[it].y}, bh = {b[it].z, b[it].w};
           const f2v tl = (HASBASE ? bl + dl : dl) * w2, th = (HASBASE ? bh + dh : dh) * w2;
@@ -2375,7 +2395,7 @@ __global__ __launch_bounds__(BLOCK, AGG_WPE) void k_aggregate(Params P, AggArgs 
       } else {
 #pragma unroll
         for (uint32_t it = 0; it < RI; ++it) {
-          const float4 d = tile[it * 64 + lane];
+          const float4 d = row(it);
           const f2v dl = {d.x, d.y}, dh = {d.z, d.w};
           const f2v bl = {b[it].x, b[it].y}, bh = {b[it].z, b[it].w};
           const f2v al = {acc[it].x, acc[it].y}, ah = {acc[it].z, acc[it].w};
@@ -2391,11 +2411,12 @@ __global__ __launch_bounds__(BLOCK, AGG_WPE) void k_aggregate(Params P, AggArgs 
       const float mn = __uint_as_float(__builtin_amdgcn_readlane(__float_as_uint(m_mn), j));
       const float sc = __uint_as_float(__builtin_amdgcn_readlane(__float_as_uint(m_sc), j));
       const bool mine = lane < ne && pos < hlen;
-      if (mine) tf[pos] = code_value<RAW>(q, mn, sc);
+      if (mine) mark(pos, code_value<RAW>(q, mn, sc));
       lds_order();
       accumulate(j);
       lds_order();
       if (mine) tf[pos] = 0.0f;
+      rflags[wv][lane] = make_uint2(0u, 0u);
       lds_order();
     };
     // any client with more than 64 kept entries in this unit (ratio >~ 1.5 %): every client in turn, its
@@ -2409,7 +2430,7 @@ __global__ __launch_bounds__(BLOCK, AGG_WPE) void k_aggregate(Params P, AggArgs 
       for (uint32_t e = lo + lane; e < hi; e += 64) {
         const uint32_t p2 = (uint32_t)P.cidx[oo + e] - U.start - e_lo;
         const float v2 = load_val<RAW>(P, oo + e, mn, sc);
-        if (p2 < hlen) tf[p2] = v2;
+        if (p2 < hlen) mark(p2, v2);
       }
       lds_order();
       accumulate(j);
