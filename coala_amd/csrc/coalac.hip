@@ -182,6 +182,7 @@ struct Params {
   const uint32_t* small_list;
   const uint32_t* large_list;
   const SegDev* lsegs;  // [n_large] the large segments' SegDev, in large_list order (one load round less)
+  const SegDev* ssegs;  // [n_small] the small segments' SegDev, in small_list order (likewise)
   uint32_t nseg, n_small, n_large, n_units, n_lunits;
   uint32_t scan_small;  // small segments encoded by k_scan's first blocks (0 when forked to k_small)
   float levels;
@@ -832,10 +833,11 @@ DEV void hist_pick2(const uint32_t* hist, uint32_t r1, uint32_t r2, uint32_t& b1
 // with k_sample / k_scan, so its latency hides under the HBM streaming.
 // ------------------------------------------------------------------------------------------------
 template <bool DELTA, bool RAW>
-DEV void small_encode(const Params& P, uint32_t s, float* vals, uint32_t* hist, uint32_t* sh) {
+DEV void small_encode(const Params& P, uint32_t si, float* vals, uint32_t* hist, uint32_t* sh) {
   constexpr int NT = BLOCK;
   const uint32_t t = threadIdx.x;
-  const SegDev sd = P.segs[s];
+  const uint32_t s = P.small_list[si];
+  const SegDev sd = P.ssegs[si];  // (the same load round as s)
   const float* xs = seg_in(P, s, sd.in_off);
   const float* bs = DELTA ? P.base + sd.in_off : xs;
   const uint32_t n = sd.n, k = sd.k;
@@ -929,7 +931,7 @@ __global__ __launch_bounds__(BLOCK) void k_small(Params P) {
   __shared__ __attribute__((aligned(16))) float vals[SMALL_MAX];
   __shared__ uint32_t hist[HIST_BINS];
   __shared__ uint32_t sh[64];
-  small_encode<DELTA, RAW>(P, P.small_list[blockIdx.x], vals, hist, sh);
+  small_encode<DELTA, RAW>(P, blockIdx.x, vals, hist, sh);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -941,7 +943,7 @@ DEV void sample_segment(const Params& P, uint32_t li, uint32_t* hist, uint32_t* 
   constexpr uint32_t MAXIT = SAMPLE_MAX / 16 / 64;  // run batches per block (64 runs of 16 per batch)
   const uint32_t t = threadIdx.x;
   const uint32_t s = P.large_list[li];
-  const SegDev sd = P.segs[s];
+  const SegDev sd = P.lsegs[li];  // (the same load round as s: no dependent segment-table lookup)
   const float* xs = seg_in(P, s, sd.in_off);
   const float* bs = DELTA ? P.base + sd.in_off : xs;
   const uint32_t n = sd.n, k = sd.k;
@@ -1054,8 +1056,7 @@ __global__ __launch_bounds__(BLOCK) void k_presel(Params P) {
   if (blockIdx.x < P.n_large) {
     sample_segment<DELTA>(P, blockIdx.x, hist, hist + HIST_BINS);
   } else {
-    small_encode<DELTA, RAW>(P, P.small_list[blockIdx.x - P.n_large], reinterpret_cast<float*>(arena), hist,
-                             hist + HIST_BINS);
+    small_encode<DELTA, RAW>(P, blockIdx.x - P.n_large, reinterpret_cast<float*>(arena), hist, hist + HIST_BINS);
   }
 }
 
@@ -1073,7 +1074,7 @@ __global__ __launch_bounds__(BLOCK, WPE) void k_scan(Params P) {
   if (WITH_SMALL && blockIdx.x < P.scan_small) {
     float* vals = reinterpret_cast<float*>(arena);
     uint32_t* hist = reinterpret_cast<uint32_t*>(arena) + SMALL_MAX;
-    small_encode<DELTA, RAW>(P, P.small_list[blockIdx.x], vals, hist, hist + HIST_BINS);
+    small_encode<DELTA, RAW>(P, blockIdx.x, vals, hist, hist + HIST_BINS);
     return;
   }
   uint2* stage = reinterpret_cast<uint2*>(arena);
@@ -2558,6 +2559,7 @@ struct coalac_plan {
   uint32_t* small_list = nullptr;
   uint32_t* large_list = nullptr;
   SegDev* lsegs = nullptr;
+  SegDev* ssegs = nullptr;
   uint4* groups = nullptr;
   uint32_t n_groups = 0;
   BChunk* bchunks = nullptr;  // aggregate: k_bounds work list
@@ -2589,6 +2591,7 @@ void fill_meta(Params& P, coalac_plan_t plan) {
   P.small_list = plan->small_list;
   P.large_list = plan->large_list;
   P.lsegs = plan->lsegs;
+  P.ssegs = plan->ssegs;
   P.groups = plan->groups;
   P.n_groups = plan->n_groups;
   P.nseg = (uint32_t)plan->nseg;
@@ -2839,10 +2842,12 @@ int coalac_plan_create(const coalac_seg_t* h_segs, int nseg, int bits, coalac_pl
   const size_t o_lunits = align_up(o_units + sizeof(UnitDev) * units.size(), 256);
   const size_t o_small = align_up(o_lunits + sizeof(UnitDev) * lunits.size(), 256);
   const size_t o_large = align_up(o_small + 4 * small_list.size(), 256);
-  std::vector<SegDev> lsegs;
+  std::vector<SegDev> lsegs, ssegs;
   for (uint32_t s2 : large_list) lsegs.push_back(segs[s2]);
+  for (uint32_t s2 : small_list) ssegs.push_back(segs[s2]);
   const size_t o_lsegs = align_up(o_large + 4 * large_list.size(), 256);
-  const size_t o_grp = align_up(o_lsegs + sizeof(SegDev) * lsegs.size(), 256);
+  const size_t o_ssegs = align_up(o_lsegs + sizeof(SegDev) * lsegs.size(), 256);
+  const size_t o_grp = align_up(o_ssegs + sizeof(SegDev) * ssegs.size(), 256);
   const size_t o_bch = align_up(o_grp + sizeof(uint4) * groups.size(), 256);
   std::vector<SChunk> schunks;
   for (const BChunk& c : bchunks)
@@ -2856,6 +2861,7 @@ int coalac_plan_create(const coalac_seg_t* h_segs, int nseg, int bits, coalac_pl
   if (!small_list.empty()) memcpy(host.data() + o_small, small_list.data(), 4 * small_list.size());
   if (!large_list.empty()) memcpy(host.data() + o_large, large_list.data(), 4 * large_list.size());
   if (!lsegs.empty()) memcpy(host.data() + o_lsegs, lsegs.data(), sizeof(SegDev) * lsegs.size());
+  if (!ssegs.empty()) memcpy(host.data() + o_ssegs, ssegs.data(), sizeof(SegDev) * ssegs.size());
   if (!groups.empty()) memcpy(host.data() + o_grp, groups.data(), sizeof(uint4) * groups.size());
   if (!bchunks.empty()) memcpy(host.data() + o_bch, bchunks.data(), sizeof(BChunk) * bchunks.size());
   if (!schunks.empty()) memcpy(host.data() + o_sch, schunks.data(), sizeof(SChunk) * schunks.size());
@@ -2877,6 +2883,7 @@ int coalac_plan_create(const coalac_seg_t* h_segs, int nseg, int bits, coalac_pl
   p->small_list = reinterpret_cast<uint32_t*>(m + o_small);
   p->large_list = reinterpret_cast<uint32_t*>(m + o_large);
   p->lsegs = reinterpret_cast<SegDev*>(m + o_lsegs);
+  p->ssegs = reinterpret_cast<SegDev*>(m + o_ssegs);
   p->groups = reinterpret_cast<uint4*>(m + o_grp);
   p->bchunks = reinterpret_cast<BChunk*>(m + o_bch);
   p->schunks = reinterpret_cast<SChunk*>(m + o_sch);
