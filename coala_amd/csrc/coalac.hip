@@ -133,7 +133,6 @@ constexpr uint32_t GU = GU_UNITS;               // units per select group (k_ghi
 #endif
 constexpr uint32_t HB2 = 512;             // bins of the per-group band histograms
 constexpr uint32_t GCAP = 256;            // in-window entries a group may hand to k_select
-constexpr uint32_t A_FLAG = 0x80000000u;  // candidate record flag: key > T_hi (kept for sure)
 constexpr uint32_t KEY_MAX = 0x7FFFFFFFu;
 constexpr int HIST_BINS = 2048;
 constexpr uint32_t BCHUNK = 4096;         // idx entries per k_bounds block (aggregate)
@@ -191,7 +190,8 @@ struct Params {
   uint32_t *tstar, *rtie, *status;
   // per large unit
   uint32_t *tlo, *thi, *cntA, *cntC, *gtC, *eqC, *eqpre, *outoff;
-  uint2* cand;  // candidate records {index | A_FLAG, value bits}, ccap slots per large unit
+  uint32_t* cval;  // candidate records, ccap slots per large unit, in index order: the value bits ...
+  uint16_t* cpos;  // ... and the position inside the unit (the emit reads both; every select sweep the values only)
   uint32_t ccap;  // record slots per large unit (< UNIT: a unit that finds more candidates overflows and its
                   // segment is selected and emitted from the raw data instead)
   // parallel select (groups of GU units of one large segment)
@@ -640,8 +640,9 @@ struct Band {
 
 // ------------------------------------------------------------------------------------------------
 // streaming classify + ordered compaction of one large unit by one wave (k_scan, exact fallback)
-// Candidates (key >= tlo) are written in index order as 8-byte records {index | A_FLAG, value}; A_FLAG
-// marks key > thi (kept for sure). With `stage` (k_scan) the first STAGE_CAP records go to a per-wave
+// Candidates (key >= tlo) are written in index order as records {position in the unit, value}: two arrays, the
+// u16 positions (cpos) and the value bits (cval) — 6 bytes per record, and the select sweeps, which read values
+// only, move 4 (round 3's interleaved 8-byte records: k_scan's writes were 4.4 % of its read traffic). With `stage` (k_scan) the first STAGE_CAP records go to a per-wave
 // LDS buffer and leave in coalesced 512-byte stores at the end; scattered per-lane global stores were
 // measured 28 % slower (tools/scan_ablate.hip). Input loads are non-temporal: the update is read once.
 // The unit is loaded in NB batches of UNIT_IT/NB float4 per lane: NB = 1 for the streaming pass (all
@@ -656,7 +657,8 @@ DEV void scan_unit(const Params& P, uint32_t lu, const UnitDev& L, const uint32_
   const uint32_t lane = lane_id();
   const uint32_t len = L.len;
   const uint64_t off = L.off;
-  uint2* R = P.cand + (uint64_t)lu * P.ccap;
+  uint32_t* RV = P.cval + (uint64_t)lu * P.ccap;
+  uint16_t* RP = P.cpos + (uint64_t)lu * P.ccap;
   const uint32_t cap = P.ccap;
   uint32_t cC = 0, cA = 0;
   // buffer resources over exactly this unit: one shared lane offset for all loads (constant offsets
@@ -666,7 +668,8 @@ DEV void scan_unit(const Params& P, uint32_t lu, const UnitDev& L, const uint32_
   const __amdgpu_buffer_rsrc_t rbase = unit_rsrc(DELTA ? P.base + off : xin, len);
   auto put = [&](uint32_t i, uint2 rec) {
     if (i >= cap) return;  // overflow: counted, not stored (the segment goes to the raw-data path)
-    R[i] = rec;
+    RV[i] = rec.y;
+    RP[i] = (uint16_t)rec.x;
   };
 
   for (uint32_t nb = 0; nb < (uint32_t)NB; ++nb) {
@@ -697,8 +700,7 @@ DEV void scan_unit(const Params& P, uint32_t lu, const UnitDev& L, const uint32_
           const uint32_t pc = cC + mbcnt(b1);
           const uint32_t j = fc[0] ? 0u : fc[1] ? 1u : fc[2] ? 2u : 3u;
           const float xj = j == 0 ? xs[0] : j == 1 ? xs[1] : j == 2 ? xs[2] : xs[3];
-          const bool aj = fa[0] || fa[1] || fa[2] || fa[3];
-          const uint2 rec = make_uint2((L.start + e0 + j) | (aj ? A_FLAG : 0u), __float_as_uint(xj));
+          const uint2 rec = make_uint2(e0 + j, __float_as_uint(xj));
           if (stage != nullptr && pc < STAGE_CAP)
             stage[pc] = rec;
           else
@@ -718,7 +720,7 @@ DEV void scan_unit(const Params& P, uint32_t lu, const UnitDev& L, const uint32_
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         if (fc[j]) {
-          const uint2 rec = make_uint2((L.start + e0 + j) | (fa[j] ? A_FLAG : 0u), __float_as_uint(xs[j]));
+          const uint2 rec = make_uint2(e0 + j, __float_as_uint(xs[j]));
           if (stage != nullptr && pc < STAGE_CAP)
             stage[pc] = rec;
           else
@@ -1130,7 +1132,7 @@ DEV uint32_t reg_prefix(uint32_t c, uint32_t cn, uint32_t* upre, uint32_t* sh) {
 // wave-uniform so per-unit counts are ballot popcounts), G units per batch with 2 records per lane per
 // unit in flight. f(x, valid, u) is called by ALL lanes (ballots allowed); fend(u) after each unit.
 template <int NW, int G, class F, class FE>
-DEV void unit_sweep(const uint2* cand, uint32_t stride, uint32_t lu0, const uint32_t* upre, uint32_t cn,
+DEV void unit_sweep(const uint32_t* cand, uint32_t stride, uint32_t lu0, const uint32_t* upre, uint32_t cn,
                     uint32_t total, F&& f, FE&& fend) {
   const uint32_t lane = lane_id(), w = threadIdx.x >> 6;
   const uint32_t J0 = (uint32_t)((uint64_t)total * w / NW), J1 = (uint32_t)((uint64_t)total * (w + 1) / NW);
@@ -1154,10 +1156,10 @@ DEV void unit_sweep(const uint2* cand, uint32_t stride, uint32_t lu0, const uint
       const uint32_t uu = min(u + g, U1 - 1);
       const uint32_t n = upre[uu + 1] - upre[uu];
       const uint32_t last = n ? n - 1 : 0u;  // region slot 0 always exists; read it when n == 0
-      const uint2* R = cand + (uint64_t)(lu0 + uu) * stride;
+      const uint32_t* R = cand + (uint64_t)(lu0 + uu) * stride;
       nn[g] = n;
-      x0[g] = R[min(lane, last)].y;
-      x1[g] = R[min(lane + 64, last)].y;
+      x0[g] = R[min(lane, last)];
+      x1[g] = R[min(lane + 64, last)];
     }
 #pragma unroll
     for (int g = 0; g < G; ++g) {
@@ -1166,8 +1168,8 @@ DEV void unit_sweep(const uint2* cand, uint32_t stride, uint32_t lu0, const uint
         f(__uint_as_float(x0[g]), lane < n, uu);
         if (n > 64) f(__uint_as_float(x1[g]), lane + 64 < n, uu);
         if (n > 128) {
-          const uint2* R = cand + (uint64_t)(lu0 + uu) * stride;
-          for (uint32_t i0 = 128; i0 < n; i0 += 64) f(__uint_as_float(R[min(i0 + lane, n - 1)].y), i0 + lane < n, uu);
+          const uint32_t* R = cand + (uint64_t)(lu0 + uu) * stride;
+          for (uint32_t i0 = 128; i0 < n; i0 += 64) f(__uint_as_float(R[min(i0 + lane, n - 1)]), i0 + lane < n, uu);
         }
         fend(uu);
       }
@@ -1204,7 +1206,7 @@ DEV void select_generic(const Params& P, uint32_t lb, uint32_t nu, uint32_t tlo,
       const uint32_t cn = min(UCAP, nu - c0);
       const uint32_t total = chunk_prefix<NT>(P.cntC + lb + c0, cn, P.ccap, S.upre, S.sh);
       unit_sweep<NW, 4>(
-          P.cand, P.ccap, lb + c0, S.upre, cn, total,
+          P.cval, P.ccap, lb + c0, S.upre, cn, total,
           [&](float x, bool valid, uint32_t) {
             if (valid) f(fkey(x));
           },
@@ -1228,7 +1230,7 @@ DEV void select_generic(const Params& P, uint32_t lb, uint32_t nu, uint32_t tlo,
     const uint32_t total = chunk_prefix<NT>(P.cntC + lb + c0, cn, P.ccap, S.upre, S.sh);
     uint32_t weq = 0, wfp = NONE, wfn = NONE, ug = 0, ue = 0;  // wave-uniform
     unit_sweep<NW, 4>(
-        P.cand, P.ccap, lb + c0, S.upre, cn, total,
+        P.cval, P.ccap, lb + c0, S.upre, cn, total,
         [&](float x, bool valid, uint32_t) {
           const uint32_t key = fkey(x);
           const bool g = valid && key > T;
@@ -1296,7 +1298,7 @@ DEV void group_hist(const Params& P, uint32_t gi, uint32_t* hist, uint32_t* upre
   const uint32_t total = reg_prefix<NT>(c, G.z, upre, sh);  // barriers inside
   const Band band(tlo, thi, hh);
   unit_sweep<NT / 64, GSWEEP>(
-      P.cand, P.ccap, G.y, upre, G.z, total,
+      P.cval, P.ccap, G.y, upre, G.z, total,
       [&](float x, bool valid, uint32_t) {
         const uint32_t key = fkey(x);
         if (valid && key >= tlo && key <= thi) atomicAdd(&hist[band.bin(key)], 1u);
@@ -1424,7 +1426,7 @@ DEV void group_window(const Params& P, uint32_t gi, const uint4 G, const uint4 s
   uint32_t wc = 0, ug = 0;
   float lmn = qnan(), lmx = qnan();
   unit_sweep<NW, GSWEEP>(
-      P.cand, P.ccap, G.y, upre, G.z, total,
+      P.cval, P.ccap, G.y, upre, G.z, total,
       [&](float x, bool valid, uint32_t u) {
         const uint32_t key = fkey(x);
         const bool g = valid && key > whi;
@@ -1877,6 +1879,7 @@ DEV void emit_units(const Params& P, uint32_t lu0, uint32_t lu1) {
   const uint32_t lug = min(lu0 + min(lane, UPW - 1), lu1 - 1);
   const uint32_t nCg = min(P.cntC[lug], P.ccap);  // stored records (a raw-path unit may have dropped some)
   const uint32_t segg = P.lunits[lug].seg;
+  const uint32_t startg = P.lunits[lug].start;
   const uint32_t stg = P.status[segg];             // != 0: the segment took the raw-data path
   const uint64_t sog = P.lunits[lug].out_off;
   const uint32_t eqpg = P.eqpre[lug], oog = P.outoff[lug];
@@ -1886,13 +1889,14 @@ DEV void emit_units(const Params& P, uint32_t lu0, uint32_t lu1) {
   // every unit's first 2 x 64 records in flight before the first is classified (at ~1.5 % candidates a
   // unit holds ~60 records, so about half of the units need the second row: loading it inside the unit
   // loop made it one dependent round per unit, 8 in a row)
-  uint2 rec0[UPW], rec1[UPW];
+  uint2 rec0[UPW], rec1[UPW];  // {position, value bits}
 #pragma unroll
   for (uint32_t g = 0; g < UPW; ++g) {
     const uint32_t lu = min(lu0 + g, lu1 - 1), nC = rl(nCg, g);
     const uint32_t last = nC ? nC - 1 : 0u;
-    rec0[g] = P.cand[(uint64_t)lu * P.ccap + min(lane, last)];  // unconditional (clamped) loads
-    if (EMIT_ROWS > 1) rec1[g] = P.cand[(uint64_t)lu * P.ccap + min(lane + 64, last)];
+    const uint64_t r0 = (uint64_t)lu * P.ccap;  // unconditional (clamped) loads
+    rec0[g] = make_uint2(P.cpos[r0 + min(lane, last)], P.cval[r0 + min(lane, last)]);
+    if (EMIT_ROWS > 1) rec1[g] = make_uint2(P.cpos[r0 + min(lane + 64, last)], P.cval[r0 + min(lane + 64, last)]);
   }
 #pragma unroll
   for (uint32_t g = 0; g < UPW; ++g) {
@@ -1908,12 +1912,15 @@ DEV void emit_units(const Params& P, uint32_t lu0, uint32_t lu1) {
       const float scale = __uint_as_float(rl(__float_as_uint(scg), g));
       const uint64_t so = ((uint64_t)rl((uint32_t)(sog >> 32), g) << 32) | rl((uint32_t)sog, g);
       const uint64_t obase = so + rl(oog, g);
-      const uint2* R = P.cand + (uint64_t)lu * P.ccap;
+      const uint32_t start = rl(startg, g);
+      const uint64_t r0 = (uint64_t)lu * P.ccap;
       uint32_t eqc = 0, outc = 0;
       for (uint32_t i0 = 0; i0 < nC; i0 += 64) {
         const uint32_t i = i0 + lane;
         const bool valid = i < nC;
-        const uint2 rec = i0 == 0 ? rec0[g] : (EMIT_ROWS > 1 && i0 == 64) ? rec1[g] : R[min(i, nC - 1)];
+        const uint32_t ic = min(i, nC - 1);
+        const uint2 rec = i0 == 0 ? rec0[g] : (EMIT_ROWS > 1 && i0 == 64) ? rec1[g]
+                                                                            : make_uint2(P.cpos[r0 + ic], P.cval[r0 + ic]);
         const float x = __uint_as_float(rec.y);
         const uint32_t key = fkey(x);
         const bool e = valid && key == T;
@@ -1924,7 +1931,7 @@ DEV void emit_units(const Params& P, uint32_t lu0, uint32_t lu1) {
         const uint64_t sb = __ballot(sel);
         if (sel) {
           const uint64_t o = obase + outc + mbcnt(sb);
-          P.idx[o] = (int32_t)(rec.x & ~A_FLAG);
+          P.idx[o] = (int32_t)(start + rec.x);
           store_val<RAW>(P, o, x, mn, scale);
         }
         outc += (uint32_t)__popcll(sb);
@@ -2508,7 +2515,7 @@ struct WsLayout {
   size_t status;
   size_t tstar, rtie;
   size_t tlo, thi, cntA, cntC, gtC, eqC, eqpre, outoff;
-  size_t cand, stamps, ghist, gcnt, glist, gmm, sstate, shhi;
+  size_t cval, cpos, stamps, ghist, gcnt, glist, gmm, sstate, shhi;
   size_t total;
 };
 
@@ -2531,7 +2538,8 @@ WsLayout ws_layout(size_t S, size_t LU, size_t NG, size_t NL, uint32_t CC) {
   L.eqC = take(4 * LU);
   L.eqpre = take(4 * LU);
   L.outoff = take(4 * LU);
-  L.cand = take(sizeof(uint2) * (size_t)CC * LU);
+  L.cval = take(4 * (size_t)CC * LU);
+  L.cpos = take(2 * (size_t)CC * LU);
   L.stamps = take(8 * NSTAMP * std::max<size_t>(S, 1));
   L.ghist = take(4 * HB2 * NG);
   L.gcnt = take(4 * NG);
@@ -2967,7 +2975,8 @@ int encode_impl(coalac_plan_t plan, const float* d_in, const float* const* d_inp
   P.eqC = reinterpret_cast<uint32_t*>(w + L.eqC);
   P.eqpre = reinterpret_cast<uint32_t*>(w + L.eqpre);
   P.outoff = reinterpret_cast<uint32_t*>(w + L.outoff);
-  P.cand = reinterpret_cast<uint2*>(w + L.cand);
+  P.cval = reinterpret_cast<uint32_t*>(w + L.cval);
+  P.cpos = reinterpret_cast<uint16_t*>(w + L.cpos);
   P.stamps = (flags & COALAC_FLAG_STAMPS) ? reinterpret_cast<uint64_t*>(w + L.stamps) : nullptr;
   P.ghist = reinterpret_cast<uint32_t*>(w + L.ghist);
   P.gcnt = reinterpret_cast<uint32_t*>(w + L.gcnt);
