@@ -138,7 +138,7 @@ constexpr int HIST_BINS = 2048;
 constexpr uint32_t BCHUNK = 4096;         // idx entries per k_bounds block (aggregate)
 constexpr uint32_t UCAP = 2048;           // units per k_select chunk (8.4 M elements)
 constexpr uint32_t NONE = 0xFFFFFFFFu;
-constexpr int NSTAMP = 16;
+constexpr int NSTAMP = 32;  // diagnostics slots per segment row (COALAC_FLAG_STAMPS)
 
 struct SegDev {
   uint64_t in_off;
@@ -944,6 +944,7 @@ DEV void sample_segment(const Params& P, uint32_t li, uint32_t* hist, uint32_t* 
   constexpr int NT = BLOCK;
   constexpr uint32_t MAXIT = SAMPLE_MAX / 16 / 64;  // run batches per block (64 runs of 16 per batch)
   const uint32_t t = threadIdx.x;
+  STAMP(P, li, 16);  // (slots 16-19: k_sample, 20-21: k_ghist, 22-24: k_gwin of the segment's last group block)
   const uint32_t s = P.large_list[li];
   const SegDev sd = P.lsegs[li];  // (the same load round as s: no dependent segment-table lookup)
   const float* xs = seg_in(P, s, sd.in_off);
@@ -1002,6 +1003,7 @@ DEV void sample_segment(const Params& P, uint32_t li, uint32_t* hist, uint32_t* 
     atomicMax(&sh[45], kmx);
   }
   __syncthreads();
+  STAMP(P, li, 17);
   const uint32_t kmin = sh[44], kmax = sh[45];
   const int shift = band_shift(kmin, kmax);
 #pragma unroll
@@ -1026,6 +1028,7 @@ DEV void sample_segment(const Params& P, uint32_t li, uint32_t* hist, uint32_t* 
     const uint64_t edge = (uint64_t)kmin + (((uint64_t)bhi + 1) << shift) - 1;
     thi = (uint32_t)min<uint64_t>(edge, kmax);
   }
+  STAMP(P, li, 18);
   const uint32_t nu = sd.unit_end - sd.unit_begin;
   const uint32_t hh = max(tlo, min(thi, kmax));  // the band histograms' upper bound (see below)
   for (uint32_t i = t; i < nu; i += NT) {
@@ -1038,6 +1041,7 @@ DEV void sample_segment(const Params& P, uint32_t li, uint32_t* hist, uint32_t* 
     P.shhi[li] = hh;
     P.status[s] = 0;
   }
+  STAMP(P, li, 19);
 }
 
 template <bool DELTA, bool RAW>
@@ -1291,6 +1295,7 @@ template <int NT = BLOCK>
 DEV void group_hist(const Params& P, uint32_t gi, uint32_t* hist, uint32_t* upre, uint32_t* sh) {
   const uint4 G = P.groups[gi];  // x: large-segment index, y: first large unit, z: units, w: segment
   const uint32_t t = threadIdx.x;
+  STAMP(P, G.x, 20);
   // one load round for everything that depends on G only
   const uint32_t tlo = P.tlo[G.y], thi = P.thi[G.y], hh = P.shhi[G.x];
   const uint32_t c = t < G.z ? min(P.cntC[G.y + t], P.ccap) : 0u;  // stored records only
@@ -1306,6 +1311,7 @@ DEV void group_hist(const Params& P, uint32_t gi, uint32_t* hist, uint32_t* upre
       [&](uint32_t) {});
   __syncthreads();
   for (uint32_t i = t; i < HB2; i += NT) pst(P, P.ghist + (uint64_t)gi * HB2 + i, hist[i]);
+  STAMP(P, G.x, 21);
 }
 
 // NT: 256 threads in batches, GHIST_NT_LAT in latency-bound plans (nothing streams beside the block)
@@ -1471,6 +1477,7 @@ DEV void group_window(const Params& P, uint32_t gi, const uint4 G, const uint4 s
 template <int NT = BLOCK>
 DEV void group_pick_window(const Params& P, uint32_t gi, GwinSmemT<NT / 64>& W, uint32_t* hist, uint32_t* sh) {
   const uint4 G = P.groups[gi];
+  STAMP(P, G.x, 22);
   // one load round for everything that depends on G only: the segment, its band, the group's counts
   const SegDev sd = P.lsegs[G.x];
   const uint32_t tlo = P.tlo[G.y], thi = P.thi[G.y], hh = P.shhi[G.x];
@@ -1478,12 +1485,14 @@ DEV void group_pick_window(const Params& P, uint32_t gi, GwinSmemT<NT / 64>& W, 
   const uint32_t total = reg_prefix<NT>(c, G.z, W.upre, sh);
   const Band band(tlo, thi, hh);
   const uint4 st = segment_pick<NT>(P, sd, band, hist, sh);
+  STAMP(P, G.x, 23);
   if (threadIdx.x == 0 && G.y == sd.lu_begin) {  // the segment's first group
     uint2* ss = reinterpret_cast<uint2*>(P.sstate + G.x);
     pst(P, ss, make_uint2(st.x, st.y));
     pst(P, ss + 1, make_uint2(st.z, st.w));
   }
   if (st.w == 0) group_window<NT>(P, gi, G, st, sd.lu_begin, total, W, sh);
+  STAMP(P, G.x, 24);
 }
 
 // NT: 256 threads in batches, GWIN_NT_LAT in latency-bound plans (nothing streams beside the block)
@@ -2293,12 +2302,8 @@ struct AggArgs {
 //   division by a host scalar)                       — coala/server/strategies.py:6-29, 57-90
 //   or out = acc (mode SUM: weighted_sum, strategies.py:57-90, whose result the distributed server hands
 //   to reduce_models, coala/distributed/distributed.py:42-57)
-// d_i goes through a per-wave LDS tile: the client's kept values are scattered into the zeroed tile and each
-// marks its row in a per-lane row-flag byte of the lane owning it; every lane then reads its rows back with
-// ds_read_b128 — a row no kept value fell into reads the tile's zero slot instead, the same address for every
-// such lane, so the read moves only the marked rows' bytes (a client keeps ~20 of a wave's 2048 elements: the
-// full read-back of every row for every client was most of the kernel's LDS traffic) — and the same positions
-// and flags are re-zeroed.
+// d_i goes through a per-wave LDS tile: the client's kept values are scattered into the zeroed tile,
+// every lane reads its 64 elements back with ds_read_b128, then the same positions are re-zeroed.
 // Latency: every client's range / mn / scale / weight is fetched lane-parallel in one round (lane j =
 // client j of a 64-client chunk); the first 64 kept entries of AGG_DEPTH clients are then loaded in one
 // batch and accumulated in client order (a unit where some client keeps more than 64 entries takes the
@@ -2309,10 +2314,7 @@ __global__ __launch_bounds__(BLOCK, AGG_WPE) void k_aggregate(Params P, AggArgs 
   // AGG_SPLIT waves per unit, each owning RI of its UNIT_IT rows: a smaller LDS tile and half the registers
   // per wave, so twice the waves are resident
   constexpr uint32_t RI = UNIT_IT / AGG_SPLIT, HE = UNIT / AGG_SPLIT;  // rows / elements per wave
-  constexpr uint32_t ZS = HE / 4;  // the tile's zero slot (float4 index), never written
-  static_assert(RI == 8, "one row-flag byte per row: 8 rows in a uint2");
-  __shared__ float4 tiles[WAVES][HE / 4 + 1];
-  __shared__ uint2 rflags[WAVES][64];  // per owner lane: byte r != 0 = a kept value landed in its row r
+  __shared__ float4 tiles[WAVES][HE / 4];
   const uint32_t lane = lane_id(), wv = threadIdx.x >> 6;
   const uint32_t wid = blockIdx.x * WAVES + wv;
   const uint32_t u = wid / AGG_SPLIT, h = wid % AGG_SPLIT;
@@ -2326,7 +2328,6 @@ __global__ __launch_bounds__(BLOCK, AGG_WPE) void k_aggregate(Params P, AggArgs 
   const uint32_t hlen = min(len - e_lo, HE);
   float4* tile = tiles[wv];
   float* tf = reinterpret_cast<float*>(tile);
-  uint8_t* rf = reinterpret_cast<uint8_t*>(rflags[wv]);
   float4 b[RI], acc[RI];
   const float* bs = HASBASE ? P.base + U.off + e_lo : nullptr;
   auto load_base = [&]() {
@@ -2346,16 +2347,9 @@ __global__ __launch_bounds__(BLOCK, AGG_WPE) void k_aggregate(Params P, AggArgs 
   auto tile_zero = [&]() {
 #pragma unroll
     for (uint32_t it = 0; it < RI; ++it) tile[it * 64 + lane] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-    rflags[wv][lane] = make_uint2(0u, 0u);
-  };
-  // a kept value at wave-relative position p: tile slot p, owner lane (p >> 2) & 63, row p >> 8
-  auto mark = [&](uint32_t p, float v) {
-    tf[p] = v;
-    rf[((p >> 2) & 63u) * 8u + (p >> 8)] = 1;
   };
   if (HASBASE) load_base();
   tile_zero();
-  if (lane == 0) tile[ZS] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
 #pragma unroll
   for (uint32_t it = 0; it < RI; ++it) acc[it] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
   for (uint32_t c0 = 0; c0 < nclients; c0 += 64) {
@@ -2386,15 +2380,10 @@ __global__ __launch_bounds__(BLOCK, AGG_WPE) void k_aggregate(Params P, AggArgs 
     auto accumulate = [&](uint32_t j) {
       const float w = __uint_as_float(__builtin_amdgcn_readlane(__float_as_uint(m_w), j));
       const f2v w2 = {w, w};
-      const uint2 fl = rflags[wv][lane];
-      auto row = [&](uint32_t it) {  // (unmarked rows read the zero slot: +0.0f, as the zeroed tile holds)
-        const uint32_t f = ((it < 4 ? fl.x : fl.y) >> (8u * (it & 3u))) & 0xFFu;
-        return tile[f ? it * 64 + lane : ZS];
-      };
       if (c0 + j == 0) {
 #pragma unroll
         for (uint32_t it = 0; it < RI; ++it) {
-          const float4 d = row(it);
+          const float4 d = tile[it * 64 + lane];
           const f2v dl = {d.x, d.y}, dh = {d.z, d.w};
           const f2v bl = {b[it].x, b[it].y}, bh = {b[it].z, b[it].w};
           const f2v tl = (HASBASE ? bl + dl : dl) * w2, th = (HASBASE ? bh + dh : dh) * w2;
@@ -2403,7 +2392,7 @@ __global__ __launch_bounds__(BLOCK, AGG_WPE) void k_aggregate(Params P, AggArgs 
       } else {
 #pragma unroll
         for (uint32_t it = 0; it < RI; ++it) {
-          const float4 d = row(it);
+          const float4 d = tile[it * 64 + lane];
           const f2v dl = {d.x, d.y}, dh = {d.z, d.w};
           const f2v bl = {b[it].x, b[it].y}, bh = {b[it].z, b[it].w};
           const f2v al = {acc[it].x, acc[it].y}, ah = {acc[it].z, acc[it].w};
@@ -2419,12 +2408,11 @@ __global__ __launch_bounds__(BLOCK, AGG_WPE) void k_aggregate(Params P, AggArgs 
       const float mn = __uint_as_float(__builtin_amdgcn_readlane(__float_as_uint(m_mn), j));
       const float sc = __uint_as_float(__builtin_amdgcn_readlane(__float_as_uint(m_sc), j));
       const bool mine = lane < ne && pos < hlen;
-      if (mine) mark(pos, code_value<RAW>(q, mn, sc));
+      if (mine) tf[pos] = code_value<RAW>(q, mn, sc);
       lds_order();
       accumulate(j);
       lds_order();
       if (mine) tf[pos] = 0.0f;
-      rflags[wv][lane] = make_uint2(0u, 0u);
       lds_order();
     };
     // any client with more than 64 kept entries in this unit (ratio >~ 1.5 %): every client in turn, its
@@ -2438,7 +2426,7 @@ __global__ __launch_bounds__(BLOCK, AGG_WPE) void k_aggregate(Params P, AggArgs 
       for (uint32_t e = lo + lane; e < hi; e += 64) {
         const uint32_t p2 = (uint32_t)P.cidx[oo + e] - U.start - e_lo;
         const float v2 = load_val<RAW>(P, oo + e, mn, sc);
-        if (p2 < hlen) mark(p2, v2);
+        if (p2 < hlen) tf[p2] = v2;
       }
       lds_order();
       accumulate(j);

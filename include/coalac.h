@@ -218,7 +218,7 @@ int coalac_aggregate_ev(coalac_plan_t plan, int clients, const int32_t* d_idx, c
  * the last encode that used workspace d_ws (synchronises `stream`). */
 int coalac_workspace_fallbacks(coalac_plan_t plan, const void* d_ws, void* stream, int* out);
 
-/* Diagnostics: copy up to n phase timestamps (16 per k_select block = per large segment, 100 MHz
+/* Diagnostics: copy up to n phase timestamps (32 per segment row: k_sample, k_ghist, k_gwin, k_select phases, 100 MHz
  * ticks; 0 = phase not reached) of the last COALAC_FLAG_STAMPS encode with d_ws to host (synchronises
  * `stream`). Returns the count copied or a negative error. */
 int coalac_debug_stamps(coalac_plan_t plan, const void* d_ws, void* stream, uint64_t* host, int n);
