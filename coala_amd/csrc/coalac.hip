@@ -131,7 +131,11 @@ constexpr uint32_t GU = GU_UNITS;               // units per select group (k_ghi
 #ifndef GSWEEP
 #define GSWEEP 4  // units per record-load batch of a group sweep (8 measured equal on one update, lower on C3)
 #endif
-constexpr uint32_t HB2 = 512;             // bins of the per-group band histograms
+constexpr uint32_t HB2 = 512;             // bins of the per-group band histograms (k_ghist; CHAIN_UNITHIST 0)
+#ifndef CHAIN_UNITHIST
+#define CHAIN_UNITHIST 1  // k_scan writes a coarse per-unit band histogram (UHB bins) that k_gwin sums: no k_ghist
+#endif
+constexpr uint32_t UHB = 64;              // bins of the per-unit coarse band histograms (u8, saturating)
 constexpr uint32_t GCAP = 256;            // in-window entries a group may hand to k_select
 constexpr uint32_t KEY_MAX = 0x7FFFFFFFu;
 constexpr int HIST_BINS = 2048;
@@ -189,13 +193,15 @@ struct Params {
   // encode workspace: per segment
   uint32_t *tstar, *rtie, *status;
   // per large unit
-  uint32_t *tlo, *thi, *cntA, *cntC, *gtC, *eqC, *eqpre, *outoff;
+  uint32_t *tlo, *thi, *hhi, *cntA, *cntC, *gtC, *eqC, *eqpre, *outoff;
+  uint32_t* uhist;  // [n_lunits][UHB / 4]: the unit's coarse band histogram, UHB u8 counts (255 = saturated)
   uint32_t* cval;  // candidate records, ccap slots per large unit, in index order: the value bits ...
   uint16_t* cpos;  // ... and the position inside the unit (the emit reads both; every select sweep the values only)
   uint32_t ccap;  // record slots per large unit (< UNIT: a unit that finds more candidates overflows and its
                   // segment is selected and emitted from the raw data instead)
   // parallel select (groups of GU units of one large segment)
   const uint4* groups;     // {large-segment index, first large unit, units, segment}
+  const uint4* gseg;       // per group, its segment: {first large unit, units, k, first group}
   uint32_t n_groups;
   uint32_t* ghist;         // [n_groups][HB2]
   uint32_t* gcnt;          // [n_groups] in-window entries found by the group
@@ -629,8 +635,8 @@ DEV uint32_t hash32(uint32_t x) {
 struct Band {
   uint32_t tlo, thi, hhi, last;
   int shift;
-  DEV Band(uint32_t lo, uint32_t hi, uint32_t hh) : tlo(lo), thi(hi), hhi(hh) {
-    shift = band_shift(lo, hh, 9);
+  DEV Band(uint32_t lo, uint32_t hi, uint32_t hh, int bits = 9) : tlo(lo), thi(hi), hhi(hh) {
+    shift = band_shift(lo, hh, bits);
     last = (hh - lo) >> shift;
   }
   DEV uint32_t bin(uint32_t key) const { return key > hhi ? last : (key - tlo) >> shift; }
@@ -652,7 +658,7 @@ struct Band {
 // tlo > 0 (its loads past len return 0, key 0 < tlo): k_scan picks the lean form then (wave-uniform).
 template <bool DELTA, int NB, bool CHECK = true>
 DEV void scan_unit(const Params& P, uint32_t lu, const UnitDev& L, const uint32_t tlo, const uint32_t thi,
-                   uint2* stage) {
+                   const uint32_t hh, uint2* stage, uint32_t* wh) {
   constexpr uint32_t IT = UNIT_IT / NB;
   const uint32_t lane = lane_id();
   const uint32_t len = L.len;
@@ -666,10 +672,21 @@ DEV void scan_unit(const Params& P, uint32_t lu, const UnitDev& L, const uint32_
   const float* xin = P.inptr != nullptr ? P.inptr[L.seg] + L.start : P.in + off;
   const __amdgpu_buffer_rsrc_t rin = unit_rsrc(xin, len);
   const __amdgpu_buffer_rsrc_t rbase = unit_rsrc(DELTA ? P.base + off : xin, len);
+  // CHAIN_UNITHIST: every stored band record (tlo <= key <= thi) is counted in the wave's coarse histogram
+  const Band cband(tlo, thi, hh, 6);
+  static_assert(UHB == 64, "coarse band histogram: 6 bits, one bin per lane");
+  if (CHAIN_UNITHIST) {
+    wh[lane] = 0u;
+    lds_order();
+  }
   auto put = [&](uint32_t i, uint2 rec) {
     if (i >= cap) return;  // overflow: counted, not stored (the segment goes to the raw-data path)
     RV[i] = rec.y;
     RP[i] = (uint16_t)rec.x;
+    if (CHAIN_UNITHIST) {
+      const uint32_t key = rec.y & KEY_MAX;
+      if (key <= thi) atomicAdd(&wh[cband.bin(key)], 1u);
+    }
   };
 
   for (uint32_t nb = 0; nb < (uint32_t)NB; ++nb) {
@@ -734,6 +751,10 @@ DEV void scan_unit(const Params& P, uint32_t lu, const UnitDev& L, const uint32_
   if (stage != nullptr) {
     wave_fence();
     for (uint32_t i = lane; i < cC && i < STAGE_CAP; i += 64) put(i, stage[i]);
+  }
+  if (CHAIN_UNITHIST) {
+    lds_order();
+    reinterpret_cast<uint8_t*>(P.uhist)[(uint64_t)lu * UHB + lane] = (uint8_t)min(wh[lane], 255u);
   }
   if (lane == 0) {
     P.cntA[lu] = cA;
@@ -1034,6 +1055,7 @@ DEV void sample_segment(const Params& P, uint32_t li, uint32_t* hist, uint32_t* 
   for (uint32_t i = t; i < nu; i += NT) {
     P.tlo[sd.lu_begin + i] = tlo;
     P.thi[sd.lu_begin + i] = thi;
+    P.hhi[sd.lu_begin + i] = hh;
   }
   // The band histograms of the parallel select span [T_lo, min(T_hi, max sampled key)] (keys above go
   // to the last bin): with T_hi = KEY_MAX a full-range histogram would be too coarse.
@@ -1077,6 +1099,7 @@ __global__ __launch_bounds__(BLOCK, WPE) void k_scan(Params P) {
   constexpr size_t SMALL_BYTES = WITH_SMALL ? (SMALL_MAX + HIST_BINS + 64) * 4 : 0;
   constexpr size_t STAGE_BYTES = WAVES * STAGE_CAP * sizeof(uint2);
   __shared__ __attribute__((aligned(16))) uint8_t arena[SMALL_BYTES > STAGE_BYTES ? SMALL_BYTES : STAGE_BYTES];
+  __shared__ uint32_t whist[CHAIN_UNITHIST ? WAVES : 1][UHB];
   if (WITH_SMALL && blockIdx.x < P.scan_small) {
     float* vals = reinterpret_cast<float*>(arena);
     uint32_t* hist = reinterpret_cast<uint32_t*>(arena) + SMALL_MAX;
@@ -1089,11 +1112,12 @@ __global__ __launch_bounds__(BLOCK, WPE) void k_scan(Params P) {
   if (lu >= P.n_lunits) return;
   const UnitDev L = P.lunits[lu];
   // delta: 4 load batches (32 float4 in flight spill)
-  const uint32_t tlo = P.tlo[lu], thi = P.thi[lu];
+  const uint32_t tlo = P.tlo[lu], thi = P.thi[lu], hh = CHAIN_UNITHIST ? P.hhi[lu] : 0u;
+  uint32_t* wh = whist[CHAIN_UNITHIST ? wv : 0];
   if (SCAN_LEAN && (L.len == UNIT || tlo > 0))
-    scan_unit<DELTA, DELTA ? 4 : NB, false>(P, lu, L, tlo, thi, stage + wv * STAGE_CAP);
+    scan_unit<DELTA, DELTA ? 4 : NB, false>(P, lu, L, tlo, thi, hh, stage + wv * STAGE_CAP, wh);
   else
-    scan_unit<DELTA, DELTA ? 4 : NB, true>(P, lu, L, tlo, thi, stage + wv * STAGE_CAP);
+    scan_unit<DELTA, DELTA ? 4 : NB, true>(P, lu, L, tlo, thi, hh, stage + wv * STAGE_CAP, wh);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -1183,7 +1207,7 @@ DEV void unit_sweep(const uint32_t* cand, uint32_t stride, uint32_t lu0, const u
 
 // LDS scratch of the segment select (k_select, and the SELECT role of the one-launch encode, whose LDS
 // must stay <= 32 KB so five streaming blocks still fit a CU): 28.3 KB
-constexpr uint32_t WLIST = 1024;  // in-window entries the fast path can hold
+constexpr uint32_t WLIST = CHAIN_UNITHIST ? 4096 : 1024;  // in-window entries the fast path can hold
 constexpr int SEL_HB = 1024;      // bins of the select's radix histograms
 struct SelSmem {
   uint32_t hist[SEL_HB];
@@ -1194,7 +1218,7 @@ struct SelSmem {
   uint32_t sh[64];
   float shf[2 * (SEL_NT_LAT / 64)];
 };
-static_assert(sizeof(SelSmem) <= 29 * 1024, "select LDS budget");
+static_assert(sizeof(SelSmem) <= 56 * 1024, "select LDS budget");
 
 // Generic path: radix select over all candidates (1-3 coalesced sweeps) + a counts sweep; handles any
 // number of ties and segments of any size (units in chunks of UCAP).
@@ -1403,6 +1427,100 @@ DEV uint4 segment_pick(const Params& P, const SegDev& sd, const Band& band, uint
   return make_uint4(band.wlo(b), band.whi(b), r, 0u);
 }
 
+// segment_pick from the units' coarse band histograms (CHAIN_UNITHIST: k_scan wrote one per unit, so no k_ghist
+// pass precedes this one): the UHB bins summed over the segment's units (16 threads per unit, 4 bins each, 8
+// units' loads in flight per thread), then the bin of the k-th key among the band keys by one wave. The window is
+// that coarse bin — about 1/64 of the band, ~8x what a fine group-histogram bin held; k_select ranks it exactly. A
+// saturated unit count (255) routes the segment to the generic path, like a bracket miss.
+struct UnitSums {
+  uint32_t b0, b1, b2, b3, sa, sc, ov, sat;
+};
+
+// this thread's share of the sums over a segment's units (lb, nu): coarse bins 4q..4q+3 (q = t % 16) and the
+// candidate counts; loads only, no barrier, so a caller's other loads issued before go out in the same round
+template <int NT>
+DEV UnitSums unit_sums(const Params& P, uint32_t lb, uint32_t nu) {
+  const uint32_t t = threadIdx.x;
+  constexpr uint32_t UPP = NT / 16, BATCH = 8;  // units per pass; passes per load batch
+  const uint32_t q = t & 15u;
+  UnitSums r{};
+  for (uint32_t u0 = t >> 4; u0 < nu; u0 += UPP * BATCH) {
+    uint32_t w[BATCH], ca[BATCH], cc[BATCH];
+#pragma unroll
+    for (uint32_t j = 0; j < BATCH; ++j) {  // one load round: the histograms and (one thread per unit) the counts
+      const uint32_t u = lb + min(u0 + j * UPP, nu - 1);
+      w[j] = P.uhist[(uint64_t)u * (UHB / 4) + q];
+      ca[j] = q == 0 ? P.cntA[u] : 0u;
+      cc[j] = q == 0 ? P.cntC[u] : 0u;
+    }
+#pragma unroll
+    for (uint32_t j = 0; j < BATCH; ++j) {
+      if (u0 + j * UPP < nu) {
+        const uint32_t x = w[j];
+        r.b0 += x & 0xFFu;
+        r.b1 += (x >> 8) & 0xFFu;
+        r.b2 += (x >> 16) & 0xFFu;
+        r.b3 += x >> 24;
+        r.sat |= ((x & 0xFFu) == 0xFFu) | (((x >> 8) & 0xFFu) == 0xFFu) | (((x >> 16) & 0xFFu) == 0xFFu) |
+                 ((x >> 24) == 0xFFu);
+        r.sa += ca[j];
+        r.sc += cc[j];
+        r.ov += cc[j] > P.ccap ? 1u : 0u;
+      }
+    }
+  }
+  return r;
+}
+
+// segment_pick from the units' coarse band histograms (CHAIN_UNITHIST: k_scan wrote one per unit, so no k_ghist
+// pass precedes this one): the UHB bins summed over the segment's units (unit_sums), then the bin of the k-th key
+// among the band keys by one wave. The window is that coarse bin — about 1/64 of the band, ~8x what a fine
+// group-histogram bin held; k_select ranks it exactly. A saturated unit count (255) routes the segment to the
+// generic path, like a bracket miss.
+template <int NT = BLOCK>
+DEV uint4 pick_from_sums(const Params& P, UnitSums u, uint32_t nu, uint32_t k, const Band& band, uint32_t* hist,
+                         uint32_t* sh) {
+  const uint32_t t = threadIdx.x, lane = lane_id(), wv = t >> 6;
+  if (t < UHB) hist[t] = 0u;
+  // lanes q, q + 16, q + 32, q + 48 of a wave hold the same bins: reduce them, then one atomic per bin per wave
+#pragma unroll
+  for (int o = 16; o < 64; o <<= 1) {
+    u.b0 += (uint32_t)__shfl_xor((int)u.b0, o, 64);
+    u.b1 += (uint32_t)__shfl_xor((int)u.b1, o, 64);
+    u.b2 += (uint32_t)__shfl_xor((int)u.b2, o, 64);
+    u.b3 += (uint32_t)__shfl_xor((int)u.b3, o, 64);
+  }
+  const uint32_t sa = block_sum<NT>(u.sa, sh);  // barriers inside (also order the zeroed bins before the atomics)
+  if (lane < 16) {
+    atomicAdd(&hist[4 * lane + 0], u.b0);
+    atomicAdd(&hist[4 * lane + 1], u.b1);
+    atomicAdd(&hist[4 * lane + 2], u.b2);
+    atomicAdd(&hist[4 * lane + 3], u.b3);
+  }
+  const uint32_t sc = block_sum<NT>(u.sc, sh);
+  const uint32_t ov = block_sum<NT>(u.ov, sh);
+  const uint32_t sat = block_sum<NT>(u.sat, sh);
+  const bool generic = (P.flags & (COALAC_FLAG_FORCE_EXACT | COALAC_FLAG_GENERIC_SELECT)) || !(sa < k && k <= sc) ||
+                       nu > UCAP || ov != 0 || sat != 0;
+  if (generic) return make_uint4(0u, 0u, 0u, 1u);
+  // (the block_sum barriers ordered the bin atomics before this read)
+  if (wv == 0) {  // the r-th largest band key: bins from the top, one per lane
+    const uint32_t r = k - sa;
+    const uint32_t v = hist[UHB - 1 - lane];
+    const uint32_t inc = wave_incl_scan(v);
+    if (inc >= r && inc - v < r) {
+      sh[40] = UHB - 1 - lane;
+      sh[41] = r - (inc - v);
+    }
+    if (lane == 0 && (uint32_t)__shfl((int)inc, 63, 64) < r) sh[40] = NONE;
+  }
+  __syncthreads();
+  const uint32_t b = sh[40], rin = sh[41];
+  __syncthreads();
+  if (b == NONE) return make_uint4(0u, 0u, 0u, 1u);
+  return make_uint4(band.wlo(b), band.whi(b), rin, 0u);
+}
+
 // k_gwin: per group — per-unit counts of keys above the window (-> gtC), the group's in-window entries
 // in index order (-> glist, count -> gcnt), min/max of the values above the window (-> gmm)
 template <int NW = WAVES>
@@ -1476,22 +1594,37 @@ DEV void group_window(const Params& P, uint32_t gi, const uint4 G, const uint4 s
 
 template <int NT = BLOCK>
 DEV void group_pick_window(const Params& P, uint32_t gi, GwinSmemT<NT / 64>& W, uint32_t* hist, uint32_t* sh) {
+  // round 1: the group and its segment's geometry (gseg: {first large unit, units, k, first group}, so nothing
+  // waits for a segment-table lookup); round 2: the band, the group's counts and (CHAIN_UNITHIST) the sums over
+  // the segment's units
   const uint4 G = P.groups[gi];
+  const uint4 GS = P.gseg[gi];
   STAMP(P, G.x, 22);
-  // one load round for everything that depends on G only: the segment, its band, the group's counts
-  const SegDev sd = P.lsegs[G.x];
-  const uint32_t tlo = P.tlo[G.y], thi = P.thi[G.y], hh = P.shhi[G.x];
+  SegDev sd{};
+  sd.lu_begin = GS.x;
+  sd.unit_end = GS.y;
+  sd.k = GS.z;
+  sd.g_begin = GS.w;
+  const uint32_t tlo = P.tlo[G.y], thi = P.thi[G.y], hh = P.hhi[G.y];
   const uint32_t c = threadIdx.x < G.z ? min(P.cntC[G.y + threadIdx.x], P.ccap) : 0u;
-  const uint32_t total = reg_prefix<NT>(c, G.z, W.upre, sh);
-  const Band band(tlo, thi, hh);
-  const uint4 st = segment_pick<NT>(P, sd, band, hist, sh);
-  STAMP(P, G.x, 23);
-  if (threadIdx.x == 0 && G.y == sd.lu_begin) {  // the segment's first group
+  uint4 st;
+  if (CHAIN_UNITHIST) {
+    const UnitSums us = unit_sums<NT>(P, GS.x, GS.y);
+    const uint32_t total = reg_prefix<NT>(c, G.z, W.upre, sh);
+    st = pick_from_sums<NT>(P, us, GS.y, GS.z, Band(tlo, thi, hh, 6), hist, sh);
+    STAMP(P, G.x, 23);
+    if (st.w == 0) group_window<NT>(P, gi, G, st, GS.x, total, W, sh);
+  } else {
+    const uint32_t total = reg_prefix<NT>(c, G.z, W.upre, sh);
+    st = segment_pick<NT>(P, sd, Band(tlo, thi, hh), hist, sh);
+    STAMP(P, G.x, 23);
+    if (st.w == 0) group_window<NT>(P, gi, G, st, GS.x, total, W, sh);
+  }
+  if (threadIdx.x == 0 && G.y == GS.x) {  // the segment's first group
     uint2* ss = reinterpret_cast<uint2*>(P.sstate + G.x);
     pst(P, ss, make_uint2(st.x, st.y));
     pst(P, ss + 1, make_uint2(st.z, st.w));
   }
-  if (st.w == 0) group_window<NT>(P, gi, G, st, sd.lu_begin, total, W, sh);
   STAMP(P, G.x, 24);
 }
 
@@ -1610,7 +1743,17 @@ DEV bool select_from_groups(const Params& P, const SegDev& sd, uint32_t lb, uint
                             uint32_t& T_out, uint32_t& rt_out, uint32_t& fp, uint32_t& fn, float& gmn, float& gmx) {
   const uint32_t t = threadIdx.x;
   const uint32_t g0 = sd.g_begin, ng = (nu + GU - 1) / GU;  // ng <= UCAP / GU = 64 <= NT
-  // one load round: the groups' list lengths, min / max above the window and the first per-unit counts
+  // one load round: the groups' list lengths, min / max above the window, the first per-unit counts, and —
+  // speculatively, before their lengths are known — the first SPEC slots of every group's in-window list (the
+  // typical window share of a group fits; a longer list's remainder is loaded after the scan)
+  constexpr uint32_t SPEC = 64, SPT = (UCAP / GU) * SPEC / NT;
+  static_assert((UCAP / GU) * SPEC % NT == 0, "speculative gather geometry");
+  uint2 sv[SPT];
+#pragma unroll
+  for (uint32_t j = 0; j < SPT; ++j) {
+    const uint32_t i = t + j * NT, g = i / SPEC;
+    sv[j] = g < ng ? P.glist[(uint64_t)(g0 + g) * GCAP + i % SPEC] : make_uint2(0u, 0u);
+  }
   const uint32_t c = t < ng ? P.gcnt[g0 + t] : 0u;
   const float gmn0 = t < ng ? P.gmm[2 * (g0 + t)] : qnan(), gmx0 = t < ng ? P.gmm[2 * (g0 + t) + 1] : qnan();
   constexpr uint32_t CB = 3;
@@ -1621,31 +1764,18 @@ DEV bool select_from_groups(const Params& P, const SegDev& sd, uint32_t lb, uint
   const uint32_t gpre = block_excl_scan<NT>(c, S.sh, W);
   const uint32_t over = block_sum<NT>(c > GCAP ? 1u : 0u, S.sh);
   if (over || W > WLIST) return false;
-  // offset of each group's entries, then gather them: entry e belongs to the last group g with
-  // upre[g] <= e (binary search in LDS); all of a thread's loads are issued before any is used
+  // each group's entries go to its offset in the segment's list (group order = index order)
   if (t < ng) S.upre[t] = gpre;
+  if (t == 0) S.upre[ng] = W;
   __syncthreads();
-  {
-    constexpr uint32_t EPT = WLIST / NT;
-    uint2 v[EPT];
 #pragma unroll
-    for (uint32_t j = 0; j < EPT; ++j) {
-      const uint32_t e = min(t + j * NT, W > 0 ? W - 1 : 0u);
-      uint32_t lo = 0, hi = ng - 1;  // ng >= 1
-      while (lo < hi) {
-        const uint32_t mid = (lo + hi + 1) >> 1;
-        if (S.upre[mid] <= e)
-          lo = mid;
-        else
-          hi = mid - 1;
-      }
-      v[j] = P.glist[(uint64_t)(g0 + lo) * GCAP + min(e - S.upre[lo], GCAP - 1)];
-    }
-#pragma unroll
-    for (uint32_t j = 0; j < EPT; ++j) {
-      const uint32_t e = t + j * NT;
-      if (e < W) S.lst[e] = v[j];
-    }
+  for (uint32_t j = 0; j < SPT; ++j) {
+    const uint32_t i = t + j * NT, g = i / SPEC, slot = i % SPEC;
+    if (g < ng && S.upre[g] + slot < S.upre[g + 1]) S.lst[S.upre[g] + slot] = sv[j];
+  }
+  for (uint32_t g = 0; g < ng; ++g) {  // (wave-uniform) lists longer than SPEC: the rest
+    const uint32_t a = S.upre[g], n = S.upre[g + 1] - a;
+    for (uint32_t slot = SPEC + t; slot < n; slot += NT) S.lst[a + slot] = P.glist[(uint64_t)(g0 + g) * GCAP + slot];
   }
 #pragma unroll
   for (uint32_t j = 0; j < CB; ++j)
@@ -2502,7 +2632,7 @@ size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 struct WsLayout {
   size_t status;
   size_t tstar, rtie;
-  size_t tlo, thi, cntA, cntC, gtC, eqC, eqpre, outoff;
+  size_t tlo, thi, hhi, uhist, cntA, cntC, gtC, eqC, eqpre, outoff;
   size_t cval, cpos, stamps, ghist, gcnt, glist, gmm, sstate, shhi;
   size_t total;
 };
@@ -2520,6 +2650,8 @@ WsLayout ws_layout(size_t S, size_t LU, size_t NG, size_t NL, uint32_t CC) {
   L.rtie = take(4 * S);
   L.tlo = take(4 * LU);
   L.thi = take(4 * LU);
+  L.hhi = take(4 * LU);
+  L.uhist = take(CHAIN_UNITHIST ? UHB * LU : 0);
   L.cntA = take(4 * LU);
   L.cntC = take(4 * LU);
   L.gtC = take(4 * LU);
@@ -2529,7 +2661,7 @@ WsLayout ws_layout(size_t S, size_t LU, size_t NG, size_t NL, uint32_t CC) {
   L.cval = take(4 * (size_t)CC * LU);
   L.cpos = take(2 * (size_t)CC * LU);
   L.stamps = take(8 * NSTAMP * std::max<size_t>(S, 1));
-  L.ghist = take(4 * HB2 * NG);
+  L.ghist = take(CHAIN_UNITHIST ? 0 : 4 * HB2 * NG);
   L.gcnt = take(4 * NG);
   L.glist = take(sizeof(uint2) * GCAP * NG);
   L.gmm = take(8 * NG);
@@ -2557,6 +2689,7 @@ struct coalac_plan {
   SegDev* lsegs = nullptr;
   SegDev* ssegs = nullptr;
   uint4* groups = nullptr;
+  uint4* gseg = nullptr;
   uint32_t n_groups = 0;
   BChunk* bchunks = nullptr;  // aggregate: k_bounds work list
   uint32_t n_bchunks = 0;
@@ -2589,6 +2722,7 @@ void fill_meta(Params& P, coalac_plan_t plan) {
   P.lsegs = plan->lsegs;
   P.ssegs = plan->ssegs;
   P.groups = plan->groups;
+  P.gseg = plan->gseg;
   P.n_groups = plan->n_groups;
   P.nseg = (uint32_t)plan->nseg;
   P.n_small = plan->n_small;
@@ -2704,7 +2838,9 @@ int launch_encode(const Params& P, coalac_plan_t plan, hipStream_t st, const coa
   }
   ENC_BOUNDARY(2);
   if ((stages & COALAC_STAGE_SELECT) && plan->n_large) {
-    if (plan->n_lunits <= LATENCY_PLAN_UNITS)
+    if (CHAIN_UNITHIST)
+      ;  // (the band histograms came with k_scan)
+    else if (plan->n_lunits <= LATENCY_PLAN_UNITS)
       hipLaunchKernelGGL(k_ghist<GHIST_NT_LAT>, dim3(plan->n_groups), dim3(GHIST_NT_LAT), 0, st, P);
     else
       hipLaunchKernelGGL(k_ghist<BLOCK>, dim3(plan->n_groups), dim3(BLOCK), 0, st, P);
@@ -2741,7 +2877,7 @@ int coalac_plan_create(const coalac_seg_t* h_segs, int nseg, int bits, coalac_pl
 
   std::vector<SegDev> segs(nseg);
   std::vector<UnitDev> units, lunits;
-  std::vector<uint4> groups;
+  std::vector<uint4> groups, gseg;
   std::vector<uint32_t> small_list, large_list;
   std::vector<BChunk> bchunks;
   uint64_t span = 0, total_k = 0;
@@ -2783,8 +2919,10 @@ int coalac_plan_create(const coalac_seg_t* h_segs, int nseg, int bits, coalac_pl
     if (large) {
       d.g_begin = (uint32_t)groups.size();
       const uint32_t nu = d.unit_end - d.unit_begin;
-      for (uint32_t g0 = 0; g0 < nu; g0 += GU)
+      for (uint32_t g0 = 0; g0 < nu; g0 += GU) {
         groups.push_back(make_uint4((uint32_t)large_list.size(), d.lu_begin + g0, std::min(GU, nu - g0), (uint32_t)s));
+        gseg.push_back(make_uint4(d.lu_begin, nu, (uint32_t)g.k, d.g_begin));
+      }
     }
     (large ? large_list : small_list).push_back((uint32_t)s);
     for (uint64_t e0 = 0; e0 < g.k; e0 += BCHUNK)
@@ -2844,7 +2982,8 @@ int coalac_plan_create(const coalac_seg_t* h_segs, int nseg, int bits, coalac_pl
   const size_t o_lsegs = align_up(o_large + 4 * large_list.size(), 256);
   const size_t o_ssegs = align_up(o_lsegs + sizeof(SegDev) * lsegs.size(), 256);
   const size_t o_grp = align_up(o_ssegs + sizeof(SegDev) * ssegs.size(), 256);
-  const size_t o_bch = align_up(o_grp + sizeof(uint4) * groups.size(), 256);
+  const size_t o_gseg = align_up(o_grp + sizeof(uint4) * groups.size(), 256);
+  const size_t o_bch = align_up(o_gseg + sizeof(uint4) * gseg.size(), 256);
   std::vector<SChunk> schunks;
   for (const BChunk& c : bchunks)
     schunks.push_back(SChunk{segs[c.seg].in_off, segs[c.seg].out_off, c.seg, segs[c.seg].n, c.e0, c.e1});
@@ -2859,6 +2998,7 @@ int coalac_plan_create(const coalac_seg_t* h_segs, int nseg, int bits, coalac_pl
   if (!lsegs.empty()) memcpy(host.data() + o_lsegs, lsegs.data(), sizeof(SegDev) * lsegs.size());
   if (!ssegs.empty()) memcpy(host.data() + o_ssegs, ssegs.data(), sizeof(SegDev) * ssegs.size());
   if (!groups.empty()) memcpy(host.data() + o_grp, groups.data(), sizeof(uint4) * groups.size());
+  if (!gseg.empty()) memcpy(host.data() + o_gseg, gseg.data(), sizeof(uint4) * gseg.size());
   if (!bchunks.empty()) memcpy(host.data() + o_bch, bchunks.data(), sizeof(BChunk) * bchunks.size());
   if (!schunks.empty()) memcpy(host.data() + o_sch, schunks.data(), sizeof(SChunk) * schunks.size());
   hipError_t e = hipMalloc(&p->meta, bytes);
@@ -2881,6 +3021,7 @@ int coalac_plan_create(const coalac_seg_t* h_segs, int nseg, int bits, coalac_pl
   p->lsegs = reinterpret_cast<SegDev*>(m + o_lsegs);
   p->ssegs = reinterpret_cast<SegDev*>(m + o_ssegs);
   p->groups = reinterpret_cast<uint4*>(m + o_grp);
+  p->gseg = reinterpret_cast<uint4*>(m + o_gseg);
   p->bchunks = reinterpret_cast<BChunk*>(m + o_bch);
   p->schunks = reinterpret_cast<SChunk*>(m + o_sch);
   *out = p;
@@ -2957,6 +3098,8 @@ int encode_impl(coalac_plan_t plan, const float* d_in, const float* const* d_inp
   P.status = reinterpret_cast<uint32_t*>(w + L.status);
   P.tlo = reinterpret_cast<uint32_t*>(w + L.tlo);
   P.thi = reinterpret_cast<uint32_t*>(w + L.thi);
+  P.hhi = reinterpret_cast<uint32_t*>(w + L.hhi);
+  P.uhist = reinterpret_cast<uint32_t*>(w + L.uhist);
   P.cntA = reinterpret_cast<uint32_t*>(w + L.cntA);
   P.cntC = reinterpret_cast<uint32_t*>(w + L.cntC);
   P.gtC = reinterpret_cast<uint32_t*>(w + L.gtC);
