@@ -53,6 +53,7 @@ SIGNATURES = [
     # aggregate: plan, clients, idx, vals, mn, scale, ustart, weights, total, mode, mask, base, out, ws, ws_bytes, stream
     ("coalac_aggregate", _I, [_P, _I, _P, _P, _P, _P, _P, _P, ctypes.c_float, _I, _P, _P, _P, _P, _U64, _P]),
     ("coalac_aggregate_ev", _I, [_P, _I, _P, _P, _P, _P, _P, _P, ctypes.c_float, _I, _P, _P, _P, _P, _U64, _P, _P]),
+    ("coalac_gather", _I, [_P, _I, _I, _P, _P]),
     ("coalac_workspace_fallbacks", _I, [_P, _P, _P, ctypes.POINTER(_I)]),
     ("coalac_debug_stamps", _I, [_P, _P, _P, ctypes.POINTER(ctypes.c_uint64), _I]),
 ]

@@ -22,11 +22,13 @@ from collections.abc import Mapping
 from itertools import repeat
 from operator import attrgetter, is_
 
+import ctypes
+
 import numpy as np
 import torch
 from torch import nn
 
-from . import wire
+from . import _lib, wire
 from .plan import CodecPlan, Encoded
 from .spec import ALIGN, RAW_BITS, UNIT, VALID_BITS, SegmentTable, align_up, k_for
 
@@ -49,6 +51,31 @@ class HipBackend:
             raise RuntimeError(f"the HIP codec runs on GPU tensors only; got tensors on {device} "
                                "(there is no CPU fallback)")
         return CodecPlan(sizes, ratio, bits, clients=clients, device=device)
+
+    def gather_scalars(self, ts):
+        """One contiguous copy of the one-element tensors ts (one dtype, one GPU) in a single launch
+        (coalac_gather), or None when they do not qualify (the caller then stacks them with torch)."""
+        t0 = ts[0]
+        if t0.device.type != "cuda":
+            return None
+        dev, size = t0.device, t0.element_size()
+        ptrs = tuple(map(_data_ptr, ts))
+        if list(map(_get_device, ts)) != [dev.index] * len(ts) or any(p % size for p in ptrs):
+            return None
+        cache = self.__dict__.setdefault("_gather_ptrs", OrderedDict())
+        d = cache.get(ptrs)
+        if d is None:
+            d = torch.tensor(ptrs, dtype=torch.int64).to(dev)
+            cache[ptrs] = d
+            while len(cache) > 16:
+                cache.popitem(last=False)
+        st = torch.cuda.current_stream(dev)
+        d.record_stream(st)  # (an eviction from the cache never hands its memory to a kernel still reading it)
+        out = torch.empty(len(ts), dtype=t0.dtype, device=dev)
+        lib = _lib.load()
+        _lib.check(lib.coalac_gather(ctypes.c_void_p(d.data_ptr()), len(ts), size, ctypes.c_void_p(out.data_ptr()),
+                                     ctypes.c_void_p(st.cuda_stream)), "coalac_gather")
+        return out
 
 
 class FlatState:
@@ -230,10 +257,11 @@ def _module_walk(module):
 _get_dtype, _get_shape = attrgetter("dtype"), attrgetter("shape")
 
 
-def describe_tensors(names, tensors, walk=None):
+def describe_tensors(names, tensors, walk=None, gather=None):
     """describe_state() over (names, tensors) in state_dict order (module_tensors). walk: the _StateWalk the
     tensors came from — the layout is then looked up again only when a dtype or shape changed since its last
-    call (list comparisons, instead of hashing the whole (name, dtype, shape) signature every call)."""
+    call (list comparisons, instead of hashing the whole (name, dtype, shape) signature every call). gather: a
+    backend's one-launch copy of one-element tensors (HipBackend.gather_scalars) for the passthrough scalars."""
     dts, shs = list(map(_get_dtype, tensors)), list(map(_get_shape, tensors))
     last = walk.last if walk is not None else None
     if last is not None and last[0] == dts and last[1] == shs:
@@ -246,11 +274,15 @@ def describe_tensors(names, tensors, walk=None):
     raw_ts = list(map(tensors.__getitem__, L.raw_idx))
     raw = None
     if L.raw_scalars is not None:
-        try:
-            with torch.no_grad():  # one stack of the scalar counters: no per-entry checks
-                raw = RawState([(torch.stack(raw_ts), L.raw_scalars)], L.raw_names)
-        except RuntimeError:  # (counters on several devices)
-            raw = None
+        flat = gather(raw_ts) if gather is not None else None
+        if flat is not None:
+            raw = RawState([(flat, L.raw_scalars)], L.raw_names)
+        else:
+            try:
+                with torch.no_grad():  # one stack of the scalar counters: no per-entry checks
+                    raw = RawState([(torch.stack(raw_ts), L.raw_scalars)], L.raw_names)
+            except RuntimeError:  # (counters on several devices)
+                raw = None
     if raw is None:
         raw = RawState.snapshot(list(zip(L.raw_names, raw_ts)))
     return L, segs, raw
@@ -735,7 +767,7 @@ class UpdateCodec:
         names, tensors, walk = _module_walk(module)
         if device is None:
             device = self._device_for(tensors)
-        L, segs, raw = describe_tensors(names, tensors, walk)
+        L, segs, raw = describe_tensors(names, tensors, walk, getattr(self.backend, "gather_scalars", None))
         return self._encode(L, segs, raw, base, device, lambda: OrderedDict(zip(names, tensors)))
 
     def _encode(self, L, segs, raw, base, device, state_fn):

@@ -120,12 +120,16 @@ class CodecPlan:
         return torch.empty(self.span, dtype=torch.float32, device=self.device)
 
     def empty_encoded(self):
-        d = self.device
-        return Encoded(torch.empty(self.total_k, dtype=torch.int32, device=d),
-                       torch.empty(self.total_k, dtype=self.vals_dtype, device=d),
-                       torch.empty(self.n_segments, dtype=torch.float32, device=d),
-                       torch.empty(self.n_segments, dtype=torch.float32, device=d),
-                       torch.empty(self.n_units, dtype=torch.int32, device=d))
+        """The five output buffers of an encode as views of ONE allocation (16-byte aligned each)."""
+        K, T, U = self.total_k, self.n_segments, self.n_units
+        vb = 4 if self.bits == RAW_BITS else 1
+        offs, o = [], 0
+        for nbytes in (4 * K, vb * K, 4 * T, 4 * T, 4 * U):
+            offs.append((o, nbytes))
+            o = (o + nbytes + 15) // 16 * 16
+        buf = torch.empty(max(o, 16), dtype=torch.uint8, device=self.device)
+        dts = (torch.int32, self.vals_dtype, torch.float32, torch.float32, torch.int32)
+        return Encoded(*(buf[a:a + n].view(dt) for (a, n), dt in zip(offs, dts)))
 
     def empty_workspace(self):
         return torch.empty(self.ws_bytes, dtype=torch.uint8, device=self.device)
@@ -226,10 +230,11 @@ class CodecPlan:
         parameters, no flattening copy. base: flat fp32[span] (delta mode), as encode()."""
         ptrs = self.segment_pointers(tensors, checked=checked, ptrs=ptrs, stream=stream)
         self._check_flat(base, "base")
+        mine = out is None  # (buffers this call allocates need no checking)
         with _on(stream):
             out = self.empty_encoded() if out is None else out
             ws = self.empty_workspace() if workspace is None else workspace
-        ust = self._check_encoded(out)
+        ust = _ptr(out.ustart) if mine else self._check_encoded(out)
         if ws.device != self.device or ws.numel() * ws.element_size() < self.ws_bytes:
             raise ValueError(f"workspace: need {self.ws_bytes} bytes on {self.device}")
         with torch.cuda.device(self.device):

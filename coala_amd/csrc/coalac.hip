@@ -131,11 +131,7 @@ constexpr uint32_t GU = GU_UNITS;               // units per select group (k_ghi
 #ifndef GSWEEP
 #define GSWEEP 4  // units per record-load batch of a group sweep (8 measured equal on one update, lower on C3)
 #endif
-constexpr uint32_t HB2 = 512;             // bins of the per-group band histograms (k_ghist; CHAIN_UNITHIST 0)
-#ifndef CHAIN_UNITHIST
-#define CHAIN_UNITHIST 1  // k_scan writes a coarse per-unit band histogram (UHB bins) that k_gwin sums: no k_ghist
-#endif
-constexpr uint32_t UHB = 64;              // bins of the per-unit coarse band histograms (u8, saturating)
+constexpr uint32_t HB2 = 512;             // bins of the per-group band histograms
 constexpr uint32_t GCAP = 256;            // in-window entries a group may hand to k_select
 constexpr uint32_t KEY_MAX = 0x7FFFFFFFu;
 constexpr int HIST_BINS = 2048;
@@ -193,8 +189,7 @@ struct Params {
   // encode workspace: per segment
   uint32_t *tstar, *rtie, *status;
   // per large unit
-  uint32_t *tlo, *thi, *hhi, *cntA, *cntC, *gtC, *eqC, *eqpre, *outoff;
-  uint32_t* uhist;  // [n_lunits][UHB / 4]: the unit's coarse band histogram, UHB u8 counts (255 = saturated)
+  uint32_t *tlo, *thi, *cntA, *cntC, *gtC, *eqC, *eqpre, *outoff;
   uint32_t* cval;  // candidate records, ccap slots per large unit, in index order: the value bits ...
   uint16_t* cpos;  // ... and the position inside the unit (the emit reads both; every select sweep the values only)
   uint32_t ccap;  // record slots per large unit (< UNIT: a unit that finds more candidates overflows and its
@@ -635,8 +630,8 @@ DEV uint32_t hash32(uint32_t x) {
 struct Band {
   uint32_t tlo, thi, hhi, last;
   int shift;
-  DEV Band(uint32_t lo, uint32_t hi, uint32_t hh, int bits = 9) : tlo(lo), thi(hi), hhi(hh) {
-    shift = band_shift(lo, hh, bits);
+  DEV Band(uint32_t lo, uint32_t hi, uint32_t hh) : tlo(lo), thi(hi), hhi(hh) {
+    shift = band_shift(lo, hh, 9);
     last = (hh - lo) >> shift;
   }
   DEV uint32_t bin(uint32_t key) const { return key > hhi ? last : (key - tlo) >> shift; }
@@ -658,7 +653,7 @@ struct Band {
 // tlo > 0 (its loads past len return 0, key 0 < tlo): k_scan picks the lean form then (wave-uniform).
 template <bool DELTA, int NB, bool CHECK = true>
 DEV void scan_unit(const Params& P, uint32_t lu, const UnitDev& L, const uint32_t tlo, const uint32_t thi,
-                   const uint32_t hh, uint2* stage, uint32_t* wh) {
+                   uint2* stage) {
   constexpr uint32_t IT = UNIT_IT / NB;
   const uint32_t lane = lane_id();
   const uint32_t len = L.len;
@@ -672,21 +667,10 @@ DEV void scan_unit(const Params& P, uint32_t lu, const UnitDev& L, const uint32_
   const float* xin = P.inptr != nullptr ? P.inptr[L.seg] + L.start : P.in + off;
   const __amdgpu_buffer_rsrc_t rin = unit_rsrc(xin, len);
   const __amdgpu_buffer_rsrc_t rbase = unit_rsrc(DELTA ? P.base + off : xin, len);
-  // CHAIN_UNITHIST: every stored band record (tlo <= key <= thi) is counted in the wave's coarse histogram
-  const Band cband(tlo, thi, hh, 6);
-  static_assert(UHB == 64, "coarse band histogram: 6 bits, one bin per lane");
-  if (CHAIN_UNITHIST) {
-    wh[lane] = 0u;
-    lds_order();
-  }
   auto put = [&](uint32_t i, uint2 rec) {
     if (i >= cap) return;  // overflow: counted, not stored (the segment goes to the raw-data path)
     RV[i] = rec.y;
     RP[i] = (uint16_t)rec.x;
-    if (CHAIN_UNITHIST) {
-      const uint32_t key = rec.y & KEY_MAX;
-      if (key <= thi) atomicAdd(&wh[cband.bin(key)], 1u);
-    }
   };
 
   for (uint32_t nb = 0; nb < (uint32_t)NB; ++nb) {
@@ -751,10 +735,6 @@ DEV void scan_unit(const Params& P, uint32_t lu, const UnitDev& L, const uint32_
   if (stage != nullptr) {
     wave_fence();
     for (uint32_t i = lane; i < cC && i < STAGE_CAP; i += 64) put(i, stage[i]);
-  }
-  if (CHAIN_UNITHIST) {
-    lds_order();
-    reinterpret_cast<uint8_t*>(P.uhist)[(uint64_t)lu * UHB + lane] = (uint8_t)min(wh[lane], 255u);
   }
   if (lane == 0) {
     P.cntA[lu] = cA;
@@ -1055,7 +1035,6 @@ DEV void sample_segment(const Params& P, uint32_t li, uint32_t* hist, uint32_t* 
   for (uint32_t i = t; i < nu; i += NT) {
     P.tlo[sd.lu_begin + i] = tlo;
     P.thi[sd.lu_begin + i] = thi;
-    P.hhi[sd.lu_begin + i] = hh;
   }
   // The band histograms of the parallel select span [T_lo, min(T_hi, max sampled key)] (keys above go
   // to the last bin): with T_hi = KEY_MAX a full-range histogram would be too coarse.
@@ -1099,7 +1078,6 @@ __global__ __launch_bounds__(BLOCK, WPE) void k_scan(Params P) {
   constexpr size_t SMALL_BYTES = WITH_SMALL ? (SMALL_MAX + HIST_BINS + 64) * 4 : 0;
   constexpr size_t STAGE_BYTES = WAVES * STAGE_CAP * sizeof(uint2);
   __shared__ __attribute__((aligned(16))) uint8_t arena[SMALL_BYTES > STAGE_BYTES ? SMALL_BYTES : STAGE_BYTES];
-  __shared__ uint32_t whist[CHAIN_UNITHIST ? WAVES : 1][UHB];
   if (WITH_SMALL && blockIdx.x < P.scan_small) {
     float* vals = reinterpret_cast<float*>(arena);
     uint32_t* hist = reinterpret_cast<uint32_t*>(arena) + SMALL_MAX;
@@ -1112,12 +1090,11 @@ __global__ __launch_bounds__(BLOCK, WPE) void k_scan(Params P) {
   if (lu >= P.n_lunits) return;
   const UnitDev L = P.lunits[lu];
   // delta: 4 load batches (32 float4 in flight spill)
-  const uint32_t tlo = P.tlo[lu], thi = P.thi[lu], hh = CHAIN_UNITHIST ? P.hhi[lu] : 0u;
-  uint32_t* wh = whist[CHAIN_UNITHIST ? wv : 0];
+  const uint32_t tlo = P.tlo[lu], thi = P.thi[lu];
   if (SCAN_LEAN && (L.len == UNIT || tlo > 0))
-    scan_unit<DELTA, DELTA ? 4 : NB, false>(P, lu, L, tlo, thi, hh, stage + wv * STAGE_CAP, wh);
+    scan_unit<DELTA, DELTA ? 4 : NB, false>(P, lu, L, tlo, thi, stage + wv * STAGE_CAP);
   else
-    scan_unit<DELTA, DELTA ? 4 : NB, true>(P, lu, L, tlo, thi, hh, stage + wv * STAGE_CAP, wh);
+    scan_unit<DELTA, DELTA ? 4 : NB, true>(P, lu, L, tlo, thi, stage + wv * STAGE_CAP);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -1207,7 +1184,10 @@ DEV void unit_sweep(const uint32_t* cand, uint32_t stride, uint32_t lu0, const u
 
 // LDS scratch of the segment select (k_select, and the SELECT role of the one-launch encode, whose LDS
 // must stay <= 32 KB so five streaming blocks still fit a CU): 28.3 KB
-constexpr uint32_t WLIST = CHAIN_UNITHIST ? 4096 : 1024;  // in-window entries the fast path can hold
+constexpr uint32_t WLIST = 1024;  // in-window entries the fast path can hold
+#ifndef SELECT_SPEC
+#define SELECT_SPEC 16u  // k_select: speculatively gathered slots per group window list (a window holds ~4 per group)
+#endif
 constexpr int SEL_HB = 1024;      // bins of the select's radix histograms
 struct SelSmem {
   uint32_t hist[SEL_HB];
@@ -1218,7 +1198,7 @@ struct SelSmem {
   uint32_t sh[64];
   float shf[2 * (SEL_NT_LAT / 64)];
 };
-static_assert(sizeof(SelSmem) <= 56 * 1024, "select LDS budget");
+static_assert(sizeof(SelSmem) <= 29 * 1024, "select LDS budget");
 
 // Generic path: radix select over all candidates (1-3 coalesced sweeps) + a counts sweep; handles any
 // number of ties and segments of any size (units in chunks of UCAP).
@@ -1427,100 +1407,6 @@ DEV uint4 segment_pick(const Params& P, const SegDev& sd, const Band& band, uint
   return make_uint4(band.wlo(b), band.whi(b), r, 0u);
 }
 
-// segment_pick from the units' coarse band histograms (CHAIN_UNITHIST: k_scan wrote one per unit, so no k_ghist
-// pass precedes this one): the UHB bins summed over the segment's units (16 threads per unit, 4 bins each, 8
-// units' loads in flight per thread), then the bin of the k-th key among the band keys by one wave. The window is
-// that coarse bin — about 1/64 of the band, ~8x what a fine group-histogram bin held; k_select ranks it exactly. A
-// saturated unit count (255) routes the segment to the generic path, like a bracket miss.
-struct UnitSums {
-  uint32_t b0, b1, b2, b3, sa, sc, ov, sat;
-};
-
-// this thread's share of the sums over a segment's units (lb, nu): coarse bins 4q..4q+3 (q = t % 16) and the
-// candidate counts; loads only, no barrier, so a caller's other loads issued before go out in the same round
-template <int NT>
-DEV UnitSums unit_sums(const Params& P, uint32_t lb, uint32_t nu) {
-  const uint32_t t = threadIdx.x;
-  constexpr uint32_t UPP = NT / 16, BATCH = 8;  // units per pass; passes per load batch
-  const uint32_t q = t & 15u;
-  UnitSums r{};
-  for (uint32_t u0 = t >> 4; u0 < nu; u0 += UPP * BATCH) {
-    uint32_t w[BATCH], ca[BATCH], cc[BATCH];
-#pragma unroll
-    for (uint32_t j = 0; j < BATCH; ++j) {  // one load round: the histograms and (one thread per unit) the counts
-      const uint32_t u = lb + min(u0 + j * UPP, nu - 1);
-      w[j] = P.uhist[(uint64_t)u * (UHB / 4) + q];
-      ca[j] = q == 0 ? P.cntA[u] : 0u;
-      cc[j] = q == 0 ? P.cntC[u] : 0u;
-    }
-#pragma unroll
-    for (uint32_t j = 0; j < BATCH; ++j) {
-      if (u0 + j * UPP < nu) {
-        const uint32_t x = w[j];
-        r.b0 += x & 0xFFu;
-        r.b1 += (x >> 8) & 0xFFu;
-        r.b2 += (x >> 16) & 0xFFu;
-        r.b3 += x >> 24;
-        r.sat |= ((x & 0xFFu) == 0xFFu) | (((x >> 8) & 0xFFu) == 0xFFu) | (((x >> 16) & 0xFFu) == 0xFFu) |
-                 ((x >> 24) == 0xFFu);
-        r.sa += ca[j];
-        r.sc += cc[j];
-        r.ov += cc[j] > P.ccap ? 1u : 0u;
-      }
-    }
-  }
-  return r;
-}
-
-// segment_pick from the units' coarse band histograms (CHAIN_UNITHIST: k_scan wrote one per unit, so no k_ghist
-// pass precedes this one): the UHB bins summed over the segment's units (unit_sums), then the bin of the k-th key
-// among the band keys by one wave. The window is that coarse bin — about 1/64 of the band, ~8x what a fine
-// group-histogram bin held; k_select ranks it exactly. A saturated unit count (255) routes the segment to the
-// generic path, like a bracket miss.
-template <int NT = BLOCK>
-DEV uint4 pick_from_sums(const Params& P, UnitSums u, uint32_t nu, uint32_t k, const Band& band, uint32_t* hist,
-                         uint32_t* sh) {
-  const uint32_t t = threadIdx.x, lane = lane_id(), wv = t >> 6;
-  if (t < UHB) hist[t] = 0u;
-  // lanes q, q + 16, q + 32, q + 48 of a wave hold the same bins: reduce them, then one atomic per bin per wave
-#pragma unroll
-  for (int o = 16; o < 64; o <<= 1) {
-    u.b0 += (uint32_t)__shfl_xor((int)u.b0, o, 64);
-    u.b1 += (uint32_t)__shfl_xor((int)u.b1, o, 64);
-    u.b2 += (uint32_t)__shfl_xor((int)u.b2, o, 64);
-    u.b3 += (uint32_t)__shfl_xor((int)u.b3, o, 64);
-  }
-  const uint32_t sa = block_sum<NT>(u.sa, sh);  // barriers inside (also order the zeroed bins before the atomics)
-  if (lane < 16) {
-    atomicAdd(&hist[4 * lane + 0], u.b0);
-    atomicAdd(&hist[4 * lane + 1], u.b1);
-    atomicAdd(&hist[4 * lane + 2], u.b2);
-    atomicAdd(&hist[4 * lane + 3], u.b3);
-  }
-  const uint32_t sc = block_sum<NT>(u.sc, sh);
-  const uint32_t ov = block_sum<NT>(u.ov, sh);
-  const uint32_t sat = block_sum<NT>(u.sat, sh);
-  const bool generic = (P.flags & (COALAC_FLAG_FORCE_EXACT | COALAC_FLAG_GENERIC_SELECT)) || !(sa < k && k <= sc) ||
-                       nu > UCAP || ov != 0 || sat != 0;
-  if (generic) return make_uint4(0u, 0u, 0u, 1u);
-  // (the block_sum barriers ordered the bin atomics before this read)
-  if (wv == 0) {  // the r-th largest band key: bins from the top, one per lane
-    const uint32_t r = k - sa;
-    const uint32_t v = hist[UHB - 1 - lane];
-    const uint32_t inc = wave_incl_scan(v);
-    if (inc >= r && inc - v < r) {
-      sh[40] = UHB - 1 - lane;
-      sh[41] = r - (inc - v);
-    }
-    if (lane == 0 && (uint32_t)__shfl((int)inc, 63, 64) < r) sh[40] = NONE;
-  }
-  __syncthreads();
-  const uint32_t b = sh[40], rin = sh[41];
-  __syncthreads();
-  if (b == NONE) return make_uint4(0u, 0u, 0u, 1u);
-  return make_uint4(band.wlo(b), band.whi(b), rin, 0u);
-}
-
 // k_gwin: per group — per-unit counts of keys above the window (-> gtC), the group's in-window entries
 // in index order (-> glist, count -> gcnt), min/max of the values above the window (-> gmm)
 template <int NW = WAVES>
@@ -1595,8 +1481,8 @@ DEV void group_window(const Params& P, uint32_t gi, const uint4 G, const uint4 s
 template <int NT = BLOCK>
 DEV void group_pick_window(const Params& P, uint32_t gi, GwinSmemT<NT / 64>& W, uint32_t* hist, uint32_t* sh) {
   // round 1: the group and its segment's geometry (gseg: {first large unit, units, k, first group}, so nothing
-  // waits for a segment-table lookup); round 2: the band, the group's counts and (CHAIN_UNITHIST) the sums over
-  // the segment's units
+  // waits for a segment-table lookup); round 2: the band and the group's counts; segment_pick's round: the
+  // segment's group histograms and unit counts
   const uint4 G = P.groups[gi];
   const uint4 GS = P.gseg[gi];
   STAMP(P, G.x, 22);
@@ -1605,21 +1491,12 @@ DEV void group_pick_window(const Params& P, uint32_t gi, GwinSmemT<NT / 64>& W, 
   sd.unit_end = GS.y;
   sd.k = GS.z;
   sd.g_begin = GS.w;
-  const uint32_t tlo = P.tlo[G.y], thi = P.thi[G.y], hh = P.hhi[G.y];
+  const uint32_t tlo = P.tlo[G.y], thi = P.thi[G.y], hh = P.shhi[G.x];
   const uint32_t c = threadIdx.x < G.z ? min(P.cntC[G.y + threadIdx.x], P.ccap) : 0u;
-  uint4 st;
-  if (CHAIN_UNITHIST) {
-    const UnitSums us = unit_sums<NT>(P, GS.x, GS.y);
-    const uint32_t total = reg_prefix<NT>(c, G.z, W.upre, sh);
-    st = pick_from_sums<NT>(P, us, GS.y, GS.z, Band(tlo, thi, hh, 6), hist, sh);
-    STAMP(P, G.x, 23);
-    if (st.w == 0) group_window<NT>(P, gi, G, st, GS.x, total, W, sh);
-  } else {
-    const uint32_t total = reg_prefix<NT>(c, G.z, W.upre, sh);
-    st = segment_pick<NT>(P, sd, Band(tlo, thi, hh), hist, sh);
-    STAMP(P, G.x, 23);
-    if (st.w == 0) group_window<NT>(P, gi, G, st, GS.x, total, W, sh);
-  }
+  const uint32_t total = reg_prefix<NT>(c, G.z, W.upre, sh);
+  const uint4 st = segment_pick<NT>(P, sd, Band(tlo, thi, hh), hist, sh);
+  STAMP(P, G.x, 23);
+  if (st.w == 0) group_window<NT>(P, gi, G, st, GS.x, total, W, sh);
   if (threadIdx.x == 0 && G.y == GS.x) {  // the segment's first group
     uint2* ss = reinterpret_cast<uint2*>(P.sstate + G.x);
     pst(P, ss, make_uint2(st.x, st.y));
@@ -1746,7 +1623,7 @@ DEV bool select_from_groups(const Params& P, const SegDev& sd, uint32_t lb, uint
   // one load round: the groups' list lengths, min / max above the window, the first per-unit counts, and —
   // speculatively, before their lengths are known — the first SPEC slots of every group's in-window list (the
   // typical window share of a group fits; a longer list's remainder is loaded after the scan)
-  constexpr uint32_t SPEC = 64, SPT = (UCAP / GU) * SPEC / NT;
+  constexpr uint32_t SPEC = SELECT_SPEC, SPT = (UCAP / GU) * SPEC / NT;
   static_assert((UCAP / GU) * SPEC % NT == 0, "speculative gather geometry");
   uint2 sv[SPT];
 #pragma unroll
@@ -2606,6 +2483,24 @@ __global__ __launch_bounds__(BLOCK, AGG_WPE) void k_aggregate(Params P, AggArgs 
   }
 }
 
+// k_gather: n scalars of `bytes` each, from their own storage (one device pointer each), into one contiguous
+// buffer — an update's passthrough entries (BatchNorm's int64 num_batches_tracked, one per layer) snapshotted
+// in one launch instead of a stack of tensor copies
+__global__ __launch_bounds__(BLOCK) void k_gather(const void* const* src, uint32_t n, uint32_t bytes, void* dst) {
+  const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
+  if (i >= n) return;
+  const void* s = src[i];
+  uint8_t* d = static_cast<uint8_t*>(dst) + (uint64_t)i * bytes;
+  if (bytes == 8)
+    *reinterpret_cast<uint64_t*>(d) = *static_cast<const uint64_t*>(s);
+  else if (bytes == 4)
+    *reinterpret_cast<uint32_t*>(d) = *static_cast<const uint32_t*>(s);
+  else if (bytes == 2)
+    *reinterpret_cast<uint16_t*>(d) = *static_cast<const uint16_t*>(s);
+  else
+    *d = *static_cast<const uint8_t*>(s);
+}
+
 // ------------------------------------------------------------------------------------------------
 // host side
 // ------------------------------------------------------------------------------------------------
@@ -2632,7 +2527,7 @@ size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 struct WsLayout {
   size_t status;
   size_t tstar, rtie;
-  size_t tlo, thi, hhi, uhist, cntA, cntC, gtC, eqC, eqpre, outoff;
+  size_t tlo, thi, cntA, cntC, gtC, eqC, eqpre, outoff;
   size_t cval, cpos, stamps, ghist, gcnt, glist, gmm, sstate, shhi;
   size_t total;
 };
@@ -2650,8 +2545,6 @@ WsLayout ws_layout(size_t S, size_t LU, size_t NG, size_t NL, uint32_t CC) {
   L.rtie = take(4 * S);
   L.tlo = take(4 * LU);
   L.thi = take(4 * LU);
-  L.hhi = take(4 * LU);
-  L.uhist = take(CHAIN_UNITHIST ? UHB * LU : 0);
   L.cntA = take(4 * LU);
   L.cntC = take(4 * LU);
   L.gtC = take(4 * LU);
@@ -2661,7 +2554,7 @@ WsLayout ws_layout(size_t S, size_t LU, size_t NG, size_t NL, uint32_t CC) {
   L.cval = take(4 * (size_t)CC * LU);
   L.cpos = take(2 * (size_t)CC * LU);
   L.stamps = take(8 * NSTAMP * std::max<size_t>(S, 1));
-  L.ghist = take(CHAIN_UNITHIST ? 0 : 4 * HB2 * NG);
+  L.ghist = take(4 * HB2 * NG);
   L.gcnt = take(4 * NG);
   L.glist = take(sizeof(uint2) * GCAP * NG);
   L.gmm = take(8 * NG);
@@ -2838,9 +2731,7 @@ int launch_encode(const Params& P, coalac_plan_t plan, hipStream_t st, const coa
   }
   ENC_BOUNDARY(2);
   if ((stages & COALAC_STAGE_SELECT) && plan->n_large) {
-    if (CHAIN_UNITHIST)
-      ;  // (the band histograms came with k_scan)
-    else if (plan->n_lunits <= LATENCY_PLAN_UNITS)
+    if (plan->n_lunits <= LATENCY_PLAN_UNITS)
       hipLaunchKernelGGL(k_ghist<GHIST_NT_LAT>, dim3(plan->n_groups), dim3(GHIST_NT_LAT), 0, st, P);
     else
       hipLaunchKernelGGL(k_ghist<BLOCK>, dim3(plan->n_groups), dim3(BLOCK), 0, st, P);
@@ -3098,8 +2989,6 @@ int encode_impl(coalac_plan_t plan, const float* d_in, const float* const* d_inp
   P.status = reinterpret_cast<uint32_t*>(w + L.status);
   P.tlo = reinterpret_cast<uint32_t*>(w + L.tlo);
   P.thi = reinterpret_cast<uint32_t*>(w + L.thi);
-  P.hhi = reinterpret_cast<uint32_t*>(w + L.hhi);
-  P.uhist = reinterpret_cast<uint32_t*>(w + L.uhist);
   P.cntA = reinterpret_cast<uint32_t*>(w + L.cntA);
   P.cntC = reinterpret_cast<uint32_t*>(w + L.cntC);
   P.gtC = reinterpret_cast<uint32_t*>(w + L.gtC);
@@ -3378,6 +3267,19 @@ int coalac_aggregate(coalac_plan_t plan, int clients, const int32_t* d_idx, cons
                      void* stream) {
   return coalac_aggregate_ev(plan, clients, d_idx, d_vals, d_mn, d_scale, d_ustart, d_weights, total, mode, d_avg_mask,
                              d_base, d_out, d_ws, ws_bytes, stream, nullptr);
+}
+
+int coalac_gather(const void* const* d_src, int n, int elem_bytes, void* d_out, void* stream) {
+  if (n < 0 || (n > 0 && (!d_src || !d_out))) return fail(COALAC_EINVAL, "coalac_gather: bad arguments");
+  if (elem_bytes != 1 && elem_bytes != 2 && elem_bytes != 4 && elem_bytes != 8)
+    return fail(COALAC_EINVAL, "coalac_gather: element size %d (1, 2, 4 or 8)", elem_bytes);
+  if (reinterpret_cast<uintptr_t>(d_out) % (uintptr_t)elem_bytes)
+    return fail(COALAC_EINVAL, "coalac_gather: output not aligned to the element size");
+  if (n == 0) return COALAC_OK;
+  hipLaunchKernelGGL(k_gather, dim3((n + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, static_cast<hipStream_t>(stream), d_src,
+                     (uint32_t)n, (uint32_t)elem_bytes, d_out);
+  HIP_CHECK(hipGetLastError());
+  return COALAC_OK;
 }
 
 int coalac_workspace_fallbacks(coalac_plan_t plan, const void* d_ws, void* stream, int* out) {

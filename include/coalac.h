@@ -214,6 +214,12 @@ int coalac_aggregate_ev(coalac_plan_t plan, int clients, const int32_t* d_idx, c
                         float total, int mode, const uint8_t* d_avg_mask, const float* d_base, float* d_out,
                         void* d_ws, uint64_t ws_bytes, void* stream, void* const* events);
 
+/* Snapshot n scalars of elem_bytes (1, 2, 4 or 8) each, read through the DEVICE pointer array d_src (each pointer
+ * aligned to elem_bytes), into the contiguous d_out, in one launch on `stream`: the passthrough entries of an
+ * update — BatchNorm's int64 num_batches_tracked, one per layer — that the carrier takes with the encoded tensors
+ * (client compression(), coala/client/base.py:330-332; they travel raw, CodecSpec v1). */
+int coalac_gather(const void* const* d_src, int n, int elem_bytes, void* d_out, void* stream);
+
 /* Diagnostics: number of segments whose sampled thresholds were rejected and re-selected exactly in
  * the last encode that used workspace d_ws (synchronises `stream`). */
 int coalac_workspace_fallbacks(coalac_plan_t plan, const void* d_ws, void* stream, int* out);

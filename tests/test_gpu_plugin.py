@@ -108,3 +108,36 @@ def test_encode_in_place_from_parameters_equals_flat_encode(cuda, mode):
     torch.cuda.synchronize()
     for f in ("idx", "vals", "mn", "scale"):
         assert torch.equal(getattr(up2.encoded, f), getattr(ref, f)), f
+
+
+def test_encode_module_snapshots_counters_in_one_launch(cuda):
+    """compression() through encode_module: the passthrough int64 counters are snapshotted by coalac_gather (one
+    launch over a cached pointer array) — the same values as state_dict(), taken at encode time (a later change
+    of the live counters does not reach the carrier), and the fp32 payload equals encode(state_dict())."""
+    from coala_amd.compression import UpdateCodec
+    from coala_amd.compression.codec import HipBackend
+    m = build_module("resnet50_tv", seed=5, device="cuda")
+    with torch.no_grad():
+        for i, (k, v) in enumerate((k, v) for k, v in m.state_dict().items() if v.dtype == torch.int64):
+            v.fill_(1000 + i)
+    codec = UpdateCodec(0.01, 8, "weights")
+    up = codec.encode_module(m)
+    ref = codec.encode(m.state_dict())
+    torch.cuda.synchronize()
+    raw_names = [k for k, v in m.state_dict().items() if v.dtype == torch.int64]
+    assert len(raw_names) == 53
+    for k in raw_names:
+        assert up.raw[k].item() == m.state_dict()[k].item() == ref.raw[k].item()
+    for f in ("idx", "vals", "mn", "scale", "ustart"):
+        assert torch.equal(getattr(up.encoded, f), getattr(ref.encoded, f)), f
+    before = {k: up.raw[k].item() for k in raw_names}
+    with torch.no_grad():
+        for k in raw_names:
+            m.state_dict()[k].add_(7)
+    torch.cuda.synchronize()
+    assert {k: up.raw[k].item() for k in raw_names} == before
+    # the gather itself, against torch.stack, on scalars of every element size
+    for dt in (torch.int64, torch.int32, torch.int16, torch.uint8):
+        ts = [torch.tensor(i * 3 + 1, dtype=dt, device="cuda") for i in range(300)]
+        got = HipBackend().gather_scalars(ts)
+        assert got is not None and torch.equal(got, torch.stack(ts)), dt
