@@ -494,6 +494,28 @@ def rank_spread(rank_el, steps):
     return {"min": round(min(ms), 4), "max": round(max(ms), 4), "per_rank": [round(m, 4) for m in ms]}
 
 
+def box_probe(torch, dev):
+    """This box's device-to-device copy rate (read + write bytes / time, torch's copy kernel on 1 GiB): a
+    per-box yardstick beside the headline, since MI355X boxes of this pool differ by a few percent in
+    streaming bandwidth (the headline's box-to-box spread tracks it). Taken after every timed region."""
+    n = 1 << 28
+    src = torch.empty(n, dtype=torch.float32, device=dev).fill_(1.0)
+    dst = torch.empty_like(src)
+    for _ in range(3):
+        dst.copy_(src)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    reps = 20
+    torch.cuda.synchronize(dev)
+    e0.record()
+    for _ in range(reps):
+        dst.copy_(src)
+    e1.record()
+    torch.cuda.synchronize(dev)
+    ms = e0.elapsed_time(e1) / reps
+    del src, dst
+    return {"copy_GBps": round(2 * 4 * n / (ms * 1e-3) / 1e9, 1), "gpu": torch.cuda.get_device_name(dev)}
+
+
 def release_workload(W):
     import torch
     for p, _ in W["slots"]:
@@ -522,14 +544,18 @@ def run_plugin(a, dev, steps):
     def per_call(fn, n):
         """Median and mean of n calls, each synchronised: the hooks return host objects, and about one call
         in twenty pays a Python garbage collection (tens of ms) that a mean would fold in."""
-        ts = []
+        ts, hs = [], []
         for _ in range(n):
             t0 = time.perf_counter()
             fn()
+            hs.append((time.perf_counter() - t0) * 1e3)  # until the call returns: its host-side cost
             torch.cuda.synchronize()
             ts.append((time.perf_counter() - t0) * 1e3)
         ts.sort()
+        hs.sort()
+        host[0] = round(hs[len(hs) // 2], 4)
         return ts[len(ts) // 2], sum(ts) / len(ts)
+    host = [None]
     for name, fn in (("in_place", lambda: codec.encode_module(m, base=base)),
                      ("flattened", lambda: codec.plan_for(
                          [e["n"] for e in base.entries if e["kind"] == "seg"], dev).encode(
@@ -540,11 +566,13 @@ def run_plugin(a, dev, steps):
         med, mean = per_call(fn, max(steps, 20))
         res[f"compression_{name}_ms"] = round(med, 4)
         res[f"compression_{name}_mean_ms"] = round(mean, 4)
+        res[f"compression_{name}_host_ms"] = host[0]
     up = codec.encode_module(m, base=base)
     for _ in range(3):
         codec.decode_module(up, g, base=base)
     torch.cuda.synchronize()
     dec_ms, dec_mean = per_call(lambda: codec.decode_module(up, g, base=base), max(steps, 20))
+    res["decompression_host_ms"] = host[0]
     N = sum(e["n"] for e in base.entries if e["kind"] == "seg")
     K, T = up.header["total_k"], up.header["n_segments"]
     alg = 16 * N + 10 * K + 16 * T
@@ -566,7 +594,8 @@ def run_plugin(a, dev, steps):
                              "desc": "compression() + 1/C of the server's fused aggregate() of C uploads "
                                      "(UpdateCodec.aggregate: decode + FedAvg in one kernel, new module built once "
                                      "per round); decompression(model) passes the carrier through"},
-            "timing": "median of per-call times (each call synchronised); means alongside",
+            "timing": "median of per-call times (each call synchronised); means alongside; *_host_ms: median "
+                      "time until the call returns (no wait inside it: its host-side cost)",
             "alg_bytes_per_client": alg,
             "step_roofline": {"achieved_GBs": round(alg / (ms * 1e-3) / 1e9, 1),
                               "frac": round(alg / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)},
@@ -700,6 +729,7 @@ def main():
         results[cfg] = time_workload(W, a, dev, world)
         release_workload(W)
     head = results.pop(a.config)
+    box = box_probe(torch, dev) if rank == 0 else None
 
     if rank == 0:
         d = head["desc"]
@@ -721,6 +751,7 @@ def main():
                                               "graph", "fill_ahead", "sample_fallbacks", "rank_ms_per_step")}
                         for k, v in results.items()},
         }
+        res["box"] = box
         if plugin is not None:
             res["configs"]["plugin"] = plugin
         if cpu is not None:

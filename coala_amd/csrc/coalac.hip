@@ -88,6 +88,9 @@ constexpr int SEL_NT_LAT = 512;           // ... in latency-bound plans, where n
 #ifndef SCAN_WPE
 #define SCAN_WPE 5
 #endif
+#ifndef SCAN_NT
+#define SCAN_NT 256  // batch plans' k_scan block size (launch bounds: SCAN_WPE waves per SIMD)
+#endif
 #ifndef SCAN_NB
 #define SCAN_NB 1  // load batches per k_scan unit (weights mode): 1 = all 16 float4 per lane in flight
 #endif
@@ -112,6 +115,9 @@ constexpr int SEL_NT_LAT = 512;           // ... in latency-bound plans, where n
 #define SCAN_NB_LAT 2   // ... and load batches per unit
 #endif
 #ifndef SAMPLE_PICK2
+#ifndef SAMPLE_NT_LAT
+#define SAMPLE_NT_LAT 256  // latency-bound plans' k_sample block size (1024 threads, 2 load batches each: 0.7 us slower)
+#endif
 #define SAMPLE_PICK2 1  // k_sample: both bracket bins from one block scan of the histogram
 #endif
 #ifndef RANK_SELECT
@@ -940,10 +946,10 @@ __global__ __launch_bounds__(BLOCK) void k_small(Params P) {
 // ------------------------------------------------------------------------------------------------
 // k_sample: per large segment, sampled thresholds [T_lo, T_hi] for every unit of the segment
 // ------------------------------------------------------------------------------------------------
-template <bool DELTA>
+template <bool DELTA, int NT = BLOCK>
 DEV void sample_segment(const Params& P, uint32_t li, uint32_t* hist, uint32_t* sh) {
-  constexpr int NT = BLOCK;
-  constexpr uint32_t MAXIT = SAMPLE_MAX / 16 / 64;  // run batches per block (64 runs of 16 per batch)
+  constexpr uint32_t RPI = NT / 4;                   // runs per load batch (4 threads per 16-element run)
+  constexpr uint32_t MAXIT = SAMPLE_MAX / 16 / RPI;  // load batches per thread
   const uint32_t t = threadIdx.x;
   STAMP(P, li, 16);  // (slots 16-19: k_sample, 20-21: k_ghist, 22-24: k_gwin of the segment's last group block)
   const uint32_t s = P.large_list[li];
@@ -956,15 +962,17 @@ DEV void sample_segment(const Params& P, uint32_t li, uint32_t* hist, uint32_t* 
   R = R < 64 ? 64 : (R > SAMPLE_MAX / 16 ? SAMPLE_MAX / 16 : R);
   R &= ~63u;
   const uint32_t m = R * 16;
-  const uint32_t nit = R / 64;
   const uint32_t stride = n / R;  // >= 16 because n > small_max >= 1024
   const uint32_t room = stride - 16;
   // The sampled keys stay in registers (4 per batch per thread): all loads in flight at once, and with
   // 8 KB of LDS per block (histogram only) twice as many sample blocks fit a CU as with an LDS key copy.
   uint32_t kk[MAXIT][4];
+  uint32_t okm = 0;  // bit it: this thread's batch-it run exists (R is a multiple of 64, not of RPI)
 #pragma unroll
   for (uint32_t it = 0; it < MAXIT; ++it) {
-    const uint32_t run = min(it, nit - 1) * 64 + (t >> 2), q = t & 3;
+    const uint32_t r0 = it * RPI + (t >> 2), q = t & 3;
+    okm |= (uint32_t)(r0 < R) << it;
+    const uint32_t run = r0 < R ? r0 : R - 1;
     uint32_t start = run * stride + hash32(run * 0x9E3779B9u ^ (s + 1u) * 0x85EBCA6Bu) % (room + 1u);
     start &= ~3u;
     const float4 v = load_x4p<DELTA>(xs + start + q * 4, bs + start + q * 4);
@@ -989,7 +997,7 @@ DEV void sample_segment(const Params& P, uint32_t li, uint32_t* hist, uint32_t* 
   uint32_t kmn = KEY_MAX, kmx = 0;
 #pragma unroll
   for (uint32_t it = 0; it < MAXIT; ++it) {
-    if (it < nit) {
+    if ((okm >> it) & 1u) {
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         kmn = min(kmn, kk[it][j]);
@@ -1009,7 +1017,7 @@ DEV void sample_segment(const Params& P, uint32_t li, uint32_t* hist, uint32_t* 
   const int shift = band_shift(kmin, kmax);
 #pragma unroll
   for (uint32_t it = 0; it < MAXIT; ++it) {
-    if (it < nit) {
+    if ((okm >> it) & 1u) {
 #pragma unroll
       for (int j = 0; j < 4; ++j) atomicAdd(&hist[(kk[it][j] - kmin) >> shift], 1u);
     }
@@ -1045,11 +1053,11 @@ DEV void sample_segment(const Params& P, uint32_t li, uint32_t* hist, uint32_t* 
   STAMP(P, li, 19);
 }
 
-template <bool DELTA, bool RAW>
-__global__ __launch_bounds__(BLOCK) void k_sample(Params P) {
+template <bool DELTA, bool RAW, int NT>
+__global__ __launch_bounds__(NT) void k_sample(Params P) {
   __shared__ uint32_t hist[HIST_BINS];
   __shared__ uint32_t sh[64];
-  sample_segment<DELTA>(P, blockIdx.x, hist, sh);
+  sample_segment<DELTA, NT>(P, blockIdx.x, hist, sh);
 }
 
 // k_presel: the samplers (blocks [0, n_large)) and the small segments (blocks after them) as one launch —
@@ -1071,12 +1079,14 @@ __global__ __launch_bounds__(BLOCK) void k_presel(Params P) {
 // small segments — no longer launched: k_presel runs them beside the samplers.)
 // (WPE / NB: launch-bound blocks per CU and load batches; the latency-bound plans' instantiation, the one
 // WITH_SMALL, takes its own — nothing streams beside it)
-template <bool DELTA, bool RAW, bool WITH_SMALL, int WPE = SCAN_WPE, int NB = SCAN_NB>
-__global__ __launch_bounds__(BLOCK, WPE) void k_scan(Params P) {
-  // one LDS arena: candidate staging (WAVES x STAGE_CAP records) or a small segment's values + histogram
+template <bool DELTA, bool RAW, bool WITH_SMALL, int WPE = SCAN_WPE, int NB = SCAN_NB, int NTS = BLOCK>
+__global__ __launch_bounds__(NTS, WPE) void k_scan(Params P) {
+  // one LDS arena: candidate staging (NTS / 64 x STAGE_CAP records) or a small segment's values + histogram
   // (WITH_SMALL only: without it the block needs 16 KB of LDS instead of 24.8 KB)
+  static_assert(!WITH_SMALL || NTS == BLOCK, "small segments take 256-thread blocks");
+  constexpr uint32_t NWS = NTS / 64;
   constexpr size_t SMALL_BYTES = WITH_SMALL ? (SMALL_MAX + HIST_BINS + 64) * 4 : 0;
-  constexpr size_t STAGE_BYTES = WAVES * STAGE_CAP * sizeof(uint2);
+  constexpr size_t STAGE_BYTES = NWS * STAGE_CAP * sizeof(uint2);
   __shared__ __attribute__((aligned(16))) uint8_t arena[SMALL_BYTES > STAGE_BYTES ? SMALL_BYTES : STAGE_BYTES];
   if (WITH_SMALL && blockIdx.x < P.scan_small) {
     float* vals = reinterpret_cast<float*>(arena);
@@ -1086,7 +1096,7 @@ __global__ __launch_bounds__(BLOCK, WPE) void k_scan(Params P) {
   }
   uint2* stage = reinterpret_cast<uint2*>(arena);
   const uint32_t wv = threadIdx.x >> 6;
-  const uint32_t lu = ((SCAN_XCD && !WITH_SMALL ? xcd_block(blockIdx.x) : blockIdx.x) - P.scan_small) * WAVES + wv;
+  const uint32_t lu = ((SCAN_XCD && !WITH_SMALL ? xcd_block(blockIdx.x) : blockIdx.x) - P.scan_small) * NWS + wv;
   if (lu >= P.n_lunits) return;
   const UnitDev L = P.lunits[lu];
   // delta: 4 load batches (32 float4 in flight spill)
@@ -1186,7 +1196,8 @@ DEV void unit_sweep(const uint32_t* cand, uint32_t stride, uint32_t lu0, const u
 // must stay <= 32 KB so five streaming blocks still fit a CU): 28.3 KB
 constexpr uint32_t WLIST = 1024;  // in-window entries the fast path can hold
 #ifndef SELECT_SPEC
-#define SELECT_SPEC 16u  // k_select: speculatively gathered slots per group window list (a window holds ~4 per group)
+#define SELECT_SPEC 64u  // k_select: speculatively gathered slots per group window list (one update: 64 -> 0.0811 ms per
+                         // step, 16 -> 0.0830, 8 -> 0.0838: longer lists otherwise cost a dependent round)
 #endif
 constexpr int SEL_HB = 1024;      // bins of the select's radix histograms
 struct SelSmem {
@@ -2254,6 +2265,9 @@ __global__ __launch_bounds__(BLOCK) void k_bounds(Params P, const BChunk* chunks
 #ifndef AGG_SPLIT
 #define AGG_SPLIT 2u  // waves per 4096-element unit in k_aggregate (each owns UNIT_IT / AGG_SPLIT rows)
 #endif
+#ifndef AGG_PAIR
+#define AGG_PAIR 0  // k_aggregate: clients two at a time through two LDS tiles (one dependent LDS round trip per pair)
+#endif
 #ifndef AGG_DEPTH
 #define AGG_DEPTH 16u  // clients whose entries k_aggregate loads together (16 ResNet-50 clients: 4 -> 73.5 us, 8 -> 70.9 us, 16 -> 69.1 us)
 #endif
@@ -2321,7 +2335,8 @@ __global__ __launch_bounds__(BLOCK, AGG_WPE) void k_aggregate(Params P, AggArgs 
   // AGG_SPLIT waves per unit, each owning RI of its UNIT_IT rows: a smaller LDS tile and half the registers
   // per wave, so twice the waves are resident
   constexpr uint32_t RI = UNIT_IT / AGG_SPLIT, HE = UNIT / AGG_SPLIT;  // rows / elements per wave
-  __shared__ float4 tiles[WAVES][HE / 4];
+  static_assert(!AGG_PAIR || AGG_DEPTH % 2 == 0, "pairs of prefetched clients");
+  __shared__ float4 tiles[WAVES][AGG_PAIR ? 2 : 1][HE / 4];
   const uint32_t lane = lane_id(), wv = threadIdx.x >> 6;
   const uint32_t wid = blockIdx.x * WAVES + wv;
   const uint32_t u = wid / AGG_SPLIT, h = wid % AGG_SPLIT;
@@ -2333,8 +2348,10 @@ __global__ __launch_bounds__(BLOCK, AGG_WPE) void k_aggregate(Params P, AggArgs 
   const uint32_t e_lo = h * HE;  // first element (within the unit) of this wave's rows
   if (e_lo >= len) return;
   const uint32_t hlen = min(len - e_lo, HE);
-  float4* tile = tiles[wv];
+  float4* tile = tiles[wv][0];
   float* tf = reinterpret_cast<float*>(tile);
+  float4* tile2 = tiles[wv][AGG_PAIR ? 1 : 0];
+  float* tf2 = reinterpret_cast<float*>(tile2);
   float4 b[RI], acc[RI];
   const float* bs = HASBASE ? P.base + U.off + e_lo : nullptr;
   auto load_base = [&]() {
@@ -2354,6 +2371,10 @@ __global__ __launch_bounds__(BLOCK, AGG_WPE) void k_aggregate(Params P, AggArgs 
   auto tile_zero = [&]() {
 #pragma unroll
     for (uint32_t it = 0; it < RI; ++it) tile[it * 64 + lane] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    if (AGG_PAIR) {
+#pragma unroll
+      for (uint32_t it = 0; it < RI; ++it) tile2[it * 64 + lane] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    }
   };
   if (HASBASE) load_base();
   tile_zero();
@@ -2384,13 +2405,13 @@ __global__ __launch_bounds__(BLOCK, AGG_WPE) void k_aggregate(Params P, AggArgs 
     // x = base + d; acc = x * w (first client) or acc + x * w: IEEE fp32 ops in this order, on float2 pairs
     // (v_pk_add_f32 / v_pk_mul_f32: half the VALU issue of scalar fp32); the first-client test is
     // wave-uniform (a branch, no per-element select)
-    auto accumulate = [&](uint32_t j) {
+    auto accumulate = [&](uint32_t j, const float4* T) {
       const float w = __uint_as_float(__builtin_amdgcn_readlane(__float_as_uint(m_w), j));
       const f2v w2 = {w, w};
       if (c0 + j == 0) {
 #pragma unroll
         for (uint32_t it = 0; it < RI; ++it) {
-          const float4 d = tile[it * 64 + lane];
+          const float4 d = T[it * 64 + lane];
           const f2v dl = {d.x, d.y}, dh = {d.z, d.w};
           const f2v bl = {b[it].x, b[it].y}, bh = {b[it].z, b[it].w};
           const f2v tl = (HASBASE ? bl + dl : dl) * w2, th = (HASBASE ? bh + dh : dh) * w2;
@@ -2399,7 +2420,7 @@ __global__ __launch_bounds__(BLOCK, AGG_WPE) void k_aggregate(Params P, AggArgs 
       } else {
 #pragma unroll
         for (uint32_t it = 0; it < RI; ++it) {
-          const float4 d = tile[it * 64 + lane];
+          const float4 d = T[it * 64 + lane];
           const f2v dl = {d.x, d.y}, dh = {d.z, d.w};
           const f2v bl = {b[it].x, b[it].y}, bh = {b[it].z, b[it].w};
           const f2v al = {acc[it].x, acc[it].y}, ah = {acc[it].z, acc[it].w};
@@ -2417,9 +2438,29 @@ __global__ __launch_bounds__(BLOCK, AGG_WPE) void k_aggregate(Params P, AggArgs 
       const bool mine = lane < ne && pos < hlen;
       if (mine) tf[pos] = code_value<RAW>(q, mn, sc);
       lds_order();
-      accumulate(j);
+      accumulate(j, tile);
       lds_order();
       if (mine) tf[pos] = 0.0f;
+      lds_order();
+    };
+    // clients j and j + 1 (both with <= 64 kept entries): both scattered, both read back, accumulated in order
+    auto process2 = [&](uint32_t j, uint32_t idx, uint32_t q, uint32_t idx2, uint32_t q2) {
+      const uint32_t pos = idx - U.start - e_lo, pos2 = idx2 - U.start - e_lo;
+      const uint32_t ne = __builtin_amdgcn_readlane(m_hi, j) - __builtin_amdgcn_readlane(m_lo, j);
+      const uint32_t ne2 = __builtin_amdgcn_readlane(m_hi, j + 1) - __builtin_amdgcn_readlane(m_lo, j + 1);
+      const float mn = __uint_as_float(__builtin_amdgcn_readlane(__float_as_uint(m_mn), j));
+      const float sc = __uint_as_float(__builtin_amdgcn_readlane(__float_as_uint(m_sc), j));
+      const float mn2 = __uint_as_float(__builtin_amdgcn_readlane(__float_as_uint(m_mn), j + 1));
+      const float sc2 = __uint_as_float(__builtin_amdgcn_readlane(__float_as_uint(m_sc), j + 1));
+      const bool mine = lane < ne && pos < hlen, mine2 = lane < ne2 && pos2 < hlen;
+      if (mine) tf[pos] = code_value<RAW>(q, mn, sc);
+      if (mine2) tf2[pos2] = code_value<RAW>(q2, mn2, sc2);
+      lds_order();
+      accumulate(j, tile);
+      accumulate(j + 1, tile2);
+      lds_order();
+      if (mine) tf[pos] = 0.0f;
+      if (mine2) tf2[pos2] = 0.0f;
       lds_order();
     };
     // any client with more than 64 kept entries in this unit (ratio >~ 1.5 %): every client in turn, its
@@ -2436,7 +2477,7 @@ __global__ __launch_bounds__(BLOCK, AGG_WPE) void k_aggregate(Params P, AggArgs 
         if (p2 < hlen) tf[p2] = v2;
       }
       lds_order();
-      accumulate(j);
+      accumulate(j, tile);
       lds_order();
       tile_zero();
       lds_order();
@@ -2452,9 +2493,19 @@ __global__ __launch_bounds__(BLOCK, AGG_WPE) void k_aggregate(Params P, AggArgs 
       uint32_t pa[AGG_DEPTH], qa[AGG_DEPTH];
 #pragma unroll
       for (uint32_t t = 0; t < AGG_DEPTH; ++t) fetch(j0 + t, pa[t], qa[t]);
+      if (AGG_PAIR) {
 #pragma unroll
-      for (uint32_t t = 0; t < AGG_DEPTH; ++t)
-        if (j0 + t < cn) process(j0 + t, pa[t], qa[t]);
+        for (uint32_t t = 0; t < AGG_DEPTH; t += 2) {
+          if (j0 + t + 1 < cn)
+            process2(j0 + t, pa[t], qa[t], pa[t + 1], qa[t + 1]);
+          else if (j0 + t < cn)
+            process(j0 + t, pa[t], qa[t]);
+        }
+      } else {
+#pragma unroll
+        for (uint32_t t = 0; t < AGG_DEPTH; ++t)
+          if (j0 + t < cn) process(j0 + t, pa[t], qa[t]);
+      }
     }
   }
   float* out = P.out + U.off + e_lo;
@@ -2717,8 +2768,10 @@ int launch_encode(const Params& P, coalac_plan_t plan, hipStream_t st, const coa
   }
   if (presel && !small_in_scan)
     hipLaunchKernelGGL((k_presel<DELTA, RAW>), dim3(plan->n_large + plan->n_small), dim3(BLOCK), 0, st, P);
+  else if ((stages & COALAC_STAGE_SAMPLE) && plan->n_large && plan->n_lunits <= LATENCY_PLAN_UNITS)
+    hipLaunchKernelGGL((k_sample<DELTA, RAW, SAMPLE_NT_LAT>), dim3(plan->n_large), dim3(SAMPLE_NT_LAT), 0, st, P);
   else if ((stages & COALAC_STAGE_SAMPLE) && plan->n_large)
-    hipLaunchKernelGGL((k_sample<DELTA, RAW>), dim3(plan->n_large), dim3(BLOCK), 0, st, P);
+    hipLaunchKernelGGL((k_sample<DELTA, RAW, BLOCK>), dim3(plan->n_large), dim3(BLOCK), 0, st, P);
   if ((stages & COALAC_STAGE_SMALL) && plan->n_small && !presel && !fork)
     hipLaunchKernelGGL((k_small<DELTA, RAW>), dim3(plan->n_small), dim3(BLOCK), 0, st, P);
   ENC_BOUNDARY(1);
@@ -2727,7 +2780,8 @@ int launch_encode(const Params& P, coalac_plan_t plan, hipStream_t st, const coa
     hipLaunchKernelGGL((k_scan<DELTA, RAW, true, SCAN_WPE_LAT, SCAN_NB_LAT>), dim3(gu + plan->n_small),
                        dim3(BLOCK), 0, st, Q);
   } else if ((stages & COALAC_STAGE_SCAN) && gu) {
-    hipLaunchKernelGGL((k_scan<DELTA, RAW, false>), dim3(gu), dim3(BLOCK), 0, st, Q);
+    hipLaunchKernelGGL((k_scan<DELTA, RAW, false, SCAN_WPE, SCAN_NB, SCAN_NT>),
+                       dim3((plan->n_lunits + SCAN_NT / 64 - 1) / (SCAN_NT / 64)), dim3(SCAN_NT), 0, st, Q);
   }
   ENC_BOUNDARY(2);
   if ((stages & COALAC_STAGE_SELECT) && plan->n_large) {

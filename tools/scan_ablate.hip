@@ -28,15 +28,16 @@ __device__ __forceinline__ uint32_t mbcnt(uint64_t m) {
   return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
 }
 
-template <int V>
-__global__ __launch_bounds__(256) void scan(const float* __restrict__ in, const Meta* meta, uint32_t nunits,
-                                            uint32_t tlo0, uint32_t thi0, int32_t* aI, float* aV, int32_t* bI,
-                                            float* bV, uint32_t* cnt) {
-  __shared__ int32_t stI[4][512];
-  __shared__ float stV[4][512];
-  __shared__ uint2 stR[V >= 8 ? 4 : 1][V >= 8 ? 512 : 1];
+template <int V, int NT = 256>
+__global__ __launch_bounds__(NT) void scan(const float* __restrict__ in, const Meta* meta, uint32_t nunits,
+                                           uint32_t tlo0, uint32_t thi0, int32_t* aI, float* aV, int32_t* bI,
+                                           float* bV, uint32_t* cnt) {
+  constexpr int NW = NT / 64;
+  __shared__ int32_t stI[V == 5 ? NW : 1][512];
+  __shared__ float stV[V == 5 ? NW : 1][512];
+  __shared__ uint2 stR[V >= 8 ? NW : 1][V >= 8 ? 512 : 1];
   const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const uint32_t u = blockIdx.x * 4 + wv;
+  const uint32_t u = blockIdx.x * NW + wv;
   if (u >= nunits) return;
   uint64_t off = (uint64_t)u * UNIT;
   uint32_t tlo = tlo0, thi = thi0;
@@ -461,5 +462,13 @@ int main() {
     run("15_half_pipeline_per" #PER "_sc" #SC "_occ" #OCC, [&] { hipLaunchKernelGGL((scan_h<PER, SC, OCC>), dim3(gp), dim3(256), 0, 0, in, nunits, tlo, thi, aI, cnt); }); }
   RUNH(1, 512, 5) RUNH(2, 256, 5) RUNH(2, 256, 6) RUNH(4, 256, 4) RUNH(4, 128, 5) RUNH(8, 128, 4)
   RUN(9, "9_combined_lds_staged_nt_again");
+  // block size: a block's slots free only when its slowest wave ends (16: one wave per block)
+#define RUNB(V, NT, name) run(name, [&] { hipLaunchKernelGGL((scan<V, NT>), dim3((nunits + NT / 64 - 1) / (NT / 64)), dim3(NT), 0, 0, in, meta, nunits, tlo, thi, aI, aV, bI, bV, cnt); })
+  RUNB(0, 64, "16_load_only_nt64");
+  RUNB(0, 128, "16_load_only_nt128");
+  RUNB(0, 512, "16_load_only_nt512");
+  RUNB(9, 64, "16_staged_nt_nt64");
+  RUNB(9, 128, "16_staged_nt_nt128");
+  RUNB(9, 256, "16_staged_nt_nt256");
   return 0;
 }
