@@ -19,8 +19,8 @@ import sys
 import threading
 from collections import OrderedDict
 from collections.abc import Mapping
-from itertools import repeat
-from operator import attrgetter, is_
+from itertools import chain, repeat
+from operator import attrgetter, is_, itemgetter
 
 import ctypes
 
@@ -52,16 +52,23 @@ class HipBackend:
                                "(there is no CPU fallback)")
         return CodecPlan(sizes, ratio, bits, clients=clients, device=device)
 
-    def gather_scalars(self, ts):
+    def gather_scalars(self, ts, described=None):
         """One contiguous copy of the one-element tensors ts (one dtype, one GPU) in a single launch
-        (coalac_gather), or None when they do not qualify (the caller then stacks them with torch)."""
+        (coalac_gather), or None when they do not qualify (the caller then stacks them with torch).
+        described: the _Described these tensors came from (their pointers; the checks run once per layout)."""
         t0 = ts[0]
+        if described is not None and described.raw_ok is False:
+            return None
         if t0.device.type != "cuda":
             return None
         dev, size = t0.device, t0.element_size()
-        ptrs = tuple(map(_data_ptr, ts))
-        if list(map(_get_device, ts)) != [dev.index] * len(ts) or any(p % size for p in ptrs):
-            return None
+        ptrs = tuple(map(_data_ptr, ts)) if described is None else described.raw_ptrs
+        if described is None or described.raw_ok is None:
+            ok = list(map(_get_device, ts)) == [dev.index] * len(ts) and not any(p % size for p in ptrs)
+            if described is not None:
+                described.raw_ok = ok
+            if not ok:
+                return None
         cache = self.__dict__.setdefault("_gather_ptrs", OrderedDict())
         d = cache.get(ptrs)
         if d is None:
@@ -168,16 +175,22 @@ def _layout_sig(sig):
     return L
 
 
+_MOD_TABLES = itemgetter("_parameters", "_buffers", "_modules", "_non_persistent_buffers_set")
+
+
 class _StateWalk:
     """The tensors of a module's state_dict, in state_dict order, without building the state_dict: the
     module tree walked once (pre-order, as Module.state_dict recurses), then per call each module's
     parameter and persistent-buffer tables read in place (no per-entry detach, no prefix strings, no
     state-dict hooks: the reference's models register none). Re-walked when a table's size changes, when a
-    submodule is replaced or added (each module's children are compared by identity: a client that keeps one
-    root module across rounds may swap `model.head`), or when the non-persistent buffer set changes."""
+    table object or a submodule is replaced (each module's children are compared by identity: a client that
+    keeps one root module across rounds may swap `model.head`), or when the non-persistent buffer set changes.
+    The per-call checks and the gather run as C-level maps over the modules' __dict__ tables (a Python loop
+    over ResNet-50's 161 modules cost more than the encode's own launches)."""
 
     def __init__(self, module):
-        self.mods, self.rows, names = [], [], []
+        self.mods, names = [], []
+        srcs, keys = [], []  # per state entry: the table it lives in, its key
         self.parents, self.npbs = [], []  # (module, children) of the modules with children; (module, set) likewise
         self.hooked = False
         for prefix, m in module.named_modules(remove_duplicate=False):
@@ -185,41 +198,52 @@ class _StateWalk:
             pn = tuple(k for k, v in m._parameters.items() if v is not None)
             bn = tuple(k for k, v in m._buffers.items() if v is not None and k not in m._non_persistent_buffers_set)
             self.mods.append(m)
-            if pn or bn:
-                self.rows.append((m, pn, bn))
+            srcs.extend([m._parameters] * len(pn) + [m._buffers] * len(bn))
+            keys.extend(pn + bn)
             if m._modules:
                 self.parents.append((m, tuple(m._modules.values())))
             if m._non_persistent_buffers_set:
                 self.npbs.append((m, frozenset(m._non_persistent_buffers_set)))
             p = prefix + "." if prefix else ""
             names.extend(p + k for k in pn + bn)
-        self.sizes = self._sizes()
+        self.dicts = [m.__dict__ for m in self.mods]
+        self.tables = self._tables()           # every module's 4 table objects, flattened
+        self.sizes = list(map(len, self.tables))
+        self.kid_dicts = [m._modules for m, _ in self.parents]
+        self.kids = [kids for _, kids in self.parents]
+        self.srcs, self.keys = srcs, keys
         self.names = tuple(names)
-        self.last = None  # (dtypes, shapes, layout) of the last describe_tensors
+        self.last = None  # _Described: the last describe_tensors of these tensors
 
-    def _sizes(self):
-        return [(len(m._parameters), len(m._buffers), len(m._modules), len(m._non_persistent_buffers_set))
-                for m in self.mods]
+    def _tables(self):
+        return list(chain.from_iterable(map(_MOD_TABLES, self.dicts)))
 
     def tensors(self):
-        """The tensors, or None when the tree changed since the walk (a table's size, a replaced or added
-        submodule, the non-persistent buffer set): the caller walks again."""
-        if self._sizes() != self.sizes:
+        """The tensors, or None when the tree changed since the walk (a table's size or object, a replaced or
+        added submodule, the non-persistent buffer set): the caller walks again."""
+        tables = self._tables()
+        if list(map(len, tables)) != self.sizes or not all(map(is_, tables, self.tables)):
             return None
-        for m, kids in self.parents:  # (tuple equality: identity first, so a replaced child compares unequal)
-            if tuple(m._modules.values()) != kids:
-                return None
+        if list(map(tuple, map(dict.values, self.kid_dicts))) != self.kids:  # (identity first: a swap is unequal)
+            return None
         for m, npb in self.npbs:
             if m._non_persistent_buffers_set != npb:
                 return None
-        out = []
-        ext = out.extend
-        for m, pn, bn in self.rows:
-            if pn:
-                ext(map(m._parameters.__getitem__, pn))
-            if bn:
-                ext(map(m._buffers.__getitem__, bn))
-        return out
+        return list(map(dict.__getitem__, self.srcs, self.keys))
+
+
+class _Described:
+    """describe_tensors' result for one list of tensors: reused while the same tensor objects sit at the same
+    storage (a dtype or shape change of a tensor in place moves its storage; a reshape of a parameter's .data
+    that keeps its storage start is not looked for)."""
+
+    __slots__ = ("tensors", "ptrs", "L", "seg_ptrs", "raw_ptrs", "raw_ok")
+
+    def __init__(self, tensors, ptrs, L):
+        self.tensors, self.ptrs, self.L = tensors, ptrs, L
+        self.seg_ptrs = tuple(ptrs[i] for i in L.seg_idx)
+        self.raw_ptrs = tuple(ptrs[i] for i in L.raw_idx)
+        self.raw_ok = None  # the gather's own checks of the raw scalars, once
 
 
 _WALKS = {}  # id(module) -> (weakref, _StateWalk)
@@ -259,22 +283,32 @@ _get_dtype, _get_shape = attrgetter("dtype"), attrgetter("shape")
 
 def describe_tensors(names, tensors, walk=None, gather=None):
     """describe_state() over (names, tensors) in state_dict order (module_tensors). walk: the _StateWalk the
-    tensors came from — the layout is then looked up again only when a dtype or shape changed since its last
-    call (list comparisons, instead of hashing the whole (name, dtype, shape) signature every call). gather: a
-    backend's one-launch copy of one-element tensors (HipBackend.gather_scalars) for the passthrough scalars."""
-    dts, shs = list(map(_get_dtype, tensors)), list(map(_get_shape, tensors))
-    last = walk.last if walk is not None else None
-    if last is not None and last[0] == dts and last[1] == shs:
-        L = last[2]
-    else:
-        L = _layout_sig(tuple(zip(names, dts, shs)))
+    tensors came from — the layout is then reused while the same tensor objects sit at the same storage (see
+    _Described), instead of reading every tensor's dtype and shape. gather: a backend's one-launch copy of
+    one-element tensors (HipBackend.gather_scalars) for the passthrough scalars."""
+    d, segs = _layout_walk(names, tensors, walk)
+    return d.L, segs, _raw_snapshot(d, tensors, gather)
+
+
+def _layout_walk(names, tensors, walk):
+    """(_Described, fp32 segment tensors) of the tensors: the layout part of describe_tensors."""
+    ptrs = tuple(map(_data_ptr, tensors))
+    d = walk.last if walk is not None else None
+    if d is None or d.ptrs != ptrs or not all(map(is_, tensors, d.tensors)):
+        dts, shs = list(map(_get_dtype, tensors)), list(map(_get_shape, tensors))
+        d = _Described(tensors, ptrs, _layout_sig(tuple(zip(names, dts, shs))))
         if walk is not None:
-            walk.last = (dts, shs, L)
-    segs = list(map(tensors.__getitem__, L.seg_idx))
+            walk.last = d
+    return d, list(map(tensors.__getitem__, d.L.seg_idx))
+
+
+def _raw_snapshot(d, tensors, gather):
+    """The passthrough entries' RawState: one gather launch for a group of scalars of one dtype."""
+    L = d.L
     raw_ts = list(map(tensors.__getitem__, L.raw_idx))
     raw = None
     if L.raw_scalars is not None:
-        flat = gather(raw_ts) if gather is not None else None
+        flat = gather(raw_ts, d) if gather is not None else None
         if flat is not None:
             raw = RawState([(flat, L.raw_scalars)], L.raw_names)
         else:
@@ -285,7 +319,7 @@ def describe_tensors(names, tensors, walk=None, gather=None):
                 raw = None
     if raw is None:
         raw = RawState.snapshot(list(zip(L.raw_names, raw_ts)))
-    return L, segs, raw
+    return raw
 
 
 def describe_state(state):
@@ -734,12 +768,23 @@ class UpdateCodec:
         self.ratio, self.bits, self.mode = float(ratio), int(bits), mode
         self.backend = backend if backend is not None else HipBackend()
         self._plans = {}
+        self._last_plan = None  # (sizes object, device, plan) of the last default-parameter plan_for
         self._checked_ptrs = {}  # id(plan) -> the segment pointers of the last in-place encode that passed the checks
         self._ws = OrderedDict()
         self._lock = threading.Lock()
         self._tls = threading.local()
 
     def plan_for(self, sizes, device, ratio=None, bits=None, clients=1):
+        if ratio is None and bits is None and clients == 1:  # (the encode's call: no 161-tuple hash per call)
+            hit = self._last_plan
+            if hit is not None and hit[0] is sizes and hit[1] == device:
+                return hit[2]
+            p = self._plan_for(sizes, device, None, None, 1)
+            self._last_plan = (sizes, device, p)
+            return p
+        return self._plan_for(sizes, device, ratio, bits, clients)
+
+    def _plan_for(self, sizes, device, ratio, bits, clients):
         ratio = self.ratio if ratio is None else float(ratio)
         bits = self.bits if bits is None else int(bits)
         key = (tuple(sizes), ratio, bits, str(device), int(clients))
@@ -767,10 +812,15 @@ class UpdateCodec:
         names, tensors, walk = _module_walk(module)
         if device is None:
             device = self._device_for(tensors)
-        L, segs, raw = describe_tensors(names, tensors, walk, getattr(self.backend, "gather_scalars", None))
-        return self._encode(L, segs, raw, base, device, lambda: OrderedDict(zip(names, tensors)))
+        d, segs = _layout_walk(names, tensors, walk)
+        gather = getattr(self.backend, "gather_scalars", None)
+        # the passthrough snapshot is taken after the encode's launches (stream order: the same values), so
+        # the GPU starts on the segments one gather launch earlier
+        return self._encode(d.L, segs, lambda: _raw_snapshot(d, tensors, gather), base, device,
+                            lambda: OrderedDict(zip(names, tensors)), d.seg_ptrs)
 
-    def _encode(self, L, segs, raw, base, device, state_fn):
+    def _encode(self, L, segs, raw, base, device, state_fn, ptrs=None):
+        """raw: the RawState, or a function that takes it (called once the encode is enqueued)."""
         if self.mode == "delta" and base is None:
             raise ValueError("delta mode needs the global-model snapshot (base)")
         entries = L.entries
@@ -779,6 +829,7 @@ class UpdateCodec:
                   "entries": entries}
         if not sizes:
             header["total_k"] = 0
+            raw = raw() if callable(raw) else raw
             z = torch.zeros(0)
             return CompressedUpdate(header, Encoded(z.int(), z.to(torch.uint8), z, z), raw)
         device = torch.device(device)
@@ -793,7 +844,8 @@ class UpdateCodec:
         dev_index = device.index if device.type == "cuda" else -1  # (Tensor.get_device(): -1 on the CPU)
         in_place = getattr(plan, "encode_segments", None) is not None
         if in_place:  # every segment on the plan's device, contiguous, 16-B aligned (one pass per property)
-            ptrs = tuple(map(_data_ptr, segs))
+            if ptrs is None:
+                ptrs = tuple(map(_data_ptr, segs))
             # (the same storage as an encode that passed the checks: a model's parameters do not move between
             # rounds; a strides-only change of a parameter in place is not looked for)
             if self._checked_ptrs.get(id(plan)) != ptrs:
@@ -810,7 +862,7 @@ class UpdateCodec:
         header["total_k"] = int(plan.table.total_k)
         if enc.ustart is not None and self.ratio < 1.0:  # wire v2 (a dense download implies its starts)
             header["n_units"] = int(plan.table.n_units)
-        return CompressedUpdate(header, enc, raw)
+        return CompressedUpdate(header, enc, raw() if callable(raw) else raw)
 
     def _thread_stream(self, device):
         """One HIP stream per (thread, device): concurrent decodes from several threads overlap on the GPU

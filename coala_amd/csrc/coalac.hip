@@ -89,7 +89,7 @@ constexpr int SEL_NT_LAT = 512;           // ... in latency-bound plans, where n
 #define SCAN_WPE 5
 #endif
 #ifndef SCAN_NT
-#define SCAN_NT 256  // batch plans' k_scan block size (launch bounds: SCAN_WPE waves per SIMD)
+#define SCAN_NT 128  // batch plans' k_scan block size (launch bounds: SCAN_WPE waves per SIMD; C3 0.584 vs 0.616 ms at 256)
 #endif
 #ifndef SCAN_NB
 #define SCAN_NB 1  // load batches per k_scan unit (weights mode): 1 = all 16 float4 per lane in flight

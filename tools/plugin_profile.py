@@ -21,13 +21,17 @@ from coala_amd.layouts import build_module  # noqa: E402
 
 
 def med(fn, n, sync=True):
+    """sync True: until the GPU is done; False: the call alone; "host": until the call returns, then the GPU
+    drained outside the timing (the host cost of a call that enqueues work)."""
     ts = []
     for _ in range(n):
         t0 = time.perf_counter()
         fn()
-        if sync:
+        if sync is True:
             torch.cuda.synchronize()
         ts.append((time.perf_counter() - t0) * 1e3)
+        if sync == "host":
+            torch.cuda.synchronize()
     ts.sort()
     return ts[len(ts) // 2]
 
@@ -42,14 +46,25 @@ def main(steps=50):
         up = codec.encode_module(m, base=base)
         codec.decode_module(up, g, base=base)
     torch.cuda.synchronize()
-    names, ts = C.module_tensors(m)
-    L, segs, raw = C.describe_tensors(names, ts)
+    names, ts, walk = C._module_walk(m)
+    d, segs = C._layout_walk(names, ts, walk)
+    L, ptrs = d.L, d.seg_ptrs
+    plan = codec.plan_for(L.sizes_key, dev)
+    ws = codec._workspace(plan)
     st = codec.decode_state(up, base=base)
     rows = [
         ("compression: encode_module (total)", lambda: codec.encode_module(m, base=base), True),
         ("  module_tensors", lambda: C.module_tensors(m), False),
         ("  describe_tensors (layout + raw snapshot)", lambda: C.describe_tensors(names, ts), False),
         ("  state_dict() (what round 2 walked)", lambda: m.state_dict(), False),
+        ("  host: encode_module returns", lambda: codec.encode_module(m, base=base), "host"),
+        ("  host: _module_walk", lambda: C._module_walk(m), "host"),
+        ("  host: _layout_walk", lambda: C._layout_walk(names, ts, walk), "host"),
+        ("  host: _raw_snapshot (gather launch)", lambda: C._raw_snapshot(d, ts, codec.backend.gather_scalars),
+         "host"),
+        ("  host: plan.encode_segments", lambda: plan.encode_segments(segs, base=base.flat, workspace=ws,
+                                                                      checked=True, ptrs=ptrs), "host"),
+        ("  host: empty_encoded", lambda: plan.empty_encoded(), "host"),
         ("decompression: decode_module (total)", lambda: codec.decode_module(up, g, base=base), True),
         ("  decode_state", lambda: codec.decode_state(up, base=base), True),
         ("  module_with_state", lambda: C.module_with_state(g, st), False),
