@@ -43,6 +43,15 @@ def _on(stream):
     return torch.cuda.stream(stream) if stream is not None else contextlib.nullcontext()
 
 
+_NULL_CTX = contextlib.nullcontext()
+
+
+def _device_ctx(device):
+    """torch.cuda.device(device), or nothing when it is already the current device (the common case: the
+    context manager's exchange costs a few us per call on the hooks' path)."""
+    return _NULL_CTX if torch.cuda.current_device() == device.index else torch.cuda.device(device)
+
+
 def _stream_handle(stream):
     s = torch.cuda.current_stream() if stream is None else stream
     return ctypes.c_void_p(s.cuda_stream)
@@ -121,15 +130,18 @@ class CodecPlan:
 
     def empty_encoded(self):
         """The five output buffers of an encode as views of ONE allocation (16-byte aligned each)."""
-        K, T, U = self.total_k, self.n_segments, self.n_units
-        vb = 4 if self.bits == RAW_BITS else 1
-        offs, o = [], 0
-        for nbytes in (4 * K, vb * K, 4 * T, 4 * T, 4 * U):
-            offs.append((o, nbytes))
-            o = (o + nbytes + 15) // 16 * 16
-        buf = torch.empty(max(o, 16), dtype=torch.uint8, device=self.device)
-        dts = (torch.int32, self.vals_dtype, torch.float32, torch.float32, torch.int32)
-        return Encoded(*(buf[a:a + n].view(dt) for (a, n), dt in zip(offs, dts)))
+        geo = self.__dict__.get("_enc_geometry")
+        if geo is None:
+            K, T, U = self.total_k, self.n_segments, self.n_units
+            vb = 4 if self.bits == RAW_BITS else 1
+            views, o = [], 0
+            dts = (torch.int32, self.vals_dtype, torch.float32, torch.float32, torch.int32)
+            for nbytes, dt in zip((4 * K, vb * K, 4 * T, 4 * T, 4 * U), dts):
+                views.append((o, nbytes, dt))
+                o = (o + nbytes + 15) // 16 * 16
+            geo = self._enc_geometry = (max(o, 16), tuple(views))
+        buf = torch.empty(geo[0], dtype=torch.uint8, device=self.device)
+        return Encoded(*[buf[a:a + n].view(dt) for a, n, dt in geo[1]])
 
     def empty_workspace(self):
         return torch.empty(self.ws_bytes, dtype=torch.uint8, device=self.device)
@@ -228,7 +240,8 @@ class CodecPlan:
                         ptrs=None):
         """Encode with segment i read from tensors[i] itself (coalac_encode_segptr): e.g. a model's
         parameters, no flattening copy. base: flat fp32[span] (delta mode), as encode()."""
-        ptrs = self.segment_pointers(tensors, checked=checked, ptrs=ptrs, stream=stream)
+        launch = torch.cuda.current_stream(self.device) if stream is None else stream
+        ptrs = self.segment_pointers(tensors, checked=checked, ptrs=ptrs, stream=launch)
         self._check_flat(base, "base")
         mine = out is None  # (buffers this call allocates need no checking)
         with _on(stream):
@@ -237,11 +250,11 @@ class CodecPlan:
         ust = _ptr(out.ustart) if mine else self._check_encoded(out)
         if ws.device != self.device or ws.numel() * ws.element_size() < self.ws_bytes:
             raise ValueError(f"workspace: need {self.ws_bytes} bytes on {self.device}")
-        with torch.cuda.device(self.device):
+        with _device_ctx(self.device):
             rc = self._lib.coalac_encode_segptr(self._h, _ptr(ptrs), _ptr(base), _ptr(out.idx), _ptr(out.vals),
                                                 _ptr(out.mn), _ptr(out.scale), ust, _ptr(ws),
                                                 ctypes.c_uint64(self.ws_bytes), ctypes.c_uint(flags),
-                                                _stream_handle(stream))
+                                                ctypes.c_void_p(launch.cuda_stream))
         _lib.check(rc, "coalac_encode_segptr")
         return out
 

@@ -25,6 +25,9 @@ timeout -k 10 240 rocprofv3 --pmc FETCH_SIZE -d "$OUT/single_fetch" -o run --out
   -- python3 bench.py --steps 6 --warmup 3 $B $S > "$OUT/bench_single_fetch.json" 2> "$OUT/single_fetch.err"
 timeout -k 10 240 rocprofv3 --pmc WRITE_SIZE -d "$OUT/single_write" -o run --output-format csv \
   -- python3 bench.py --steps 6 --warmup 3 $B $S > "$OUT/bench_single_write.json" 2> "$OUT/single_write.err"
+timeout -k 10 240 rocprofv3 --kernel-trace --stats -d "$OUT/agg" -o run --output-format csv \
+  -- python3 tools/bench_aggregate.py > "$OUT/bench_aggregate_trace.json" 2> "$OUT/agg.err"
+timeout -k 10 120 python3 tools/bench_aggregate.py > "$OUT/bench_aggregate.json" 2>> "$OUT/agg.err"
 python3 tools/pmc_summary.py "$OUT" > "$OUT/summary.json"
 mkdir -p "$OUT/s"
 ln -s ../single "$OUT/s/trace"; ln -s ../single_fetch "$OUT/s/fetch"; ln -s ../single_write "$OUT/s/write"
@@ -35,10 +38,11 @@ rm -rf "$OUT/s"
 python3 tools/timeline.py "$OUT/trace" --group 2 --last-groups 8 > "$OUT/timeline_union.json"
 find "$OUT/trace" -name "*kernel_stats.csv" -exec python3 tools/filter_stats.py {} "$OUT/kernel_stats_codec.csv" \;
 find "$OUT/single" -name "*kernel_stats.csv" -exec python3 tools/filter_stats.py {} "$OUT/kernel_stats_single.csv" \;
+find "$OUT/agg" -name "*kernel_stats.csv" -exec python3 tools/filter_stats.py {} "$OUT/kernel_stats_aggregate.csv" \;
 # keep the small summaries only (raw per-dispatch CSVs can exceed gpurun's 64 MiB pull limit)
-du -sh "$OUT"/trace "$OUT"/single "$OUT"/fetch "$OUT"/write || true
+du -sh "$OUT"/trace "$OUT"/single "$OUT"/fetch "$OUT"/write "$OUT"/agg || true
 for s in trace single fetch write single_fetch single_write; do
   find "$OUT/$s" -name '*kernel_stats.csv' -exec cp {} "$OUT/${s}_kernel_stats.csv" \; || true
 done
-rm -rf "$OUT/trace" "$OUT/single" "$OUT/fetch" "$OUT/write" "$OUT/single_fetch" "$OUT/single_write"
+rm -rf "$OUT/trace" "$OUT/single" "$OUT/fetch" "$OUT/write" "$OUT/single_fetch" "$OUT/single_write" "$OUT/agg"
 ls -la "$OUT"
