@@ -91,6 +91,9 @@ constexpr int SEL_NT_LAT = 512;           // ... in latency-bound plans, where n
 #ifndef SCAN_NT
 #define SCAN_NT 128  // batch plans' k_scan block size (launch bounds: SCAN_WPE waves per SIMD; C3 0.584 vs 0.616 ms at 256)
 #endif
+#ifndef SCAN_NT_LAT
+#define SCAN_NT_LAT 256  // latency-bound plans' k_scan block size (its first blocks encode the small segments)
+#endif
 #ifndef SCAN_NB
 #define SCAN_NB 1  // load batches per k_scan unit (weights mode): 1 = all 16 float4 per lane in flight
 #endif
@@ -98,7 +101,7 @@ constexpr int SEL_NT_LAT = 512;           // ... in latency-bound plans, where n
 #define DECODE_XCD 1  // batch k_decode_lds: XCD-aware unit order (xcd_block)
 #endif
 #ifndef SCAN_XCD
-#define SCAN_XCD 0    // k_scan: XCD-aware unit order
+#define SCAN_XCD 1    // k_scan: XCD-aware unit order (128-thread blocks: C3 0.600-0.602 vs 0.604-0.606 ms)
 #endif
 #ifndef SCAN_LEAN
 #define SCAN_LEAN 1  // k_scan: no per-element length test on units that cannot need it (scan_unit CHECK)
@@ -841,9 +844,8 @@ DEV void hist_pick2(const uint32_t* hist, uint32_t r1, uint32_t r2, uint32_t& b1
 // compaction, min/max, codes. Runs as its own kernel (k_small) on the plan's side stream, concurrently
 // with k_sample / k_scan, so its latency hides under the HBM streaming.
 // ------------------------------------------------------------------------------------------------
-template <bool DELTA, bool RAW>
+template <bool DELTA, bool RAW, int NT = BLOCK>
 DEV void small_encode(const Params& P, uint32_t si, float* vals, uint32_t* hist, uint32_t* sh) {
-  constexpr int NT = BLOCK;
   const uint32_t t = threadIdx.x;
   const uint32_t s = P.small_list[si];
   const SegDev sd = P.ssegs[si];  // (the same load round as s)
@@ -1083,7 +1085,6 @@ template <bool DELTA, bool RAW, bool WITH_SMALL, int WPE = SCAN_WPE, int NB = SC
 __global__ __launch_bounds__(NTS, WPE) void k_scan(Params P) {
   // one LDS arena: candidate staging (NTS / 64 x STAGE_CAP records) or a small segment's values + histogram
   // (WITH_SMALL only: without it the block needs 16 KB of LDS instead of 24.8 KB)
-  static_assert(!WITH_SMALL || NTS == BLOCK, "small segments take 256-thread blocks");
   constexpr uint32_t NWS = NTS / 64;
   constexpr size_t SMALL_BYTES = WITH_SMALL ? (SMALL_MAX + HIST_BINS + 64) * 4 : 0;
   constexpr size_t STAGE_BYTES = NWS * STAGE_CAP * sizeof(uint2);
@@ -1091,7 +1092,7 @@ __global__ __launch_bounds__(NTS, WPE) void k_scan(Params P) {
   if (WITH_SMALL && blockIdx.x < P.scan_small) {
     float* vals = reinterpret_cast<float*>(arena);
     uint32_t* hist = reinterpret_cast<uint32_t*>(arena) + SMALL_MAX;
-    small_encode<DELTA, RAW>(P, blockIdx.x, vals, hist, hist + HIST_BINS);
+    small_encode<DELTA, RAW, NTS>(P, blockIdx.x, vals, hist, hist + HIST_BINS);
     return;
   }
   uint2* stage = reinterpret_cast<uint2*>(arena);
@@ -2777,8 +2778,9 @@ int launch_encode(const Params& P, coalac_plan_t plan, hipStream_t st, const coa
   ENC_BOUNDARY(1);
   if (small_in_scan) {
     Q.scan_small = plan->n_small;
-    hipLaunchKernelGGL((k_scan<DELTA, RAW, true, SCAN_WPE_LAT, SCAN_NB_LAT>), dim3(gu + plan->n_small),
-                       dim3(BLOCK), 0, st, Q);
+    hipLaunchKernelGGL((k_scan<DELTA, RAW, true, SCAN_WPE_LAT, SCAN_NB_LAT, SCAN_NT_LAT>),
+                       dim3((plan->n_lunits + SCAN_NT_LAT / 64 - 1) / (SCAN_NT_LAT / 64) + plan->n_small),
+                       dim3(SCAN_NT_LAT), 0, st, Q);
   } else if ((stages & COALAC_STAGE_SCAN) && gu) {
     hipLaunchKernelGGL((k_scan<DELTA, RAW, false, SCAN_WPE, SCAN_NB, SCAN_NT>),
                        dim3((plan->n_lunits + SCAN_NT / 64 - 1) / (SCAN_NT / 64)), dim3(SCAN_NT), 0, st, Q);
