@@ -185,3 +185,25 @@ def test_recycling_survives_a_template_change():
     m = codec.decode_module(ups[1], g, base=base)
     assert torch.equal(m.extra_note, torch.ones(2)) and m.extra_note is not g.extra_note
     assert _equal_state(m, fresh[1])
+
+
+def test_layout_reused_only_while_tensors_and_storage_are_unchanged():
+    """describe_tensors keeps the layout of the last call while the same tensor objects sit at the same storage;
+    a parameter whose .data is swapped for another shape (new storage) or a replaced parameter object is seen."""
+    from coala_amd.compression.codec import _module_walk, describe_tensors
+    m = Net()
+    names, ts, w = _module_walk(m)
+    L1 = describe_tensors(names, ts, w)[0]
+    names, ts, w = _module_walk(m)
+    assert describe_tensors(names, ts, w)[0] is L1
+    with torch.no_grad():
+        m.shared.weight.data = torch.randn(2, 8)  # same element count, new storage and shape
+    names, ts, w = _module_walk(m)
+    L2 = describe_tensors(names, ts, w)[0]
+    shapes = {e["name"]: tuple(e["shape"]) for e in L2.entries}
+    assert L2 is not L1 and shapes["shared.weight"] == (2, 8)
+    m.b1.conv.bias = nn.Parameter(torch.zeros(3))  # a replaced parameter object
+    names, ts, w = _module_walk(m)
+    L3, segs, _ = describe_tensors(names, ts, w)
+    assert any(t is m.b1.conv.bias for t in segs)
+    assert [e["name"] for e in L3.entries] == list(m.state_dict())
