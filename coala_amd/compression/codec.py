@@ -1160,6 +1160,7 @@ def _segment_views(flat, table, entries):
 _PLAIN_TYPES = frozenset((bool, int, float, complex, str, bytes, type(None), torch.dtype, torch.device))
 _CONTAINER_TYPES = frozenset((dict, OrderedDict, list, set))
 _MODULE_TABLES = frozenset(("_parameters", "_buffers", "_modules"))
+_TABLES3 = itemgetter("_parameters", "_buffers", "_modules")
 _make_param = torch.Tensor._make_subclass
 
 
@@ -1245,6 +1246,8 @@ class _TreeRecipe:
         mods, info = self.mods, self.info
         if not hasattr(self, "getters"):
             self._getters()
+        if self.__dict__.get("fast") is not None and self._unchanged():
+            return self.fast
         stale = [i for i in range(len(mods)) if not self.valid(i)]
         if stale:
             for i in stale:
@@ -1257,7 +1260,42 @@ class _TreeRecipe:
             fast = self.fast = [self._fast(x) for x in info]
             self.plain = [tuple(k for k in m.__dict__ if k not in _MODULE_TABLES and k not in set(f[5] + f[9] + f[10]))
                           for m, f in zip(mods, fast)]
+            self._flat_tables()
         return fast
+
+    def _flat_tables(self):
+        """The per-call checks and the refresh as C-level maps over the whole tree (a Python loop over a
+        ResNet-50's 132 modules and their ~1,600 hook containers cost more than the decode itself)."""
+        dicts = self.t_dicts = [m.__dict__ for m in self.mods]
+        self.t_dlens = list(map(len, dicts))
+        self.t_tables = list(chain.from_iterable(map(_TABLES3, dicts)))
+        self.t_sizes = list(map(len, self.t_tables))
+        self.t_fresh = [d[k] for d, x in zip(dicts, self.info) for k, _ in x[1]]  # the template's empty containers
+        self.t_typed = [(d, k, tv) for d, x in zip(dicts, self.info) for k, tv in x[3] + x[2]]
+        self.p_src = [d for d, keys in zip(dicts, self.plain) for _ in keys]
+        self.p_keys = [k for keys in self.plain for k in keys]
+        self.p_mod = [i for i, keys in enumerate(self.plain) for _ in keys]
+        self.special = [i for i, f in enumerate(self.fast) if f[9] or f[10]]
+
+    def _unchanged(self):
+        """Every template module as classified: __dict__ and table sizes, the same table objects, its fresh
+        containers still empty (a hook registered later must be deep-copied), its special attributes' types."""
+        dicts = self.t_dicts
+        if list(map(len, dicts)) != self.t_dlens or any(self.t_fresh):
+            return False
+        tabs = list(chain.from_iterable(map(_TABLES3, dicts)))
+        if not all(map(is_, tabs, self.t_tables)) or list(map(len, tabs)) != self.t_sizes:
+            return False
+        return all(type(d.get(k)) is tv for d, k, tv in self.t_typed)
+
+    def tree_unchanged(self):
+        """The template's module tree is still the one this recipe walked: every child slot holds the same
+        module object (a replaced submodule — model.head = nn.Linear(...) — needs a new recipe)."""
+        kids = self.__dict__.get("t_kids")
+        if kids is None:
+            self.t_kid_dicts = [m._modules for m in self.mods if m._modules]
+            kids = self.t_kids = [tuple(d.values()) for d in self.t_kid_dicts]
+        return list(map(tuple, map(dict.values, self.t_kid_dicts))) == kids
 
     def build(self, state):
         return self._build(state)[0]
@@ -1321,6 +1359,7 @@ class _TreeRecipe:
             if sum(sk.nbytes for sk in self.pool) + nbytes > self.POOL_BYTES or len(self.pool) >= self.POOL_MAX:
                 return root
             sk = _Skeleton(root, new, flat, list(raws or ()), D, raw.signature(), device, nbytes)
+            sk.adopt(self)
             del new
             sk.base = sk.counts()
             sk.base[0][0] -= 1  # the root: this frame's `root` is the only transient reference
@@ -1347,14 +1386,18 @@ class _TreeRecipe:
         plain attributes copied, hook containers emptied if a previous holder registered hooks, special
         attributes re-copied unless still equal."""
         memo = None
-        for i, (m, c) in enumerate(zip(self.mods, sk.mods)):
+        list(map(dict.__setitem__, sk.p_dst, self.p_keys, map(dict.__getitem__, self.p_src, self.p_keys)))
+        if any(sk.fresh):  # a previous holder registered hooks on the recycled tree: empty containers again
+            for i, c in enumerate(sk.mods):
+                nd, f = c.__dict__, self.fast[i]
+                for k, tv in zip(f[5], f[6]):
+                    if nd.get(k):
+                        nd[k] = tv()
+            sk.adopt(self)
+        for i in self.special:
+            m, c = self.mods[i], sk.mods[i]
             d, nd = m.__dict__, c.__dict__
             f = self.fast[i]
-            for k in self.plain[i]:
-                nd[k] = d[k]
-            for k, tv in zip(f[5], f[6]):
-                if nd.get(k):
-                    nd[k] = tv()
             for k in f[9]:
                 nd[k] = d[k].clone()
             for k in f[10]:
@@ -1396,8 +1439,8 @@ class _Skeleton:
     decoded storage they view (the flat fp32 decode output and the passthrough groups) and their idle
     reference counts."""
 
-    __slots__ = ("root", "mods", "objs", "sizes", "flat", "raws", "D", "raw_sig", "device", "nbytes", "base",
-                 "generation")
+    __slots__ = ("root", "mods", "objs", "dicts", "dlens", "tables", "tsizes", "flat", "raws", "D", "raw_sig",
+                 "device", "nbytes", "base", "generation", "p_dst", "fresh")
 
     def __init__(self, root, mods, flat, raws, D, raw_sig, device, nbytes):
         self.root, self.mods = root, mods
@@ -1405,16 +1448,30 @@ class _Skeleton:
         for c in mods:
             self.objs.extend(t for t in c._parameters.values() if t is not None)
             self.objs.extend(t for t in c._buffers.values() if t is not None)
-        self.sizes = [(len(c._parameters), len(c._buffers), len(c._modules)) for c in mods]
+        self.dicts = [c.__dict__ for c in mods]
+        self.dlens = list(map(len, self.dicts))
+        self.tables = list(chain.from_iterable(map(_TABLES3, self.dicts)))
+        self.tsizes = list(map(len, self.tables))
         self.flat, self.raws, self.D, self.raw_sig, self.device, self.nbytes = flat, raws, D, raw_sig, device, nbytes
         self.generation = 0
 
+    def adopt(self, recipe):
+        """The recipe's flat refresh tables for this tree: where each plain attribute goes, and the tree's own
+        (empty) hook containers, checked in one pass per recycle."""
+        self.p_dst = [self.dicts[i] for i in recipe.p_mod]
+        self.fresh = [c.__dict__[k] for c, f in zip(self.mods, recipe.fast) for k in f[5]]
+
     def counts(self):
+        """Idle fingerprint: every object's reference count, the decoded storage's use counts, and whether every
+        module still has its attribute count and its very table objects at their sizes (an attribute added or a
+        table replaced by a previous holder keeps the tree from being recycled)."""
         refs = list(map(sys.getrefcount, self.objs))
         store = [torch._C._storage_Use_Count(t.untyped_storage()._cdata) for t in [self.flat] + self.raws
                  if t is not None]
-        sizes = [(len(c._parameters), len(c._buffers), len(c._modules)) for c in self.mods]
-        return [refs, store, sizes == self.sizes]
+        tabs = list(chain.from_iterable(map(_TABLES3, self.dicts)))
+        same = (list(map(len, self.dicts)) == self.dlens and all(map(is_, tabs, self.tables))
+                and list(map(len, tabs)) == self.tsizes)
+        return [refs, store, same]
 
 
 _RECIPES = {}  # id(template) -> (weakref to it, recipe)
@@ -1426,7 +1483,7 @@ def _recipe(template):
     key = id(template)
     with _RECIPES_LOCK:
         hit = _RECIPES.get(key)
-        if hit is None or hit[0]() is not template:
+        if hit is None or hit[0]() is not template or not hit[1].tree_unchanged():
             import weakref
             hit = (weakref.ref(template), _TreeRecipe(template))
             _RECIPES[key] = hit

@@ -207,3 +207,29 @@ def test_layout_reused_only_while_tensors_and_storage_are_unchanged():
     L3, segs, _ = describe_tensors(names, ts, w)
     assert any(t is m.b1.conv.bias for t in segs)
     assert [e["name"] for e in L3.entries] == list(m.state_dict())
+
+
+def test_recycling_checks_attributes_tables_and_template_children():
+    """A tree a previous holder gave a new attribute is not recycled; hooks registered on a recycled tree are
+    dropped; a template whose submodule was replaced gets a new recipe (the decoded module follows the new
+    child's attributes)."""
+    codec, g, base, ups, fresh = _codec_round()
+    m = codec.decode_module(ups[0], g, base=base)
+    first = id(m)
+    list(m.modules())[1].note = "held"  # an attribute a fresh build would not have
+    del m
+    m = codec.decode_module(ups[1], g, base=base)
+    assert id(m) != first and not hasattr(list(m.modules())[1], "note") and _equal_state(m, fresh[1])
+    second = id(m)
+    list(m.modules())[2].register_forward_hook(lambda *a: None)
+    del m
+    m = codec.decode_module(ups[2], g, base=base)
+    assert id(m) == second and not list(m.modules())[2]._forward_hooks and _equal_state(m, fresh[2])
+    del m
+    name, child = next(iter(g.named_children()))
+    new_child = copy.deepcopy(child)
+    new_child.tag = 7
+    setattr(g, name, new_child)
+    m = codec.decode_module(ups[1], g, base=base)
+    got = getattr(m, name)
+    assert got is not new_child and got is not child and got.tag == 7 and _equal_state(m, fresh[1])
