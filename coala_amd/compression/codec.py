@@ -768,21 +768,24 @@ class UpdateCodec:
         self.ratio, self.bits, self.mode = float(ratio), int(bits), mode
         self.backend = backend if backend is not None else HipBackend()
         self._plans = {}
-        self._last_plan = None  # (sizes object, device, plan) of the last default-parameter plan_for
+        self._plan_fast = OrderedDict()  # (id(sizes), ratio, bits, clients) -> (sizes, device, plan)
         self._checked_ptrs = {}  # id(plan) -> the segment pointers of the last in-place encode that passed the checks
         self._ws = OrderedDict()
         self._lock = threading.Lock()
         self._tls = threading.local()
 
     def plan_for(self, sizes, device, ratio=None, bits=None, clients=1):
-        if ratio is None and bits is None and clients == 1:  # (the encode's call: no 161-tuple hash per call)
-            hit = self._last_plan
-            if hit is not None and hit[0] is sizes and hit[1] == device:
-                return hit[2]
-            p = self._plan_for(sizes, device, None, None, 1)
-            self._last_plan = (sizes, device, p)
-            return p
-        return self._plan_for(sizes, device, ratio, bits, clients)
+        # (per sizes OBJECT — a layout's cached tuple — no hash of a 161-entry tuple per hook call)
+        fk = (id(sizes), ratio, bits, clients)
+        hit = self._plan_fast.get(fk)
+        if hit is not None and hit[0] is sizes and hit[1] == device:
+            return hit[2]
+        p = self._plan_for(sizes, device, ratio, bits, clients)
+        with self._lock:
+            self._plan_fast[fk] = (sizes, device, p)
+            while len(self._plan_fast) > 32:
+                self._plan_fast.popitem(last=False)
+        return p
 
     def _plan_for(self, sizes, device, ratio, bits, clients):
         ratio = self.ratio if ratio is None else float(ratio)
@@ -901,8 +904,9 @@ class UpdateCodec:
 
     WS_CACHE = 16  # encode workspaces kept per codec (one per plan and launch stream in use)
 
-    def _workspace(self, plan):
-        """The encode workspace of `plan` for the current thread and stream, reused across calls (kernels on
+    def _workspace(self, plan, stream=None, decode=False):
+        """The encode (or, decode=True, decode) workspace of `plan` for this thread and `stream` (default: the
+        current one), reused across calls (kernels on
         one stream run in order, so consecutive encodes of one thread can share it). Keyed by thread too: two
         threads encoding on one stream (e.g. both on the default stream) interleave their launches, since the
         ctypes call releases the GIL, and one encode's select would read the other's scan results. A bounded
@@ -910,14 +914,19 @@ class UpdateCodec:
         can reuse it (stream-ordered)."""
         if not hasattr(plan, "empty_workspace"):
             return None
-        stream = torch.cuda.current_stream(plan.device) if plan.device.type == "cuda" else None
-        key = (id(plan), threading.get_ident(), None if stream is None else stream.cuda_stream)
+        if stream is None:
+            stream = torch.cuda.current_stream(plan.device) if plan.device.type == "cuda" else None
+        key = (id(plan), threading.get_ident(), None if stream is None else stream.cuda_stream, decode)
         with self._lock:
             hit = self._ws.get(key)
             if hit is not None and hit[0] is plan:
                 self._ws.move_to_end(key)
                 return hit[1]
-            ws = plan.empty_workspace()
+            if decode:
+                with torch.cuda.stream(stream):  # (allocated on the stream that uses it)
+                    ws = plan.empty_decode_workspace()
+            else:
+                ws = plan.empty_workspace()
             self._ws[key] = (plan, ws)
             self._ws.move_to_end(key)
             while len(self._ws) > self.WS_CACHE:
@@ -976,7 +985,8 @@ class UpdateCodec:
                 with torch.cuda.stream(side):
                     enc = update.encoded_to(device, staging=self._staging)
                     self._staged(side)
-                    flat = plan.decode(enc, base=base_flat, out=out, stream=side)
+                    flat = plan.decode(enc, base=base_flat, out=out, stream=side,
+                                       workspace=self._workspace(plan, side, decode=True))
                     if into is not None:
                         for dst, (src, _) in zip(into.raws, raw._groups):
                             dst.copy_(src, non_blocking=True)
