@@ -137,9 +137,6 @@ constexpr uint32_t STAGE_CAP = 512;       // candidate records staged in LDS per
 #define GU_UNITS 32
 #endif
 constexpr uint32_t GU = GU_UNITS;               // units per select group (k_ghist / k_gwin block)
-#ifndef GSWEEP
-#define GSWEEP 4  // units per record-load batch of a group sweep (8 measured equal on one update, lower on C3)
-#endif
 constexpr uint32_t HB2 = 512;             // bins of the per-group band histograms
 constexpr uint32_t GCAP = 256;            // in-window entries a group may hand to k_select
 constexpr uint32_t KEY_MAX = 0x7FFFFFFFu;
@@ -199,6 +196,7 @@ struct Params {
   uint32_t *tstar, *rtie, *status;
   // per large unit
   uint32_t *tlo, *thi, *cntA, *cntC, *gtC, *eqC, *eqpre, *outoff;
+  uint4* uemit;  // per large unit, from k_select: {T*, tie budget | raw-path flag << 31, mn bits, scale bits}
   uint32_t* cval;  // candidate records, ccap slots per large unit, in index order: the value bits ...
   uint16_t* cpos;  // ... and the position inside the unit (the emit reads both; every select sweep the values only)
   uint32_t ccap;  // record slots per large unit (< UNIT: a unit that finds more candidates overflows and its
@@ -1129,18 +1127,6 @@ DEV uint32_t chunk_prefix(const uint32_t* cnt, uint32_t cn, uint32_t cap, uint32
   return carry;
 }
 
-// The same prefix from counts already in registers (thread i < cn holds unit i's count, cn <= NT): the
-// loads were issued with the caller's other loads of the same round.
-template <int NT>
-DEV uint32_t reg_prefix(uint32_t c, uint32_t cn, uint32_t* upre, uint32_t* sh) {
-  const uint32_t t = threadIdx.x;
-  uint32_t tot;
-  const uint32_t ex = block_excl_scan<NT>(t < cn ? c : 0u, sh, tot);
-  if (t < cn) upre[t] = ex;
-  if (t == 0) upre[cn] = tot;
-  __syncthreads();
-  return tot;
-}
 
 // Wave w owns the units whose first record index (upre[u]) lies in [w*total/NW, (w+1)*total/NW):
 // contiguous unit ranges balanced by record count, so segment order = (wave, unit, lane) order. A wave
@@ -1192,6 +1178,50 @@ DEV void unit_sweep(const uint32_t* cand, uint32_t stride, uint32_t lu0, const u
     }
   }
 }
+
+// A group's records swept by a block WITHOUT waiting for the units' counts first: wave w owns the UPW
+// consecutive units [w * UPW, (w + 1) * UPW) of the group (index order = wave order) and loads their counts
+// and the first two 64-record rows of every unit in ONE round, speculatively (slots past a unit's count hold
+// stale words, never used; ccap >= 128). unit_sweep instead balances the waves by record count, which needs
+// the counts and a block prefix before the first record load — one more dependent round on the select chain.
+template <uint32_t UPW>
+struct SpecSweep {
+  uint32_t x0[UPW], x1[UPW], n;  // lane g < UPW: unit g's stored-record count
+  uint32_t u0, cn;
+  DEV void load(const Params& P, uint32_t lu0, uint32_t units) {
+    const uint32_t lane = lane_id();
+    u0 = (threadIdx.x >> 6) * UPW;
+    cn = units;
+    const uint32_t uc = min(u0 + min(lane, UPW - 1), units - 1);
+    const uint32_t nr = P.cntC[lu0 + uc];
+#pragma unroll
+    for (uint32_t g = 0; g < UPW; ++g) {
+      const uint32_t* R = P.cval + (uint64_t)(lu0 + min(u0 + g, units - 1)) * P.ccap;
+      x0[g] = R[lane];
+      x1[g] = R[lane + 64];
+    }
+    n = (lane < UPW && u0 + lane < units) ? min(nr, P.ccap) : 0u;
+  }
+  // f(x, valid, u) for every lane (ballots allowed), fend(u) after each unit; u = unit index in the group
+  template <class F, class FE>
+  DEV void run(const Params& P, uint32_t lu0, F&& f, FE&& fend) const {
+    const uint32_t lane = lane_id();
+#pragma unroll
+    for (uint32_t g = 0; g < UPW; ++g) {
+      const uint32_t u = u0 + g;
+      if (u < cn) {
+        const uint32_t nn = (uint32_t)__builtin_amdgcn_readlane((int)n, (int)g);
+        f(__uint_as_float(x0[g]), lane < nn, u);
+        if (nn > 64) f(__uint_as_float(x1[g]), lane + 64 < nn, u);
+        if (nn > 128) {
+          const uint32_t* R = P.cval + (uint64_t)(lu0 + u) * P.ccap;
+          for (uint32_t i0 = 128; i0 < nn; i0 += 64) f(__uint_as_float(R[min(i0 + lane, nn - 1)]), i0 + lane < nn, u);
+        }
+        fend(u);
+      }
+    }
+  }
+};
 
 // LDS scratch of the segment select (k_select, and the SELECT role of the one-launch encode, whose LDS
 // must stay <= 32 KB so five streaming blocks still fit a CU): 28.3 KB
@@ -1308,18 +1338,20 @@ DEV void select_generic(const Params& P, uint32_t lb, uint32_t nu, uint32_t tlo,
 // which the segment's last-arriving group block ran segment_pick needed an agent-scope release fence in
 // every block — an L2 writeback on gfx950 — and was ~100x slower; kernel boundaries are cheaper.)
 template <int NT = BLOCK>
-DEV void group_hist(const Params& P, uint32_t gi, uint32_t* hist, uint32_t* upre, uint32_t* sh) {
+DEV void group_hist(const Params& P, uint32_t gi, uint32_t* hist) {
   const uint4 G = P.groups[gi];  // x: large-segment index, y: first large unit, z: units, w: segment
   const uint32_t t = threadIdx.x;
   STAMP(P, G.x, 20);
-  // one load round for everything that depends on G only
+  // one load round for everything that depends on G only: the band, and every unit's count and first
+  // records (the histogram needs no index order, so no count prefix before the record loads)
   const uint32_t tlo = P.tlo[G.y], thi = P.thi[G.y], hh = P.shhi[G.x];
-  const uint32_t c = t < G.z ? min(P.cntC[G.y + t], P.ccap) : 0u;  // stored records only
+  SpecSweep<(GU + NT / 64 - 1) / (NT / 64)> sw;
+  sw.load(P, G.y, G.z);
   for (uint32_t i = t; i < HB2; i += NT) hist[i] = 0;
-  const uint32_t total = reg_prefix<NT>(c, G.z, upre, sh);  // barriers inside
+  __syncthreads();
   const Band band(tlo, thi, hh);
-  unit_sweep<NT / 64, GSWEEP>(
-      P.cval, P.ccap, G.y, upre, G.z, total,
+  sw.run(
+      P, G.y,
       [&](float x, bool valid, uint32_t) {
         const uint32_t key = fkey(x);
         if (valid && key >= tlo && key <= thi) atomicAdd(&hist[band.bin(key)], 1u);
@@ -1334,9 +1366,7 @@ DEV void group_hist(const Params& P, uint32_t gi, uint32_t* hist, uint32_t* upre
 template <int NT = BLOCK>
 __global__ __launch_bounds__(NT) void k_ghist(Params P) {
   __shared__ uint32_t hist[HB2];
-  __shared__ uint32_t upre[GU + 1];
-  __shared__ uint32_t sh[64];
-  group_hist<NT>(P, blockIdx.x, hist, upre, sh);
+  group_hist<NT>(P, blockIdx.x, hist);
 }
 
 // segment_pick: per large segment — validate the sampled bracket, sum the group histograms, pick the bin of
@@ -1423,7 +1453,6 @@ DEV uint4 segment_pick(const Params& P, const SegDev& sd, const Band& band, uint
 // in index order (-> glist, count -> gcnt), min/max of the values above the window (-> gmm)
 template <int NW = WAVES>
 struct GwinSmemT {
-  uint32_t upre[GU + 1];
   uint2 slots[NW][GCAP];
   uint32_t wcnt[NW];
   float shf[2 * NW];
@@ -1433,12 +1462,11 @@ using GwinSmem = GwinSmemT<WAVES>;
 template <int NT, bool DELTA, bool RAW>
 DEV void segment_select(const Params& P, uint32_t li, SelSmem& S);
 
-// (upre / total: the group's record prefix, already in W_.upre)
-template <int NT = BLOCK>
-DEV void group_window(const Params& P, uint32_t gi, const uint4 G, const uint4 st, uint32_t lu_begin, uint32_t total,
+// (sw: the group's counts and first records, loaded by the caller with its other loads)
+template <int NT, class SW>
+DEV void group_window(const Params& P, uint32_t gi, const uint4 G, const uint4 st, uint32_t lu_begin, const SW& sw,
                       GwinSmemT<NT / 64>& W_, uint32_t* sh) {
   constexpr int NW = NT / 64;
-  uint32_t* upre = W_.upre;
   auto& slots = W_.slots;
   uint32_t* wcnt = W_.wcnt;
   float* shf = W_.shf;
@@ -1447,8 +1475,8 @@ DEV void group_window(const Params& P, uint32_t gi, const uint4 G, const uint4 s
   const uint32_t useg0 = G.y - lu_begin;  // unit index (within the segment) of the group's first unit
   uint32_t wc = 0, ug = 0;
   float lmn = qnan(), lmx = qnan();
-  unit_sweep<NW, GSWEEP>(
-      P.cval, P.ccap, G.y, upre, G.z, total,
+  sw.run(
+      P, G.y,
       [&](float x, bool valid, uint32_t u) {
         const uint32_t key = fkey(x);
         const bool g = valid && key > whi;
@@ -1493,8 +1521,8 @@ DEV void group_window(const Params& P, uint32_t gi, const uint4 G, const uint4 s
 template <int NT = BLOCK>
 DEV void group_pick_window(const Params& P, uint32_t gi, GwinSmemT<NT / 64>& W, uint32_t* hist, uint32_t* sh) {
   // round 1: the group and its segment's geometry (gseg: {first large unit, units, k, first group}, so nothing
-  // waits for a segment-table lookup); round 2: the band and the group's counts; segment_pick's round: the
-  // segment's group histograms and unit counts
+  // waits for a segment-table lookup); round 2: the band, the group's unit counts and first records
+  // (SpecSweep), the segment's group histograms and unit counts — everything the block reads, in one round
   const uint4 G = P.groups[gi];
   const uint4 GS = P.gseg[gi];
   STAMP(P, G.x, 22);
@@ -1504,11 +1532,11 @@ DEV void group_pick_window(const Params& P, uint32_t gi, GwinSmemT<NT / 64>& W, 
   sd.k = GS.z;
   sd.g_begin = GS.w;
   const uint32_t tlo = P.tlo[G.y], thi = P.thi[G.y], hh = P.shhi[G.x];
-  const uint32_t c = threadIdx.x < G.z ? min(P.cntC[G.y + threadIdx.x], P.ccap) : 0u;
-  const uint32_t total = reg_prefix<NT>(c, G.z, W.upre, sh);
+  SpecSweep<(GU + NT / 64 - 1) / (NT / 64)> sw;
+  sw.load(P, G.y, G.z);
   const uint4 st = segment_pick<NT>(P, sd, Band(tlo, thi, hh), hist, sh);
   STAMP(P, G.x, 23);
-  if (st.w == 0) group_window<NT>(P, gi, G, st, GS.x, total, W, sh);
+  if (st.w == 0) group_window<NT>(P, gi, G, st, GS.x, sw, W, sh);
   if (threadIdx.x == 0 && G.y == GS.x) {  // the segment's first group
     uint2* ss = reinterpret_cast<uint2*>(P.sstate + G.x);
     pst(P, ss, make_uint2(st.x, st.y));
@@ -1732,6 +1760,7 @@ DEV void segment_select(const Params& P, uint32_t li, SelSmem& S) {
   uint32_t T, rt, fp_rank, fn_rank;
   float gmn, gmx;
   bool done = st.w == 0 && select_from_groups<NT>(P, sd, lb, nu, st, S, T, rt, fp_rank, fn_rank, gmn, gmx);
+  uint32_t raw_path = 0;
   STAMP(P, li, 1);
   if (!done) {
   uint32_t sa = 0, sc = 0;
@@ -1762,6 +1791,7 @@ DEV void segment_select(const Params& P, uint32_t li, SelSmem& S) {
         0u, KEY_MAX, rk, S.hist, S.sh);
     rt = rk;
     raw_counts<NT, DELTA>(P, lb, nu, T, S.sh, S.wcnt, fp_rank, fn_rank, gmn, gmx);
+    raw_path = 1u;
     if (t == 0) pst(P, P.status + s, 1u);
   } else {
     // rank of the k-th key among candidates with key <= thi (0: none of them)
@@ -1814,6 +1844,9 @@ DEV void segment_select(const Params& P, uint32_t li, SelSmem& S) {
     pst(P, P.mn + s, mn);
     pst(P, P.scale + s, scale);
   }
+  // the segment's emit parameters per unit: k_emit then loads them with the unit's own words, in one round
+  const uint4 ue = make_uint4(T, rt | (raw_path << 31), __float_as_uint(mn), __float_as_uint(scale));
+  for (uint32_t i = t; i < nu; i += NT) P.uemit[lb + i] = ue;
   STAMP(P, li, 12);
 }
 
@@ -1902,30 +1935,28 @@ DEV void emit_raw_unit(const Params& P, const UnitDev& L, uint32_t T, uint32_t r
 template <bool DELTA, bool RAW, uint32_t UPW = EMIT_UPW>
 DEV void emit_units(const Params& P, uint32_t lu0, uint32_t lu1) {
   const uint32_t lane = lane_id();
-  // round 1 / 2: lane g < UPW holds unit lu0 + g's count, offsets and its segment's T*, tie budget,
-  // mn, scale (lanes past UPW or past the last unit repeat a valid unit; never used)
+  // lane g < UPW holds unit lu0 + g's count, offsets and its segment's T*, tie budget, mn, scale (lanes past
+  // UPW or past the last unit repeat a valid unit; never used)
   const uint32_t lug = min(lu0 + min(lane, UPW - 1), lu1 - 1);
-  const uint32_t nCg = min(P.cntC[lug], P.ccap);  // stored records (a raw-path unit may have dropped some)
-  const uint32_t segg = P.lunits[lug].seg;
+  // ONE load round: the unit's count, record, offsets and its segment's emit parameters (k_select copies them
+  // to every unit), and — before the count is known — every unit's first 64 (128) record slots (ccap >= 128:
+  // slots past the count hold stale words, never used)
+  const uint32_t nCr = P.cntC[lug];
   const uint32_t startg = P.lunits[lug].start;
-  const uint32_t stg = P.status[segg];             // != 0: the segment took the raw-data path
   const uint64_t sog = P.lunits[lug].out_off;
   const uint32_t eqpg = P.eqpre[lug], oog = P.outoff[lug];
-  const uint32_t Tg = P.tstar[segg], rtg = P.rtie[segg];
-  const float mng = RAW ? 0.0f : P.mn[segg];
-  const float scg = RAW ? 0.0f : P.scale[segg];
-  // every unit's first 2 x 64 records in flight before the first is classified (at ~1.5 % candidates a
-  // unit holds ~60 records, so about half of the units need the second row: loading it inside the unit
-  // loop made it one dependent round per unit, 8 in a row)
+  const uint4 ue = P.uemit[lug];
   uint2 rec0[UPW], rec1[UPW];  // {position, value bits}
 #pragma unroll
   for (uint32_t g = 0; g < UPW; ++g) {
-    const uint32_t lu = min(lu0 + g, lu1 - 1), nC = rl(nCg, g);
-    const uint32_t last = nC ? nC - 1 : 0u;
-    const uint64_t r0 = (uint64_t)lu * P.ccap;  // unconditional (clamped) loads
-    rec0[g] = make_uint2(P.cpos[r0 + min(lane, last)], P.cval[r0 + min(lane, last)]);
-    if (EMIT_ROWS > 1) rec1[g] = make_uint2(P.cpos[r0 + min(lane + 64, last)], P.cval[r0 + min(lane + 64, last)]);
+    const uint64_t r0 = (uint64_t)min(lu0 + g, lu1 - 1) * P.ccap;
+    rec0[g] = make_uint2(P.cpos[r0 + lane], P.cval[r0 + lane]);
+    if (EMIT_ROWS > 1) rec1[g] = make_uint2(P.cpos[r0 + lane + 64], P.cval[r0 + lane + 64]);
   }
+  const uint32_t nCg = min(nCr, P.ccap);  // stored records (a raw-path unit may have dropped some)
+  const uint32_t Tg = ue.x, rtg = ue.y & 0x7FFFFFFFu, stg = ue.y >> 31;  // stg: the raw-data path
+  const float mng = RAW ? 0.0f : __uint_as_float(ue.z);
+  const float scg = RAW ? 0.0f : __uint_as_float(ue.w);
 #pragma unroll
   for (uint32_t g = 0; g < UPW; ++g) {
     const uint32_t nC = rl(nCg, g);
@@ -2266,9 +2297,6 @@ __global__ __launch_bounds__(BLOCK) void k_bounds(Params P, const BChunk* chunks
 #ifndef AGG_SPLIT
 #define AGG_SPLIT 2u  // waves per 4096-element unit in k_aggregate (each owns UNIT_IT / AGG_SPLIT rows)
 #endif
-#ifndef AGG_PAIR
-#define AGG_PAIR 0  // k_aggregate: clients two at a time through two LDS tiles (one dependent LDS round trip per pair)
-#endif
 #ifndef AGG_DEPTH
 #define AGG_DEPTH 16u  // clients whose entries k_aggregate loads together (16 ResNet-50 clients: 4 -> 73.5 us, 8 -> 70.9 us, 16 -> 69.1 us)
 #endif
@@ -2336,8 +2364,7 @@ __global__ __launch_bounds__(BLOCK, AGG_WPE) void k_aggregate(Params P, AggArgs 
   // AGG_SPLIT waves per unit, each owning RI of its UNIT_IT rows: a smaller LDS tile and half the registers
   // per wave, so twice the waves are resident
   constexpr uint32_t RI = UNIT_IT / AGG_SPLIT, HE = UNIT / AGG_SPLIT;  // rows / elements per wave
-  static_assert(!AGG_PAIR || AGG_DEPTH % 2 == 0, "pairs of prefetched clients");
-  __shared__ float4 tiles[WAVES][AGG_PAIR ? 2 : 1][HE / 4];
+  __shared__ float4 tiles[WAVES][HE / 4];
   const uint32_t lane = lane_id(), wv = threadIdx.x >> 6;
   const uint32_t wid = blockIdx.x * WAVES + wv;
   const uint32_t u = wid / AGG_SPLIT, h = wid % AGG_SPLIT;
@@ -2349,10 +2376,8 @@ __global__ __launch_bounds__(BLOCK, AGG_WPE) void k_aggregate(Params P, AggArgs 
   const uint32_t e_lo = h * HE;  // first element (within the unit) of this wave's rows
   if (e_lo >= len) return;
   const uint32_t hlen = min(len - e_lo, HE);
-  float4* tile = tiles[wv][0];
+  float4* tile = tiles[wv];
   float* tf = reinterpret_cast<float*>(tile);
-  float4* tile2 = tiles[wv][AGG_PAIR ? 1 : 0];
-  float* tf2 = reinterpret_cast<float*>(tile2);
   float4 b[RI], acc[RI];
   const float* bs = HASBASE ? P.base + U.off + e_lo : nullptr;
   auto load_base = [&]() {
@@ -2372,10 +2397,6 @@ __global__ __launch_bounds__(BLOCK, AGG_WPE) void k_aggregate(Params P, AggArgs 
   auto tile_zero = [&]() {
 #pragma unroll
     for (uint32_t it = 0; it < RI; ++it) tile[it * 64 + lane] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-    if (AGG_PAIR) {
-#pragma unroll
-      for (uint32_t it = 0; it < RI; ++it) tile2[it * 64 + lane] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-    }
   };
   if (HASBASE) load_base();
   tile_zero();
@@ -2444,26 +2465,6 @@ __global__ __launch_bounds__(BLOCK, AGG_WPE) void k_aggregate(Params P, AggArgs 
       if (mine) tf[pos] = 0.0f;
       lds_order();
     };
-    // clients j and j + 1 (both with <= 64 kept entries): both scattered, both read back, accumulated in order
-    auto process2 = [&](uint32_t j, uint32_t idx, uint32_t q, uint32_t idx2, uint32_t q2) {
-      const uint32_t pos = idx - U.start - e_lo, pos2 = idx2 - U.start - e_lo;
-      const uint32_t ne = __builtin_amdgcn_readlane(m_hi, j) - __builtin_amdgcn_readlane(m_lo, j);
-      const uint32_t ne2 = __builtin_amdgcn_readlane(m_hi, j + 1) - __builtin_amdgcn_readlane(m_lo, j + 1);
-      const float mn = __uint_as_float(__builtin_amdgcn_readlane(__float_as_uint(m_mn), j));
-      const float sc = __uint_as_float(__builtin_amdgcn_readlane(__float_as_uint(m_sc), j));
-      const float mn2 = __uint_as_float(__builtin_amdgcn_readlane(__float_as_uint(m_mn), j + 1));
-      const float sc2 = __uint_as_float(__builtin_amdgcn_readlane(__float_as_uint(m_sc), j + 1));
-      const bool mine = lane < ne && pos < hlen, mine2 = lane < ne2 && pos2 < hlen;
-      if (mine) tf[pos] = code_value<RAW>(q, mn, sc);
-      if (mine2) tf2[pos2] = code_value<RAW>(q2, mn2, sc2);
-      lds_order();
-      accumulate(j, tile);
-      accumulate(j + 1, tile2);
-      lds_order();
-      if (mine) tf[pos] = 0.0f;
-      if (mine2) tf2[pos2] = 0.0f;
-      lds_order();
-    };
     // any client with more than 64 kept entries in this unit (ratio >~ 1.5 %): every client in turn, its
     // entries loaded chunk by chunk, no prefetch (the fast path below has no load loop inside: with one, the
     // compiler's wait counting falls back to draining every load in flight)
@@ -2494,19 +2495,9 @@ __global__ __launch_bounds__(BLOCK, AGG_WPE) void k_aggregate(Params P, AggArgs 
       uint32_t pa[AGG_DEPTH], qa[AGG_DEPTH];
 #pragma unroll
       for (uint32_t t = 0; t < AGG_DEPTH; ++t) fetch(j0 + t, pa[t], qa[t]);
-      if (AGG_PAIR) {
 #pragma unroll
-        for (uint32_t t = 0; t < AGG_DEPTH; t += 2) {
-          if (j0 + t + 1 < cn)
-            process2(j0 + t, pa[t], qa[t], pa[t + 1], qa[t + 1]);
-          else if (j0 + t < cn)
-            process(j0 + t, pa[t], qa[t]);
-        }
-      } else {
-#pragma unroll
-        for (uint32_t t = 0; t < AGG_DEPTH; ++t)
-          if (j0 + t < cn) process(j0 + t, pa[t], qa[t]);
-      }
+      for (uint32_t t = 0; t < AGG_DEPTH; ++t)
+        if (j0 + t < cn) process(j0 + t, pa[t], qa[t]);
     }
   }
   float* out = P.out + U.off + e_lo;
@@ -2579,7 +2570,7 @@ size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 struct WsLayout {
   size_t status;
   size_t tstar, rtie;
-  size_t tlo, thi, cntA, cntC, gtC, eqC, eqpre, outoff;
+  size_t tlo, thi, cntA, cntC, gtC, eqC, eqpre, outoff, uemit;
   size_t cval, cpos, stamps, ghist, gcnt, glist, gmm, sstate, shhi;
   size_t total;
 };
@@ -2603,6 +2594,7 @@ WsLayout ws_layout(size_t S, size_t LU, size_t NG, size_t NL, uint32_t CC) {
   L.eqC = take(4 * LU);
   L.eqpre = take(4 * LU);
   L.outoff = take(4 * LU);
+  L.uemit = take(16 * LU);
   L.cval = take(4 * (size_t)CC * LU);
   L.cpos = take(2 * (size_t)CC * LU);
   L.stamps = take(8 * NSTAMP * std::max<size_t>(S, 1));
@@ -3051,6 +3043,7 @@ int encode_impl(coalac_plan_t plan, const float* d_in, const float* const* d_inp
   P.eqC = reinterpret_cast<uint32_t*>(w + L.eqC);
   P.eqpre = reinterpret_cast<uint32_t*>(w + L.eqpre);
   P.outoff = reinterpret_cast<uint32_t*>(w + L.outoff);
+  P.uemit = reinterpret_cast<uint4*>(w + L.uemit);
   P.cval = reinterpret_cast<uint32_t*>(w + L.cval);
   P.cpos = reinterpret_cast<uint16_t*>(w + L.cpos);
   P.stamps = (flags & COALAC_FLAG_STAMPS) ? reinterpret_cast<uint64_t*>(w + L.stamps) : nullptr;
