@@ -53,6 +53,7 @@
 #include <cstring>
 #include <mutex>
 #include <string>
+#include <type_traits>
 #include <vector>
 
 #include "../../include/coalac.h"
@@ -135,6 +136,9 @@ constexpr int SEL_NT_LAT = 512;           // ... in latency-bound plans, where n
 constexpr uint32_t STAGE_CAP = 512;       // candidate records staged in LDS per k_scan wave
 #ifndef GU_UNITS
 #define GU_UNITS 32
+#endif
+#ifndef GSWEEP
+#define GSWEEP 4  // units per record-load batch of a balanced group sweep (batch plans)
 #endif
 constexpr uint32_t GU = GU_UNITS;               // units per select group (k_ghist / k_gwin block)
 constexpr uint32_t HB2 = 512;             // bins of the per-group band histograms
@@ -1179,6 +1183,38 @@ DEV void unit_sweep(const uint32_t* cand, uint32_t stride, uint32_t lu0, const u
   }
 }
 
+// The same prefix from counts already in registers (thread i < cn holds unit i's count, cn <= NT): the
+// loads were issued with the caller's other loads of the same round.
+template <int NT>
+DEV uint32_t reg_prefix(uint32_t c, uint32_t cn, uint32_t* upre, uint32_t* sh) {
+  const uint32_t t = threadIdx.x;
+  uint32_t tot;
+  const uint32_t ex = block_excl_scan<NT>(t < cn ? c : 0u, sh, tot);
+  if (t < cn) upre[t] = ex;
+  if (t == 0) upre[cn] = tot;
+  __syncthreads();
+  return tot;
+}
+
+// A group's records swept by the block's waves balanced by record count (unit_sweep): the counts and a block
+// prefix come first, then the record loads — batch plans, where the select kernels run beside the other
+// sub-batch's streaming waves (the speculative sweep below measured slower there: C3 0.617-0.636 vs 0.600-0.604 ms)
+template <int NT>
+struct BalancedSweep {
+  uint32_t* upre;
+  uint32_t total, cn;
+  DEV void load(const Params& P, uint32_t lu0, uint32_t units, uint32_t* upre_, uint32_t* sh) {
+    upre = upre_;
+    cn = units;
+    const uint32_t c = threadIdx.x < units ? min(P.cntC[lu0 + threadIdx.x], P.ccap) : 0u;
+    total = reg_prefix<NT>(c, units, upre, sh);  // barriers inside
+  }
+  template <class F, class FE>
+  DEV void run(const Params& P, uint32_t lu0, F&& f, FE&& fend) const {
+    unit_sweep<NT / 64, GSWEEP>(P.cval, P.ccap, lu0, upre, cn, total, f, fend);
+  }
+};
+
 // A group's records swept by a block WITHOUT waiting for the units' counts first: wave w owns the UPW
 // consecutive units [w * UPW, (w + 1) * UPW) of the group (index order = wave order) and loads their counts
 // and the first two 64-record rows of every unit in ONE round, speculatively (slots past a unit's count hold
@@ -1188,7 +1224,7 @@ template <uint32_t UPW>
 struct SpecSweep {
   uint32_t x0[UPW], x1[UPW], n;  // lane g < UPW: unit g's stored-record count
   uint32_t u0, cn;
-  DEV void load(const Params& P, uint32_t lu0, uint32_t units) {
+  DEV void load(const Params& P, uint32_t lu0, uint32_t units, uint32_t*, uint32_t*) {
     const uint32_t lane = lane_id();
     u0 = (threadIdx.x >> 6) * UPW;
     cn = units;
@@ -1337,17 +1373,20 @@ DEV void select_generic(const Params& P, uint32_t lb, uint32_t nu, uint32_t tlo,
 // k_ghist: the group's HB2-bin histogram of the band keys [tlo, thi] -> ghist[group]. (A fused variant in
 // which the segment's last-arriving group block ran segment_pick needed an agent-scope release fence in
 // every block — an L2 writeback on gfx950 — and was ~100x slower; kernel boundaries are cheaper.)
-template <int NT = BLOCK>
-DEV void group_hist(const Params& P, uint32_t gi, uint32_t* hist) {
+template <int NT, bool SPEC>
+using GroupSweep = std::conditional_t<SPEC, SpecSweep<(GU + NT / 64 - 1) / (NT / 64)>, BalancedSweep<NT>>;
+
+template <int NT, bool SPEC>
+DEV void group_hist(const Params& P, uint32_t gi, uint32_t* hist, uint32_t* upre, uint32_t* sh) {
   const uint4 G = P.groups[gi];  // x: large-segment index, y: first large unit, z: units, w: segment
   const uint32_t t = threadIdx.x;
   STAMP(P, G.x, 20);
   // one load round for everything that depends on G only: the band, and every unit's count and first
   // records (the histogram needs no index order, so no count prefix before the record loads)
   const uint32_t tlo = P.tlo[G.y], thi = P.thi[G.y], hh = P.shhi[G.x];
-  SpecSweep<(GU + NT / 64 - 1) / (NT / 64)> sw;
-  sw.load(P, G.y, G.z);
+  GroupSweep<NT, SPEC> sw;
   for (uint32_t i = t; i < HB2; i += NT) hist[i] = 0;
+  sw.load(P, G.y, G.z, upre, sh);
   __syncthreads();
   const Band band(tlo, thi, hh);
   sw.run(
@@ -1362,11 +1401,14 @@ DEV void group_hist(const Params& P, uint32_t gi, uint32_t* hist) {
   STAMP(P, G.x, 21);
 }
 
-// NT: 256 threads in batches, GHIST_NT_LAT in latency-bound plans (nothing streams beside the block)
-template <int NT = BLOCK>
+// NT: 256 threads in batches, GHIST_NT_LAT in latency-bound plans (nothing streams beside the block); SPEC: the
+// speculative group sweep (latency-bound plans)
+template <int NT, bool SPEC>
 __global__ __launch_bounds__(NT) void k_ghist(Params P) {
   __shared__ uint32_t hist[HB2];
-  group_hist<NT>(P, blockIdx.x, hist);
+  __shared__ uint32_t upre[GU + 1];
+  __shared__ uint32_t sh[64];
+  group_hist<NT, SPEC>(P, blockIdx.x, hist, upre, sh);
 }
 
 // segment_pick: per large segment — validate the sampled bracket, sum the group histograms, pick the bin of
@@ -1453,6 +1495,7 @@ DEV uint4 segment_pick(const Params& P, const SegDev& sd, const Band& band, uint
 // in index order (-> glist, count -> gcnt), min/max of the values above the window (-> gmm)
 template <int NW = WAVES>
 struct GwinSmemT {
+  uint32_t upre[GU + 1];
   uint2 slots[NW][GCAP];
   uint32_t wcnt[NW];
   float shf[2 * NW];
@@ -1518,7 +1561,7 @@ DEV void group_window(const Params& P, uint32_t gi, const uint4 G, const uint4 s
   }
 }
 
-template <int NT = BLOCK>
+template <int NT, bool SPEC>
 DEV void group_pick_window(const Params& P, uint32_t gi, GwinSmemT<NT / 64>& W, uint32_t* hist, uint32_t* sh) {
   // round 1: the group and its segment's geometry (gseg: {first large unit, units, k, first group}, so nothing
   // waits for a segment-table lookup); round 2: the band, the group's unit counts and first records
@@ -1532,8 +1575,8 @@ DEV void group_pick_window(const Params& P, uint32_t gi, GwinSmemT<NT / 64>& W, 
   sd.k = GS.z;
   sd.g_begin = GS.w;
   const uint32_t tlo = P.tlo[G.y], thi = P.thi[G.y], hh = P.shhi[G.x];
-  SpecSweep<(GU + NT / 64 - 1) / (NT / 64)> sw;
-  sw.load(P, G.y, G.z);
+  GroupSweep<NT, SPEC> sw;
+  sw.load(P, G.y, G.z, W.upre, sh);
   const uint4 st = segment_pick<NT>(P, sd, Band(tlo, thi, hh), hist, sh);
   STAMP(P, G.x, 23);
   if (st.w == 0) group_window<NT>(P, gi, G, st, GS.x, sw, W, sh);
@@ -1546,12 +1589,12 @@ DEV void group_pick_window(const Params& P, uint32_t gi, GwinSmemT<NT / 64>& W, 
 }
 
 // NT: 256 threads in batches, GWIN_NT_LAT in latency-bound plans (nothing streams beside the block)
-template <int NT = BLOCK>
+template <int NT, bool SPEC>
 __global__ __launch_bounds__(NT) void k_gwin(Params P) {
   __shared__ GwinSmemT<NT / 64> W;
   __shared__ uint32_t hist[HB2];
   __shared__ uint32_t sh[64];
-  group_pick_window<NT>(P, blockIdx.x, W, hist, sh);
+  group_pick_window<NT, SPEC>(P, blockIdx.x, W, hist, sh);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -1938,25 +1981,52 @@ DEV void emit_units(const Params& P, uint32_t lu0, uint32_t lu1) {
   // lane g < UPW holds unit lu0 + g's count, offsets and its segment's T*, tie budget, mn, scale (lanes past
   // UPW or past the last unit repeat a valid unit; never used)
   const uint32_t lug = min(lu0 + min(lane, UPW - 1), lu1 - 1);
-  // ONE load round: the unit's count, record, offsets and its segment's emit parameters (k_select copies them
-  // to every unit), and — before the count is known — every unit's first 64 (128) record slots (ccap >= 128:
-  // slots past the count hold stale words, never used)
-  const uint32_t nCr = P.cntC[lug];
-  const uint32_t startg = P.lunits[lug].start;
-  const uint64_t sog = P.lunits[lug].out_off;
-  const uint32_t eqpg = P.eqpre[lug], oog = P.outoff[lug];
-  const uint4 ue = P.uemit[lug];
+  uint32_t nCg, startg, eqpg, oog, Tg, rtg, stg;
+  uint64_t sog;
+  float mng, scg;
   uint2 rec0[UPW], rec1[UPW];  // {position, value bits}
+  if constexpr (UPW == 1) {
+    // latency-bound plans — ONE load round: the unit's count, record, offsets and its segment's emit parameters
+    // (k_select copies them to every unit), and, before the count is known, the unit's first 64 (128) record
+    // slots (ccap >= 128: slots past the count hold stale words, never used)
+    const uint32_t nCr = P.cntC[lug];
+    startg = P.lunits[lug].start;
+    sog = P.lunits[lug].out_off;
+    eqpg = P.eqpre[lug];
+    oog = P.outoff[lug];
+    const uint4 ue = P.uemit[lug];
+    const uint64_t r0 = (uint64_t)lu0 * P.ccap;
+    rec0[0] = make_uint2(P.cpos[r0 + lane], P.cval[r0 + lane]);
+    if (EMIT_ROWS > 1) rec1[0] = make_uint2(P.cpos[r0 + lane + 64], P.cval[r0 + lane + 64]);
+    nCg = min(nCr, P.ccap);  // stored records (a raw-path unit may have dropped some)
+    Tg = ue.x;
+    rtg = ue.y & 0x7FFFFFFFu;
+    stg = ue.y >> 31;  // the raw-data path
+    mng = RAW ? 0.0f : __uint_as_float(ue.z);
+    scg = RAW ? 0.0f : __uint_as_float(ue.w);
+  } else {
+    // batches: round 1 / 2 — unit, then its segment's parameters; then every unit's first rows of records
+    // (clamped to the count: the one-round form measured slower beside the other sub-batch's streaming)
+    nCg = min(P.cntC[lug], P.ccap);
+    const uint32_t segg = P.lunits[lug].seg;
+    startg = P.lunits[lug].start;
+    stg = P.status[segg];
+    sog = P.lunits[lug].out_off;
+    eqpg = P.eqpre[lug];
+    oog = P.outoff[lug];
+    Tg = P.tstar[segg];
+    rtg = P.rtie[segg];
+    mng = RAW ? 0.0f : P.mn[segg];
+    scg = RAW ? 0.0f : P.scale[segg];
 #pragma unroll
-  for (uint32_t g = 0; g < UPW; ++g) {
-    const uint64_t r0 = (uint64_t)min(lu0 + g, lu1 - 1) * P.ccap;
-    rec0[g] = make_uint2(P.cpos[r0 + lane], P.cval[r0 + lane]);
-    if (EMIT_ROWS > 1) rec1[g] = make_uint2(P.cpos[r0 + lane + 64], P.cval[r0 + lane + 64]);
+    for (uint32_t g = 0; g < UPW; ++g) {
+      const uint32_t lu = min(lu0 + g, lu1 - 1), nC = rl(nCg, g);
+      const uint32_t last = nC ? nC - 1 : 0u;
+      const uint64_t r0 = (uint64_t)lu * P.ccap;  // unconditional (clamped) loads
+      rec0[g] = make_uint2(P.cpos[r0 + min(lane, last)], P.cval[r0 + min(lane, last)]);
+      if (EMIT_ROWS > 1) rec1[g] = make_uint2(P.cpos[r0 + min(lane + 64, last)], P.cval[r0 + min(lane + 64, last)]);
+    }
   }
-  const uint32_t nCg = min(nCr, P.ccap);  // stored records (a raw-path unit may have dropped some)
-  const uint32_t Tg = ue.x, rtg = ue.y & 0x7FFFFFFFu, stg = ue.y >> 31;  // stg: the raw-data path
-  const float mng = RAW ? 0.0f : __uint_as_float(ue.z);
-  const float scg = RAW ? 0.0f : __uint_as_float(ue.w);
 #pragma unroll
   for (uint32_t g = 0; g < UPW; ++g) {
     const uint32_t nC = rl(nCg, g);
@@ -2780,13 +2850,13 @@ int launch_encode(const Params& P, coalac_plan_t plan, hipStream_t st, const coa
   ENC_BOUNDARY(2);
   if ((stages & COALAC_STAGE_SELECT) && plan->n_large) {
     if (plan->n_lunits <= LATENCY_PLAN_UNITS)
-      hipLaunchKernelGGL(k_ghist<GHIST_NT_LAT>, dim3(plan->n_groups), dim3(GHIST_NT_LAT), 0, st, P);
+      hipLaunchKernelGGL((k_ghist<GHIST_NT_LAT, true>), dim3(plan->n_groups), dim3(GHIST_NT_LAT), 0, st, P);
     else
-      hipLaunchKernelGGL(k_ghist<BLOCK>, dim3(plan->n_groups), dim3(BLOCK), 0, st, P);
+      hipLaunchKernelGGL((k_ghist<BLOCK, false>), dim3(plan->n_groups), dim3(BLOCK), 0, st, P);
     if (plan->n_lunits <= LATENCY_PLAN_UNITS)
-      hipLaunchKernelGGL(k_gwin<GWIN_NT_LAT>, dim3(plan->n_groups), dim3(GWIN_NT_LAT), 0, st, P);
+      hipLaunchKernelGGL((k_gwin<GWIN_NT_LAT, true>), dim3(plan->n_groups), dim3(GWIN_NT_LAT), 0, st, P);
     else
-      hipLaunchKernelGGL(k_gwin<BLOCK>, dim3(plan->n_groups), dim3(BLOCK), 0, st, P);
+      hipLaunchKernelGGL((k_gwin<BLOCK, false>), dim3(plan->n_groups), dim3(BLOCK), 0, st, P);
     if (plan->n_lunits <= LATENCY_PLAN_UNITS)
       hipLaunchKernelGGL((k_select<DELTA, RAW, SEL_NT_LAT>), dim3(plan->n_large), dim3(SEL_NT_LAT), 0, st, P);
     else
