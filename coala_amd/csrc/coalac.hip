@@ -25,15 +25,17 @@
 //     k_presel  the samplers (one block per large segment: stratified sample -> [T_lo, T_hi]) and the small
 //               segments side by side (batches; latency-bound plans run k_sample alone and the small
 //               segments in k_scan's first blocks)
-//     k_scan    one wave per large unit: single HBM read, classify A / B, 8-byte records in index order
+//     k_scan    one wave per large unit (128-thread blocks in batches): single HBM read, classify A / B,
+//               candidate records in index order (u16 position + u32 value bits, 6 B each)
 //     k_ghist   one block per 32-unit group: band histogram of the group's B records
 //     k_gwin    one block per group: sum the segment's group histograms -> key window of the k-th key
 //               (every group block of the segment, redundantly); per-unit counts above the window + the
-//               group's in-window entries
+//               group's in-window entries (latency-bound plans: both sweep their records speculatively)
 //     k_select  one block per large segment: exact k-th key + tie quota from the window lists (generic
 //               multi-pass select / exact re-select on a bracket miss), per-unit output offsets (= the
-//               payload's per-unit starts, wire v2), min / max -> scale
-//     k_emit    one wave per 8 large units (1 in latency-bound plans): kept records -> ascending idx + codes
+//               payload's per-unit starts, wire v2), min / max -> scale, per-unit emit parameters
+//     k_emit    one wave per 8 large units (1 in latency-bound plans, one load round): kept records ->
+//               ascending idx + codes
 //   Decode: k_decode_lds — every output line written once, the unit's kept values placed through a per-wave
 //   LDS tile; entry ranges from the payload's per-unit starts, or from k_bounds (batches) / an in-kernel
 //   search (k_fillscatter, latency-bound plans) for a payload without them.
@@ -114,6 +116,10 @@ constexpr int SEL_NT_LAT = 512;           // ... in latency-bound plans, where n
 #ifndef SCAN_WPE_LAT
 #define SCAN_WPE_LAT 6  // latency-bound plans' k_scan: blocks per CU (5 / 1 batch: 24.5 us, 6 / 2: 23.0, 6 / 1
                         // spills: 31.7, 8 / 4: 24.2 on one update; batches keep SCAN_WPE / SCAN_NB)
+#endif
+#ifndef SCAN_WPE_LAT_1K
+#define SCAN_WPE_LAT_1K 7  // ... with the default 1024-element small segments (a 16 KB arena): 7 blocks per CU, so
+                           // one ResNet-50 update's ~1,660 blocks fit one round of the chip's block slots
 #endif
 #ifndef SCAN_NB_LAT
 #define SCAN_NB_LAT 2   // ... and load batches per unit
@@ -1089,17 +1095,20 @@ __global__ __launch_bounds__(BLOCK) void k_presel(Params P) {
 // small segments — no longer launched: k_presel runs them beside the samplers.)
 // (WPE / NB: launch-bound blocks per CU and load batches; the latency-bound plans' instantiation, the one
 // WITH_SMALL, takes its own — nothing streams beside it)
-template <bool DELTA, bool RAW, bool WITH_SMALL, int WPE = SCAN_WPE, int NB = SCAN_NB, int NTS = BLOCK>
+template <bool DELTA, bool RAW, bool WITH_SMALL, int WPE = SCAN_WPE, int NB = SCAN_NB, int NTS = BLOCK,
+          uint32_t SCAP = SMALL_MAX>
 __global__ __launch_bounds__(NTS, WPE) void k_scan(Params P) {
   // one LDS arena: candidate staging (NTS / 64 x STAGE_CAP records) or a small segment's values + histogram
   // (WITH_SMALL only: without it the block needs 16 KB of LDS instead of 24.8 KB)
   constexpr uint32_t NWS = NTS / 64;
-  constexpr size_t SMALL_BYTES = WITH_SMALL ? (SMALL_MAX + HIST_BINS + 64) * 4 : 0;
+  // (SCAP: the plan's small-segment limit, <= SMALL_MAX — 1024 by default for latency-bound plans, whose
+  // arena then leaves room for a seventh block per CU)
+  constexpr size_t SMALL_BYTES = WITH_SMALL ? (SCAP + HIST_BINS + 64) * 4 : 0;
   constexpr size_t STAGE_BYTES = NWS * STAGE_CAP * sizeof(uint2);
   __shared__ __attribute__((aligned(16))) uint8_t arena[SMALL_BYTES > STAGE_BYTES ? SMALL_BYTES : STAGE_BYTES];
   if (WITH_SMALL && blockIdx.x < P.scan_small) {
     float* vals = reinterpret_cast<float*>(arena);
-    uint32_t* hist = reinterpret_cast<uint32_t*>(arena) + SMALL_MAX;
+    uint32_t* hist = reinterpret_cast<uint32_t*>(arena) + SCAP;
     small_encode<DELTA, RAW, NTS>(P, blockIdx.x, vals, hist, hist + HIST_BINS);
     return;
   }
@@ -2691,6 +2700,7 @@ struct coalac_plan {
   int bits = 8;
   int nseg = 0;
   uint32_t n_small = 0, n_large = 0, n_units = 0, n_lunits = 0;
+  uint32_t small_max = SMALL_MAX;  // segments of <= this many elements are "small" (encoded whole by one block)
   uint32_t ccap = UNIT;  // candidate record slots per large unit
   uint64_t span = 0, total_k = 0;
   void* meta = nullptr;
@@ -2846,9 +2856,13 @@ int launch_encode(const Params& P, coalac_plan_t plan, hipStream_t st, const coa
   ENC_BOUNDARY(1);
   if (small_in_scan) {
     Q.scan_small = plan->n_small;
-    hipLaunchKernelGGL((k_scan<DELTA, RAW, true, SCAN_WPE_LAT, SCAN_NB_LAT, SCAN_NT_LAT>),
-                       dim3((plan->n_lunits + SCAN_NT_LAT / 64 - 1) / (SCAN_NT_LAT / 64) + plan->n_small),
-                       dim3(SCAN_NT_LAT), 0, st, Q);
+    const dim3 gs((plan->n_lunits + SCAN_NT_LAT / 64 - 1) / (SCAN_NT_LAT / 64) + plan->n_small);
+    if (plan->small_max <= SMALL_MAX_LATENCY)
+      hipLaunchKernelGGL((k_scan<DELTA, RAW, true, SCAN_WPE_LAT_1K, SCAN_NB_LAT, SCAN_NT_LAT, SMALL_MAX_LATENCY>), gs,
+                         dim3(SCAN_NT_LAT), 0, st, Q);
+    else
+      hipLaunchKernelGGL((k_scan<DELTA, RAW, true, SCAN_WPE_LAT, SCAN_NB_LAT, SCAN_NT_LAT>), gs, dim3(SCAN_NT_LAT), 0, st,
+                         Q);
   } else if ((stages & COALAC_STAGE_SCAN) && gu) {
     hipLaunchKernelGGL((k_scan<DELTA, RAW, false, SCAN_WPE, SCAN_NB, SCAN_NT>),
                        dim3((plan->n_lunits + SCAN_NT / 64 - 1) / (SCAN_NT / 64)), dim3(SCAN_NT), 0, st, Q);
@@ -2984,6 +2998,7 @@ int coalac_plan_create(const coalac_seg_t* h_segs, int nseg, int bits, coalac_pl
   if (const char* e = getenv("COALAC_CCAP")) ccap = (uint32_t)atoi(e);  // tests: force overflow
   ccap = std::max<uint32_t>(STAGE_CAP, std::min<uint32_t>(UNIT, ccap));
   p->ccap = ccap;
+  p->small_max = small_max;
   p->ws = ws_layout((size_t)nseg, lunits.size(), groups.size(), large_list.size(), ccap);
 
   const size_t o_segs = 0;
