@@ -77,7 +77,10 @@ constexpr uint32_t SMALL_MAX_LATENCY = 1024;  // ... in latency-bound plans (<= 
                                               // 4096: 14 us, alone on a CU) and the slowest small segment set
                                               // the length of k_presel; bigger segments take the sampled path
 constexpr uint32_t LATENCY_PLAN_UNITS = 8192;  // ~1.3 ResNet-50 updates
-constexpr uint32_t SAMPLE_MAX = 8192;     // sampled keys per large segment
+#ifndef SAMPLE_KEYS
+#define SAMPLE_KEYS 8192u
+#endif
+constexpr uint32_t SAMPLE_MAX = SAMPLE_KEYS;  // sampled keys per large segment
 constexpr int SEL_NT = 256;               // threads of a k_select block in batches (4 waves: one per SIMD, so
                                           // a block finds room beside a streaming kernel's waves)
 #ifndef GWIN_NT_LAT
