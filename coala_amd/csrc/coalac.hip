@@ -133,9 +133,6 @@ constexpr int SEL_NT_LAT = 512;           // ... in latency-bound plans, where n
 #endif
 #define SAMPLE_PICK2 1  // k_sample: both bracket bins from one block scan of the histogram
 #endif
-#ifndef SELECT_DIRECT_RANK
-#define SELECT_DIRECT_RANK 1  // k_select's window of <= RANK_MAX keys: ranked directly (no radix histogram pass)
-#endif
 #ifndef RANK_SELECT
 #define RANK_SELECT 1  // block_select: rank the <= RANK_MAX keys of the chosen bin instead of more radix passes
 #endif
@@ -428,14 +425,11 @@ DEV uint32_t rank_select(ForEach&& for_each, uint32_t lo, uint32_t hi, uint32_t&
 
 template <int NT, int NB = HIST_BINS, class ForEach>
 DEV uint32_t block_select(ForEach&& for_each, uint32_t lo, uint32_t hi, uint32_t& r, uint32_t* hist,
-                          uint32_t* sh, uint32_t nkeys = NONE) {
+                          uint32_t* sh) {
   constexpr int BPT = NB / NT;  // bins per thread
   constexpr int BITS = NB == 2048 ? 11 : NB == 1024 ? 10 : NB == 512 ? 9 : 8;
   static_assert((1 << BITS) == NB, "power-of-two bins");
   const uint32_t t = threadIdx.x;
-  // nkeys (when the caller knows how many keys it enumerates): few enough to rank directly, no radix pass
-  if (RANK_SELECT && SELECT_DIRECT_RANK && nkeys <= RANK_MAX && lo < hi && NB >= (int)RANK_MAX)
-    return rank_select<NT>(for_each, lo, hi, r, hist, sh);
   while (lo < hi) {
     const uint32_t w = hi - lo;
     const int bl = 32 - __clz(w);
@@ -1765,7 +1759,7 @@ DEV bool select_from_groups(const Params& P, const SegDev& sd, uint32_t lb, uint
       [&](auto&& f) {
         for (uint32_t i = t; i < W; i += NT) f(S.lst[i].x & KEY_MAX);
       },
-      st.x, st.y, rt, S.hist, S.sh, W);
+      st.x, st.y, rt, S.hist, S.sh);
   constexpr uint32_t EPT = WLIST / NT;
   const uint32_t q0 = min(W, t * EPT), q1 = min(W, q0 + EPT);
   float lmn = qnan(), lmx = qnan();
