@@ -2434,8 +2434,9 @@ struct AggArgs {
 //   division by a host scalar)                       — coala/server/strategies.py:6-29, 57-90
 //   or out = acc (mode SUM: weighted_sum, strategies.py:57-90, whose result the distributed server hands
 //   to reduce_models, coala/distributed/distributed.py:42-57)
-// d_i goes through a per-wave LDS tile: the client's kept values are scattered into the zeroed tile,
-// every lane reads its 64 elements back with ds_read_b128, then the same positions are re-zeroed.
+// x_i goes through a per-wave LDS tile holding base + 0.0f (= base, checked per wave; zero without a base):
+// at the client's kept positions base + d_i is written, every lane reads its rows back with ds_read_b128
+// (x_i itself: one multiply and one add per element and client), then the base value is put back.
 // Latency: every client's range / mn / scale / weight is fetched lane-parallel in one round (lane j =
 // client j of a 64-client chunk); the first 64 kept entries of AGG_DEPTH clients are then loaded in one
 // batch and accumulated in client order (a unit where some client keeps more than 64 entries takes the
@@ -2449,163 +2450,204 @@ __global__ __launch_bounds__(BLOCK, AGG_WPE) void k_aggregate(Params P, AggArgs 
   __shared__ float4 tiles[WAVES][HE / 4];
   const uint32_t lane = lane_id(), wv = threadIdx.x >> 6;
   const uint32_t wid = blockIdx.x * WAVES + wv;
-  const uint32_t u = wid / AGG_SPLIT, h = wid % AGG_SPLIT;
+  const uint32_t u = __builtin_amdgcn_readfirstlane(wid / AGG_SPLIT), h = __builtin_amdgcn_readfirstlane(wid % AGG_SPLIT);
   if (u >= A.U0) return;
+  // round 1: the unit (scalar loads), and the first 64 clients' starts in it (lane j: client j; they need
+  // only u), pinned above the first use of either
   const UnitDev U = P.units[u];
+  const uint32_t ucl0 = u + min(lane, min(64u, A.clients) - 1) * A.U0;
+  uint32_t us0 = A.ustart[ucl0], us1 = A.ustart[min(ucl0 + 1, P.n_units - 1)];
+  asm volatile("" : "+v"(us0), "+v"(us1)::"memory");
   const uint32_t len = U.len, kseg = U.k;
-  const bool avg = A.avg_mask == nullptr || A.avg_mask[U.seg] != 0;
-  const uint32_t nclients = avg ? A.clients : 1u;
   const uint32_t e_lo = h * HE;  // first element (within the unit) of this wave's rows
   if (e_lo >= len) return;
   const uint32_t hlen = min(len - e_lo, HE);
   float4* tile = tiles[wv];
   float* tf = reinterpret_cast<float*>(tile);
-  float4 b[RI], acc[RI];
   const float* bs = HASBASE ? P.base + U.off + e_lo : nullptr;
-  auto load_base = [&]() {
-#pragma unroll
-    for (uint32_t it = 0; it < RI; ++it) {
+  // the body twice: full 2048-element rows (every load and store a float4, no length test, so no control-flow
+  // merge drains the loads in flight) and a unit's partial last rows
+  auto body = [&](auto full_tag) {
+    constexpr bool FULL = decltype(full_tag)::value;
+    const uint32_t hl = FULL ? HE : hlen;
+    auto load_base = [&](uint32_t it) -> float4 {
       const uint32_t e = (it * 64 + lane) * 4;
-      if (hlen == HE) {
-        b[it] = *reinterpret_cast<const float4*>(bs + e);
-      } else {
-        b[it].x = e + 0 < hlen ? bs[e + 0] : 0.0f;
-        b[it].y = e + 1 < hlen ? bs[e + 1] : 0.0f;
-        b[it].z = e + 2 < hlen ? bs[e + 2] : 0.0f;
-        b[it].w = e + 3 < hlen ? bs[e + 3] : 0.0f;
-      }
-    }
-  };
-  auto tile_zero = [&]() {
-#pragma unroll
-    for (uint32_t it = 0; it < RI; ++it) tile[it * 64 + lane] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-  };
-  if (HASBASE) load_base();
-  tile_zero();
-#pragma unroll
-  for (uint32_t it = 0; it < RI; ++it) acc[it] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-  for (uint32_t c0 = 0; c0 < nclients; c0 += 64) {
-    const uint32_t cn = min(64u, nclients - c0);
-    // lane j: metadata of client c0 + j (unconditional loads at a clamped client index)
-    const uint32_t cl = c0 + min(lane, cn - 1);
-    const uint32_t ucl = u + cl * A.U0;
-    const uint32_t m_lo = min(A.ustart[ucl], kseg);
-    const uint32_t m_hi = max(m_lo, min(min(U.last ? kseg : A.ustart[min(ucl + 1, P.n_units - 1)], kseg), m_lo + len));
-    const uint32_t sl = U.seg + cl * A.T;
-    const float m_mn = RAW ? 0.0f : P.cmn[sl];
-    const float m_sc = RAW ? 0.0f : P.cscale[sl];
-    const float m_w = avg ? A.weights[cl] : 1.0f;  // (x_0 * 1.0f == x_0)
-    auto entries = [&](uint32_t j) -> uint64_t { return U.out_off + (uint64_t)(c0 + j) * A.Kc; };
-    // fetch: the raw loaded words only — any arithmetic on them here would make the wave wait for the loads
-    // right away (in-order vmcnt), turning the AGG_DEPTH-deep prefetch into one exposed latency per client
-    auto fetch = [&](uint32_t j, uint32_t& idx, uint32_t& q) {
-      const uint32_t jj = min(j, cn - 1);
-      const uint32_t lo = __builtin_amdgcn_readlane(m_lo, jj), hi = __builtin_amdgcn_readlane(m_hi, jj);
-      const uint64_t oo = entries(jj);
+      if (FULL) return *reinterpret_cast<const float4*>(bs + e);
+      return make_float4(e + 0 < hl ? bs[e + 0] : 0.0f, e + 1 < hl ? bs[e + 1] : 0.0f,
+                         e + 2 < hl ? bs[e + 2] : 0.0f, e + 3 < hl ? bs[e + 3] : 0.0f);
+    };
+    // ---- round 2, every request of it issued before any is used: the avg flag, the clients' mn / scale /
+    // weight, the base rows and the first AGG_DEPTH clients' entries (all unconditional: a select after a
+    // load, never a branch around it)
+    struct Meta {
+      uint32_t lo, hi;
+      float mn, sc, w;
+    };
+    // lane j: client c0 + j (clamped to the last client of the chunk)
+    auto meta_of = [&](uint32_t c0, uint32_t s0, uint32_t s1) -> Meta {
+      const uint32_t cl = c0 + min(lane, min(64u, A.clients - c0) - 1);
+      const uint32_t sl = U.seg + cl * A.T;
+      Meta m;
+      m.lo = min(s0, kseg);
+      m.hi = max(m.lo, min(min(U.last ? kseg : s1, kseg), m.lo + len));
+      m.mn = RAW ? 0.0f : P.cmn[sl];
+      m.sc = RAW ? 0.0f : P.cscale[sl];
+      m.w = A.weights[cl];
+      return m;
+    };
+    auto meta = [&](uint32_t c0) -> Meta {
+      const uint32_t ucl = u + (c0 + min(lane, min(64u, A.clients - c0) - 1)) * A.U0;
+      return meta_of(c0, A.ustart[ucl], A.ustart[min(ucl + 1, P.n_units - 1)]);
+    };
+    // entries of client c0 + j: the raw loaded words only (any arithmetic on them here would make the wave
+    // wait for the loads right away, in-order vmcnt)
+    auto fetch = [&](const Meta& M, uint32_t c0, uint32_t j, uint32_t& idx, uint32_t& q) {
+      const uint32_t jj = min(j, min(64u, A.clients - c0) - 1);
+      const uint32_t lo = __builtin_amdgcn_readlane(M.lo, jj), hi = __builtin_amdgcn_readlane(M.hi, jj);
+      const uint64_t oo = U.out_off + (uint64_t)(c0 + jj) * A.Kc;
       const uint32_t e = min(lo + lane, hi > lo ? hi - 1 : lo);  // kseg >= 1: entry lo always exists
       idx = (uint32_t)P.cidx[oo + min(e, kseg - 1)];
       q = load_code<RAW>(P, oo + min(e, kseg - 1));
     };
-    // x = base + d; acc = x * w (first client) or acc + x * w: IEEE fp32 ops in this order, on float2 pairs
-    // (v_pk_add_f32 / v_pk_mul_f32: half the VALU issue of scalar fp32); the first-client test is
-    // wave-uniform (a branch, no per-element select)
-    auto accumulate = [&](uint32_t j, const float4* T) {
-      const float w = __uint_as_float(__builtin_amdgcn_readlane(__float_as_uint(m_w), j));
+    float4 bv[RI];
+#pragma unroll
+    for (uint32_t it = 0; it < RI; ++it) bv[it] = HASBASE ? load_base(it) : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    lds_order();  // the requests below stay in this body (common to both, the compiler would hoist them above
+                  // the length test, whose branch then drains them)
+    const uint8_t* amp = A.avg_mask != nullptr ? A.avg_mask + U.seg : reinterpret_cast<const uint8_t*>(A.weights);
+    uint32_t am = *amp;
+    Meta M = meta_of(0, us0, us1);
+    uint32_t pa[AGG_DEPTH], qa[AGG_DEPTH];
+#pragma unroll
+    for (uint32_t t = 0; t < AGG_DEPTH; ++t) fetch(M, 0, t, pa[t], qa[t]);
+    // pinned: no request above moves below this point (the compiler sinks loads toward their first use,
+    // which would put the entries' round behind the base's)
+    asm volatile("" : "+v"(M.lo), "+v"(M.hi), "+v"(M.mn), "+v"(M.sc), "+v"(M.w), "+v"(am)::"memory");
+    const bool avg = A.avg_mask == nullptr || am != 0;
+    const uint32_t nclients = avg ? A.clients : 1u;
+    if (!avg) M.w = 1.0f;  // (x_0 * 1.0f == x_0)
+    // The tile holds x_i where client i kept nothing: base + 0.0f (HASBASE) or +0.0f. The fast path writes
+    // tile + d_i at a client's kept positions, which is base + d_i only where base + 0.0f == base: a wave
+    // whose rows hold a -0.0f or a NaN base ("odd") takes the generic path, which adds the base read from
+    // global memory
+    bool odd = false;
+#pragma unroll
+    for (uint32_t it = 0; it < RI; ++it) {
+      const float v[4] = {bv[it].x, bv[it].y, bv[it].z, bv[it].w};
+      if (HASBASE) {
+#pragma unroll
+        for (int c = 0; c < 4; ++c) odd |= __float_as_uint(v[c]) == 0x80000000u || v[c] != v[c];
+      }
+      const f2v l = f2v{v[0], v[1]} + f2v{0.0f, 0.0f}, h2 = f2v{v[2], v[3]} + f2v{0.0f, 0.0f};
+      tile[it * 64 + lane] = HASBASE ? make_float4(l.x, l.y, h2.x, h2.y) : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    }
+    odd = HASBASE && __ballot(odd) != 0;
+    // acc starts at -0.0f, the exact additive identity (-0 + t == t for every t, signed zeros included): the
+    // first client's acc + x_0 * w_0 is torch's x_0 * w_0 bit for bit, and no client is special
+    float4 acc[RI];
+#pragma unroll
+    for (uint32_t it = 0; it < RI; ++it) acc[it] = make_float4(-0.0f, -0.0f, -0.0f, -0.0f);
+    // acc = acc + x * w: IEEE fp32 ops in this order, on float2 pairs (v_pk_mul_f32 / v_pk_add_f32), x read
+    // from the tile
+    auto accumulate = [&](float w) {
       const f2v w2 = {w, w};
-      if (c0 + j == 0) {
 #pragma unroll
-        for (uint32_t it = 0; it < RI; ++it) {
-          const float4 d = T[it * 64 + lane];
-          const f2v dl = {d.x, d.y}, dh = {d.z, d.w};
-          const f2v bl = {b[it].x, b[it].y}, bh = {b[it].z, b[it].w};
-          const f2v tl = (HASBASE ? bl + dl : dl) * w2, th = (HASBASE ? bh + dh : dh) * w2;
-          acc[it] = make_float4(tl.x, tl.y, th.x, th.y);
+      for (uint32_t it = 0; it < RI; ++it) {
+        const float4 x = tile[it * 64 + lane];
+        const f2v tl = f2v{x.x, x.y} * w2, th = f2v{x.z, x.w} * w2;
+        const f2v sl2 = f2v{acc[it].x, acc[it].y} + tl, sh2 = f2v{acc[it].z, acc[it].w} + th;
+        acc[it] = make_float4(sl2.x, sl2.y, sh2.x, sh2.y);
+      }
+    };
+    auto lanef = [](float v, uint32_t j) { return __uint_as_float(__builtin_amdgcn_readlane(__float_as_uint(v), j)); };
+    const uint32_t pbase = U.start + e_lo;
+    for (uint32_t c0 = 0; c0 < nclients; c0 += 64) {
+      if (c0 > 0) {
+        M = meta(c0);
+#pragma unroll
+        for (uint32_t t = 0; t < AGG_DEPTH; ++t) fetch(M, c0, t, pa[t], qa[t]);
+      }
+      const uint32_t cn = min(64u, nclients - c0);
+      // generic path (an odd wave, or any client with more than 64 kept entries in this unit, ratio >~ 1.5 %):
+      // every client in turn, its entries loaded chunk by chunk, x_i = base + d_i with the base from global
+      // memory, put back as base + 0.0f after the rows are read
+      if (odd || __ballot(lane < cn && M.hi - M.lo > 64) != 0) {
+        for (uint32_t j = 0; j < cn; ++j) {
+          const uint32_t lo = __builtin_amdgcn_readlane(M.lo, j), hi = __builtin_amdgcn_readlane(M.hi, j);
+          const float mn = lanef(M.mn, j), sc = lanef(M.sc, j);
+          const uint64_t oo = U.out_off + (uint64_t)(c0 + j) * A.Kc;
+          for (uint32_t e = lo + lane; e < hi; e += 64) {
+            const uint32_t p2 = (uint32_t)P.cidx[oo + e] - pbase;
+            const float v2 = load_val<RAW>(P, oo + e, mn, sc);
+            if (p2 < hl) tf[p2] = HASBASE ? bs[p2] + v2 : v2;
+          }
+          lds_order();
+          accumulate(lanef(M.w, j));
+          lds_order();
+          for (uint32_t e = lo + lane; e < hi; e += 64) {
+            const uint32_t p2 = (uint32_t)P.cidx[oo + e] - pbase;
+            if (p2 < hl) tf[p2] = HASBASE ? bs[p2] + 0.0f : 0.0f;
+          }
+          lds_order();
         }
+        continue;
+      }
+      // fast path, in client order: x = tile + d written at the client's positions, the rows read and
+      // accumulated, the tile's value put back. The tile value under the next client's entries is read right
+      // after this client's put-back, so the wave never waits on it
+      for (uint32_t j0 = 0; j0 < cn; j0 += AGG_DEPTH) {
+        if (j0 > 0) {
+#pragma unroll
+          for (uint32_t t = 0; t < AGG_DEPTH; ++t) fetch(M, c0, j0 + t, pa[t], qa[t]);
+        }
+        float tb = HASBASE ? tf[min(pa[0] - pbase, HE - 1)] : 0.0f;
+#pragma unroll
+        for (uint32_t t = 0; t < AGG_DEPTH; ++t) {
+          const uint32_t j = j0 + t;
+          if (j >= cn) continue;
+          const uint32_t pos = pa[t] - pbase;  // wraps (>= hl) outside this wave's rows
+          const uint32_t ne = __builtin_amdgcn_readlane(M.hi, j) - __builtin_amdgcn_readlane(M.lo, j);
+          const bool mine = lane < ne && pos < hl;
+          const float d = code_value<RAW>(qa[t], lanef(M.mn, j), lanef(M.sc, j));
+          if (mine) tf[pos] = HASBASE ? tb + d : d;
+          lds_order();
+          accumulate(lanef(M.w, j));
+          lds_order();
+          if (mine) tf[pos] = tb;
+          if (HASBASE && t + 1 < AGG_DEPTH) tb = tf[min(pa[t + 1] - pbase, HE - 1)];
+          lds_order();
+        }
+      }
+    }
+    float* out = P.out + U.off + e_lo;
+#pragma unroll
+    for (uint32_t it = 0; it < RI; ++it) {
+      float4 o;
+      if (!avg) {
+        o = acc[it];
+      } else if (MODE == COALAC_AGG_DIV) {
+        o = make_float4(acc[it].x / A.total, acc[it].y / A.total, acc[it].z / A.total, acc[it].w / A.total);
+      } else if (MODE == COALAC_AGG_SUM) {
+        o = acc[it];
       } else {
-#pragma unroll
-        for (uint32_t it = 0; it < RI; ++it) {
-          const float4 d = T[it * 64 + lane];
-          const f2v dl = {d.x, d.y}, dh = {d.z, d.w};
-          const f2v bl = {b[it].x, b[it].y}, bh = {b[it].z, b[it].w};
-          const f2v al = {acc[it].x, acc[it].y}, ah = {acc[it].z, acc[it].w};
-          const f2v sl = al + (HASBASE ? bl + dl : dl) * w2, sh = ah + (HASBASE ? bh + dh : dh) * w2;
-          acc[it] = make_float4(sl.x, sl.y, sh.x, sh.y);
-        }
+        o = make_float4(acc[it].x * A.inv_total, acc[it].y * A.inv_total, acc[it].z * A.inv_total,
+                        acc[it].w * A.inv_total);
       }
-    };
-    // client j with <= 64 kept entries in this unit (the prefetched ones): scatter, accumulate, re-zero
-    auto process = [&](uint32_t j, uint32_t idx, uint32_t q) {
-      const uint32_t pos = idx - U.start - e_lo;  // wraps (>= hlen) outside this wave's rows
-      const uint32_t ne = __builtin_amdgcn_readlane(m_hi, j) - __builtin_amdgcn_readlane(m_lo, j);
-      const float mn = __uint_as_float(__builtin_amdgcn_readlane(__float_as_uint(m_mn), j));
-      const float sc = __uint_as_float(__builtin_amdgcn_readlane(__float_as_uint(m_sc), j));
-      const bool mine = lane < ne && pos < hlen;
-      if (mine) tf[pos] = code_value<RAW>(q, mn, sc);
-      lds_order();
-      accumulate(j, tile);
-      lds_order();
-      if (mine) tf[pos] = 0.0f;
-      lds_order();
-    };
-    // any client with more than 64 kept entries in this unit (ratio >~ 1.5 %): every client in turn, its
-    // entries loaded chunk by chunk, no prefetch (the fast path below has no load loop inside: with one, the
-    // compiler's wait counting falls back to draining every load in flight)
-    auto process_all = [&](uint32_t j) {
-      const uint32_t lo = __builtin_amdgcn_readlane(m_lo, j), hi = __builtin_amdgcn_readlane(m_hi, j);
-      const float mn = __uint_as_float(__builtin_amdgcn_readlane(__float_as_uint(m_mn), j));
-      const float sc = __uint_as_float(__builtin_amdgcn_readlane(__float_as_uint(m_sc), j));
-      const uint64_t oo = entries(j);
-      for (uint32_t e = lo + lane; e < hi; e += 64) {
-        const uint32_t p2 = (uint32_t)P.cidx[oo + e] - U.start - e_lo;
-        const float v2 = load_val<RAW>(P, oo + e, mn, sc);
-        if (p2 < hlen) tf[p2] = v2;
+      const uint32_t e = (it * 64 + lane) * 4;
+      if (FULL) {
+        *reinterpret_cast<float4*>(out + e) = o;
+      } else {
+        if (e + 0 < hl) out[e + 0] = o.x;
+        if (e + 1 < hl) out[e + 1] = o.y;
+        if (e + 2 < hl) out[e + 2] = o.z;
+        if (e + 3 < hl) out[e + 3] = o.w;
       }
-      lds_order();
-      accumulate(j, tile);
-      lds_order();
-      tile_zero();
-      lds_order();
-    };
-    if (__ballot(lane < cn && m_hi - m_lo > 64) != 0) {
-      for (uint32_t j = 0; j < cn; ++j) process_all(j);
-      continue;
     }
-    // AGG_DEPTH clients' entries loaded together (unconditionally: past cn the clamped client's words are
-    // read again), then accumulated in client order. No load stays in flight across the loop's back edge:
-    // with one, the compiler's wait counting merges the two paths into the loop header and drains them all
-    for (uint32_t j0 = 0; j0 < cn; j0 += AGG_DEPTH) {
-      uint32_t pa[AGG_DEPTH], qa[AGG_DEPTH];
-#pragma unroll
-      for (uint32_t t = 0; t < AGG_DEPTH; ++t) fetch(j0 + t, pa[t], qa[t]);
-#pragma unroll
-      for (uint32_t t = 0; t < AGG_DEPTH; ++t)
-        if (j0 + t < cn) process(j0 + t, pa[t], qa[t]);
-    }
-  }
-  float* out = P.out + U.off + e_lo;
-#pragma unroll
-  for (uint32_t it = 0; it < RI; ++it) {
-    float4 o;
-    if (!avg) {
-      o = acc[it];
-    } else if (MODE == COALAC_AGG_DIV) {
-      o = make_float4(acc[it].x / A.total, acc[it].y / A.total, acc[it].z / A.total, acc[it].w / A.total);
-    } else if (MODE == COALAC_AGG_SUM) {
-      o = acc[it];
-    } else {
-      o = make_float4(acc[it].x * A.inv_total, acc[it].y * A.inv_total, acc[it].z * A.inv_total,
-                      acc[it].w * A.inv_total);
-    }
-    const uint32_t e = (it * 64 + lane) * 4;
-    if (hlen == HE) {
-      *reinterpret_cast<float4*>(out + e) = o;
-    } else {
-      if (e + 0 < hlen) out[e + 0] = o.x;
-      if (e + 1 < hlen) out[e + 1] = o.y;
-      if (e + 2 < hlen) out[e + 2] = o.z;
-      if (e + 3 < hlen) out[e + 3] = o.w;
-    }
-  }
+  };
+  if (hlen == HE)
+    body(std::true_type{});
+  else
+    body(std::false_type{});
 }
 
 // k_gather: n scalars of `bytes` each, from their own storage (one device pointer each), into one contiguous

@@ -208,3 +208,41 @@ def test_aggregate_many_clients_matches_oracle(cuda, ratio, delta, mode, om):
         g = out.cpu().numpy()
         for off, n in zip(plan.table.offsets, plan.table.sizes):
             np.testing.assert_array_equal(g[off:off + n].view(np.uint32), ref[off:off + n].view(np.uint32))
+
+
+@pytest.mark.parametrize("bits", [8, 32])
+@pytest.mark.parametrize("ratio", [0.01, 0.3])
+def test_aggregate_signed_zero_and_nan_base_matches_oracle(cuda, bits, ratio):
+    """x_i = base + d_i where a base of -0.0 or NaN is not base + 0.0 bit for bit: those units take the
+    kernel's generic path (base from global memory), the rest the tile path. Kept -0.0 values, a zero weight
+    for the first client (x_0 * 0 = -0.0 for negative x_0) and NaN bases compared NaN-for-NaN."""
+    sizes = [5000, 8192, 300, 4096]
+    C = 3
+    plan = CodecPlan(sizes, ratio, bits, clients=C)
+    one = CodecPlan(sizes, ratio, bits, clients=1)
+    dev = torch.device("cuda", 0)
+    flat = synth_batch(plan.table, dev, client_ids=[40 + i for i in range(C)])
+    S = plan.table.span_per_client
+    for c in range(C):  # a mostly-zero third segment: -0.0 entries get kept
+        o = c * S + int(plan.table.offsets[2])
+        flat[o:o + 300] = -0.0
+        flat[o + 7] = 0.5
+    base = synth_batch(one.table, dev, client_ids=[91])
+    base[int(plan.table.offsets[0]):int(plan.table.offsets[0]) + 5000:97] = -0.0
+    base[int(plan.table.offsets[1]) + 3] = float("nan")
+    base[int(plan.table.offsets[2]):int(plan.table.offsets[2]) + 300] = 0.0
+    enc = plan.encode(flat)
+    weights = [0, 3, 5]
+    segs = plan.table.segs.astype(np.int64)
+    h = [t.cpu().numpy() for t in (enc.idx, enc.vals, enc.mn, enc.scale)]
+    b = base.cpu().numpy()
+    for mode, om in (("recip", O.AGG_RECIP), ("sum", O.AGG_SUM)):
+        out = plan.aggregate(enc, weights, base=base, mode=mode)
+        torch.cuda.synchronize()
+        ref = O.aggregate(*h, segs, bits, C, weights, sum(weights), om, base=b, out_span=S)
+        g = out.cpu().numpy()
+        for off, n in zip(plan.table.offsets, plan.table.sizes):
+            gg, rr = g[off:off + n], ref[off:off + n]
+            nan = np.isnan(rr)
+            np.testing.assert_array_equal(np.isnan(gg), nan)
+            np.testing.assert_array_equal(gg[~nan].view(np.uint32), rr[~nan].view(np.uint32))
