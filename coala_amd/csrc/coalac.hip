@@ -39,7 +39,9 @@
 //   Decode: k_decode_lds — every output line written once, the unit's kept values placed through a per-wave
 //   LDS tile; entry ranges from the payload's per-unit starts, or from k_bounds (batches) / an in-kernel
 //   search (k_fillscatter, latency-bound plans) for a payload without them.
-//   Aggregate (fused decode + FedAvg, server side): k_aggregate (+ k_bounds without per-unit starts).
+//   Aggregate (fused decode + FedAvg, server side): k_aggregate — two waves per unit, a per-wave LDS tile
+//   holding the unkept x (base + 0), each client's kept values written in and read back in client order
+//   (+ k_bounds for payloads without per-unit starts).
 //
 // Numerics: built with -ffp-contract=off; fp32 sub/div/mul/add are separate IEEE ops, rintf is
 // round-half-even — the same op sequence as the oracle, so decoded values are bit-identical.
