@@ -843,7 +843,8 @@ class UpdateCodec:
             # set_model runs before pretrain moves the model to its device, client/base.py:138 vs :245)
             base_flat = base.flat_on(device)
         plan = self.plan_for(L.sizes_key, device)
-        ws = self._workspace(plan)
+        cur = torch.cuda.current_stream(device) if device.type == "cuda" else None  # (looked up once per call)
+        ws = self._workspace(plan, cur)
         dev_index = device.index if device.type == "cuda" else -1  # (Tensor.get_device(): -1 on the CPU)
         in_place = getattr(plan, "encode_segments", None) is not None
         if in_place:  # every segment on the plan's device, contiguous, 16-B aligned (one pass per property)
@@ -851,14 +852,15 @@ class UpdateCodec:
                 ptrs = tuple(map(_data_ptr, segs))
             # (the same storage as an encode that passed the checks: a model's parameters do not move between
             # rounds; a strides-only change of a parameter in place is not looked for)
-            if self._checked_ptrs.get(id(plan)) != ptrs:
+            last = self._checked_ptrs.get(id(plan))
+            if last is not ptrs and last != ptrs:
                 in_place = (all(map(_is_contig, segs)) and list(map(_get_device, segs)) == [dev_index] * len(segs)
                             and not any(p & 15 for p in ptrs))
                 if in_place:
                     self._checked_ptrs[id(plan)] = ptrs
         if in_place:  # read the parameters where they live: no flattening copy (+8 B/element of traffic)
             # (dtype and sizes hold by construction: the plan was made from this layout's segments)
-            enc = plan.encode_segments(segs, base=base_flat, workspace=ws, checked=True, ptrs=ptrs)
+            enc = plan.encode_segments(segs, base=base_flat, workspace=ws, checked=True, ptrs=ptrs, launch=cur)
         else:
             fs = flatten_state(state_fn(), device=device)
             enc = plan.encode(fs.flat, base=base_flat, workspace=ws)

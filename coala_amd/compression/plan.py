@@ -221,8 +221,11 @@ class CodecPlan:
             if t.data_ptr() % 16:
                 raise ValueError(f"segment {i}: storage must be 16-byte aligned")
         key = ptrs if ptrs is not None else tuple(t.data_ptr() for t in tensors)
-        cache = self.__dict__.setdefault("_segptr_cache", {})
         st = torch.cuda.current_stream(self.device) if stream is None else stream
+        last = self.__dict__.get("_segptr_last")  # the same pointer tuple object on the same stream: no hashing
+        if last is not None and last[0] is key and last[2] == st:
+            return last[1]
+        cache = self.__dict__.setdefault("_segptr_cache", {})
         d = cache.get(key)
         if d is None:
             if len(cache) >= 8:  # LRU-ish: drop the oldest entry (dicts keep insertion order)
@@ -234,13 +237,16 @@ class CodecPlan:
             d, home = d
             if home != st:
                 d.record_stream(st)
+        self._segptr_last = (key, d, st)
         return d
 
     def encode_segments(self, tensors, base=None, out=None, workspace=None, flags=0, stream=None, checked=False,
-                        ptrs=None):
+                        ptrs=None, launch=None):
         """Encode with segment i read from tensors[i] itself (coalac_encode_segptr): e.g. a model's
-        parameters, no flattening copy. base: flat fp32[span] (delta mode), as encode()."""
-        launch = torch.cuda.current_stream(self.device) if stream is None else stream
+        parameters, no flattening copy. base: flat fp32[span] (delta mode), as encode(). launch: the current
+        stream when stream is None, if the caller already has it."""
+        if launch is None:
+            launch = torch.cuda.current_stream(self.device) if stream is None else stream
         ptrs = self.segment_pointers(tensors, checked=checked, ptrs=ptrs, stream=launch)
         self._check_flat(base, "base")
         mine = out is None  # (buffers this call allocates need no checking)
