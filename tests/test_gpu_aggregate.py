@@ -248,15 +248,17 @@ def test_aggregate_signed_zero_and_nan_base_matches_oracle(cuda, bits, ratio):
             np.testing.assert_array_equal(gg[~nan].view(np.uint32), rr[~nan].view(np.uint32))
 
 
+@pytest.mark.parametrize("bits", [8, 32])
 @pytest.mark.parametrize("ratio", [0.01, 0.3])
 @pytest.mark.parametrize("delta", [True, False])
-def test_aggregate_more_than_64_clients_matches_oracle(cuda, ratio, delta):
+def test_aggregate_more_than_64_clients_matches_oracle(cuda, bits, ratio, delta):
     """70 clients: the kernel's second 64-client chunk (its metadata and entries loaded inside the client
-    loop, not with the base rows), on the fast path (0.01) and the generic one (0.3)."""
+    loop, not with the base rows), on the fast path (0.01) and the generic one (0.3), with and without an
+    averaging mask."""
     sizes = [300, 5000, 4097, 8192]
     C = 70
-    plan = CodecPlan(sizes, ratio, 8, clients=C)
-    one = CodecPlan(sizes, ratio, 8, clients=1)
+    plan = CodecPlan(sizes, ratio, bits, clients=C)
+    one = CodecPlan(sizes, ratio, bits, clients=1)
     dev = torch.device("cuda", 0)
     flat = synth_batch(plan.table, dev, client_ids=[900 + i for i in range(C)])
     base = synth_batch(one.table, dev, client_ids=[901]) if delta else None
@@ -265,10 +267,12 @@ def test_aggregate_more_than_64_clients_matches_oracle(cuda, ratio, delta):
     segs = plan.table.segs.astype(np.int64)
     h = [t.cpu().numpy() for t in (enc.idx, enc.vals, enc.mn, enc.scale)]
     b = None if base is None else base.cpu().numpy()
-    for mode, om in (("recip", O.AGG_RECIP), ("div", O.AGG_DIV)):
-        out = plan.aggregate(enc, weights, base=base, mode=mode)
+    for mode, om, am in (("recip", O.AGG_RECIP, None), ("div", O.AGG_DIV, None),
+                         ("sum", O.AGG_SUM, [True, False, True, False])):
+        out = plan.aggregate(enc, weights, base=base, mode=mode, avg_mask=am)
         torch.cuda.synchronize()
-        ref = O.aggregate(*h, segs, 8, C, weights, sum(weights), om, base=b, out_span=plan.table.span_per_client)
+        ref = O.aggregate(*h, segs, bits, C, weights, sum(weights), om, base=b, out_span=plan.table.span_per_client,
+                          avg_mask=am)
         g = out.cpu().numpy()
         for off, n in zip(plan.table.offsets, plan.table.sizes):
             np.testing.assert_array_equal(g[off:off + n].view(np.uint32), ref[off:off + n].view(np.uint32))
