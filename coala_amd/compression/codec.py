@@ -1081,9 +1081,10 @@ class UpdateCodec:
             base_flat = base.flat_on(device)
         state = OrderedDict()
         flat = None
-        offs = None
         if params_only:
             pnames = {n for n, _ in template.named_parameters(remove_duplicate=False)}
+        raw_avg = _aggregate_raw(updates, weights, total, mode, device,
+                                 keep=(lambda n: n not in pnames) if params_only else None)
         if sizes:
             C = len(updates)
             plan = self.plan_for(sizes, device, ratio=h0["ratio"], bits=h0["bits"], clients=C)
@@ -1095,13 +1096,11 @@ class UpdateCodec:
                 pnames = {n for n, _ in template.named_parameters(remove_duplicate=False)}
                 avg_mask = [e["name"] in pnames for e in h0["entries"] if e["kind"] == "seg"]
             flat = plan.aggregate(batched, weights, total=total, base=base_flat, mode=mode, avg_mask=avg_mask)
-            offs = plan.table.offsets
-        raw_avg = _aggregate_raw(updates, weights, total, mode, device,
-                                 keep=(lambda n: n not in pnames) if params_only else None)
+        # the fp32 entries: one split of the output (_segment_views), not a slice + view per entry
+        seg_views = iter(_segment_views(flat, plan.table, h0["entries"])) if sizes else None
         for e in h0["entries"]:
             if e["kind"] == "seg":
-                o = offs[e["seg"]]
-                state[e["name"]] = flat[o:o + e["n"]].view(e["shape"])
+                state[e["name"]] = next(seg_views)
             elif raw_avg is not None:
                 state[e["name"]] = raw_avg[e["name"]]
             elif params_only and e["name"] not in pnames:  # a buffer: update 0's (deepcopy(models[0]))
@@ -1129,11 +1128,20 @@ def _aggregate_raw(updates, weights, total, mode, device, keep=None):
     if any([(f.dtype, f.numel(), tuple(m)) for f, m in r._groups] != sig for r in raws[1:]):
         return None
     out = {}
+    int_weights = all(type(w) is int and -(1 << 62) < w < (1 << 62) for w in weights)
     for gi, (f0, members) in enumerate(g0):
-        acc = f0.to(device, copy=True)
-        acc *= weights[0]
-        for i in range(1, len(raws)):
-            acc += raws[i]._groups[gi][0].to(device) * weights[i]
+        if int_weights and f0.dtype in (torch.int64, torch.int32) and len(raws) > 2:
+            # integer entries, integer weights: two's-complement sums do not depend on their order, so the
+            # update-order loop is one stacked product and sum (3 launches instead of 2 per update), cast back
+            # to the entry dtype (the loop's in-place ops wrap the same way)
+            X = torch.stack([r._groups[gi][0].to(device) for r in raws])
+            W = torch.tensor(weights, dtype=torch.int64, device=device)
+            acc = (X.to(torch.int64) * W[:, None]).sum(0).to(f0.dtype)
+        else:
+            acc = f0.to(device, copy=True)
+            acc *= weights[0]
+            for i in range(1, len(raws)):
+                acc += raws[i]._groups[gi][0].to(device) * weights[i]
         if mode != "sum":
             acc = torch.div(acc, total).to(acc.dtype)
         first = f0.to(device, copy=True) if keep is not None else None
