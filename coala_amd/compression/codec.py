@@ -1081,10 +1081,22 @@ class UpdateCodec:
             base_flat = base.flat_on(device)
         state = OrderedDict()
         flat = None
+        # the output module is recycled like decode_module's (the same pool: modules this codec returned that
+        # nothing outside it references any more); not for params_only, whose buffers are update 0's values
+        recipe = D = sk = root = None
+        if not params_only and isinstance(updates[0].raw, RawState):
+            D = _decode_layout(h0["entries"])
+            recipe = _recipe(template)
+            sk = recipe.idle_skeleton(D, updates[0].raw, device)
+            if sk is not None:
+                root = sk.root  # (taken at once, as decode_module does: no longer idle for other threads)
         if params_only:
             pnames = {n for n, _ in template.named_parameters(remove_duplicate=False)}
+        accs = []
         raw_avg = _aggregate_raw(updates, weights, total, mode, device,
-                                 keep=(lambda n: n not in pnames) if params_only else None)
+                                 keep=(lambda n: n not in pnames) if params_only else None, accs=accs)
+        if raw_avg is None:  # (the passthrough entries are combined one by one below: nothing to recycle into)
+            recipe = sk = root = None
         if sizes:
             C = len(updates)
             plan = self.plan_for(sizes, device, ratio=h0["ratio"], bits=h0["bits"], clients=C)
@@ -1095,7 +1107,15 @@ class UpdateCodec:
             if params_only:
                 pnames = {n for n, _ in template.named_parameters(remove_duplicate=False)}
                 avg_mask = [e["name"] in pnames for e in h0["entries"] if e["kind"] == "seg"]
-            flat = plan.aggregate(batched, weights, total=total, base=base_flat, mode=mode, avg_mask=avg_mask)
+            flat = plan.aggregate(batched, weights, total=total, base=base_flat, mode=mode, avg_mask=avg_mask,
+                                  out=None if sk is None else sk.flat)
+            if sk is not None and flat.data_ptr() != sk.flat.data_ptr():  # a backend that returns its own buffer
+                sk = root = None
+        if sk is not None:
+            for dst, acc in zip(sk.raws, accs):
+                dst.copy_(acc, non_blocking=True)
+            recipe.refresh(sk)
+            return root
         # the fp32 entries: one split of the output (_segment_views), not a slice + view per entry
         seg_views = iter(_segment_views(flat, plan.table, h0["entries"])) if sizes else None
         for e in h0["entries"]:
@@ -1111,15 +1131,22 @@ class UpdateCodec:
                 for i in range(1, len(updates)):
                     acc += updates[i].raw[e["name"]].to(device) * weights[i]
                 state[e["name"]] = acc if mode == "sum" else torch.div(acc, total).to(acc.dtype)
+        if recipe is not None:
+            # no view of the output may outlive this frame beside the module's own: the pool's idle
+            # fingerprint is taken inside build_and_adopt
+            box = [state]
+            del state, seg_views, raw_avg
+            return recipe.build_and_adopt(box, D, flat, accs, updates[0].raw, device)
         return module_with_state(template, state)
 
 
-def _aggregate_raw(updates, weights, total, mode, device, keep=None):
+def _aggregate_raw(updates, weights, total, mode, device, keep=None, accs=None):
     """The passthrough entries of several updates combined as the per-entry loop in UpdateCodec.aggregate
     does — acc = x_0 * w_0; acc += x_i * w_i in update order; then torch.div(acc, total) cast back (not in
     mode "sum"); entries for which keep(name) is true take update 0's value — but with the same elementwise
     ops on each dtype group's flat tensor at once (a BatchNorm model's 53 counters: 2 ops per update instead
-    of 2 per update and counter). None when the updates' RawStates are not grouped alike."""
+    of 2 per update and counter). None when the updates' RawStates are not grouped alike. accs (a list):
+    receives each dtype group's result buffer, the storage the returned entries view."""
     raws = [u.raw for u in updates]
     if not all(isinstance(r, RawState) for r in raws):
         return None
@@ -1144,6 +1171,8 @@ def _aggregate_raw(updates, weights, total, mode, device, keep=None):
                 acc += raws[i]._groups[gi][0].to(device) * weights[i]
         if mode != "sum":
             acc = torch.div(acc, total).to(acc.dtype)
+        if accs is not None:
+            accs.append(acc)
         first = f0.to(device, copy=True) if keep is not None else None
         views = raws[0]._make_views([(acc, members)])
         firsts = raws[0]._make_views([(first, members)]) if first is not None else None

@@ -326,7 +326,9 @@ class CodecPlan:
                 if len(avg_mask) != len(self.table.sizes):
                     raise ValueError(f"avg_mask: need {len(self.table.sizes)} entries, got {len(avg_mask)}")
                 m = torch.tensor([1 if x else 0 for x in avg_mask], dtype=torch.uint8).to(self.device)
-        self._check_flat(out, "output", n_out)
+        # (the kernel writes the segments' elements only: an output that ends with the last segment suffices,
+        # e.g. a decoded module's buffer, which has no trailing alignment pad)
+        self._check_flat(out, "output", self.table.offsets[-1] + self.table.sizes[-1] if self.table.sizes else 0)
         if ws.device != self.device or ws.numel() * ws.element_size() < self.dec_ws_bytes:
             raise ValueError(f"aggregate workspace: need {self.dec_ws_bytes} bytes on {self.device}")
         total = float(sum(weights)) if total is None else float(total)
