@@ -1043,7 +1043,8 @@ class UpdateCodec:
 
     # -- fused server-side aggregation ------------------------------------------------------------
     def aggregate(self, updates, weights, template, base=None, mode="recip", device=None, params_only=False):
-        """Fused decode + FedAvg of several CompressedUpdates of one layout -> new nn.Module.
+        """Fused decode + FedAvg of several CompressedUpdates of one layout -> nn.Module (recycled from the
+        decode pool once idle, as decode_module's are: a dropped earlier result is aggregated into).
 
         Equivalent to decode_module() of every update followed by the reference's
         strategies.federated_averaging(models, weights) (coala/server/strategies.py:6-29, 57-90), with
