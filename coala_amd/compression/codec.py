@@ -62,6 +62,8 @@ class HipBackend:
         if t0.device.type != "cuda":
             return None
         dev, size = t0.device, t0.element_size()
+        if size not in (1, 2, 4, 8):  # (coalac_gather copies 1/2/4/8-byte elements; complex128 is stacked)
+            return None
         ptrs = tuple(map(_data_ptr, ts)) if described is None else described.raw_ptrs
         if described is None or described.raw_ok is None:
             ok = list(map(_get_device, ts)) == [dev.index] * len(ts) and not any(p % size for p in ptrs)
@@ -756,9 +758,12 @@ class UpdateCodec:
         mode:  "delta" encodes w_local - w_global (decode adds w_global back, fused in the kernel);
                "weights" encodes the weights themselves.
         backend: object with make_plan(sizes, ratio, bits, device); default HipBackend.
+        recycle: decode_module / aggregate decode into a module this codec returned earlier once nothing
+               outside the codec references it (_TreeRecipe.idle_skeleton); False builds a new module
+               every call. release_pool() drops every pooled module.
     """
 
-    def __init__(self, ratio=0.01, bits=8, mode="delta", backend=None):
+    def __init__(self, ratio=0.01, bits=8, mode="delta", backend=None, recycle=True):
         if not (0.0 < float(ratio) <= 1.0):
             raise ValueError(f"ratio must be in (0, 1], got {ratio}")
         if bits not in VALID_BITS:
@@ -766,6 +771,7 @@ class UpdateCodec:
         if mode not in MODES:
             raise ValueError(f"mode must be one of {MODES}, got {mode}")
         self.ratio, self.bits, self.mode = float(ratio), int(bits), mode
+        self.recycle = bool(recycle)
         self.backend = backend if backend is not None else HipBackend()
         self._plans = {}
         self._plan_fast = OrderedDict()  # (id(sizes), ratio, bits, clients) -> (sizes, device, plan)
@@ -797,6 +803,13 @@ class UpdateCodec:
                 p = self.backend.make_plan(list(sizes), ratio, bits, device, clients=clients)
                 self._plans[key] = p
         return p
+
+    @staticmethod
+    def release_pool():
+        """Drop every pooled decoded module (of every template): their storage is freed once their holders
+        drop them too. For a server that ends training or changes its model; the pool also evicts trees
+        unused for a while (_TreeRecipe.idle_skeleton) and is bounded by the device's memory."""
+        release_decode_pool()
 
     # -- encode -----------------------------------------------------------------------------------
     def encode(self, state, base=None, device=None):
@@ -851,8 +864,12 @@ class UpdateCodec:
             if ptrs is None:
                 ptrs = tuple(map(_data_ptr, segs))
             # (the same storage as an encode that passed the checks: a model's parameters do not move between
-            # rounds; a strides-only change of a parameter in place is not looked for)
+            # rounds; contiguity is re-read every call — a parameter re-strided in place keeps its start,
+            # `p.data = p.data.t()`, and would otherwise be read in storage order)
             last = self._checked_ptrs.get(id(plan))
+            if (last is ptrs or last == ptrs) and not all(map(_is_contig, segs)):
+                self._checked_ptrs.pop(id(plan), None)
+                last = None
             if last is not ptrs and last != ptrs:
                 in_place = (all(map(_is_contig, segs)) and list(map(_get_device, segs)) == [dev_index] * len(segs)
                             and not any(p & 15 for p in ptrs))
@@ -981,8 +998,9 @@ class UpdateCodec:
                 cur = torch.cuda.current_stream(device)
                 side = self._thread_stream(device)
                 side.wait_stream(cur)
-                # (the caller's stream's pool; a recycled skeleton's buffer is only reused once its consumers,
-                # ordered on that stream, are done: the side stream waits for it above)
+                if into is not None:  # a recycled tree: after its previous holder's work (_reuse_after)
+                    _reuse_after(into, side, cur)
+                # (the caller's stream's pool)
                 out = into.flat if into is not None else torch.empty(plan.span, dtype=torch.float32, device=device)
                 with torch.cuda.stream(side):
                     enc = update.encoded_to(device, staging=self._staging)
@@ -994,6 +1012,8 @@ class UpdateCodec:
                             dst.copy_(src, non_blocking=True)
                 cur.wait_stream(side)
             else:
+                if into is not None:
+                    _reuse_after(into, None, None)
                 enc = update.encoded.to(device, non_blocking=True)
                 flat = plan.decode(enc, base=base_flat, out=None if into is None else into.flat)
                 if into is not None:
@@ -1031,15 +1051,15 @@ class UpdateCodec:
         D = _decode_layout(update.header["entries"])
         recipe = _recipe(template)
         device = self.backend.default_device() if D.sizes else None
-        sk = recipe.idle_skeleton(D, update.raw, device)
+        # (the root comes back taken under the pool lock: no other thread can be handed this tree)
+        sk, root = recipe.idle_skeleton(D, update.raw, device) if self.recycle else (None, None)
         if sk is not None:
-            root = sk.root  # (a reference of this frame: the skeleton is no longer idle for other threads)
             self._decode(update, base, device, into=sk)
             recipe.refresh(sk)
             return root
         box = [None]
         box[0], flat, raws = self._decode(update, base, device)  # (the state lives in `box` only)
-        return recipe.build_and_adopt(box, D, flat, raws, update.raw, device)
+        return recipe.build_and_adopt(box, D, flat, raws, update.raw, device, adopt=self.recycle)
 
     # -- fused server-side aggregation ------------------------------------------------------------
     def aggregate(self, updates, weights, template, base=None, mode="recip", device=None, params_only=False):
@@ -1085,12 +1105,13 @@ class UpdateCodec:
         # the output module is recycled like decode_module's (the same pool: modules this codec returned that
         # nothing outside it references any more); not for params_only, whose buffers are update 0's values
         recipe = D = sk = root = None
-        if not params_only and isinstance(updates[0].raw, RawState):
+        if self.recycle and not params_only and isinstance(updates[0].raw, RawState):
             D = _decode_layout(h0["entries"])
             recipe = _recipe(template)
-            sk = recipe.idle_skeleton(D, updates[0].raw, device)
+            sk, root = recipe.idle_skeleton(D, updates[0].raw, device)  # (root taken under the pool lock)
             if sk is not None:
-                root = sk.root  # (taken at once, as decode_module does: no longer idle for other threads)
+                cur = torch.cuda.current_stream(device) if device.type == "cuda" else None
+                _reuse_after(sk, cur, cur)  # the kernel runs on the current stream
         if params_only:
             pnames = {n for n, _ in template.named_parameters(remove_duplicate=False)}
         accs = []
@@ -1236,6 +1257,7 @@ class _TreeRecipe:
 
     def __init__(self, template):
         self.pool, self.pool_lock = [], threading.Lock()
+        self.tick = 0  # idle_skeleton calls so far (a pooled tree's last use is one of these)
         self.mods, self.prefixes, self.index = [], [], {}
         stack = [(template, "")]
         while stack:
@@ -1393,23 +1415,39 @@ class _TreeRecipe:
     # -- recycling of decoded modules (UpdateCodec.decode_module) ------------------------------------------
     POOL_MAX = 64            # skeletons kept per template (a server needs two rounds' uploads: 2 x clients)
     POOL_BYTES = 16 << 30    # ... and at most this many bytes of decoded storage
+    POOL_FRACTION = 8        # ... nor more than 1/8 of the device's memory
+    EVICT_SLACK = 16         # a tree not handed out for 2 x pool size + this many calls is dropped from the pool
 
-    def build_and_adopt(self, box, D, flat, raws, raw, device):
+    def pool_limit(self, device):
+        lim = self.__dict__.get("_pool_limit")
+        if lim is None or lim[0] != device:
+            total = None
+            if device is not None and device.type == "cuda":
+                total = torch.cuda.get_device_properties(device).total_memory
+            lim = self._pool_limit = (device, self.POOL_BYTES if total is None else
+                                      min(self.POOL_BYTES, total // self.POOL_FRACTION))
+        return lim[1]
+
+    def build_and_adopt(self, box, D, flat, raws, raw, device, adopt=True):
         """Build the module tree for the decoded state in box (a one-element list, emptied here: the caller
         keeps no reference to the state) and keep it in the pool as a skeleton for later decodes of the same
-        layout. Returns the root module."""
+        layout (unless adopt is False). Returns the root module."""
         state = box.pop()
         new = self._build(state)
         del state
         root = new[0]
-        if (flat is None and not raws) or not isinstance(raw, RawState) or len(self.pool) >= self.POOL_MAX:
+        if (not adopt or (flat is None and not raws) or not isinstance(raw, RawState)
+                or len(self.pool) >= self.POOL_MAX):
             return root
         nbytes = (flat.numel() * 4 if flat is not None else 0) + sum(r.numel() * r.element_size() for r in raws or ())
+        limit = self.pool_limit(device)
+        stream = torch.cuda.current_stream(device) if device is not None and device.type == "cuda" else None
         with self.pool_lock:
-            if sum(sk.nbytes for sk in self.pool) + nbytes > self.POOL_BYTES or len(self.pool) >= self.POOL_MAX:
+            if sum(sk.nbytes for sk in self.pool) + nbytes > limit or len(self.pool) >= self.POOL_MAX:
                 return root
             sk = _Skeleton(root, new, flat, list(raws or ()), D, raw.signature(), device, nbytes)
             sk.adopt(self)
+            sk.stream, sk.last = stream, self.tick
             del new
             sk.base = sk.counts()
             sk.base[0][0] -= 1  # the root: this frame's `root` is the only transient reference
@@ -1419,17 +1457,28 @@ class _TreeRecipe:
     def idle_skeleton(self, D, raw, device):
         """A pooled skeleton of this layout that nothing outside the pool references any more (every module,
         parameter and buffer object at its idle reference count, the decoded storage at its idle use count,
-        every module's tables unchanged), or None."""
+        every module's tables unchanged) and its root — (None, None) if there is none. The root is taken
+        while the pool lock is held, so the moment a tree is chosen it is no longer idle for any other
+        thread (the remote server decodes from one thread per upload, coala/server/service.py:74).
+        Trees not handed out for a while (2 x the pool size + EVICT_SLACK calls: more than a round needs)
+        are dropped from the pool."""
         if not self.pool or not isinstance(raw, RawState):
-            return None
+            return None, None
         self._current()
         sig = raw.signature()
         with self.pool_lock:
+            self.tick += 1
+            found = root = None
             for sk in self.pool:
                 if sk.D is D and sk.device == device and sk.raw_sig == sig and sk.counts() == sk.base:
-                    sk.generation += 1  # (the caller takes `sk.root` before releasing the lock's protection)
-                    return sk
-        return None
+                    found, root = sk, sk.root
+                    sk.generation += 1
+                    sk.last = self.tick
+                    break
+            horizon = 2 * len(self.pool) + self.EVICT_SLACK
+            if any(self.tick - sk.last > horizon for sk in self.pool):
+                self.pool[:] = [sk for sk in self.pool if self.tick - sk.last <= horizon]
+            return found, root
 
     def refresh(self, sk):
         """Bring a recycled tree's attributes in line with the template's CURRENT ones, as a fresh build would:
@@ -1490,7 +1539,7 @@ class _Skeleton:
     reference counts."""
 
     __slots__ = ("root", "mods", "objs", "dicts", "dlens", "tables", "tsizes", "flat", "raws", "D", "raw_sig",
-                 "device", "nbytes", "base", "generation", "p_dst", "fresh")
+                 "device", "nbytes", "base", "generation", "p_dst", "fresh", "stream", "last")
 
     def __init__(self, root, mods, flat, raws, D, raw_sig, device, nbytes):
         self.root, self.mods = root, mods
@@ -1504,6 +1553,7 @@ class _Skeleton:
         self.tsizes = list(map(len, self.tables))
         self.flat, self.raws, self.D, self.raw_sig, self.device, self.nbytes = flat, raws, D, raw_sig, device, nbytes
         self.generation = 0
+        self.stream, self.last = None, 0
 
     def adopt(self, recipe):
         """The recipe's flat refresh tables for this tree: where each plain attribute goes, and the tree's own
@@ -1541,6 +1591,30 @@ def _recipe(template):
                 for k in [k for k, (r, _) in _RECIPES.items() if r() is None]:
                     del _RECIPES[k]
     return hit[1]
+
+
+def release_decode_pool():
+    """Drop every template's pooled decoded modules (UpdateCodec.release_pool)."""
+    with _RECIPES_LOCK:
+        recipes = [r for _, r in _RECIPES.values()]
+    for r in recipes:
+        with r.pool_lock:
+            r.pool.clear()
+
+
+def _reuse_after(sk, stream, caller):
+    """Order a recycled tree's rewrite after its previous holder's work and retire stale autograd state.
+    `stream` (None on the CPU) is where the rewrite runs, `caller` the caller's current stream (the stream
+    the module is handed out on). The host reference counts that made the tree idle do not see GPU work:
+    the rewrite waits for everything enqueued so far on the stream the tree was last handed out on (where
+    its holder's work ran, unless the holder moved it to another stream itself — torch's own contract for
+    that is Tensor.record_stream, which a recycled tree cannot honour: pass recycle=False then). The decode
+    kernel writes through raw pointers, so the storage's version counter is bumped here: an autograd graph
+    that saved the previous values raises in backward instead of using the new ones."""
+    if stream is not None and sk.stream is not None and sk.stream != stream and sk.stream != caller:
+        stream.wait_stream(sk.stream)  # (the rewrite's stream already waits for the caller's)
+    sk.stream = caller
+    torch._C._increment_version([t for t in [sk.flat] + sk.raws if t is not None])
 
 
 def module_with_state(template, state):

@@ -92,11 +92,13 @@ class _CodecOwner:
     codec_bits = 8
     codec_mode = "delta"
     codec_backend = None
+    codec_recycle = True  # decoded modules are reused once released (UpdateCodec recycle; False: never)
 
     def _codec(self):
         c = self.__dict__.get("_update_codec")
         if c is None:
-            c = UpdateCodec(self.codec_ratio, self.codec_bits, self.codec_mode, self.codec_backend)
+            c = UpdateCodec(self.codec_ratio, self.codec_bits, self.codec_mode, self.codec_backend,
+                            recycle=self.codec_recycle)
             self.__dict__["_update_codec"] = c
         return c
 

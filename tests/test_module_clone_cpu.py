@@ -5,6 +5,8 @@ attributes follow the template's CURRENT values (the recipe is cached per templa
 state walk (module_tensors) returns exactly state_dict()'s names and storage, and follows changes."""
 import copy
 
+import pytest
+
 import torch
 from torch import nn
 
@@ -233,3 +235,95 @@ def test_recycling_checks_attributes_tables_and_template_children():
     m = codec.decode_module(ups[1], g, base=base)
     got = getattr(m, name)
     assert got is not new_child and got is not child and got.tag == 7 and _equal_state(m, fresh[1])
+
+
+def test_recycler_hands_one_idle_module_to_one_thread_only(monkeypatch):
+    """Two upload threads (the remote server runs decompression in one thread per upload,
+    coala/server/service.py:74) that both find the same idle pooled tree must not both decode into it: a
+    barrier injected right after idle_skeleton returns forces both threads through the window between the
+    idle check and the caller taking the tree."""
+    import threading
+    from coala_amd.compression.codec import _TreeRecipe
+    codec, g, base, ups, fresh = _codec_round(seed_global=3)
+    m = codec.decode_module(ups[0], g, base=base)
+    del m  # one idle tree in the pool
+    orig = _TreeRecipe.idle_skeleton
+    barrier = threading.Barrier(2, timeout=30)
+
+    def forced(self, *a, **kw):
+        res = orig(self, *a, **kw)
+        barrier.wait()  # both threads have checked idleness before either decodes
+        return res
+    monkeypatch.setattr(_TreeRecipe, "idle_skeleton", forced)
+    out, errs = [None, None], []
+
+    def run(i):
+        try:
+            out[i] = codec.decode_module(ups[1 + i], g, base=base)
+        except Exception as e:  # pragma: no cover - reported below
+            errs.append(e)
+    ts = [threading.Thread(target=run, args=(i,)) for i in range(2)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    assert not errs
+    assert out[0] is not out[1]
+    assert _equal_state(out[0], fresh[1]) and _equal_state(out[1], fresh[2])
+
+
+def test_recycled_storage_bumps_the_version_counter():
+    """A live autograd graph that saved a decoded parameter keeps its tree out of reuse (the saved tensor holds
+    the parameter object); a recycled tree's storage, written through raw pointers, has its version counter
+    bumped, so anything that still saved it raises in backward instead of using the new values."""
+    codec, g, base, ups, fresh = _codec_round(seed_global=4)
+    m = codec.decode_module(ups[0], g, base=base)
+    p = next(m.parameters())
+    loss = (p * p).sum()  # saves p for backward
+    first = id(m)
+    del m, p
+    m = codec.decode_module(ups[1], g, base=base)
+    assert id(m) != first and _equal_state(m, fresh[1])
+    loss.backward()  # the saved values were never overwritten
+    del loss, m
+    m = codec.decode_module(ups[2], g, base=base)  # one of the two idle trees
+    ids = set()
+    for i in range(3):  # the same tree again and again: its version moves every time
+        vs = next(m.parameters())._version
+        mid = id(m)
+        del m
+        m = codec.decode_module(ups[i], g, base=base)
+        if id(m) == mid:
+            ids.add(mid)
+            assert next(m.parameters())._version > vs
+    assert ids
+
+
+def test_pool_release_eviction_and_opt_out():
+    """release_pool() empties the pool; trees not handed out for a while are evicted; recycle=False never
+    pools or reuses a module."""
+    from coala_amd.compression import UpdateCodec
+    from coala_amd.compression.codec import _TreeRecipe, _recipe
+    from tests.oracle_backend import OracleBackend
+    codec, g, base, ups, fresh = _codec_round(seed_global=5)
+    ms = [codec.decode_module(u, g, base=base) for u in ups]
+    rec = _recipe(g)
+    assert len(rec.pool) == 3
+    codec.release_pool()
+    assert not rec.pool
+    # eviction: with the pool of 3, trees 1 and 2 stay held while tree 0 is reused again and again
+    ms = [codec.decode_module(u, g, base=base) for u in ups]
+    keep = ms[1:]
+    del ms
+    for i in range(2 * 3 + _TreeRecipe.EVICT_SLACK + 3):
+        m = codec.decode_module(ups[i % 3], g, base=base)
+        del m
+    assert len(rec.pool) == 1  # the held trees were not handed out for longer than the horizon
+    assert all(_equal_state(k, fresh[1 + j]) for j, k in enumerate(keep))  # (evicted, not overwritten)
+    # opt-out
+    off = UpdateCodec(0.05, 8, "delta", OracleBackend(), recycle=False)
+    codec.release_pool()
+    a = off.decode_module(ups[0], g, base=base)
+    b = off.decode_module(ups[1], g, base=base)
+    assert not rec.pool and a is not b
+    assert _equal_state(a, fresh[0]) and _equal_state(b, fresh[1])
