@@ -17,6 +17,12 @@ collective on the data path — torch.distributed only for the barrier and the m
           concurrent uploads, one thread each: coala/server/service.py:71-111)
   plugin  the hooks' own path per ResNet-50 client, delta mode: client compression() encoding the trained
           module's parameters in place + server decompression(model) into a new module on w_global
+  C3_delta   the C3 share in delta mode (what the plugin runs by default: w_local - w_global on encode, + w_global
+          fused into the decode; +8N bytes per client, SURVEY.md §8(d) "report these variants separately")
+  C3_r0.001 / C3_r0.1  the C3 share at the other BASELINE.md top-k ratios
+  C4_delta   the C4 share in delta mode
+  C4_frozen  the C4 share in delta mode with the backbone frozen as FedPEFT does (application/FedPEFT/lora.py:64,
+          main.py:62-67): every tensor but the classifier head is an exact-zero delta
 value = 4 * N * clients * steps / elapsed (GB/s of fp32 update processed, whole job).
 roofline: the dominant kernel's algorithmic bytes per launch / its mean HIP-event duration, vs 8 TB/s.
 cpu_baseline: the numpy oracle (oracle/codec_oracle.py) on a bounded sample of the same workload, on the
@@ -39,19 +45,31 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md: 8.0 TB/s)
 SPLIT = 2  # sub-batches per step: two independent pipelines side by side fill the CUs the other leaves
            # idle in its latency-bound stages and launch tails (+11 % over one 16-client pipeline)
 ROOF_STEPS = 8  # joined steps after the timed region that carry the per-kernel timing events
-CONFIGS = {  # name -> (layout | "c5", clients per GPU, sub-batches: the best of 1..4 on the box)
-    "C2": ("resnet18", 16, 3),
-    "C3": ("resnet50_tv", 16, SPLIT),
-    "C4": ("vit_b16", 16, SPLIT),
-    "C5": ("c5", None, 1),  # one latency-bound plan (<= 8192 units): 0.116 ms vs 0.122 as 2 sub-batches
-    "single": ("resnet50_tv", 1, "single"),
-    "single_x2": ("resnet50_tv", 1, "single"),
+CONFIGS = {  # name -> (layout | "c5", clients per GPU, sub-batches: the best of 1..4 on the box, DESIGN.md §7,
+             #          options: ratio / mode / frozen override the command line's for that config)
+    "C2": ("resnet18", 16, 3, {}),
+    "C3": ("resnet50_tv", 16, SPLIT, {}),
+    "C3_delta": ("resnet50_tv", 16, SPLIT, {"mode": "delta"}),
+    "C3_r0.001": ("resnet50_tv", 16, SPLIT, {"ratio": 0.001}),
+    "C3_r0.1": ("resnet50_tv", 16, SPLIT, {"ratio": 0.1}),
+    "C4": ("vit_b16", 16, SPLIT, {}),
+    "C4_delta": ("vit_b16", 16, SPLIT, {"mode": "delta"}),
+    "C4_frozen": ("vit_b16", 16, SPLIT, {"mode": "delta", "frozen": True}),
+    "C5": ("c5", None, 1, {}),  # one latency-bound plan (<= 8192 units): 0.116 ms vs 0.122 as 2 sub-batches
+    "single": ("resnet50_tv", 1, "single", {}),
+    "single_x2": ("resnet50_tv", 1, "single", {}),
 }
 # updates in flight per extra config: single_x2 = one update per step, consecutive steps on two streams (a
 # server decodes concurrent uploads from one thread each, coala/server/service.py:71-111)
 CONFIG_INFLIGHT = {"single_x2": 2}
 SINGLE_SPLIT = 1  # segment ranges of the single update run as this many concurrent sub-plans
-DEFAULT_EXTRAS = "C2,C4,C5,single,single_x2,plugin"
+DEFAULT_EXTRAS = "C2,C3_delta,C3_r0.001,C3_r0.1,C4,C4_delta,C4_frozen,C5,single,single_x2,plugin"
+
+
+def cfg_opts(cfg, a):
+    """(ratio, mode, frozen) of a config: its own overrides, else the command line's."""
+    o = CONFIGS[cfg][3]
+    return o.get("ratio", a.ratio), o.get("mode", a.mode), bool(o.get("frozen", False))
 
 
 def parse():
@@ -241,7 +259,8 @@ def build_table(cfg, a, rank, headline):
     from coala_amd.compression import SegmentTable
     from coala_amd.layouts import fp32_sizes
     from coala_amd.workload import c5_share, mixed_table
-    layout, clients, split = CONFIGS[cfg]
+    layout, clients, split, _ = CONFIGS[cfg]
+    ratio = cfg_opts(cfg, a)[0]
     if split == "single":
         split = a.single_split
     elif not headline and a.extras_split is not None:
@@ -252,12 +271,14 @@ def build_table(cfg, a, rank, headline):
         split = a.split if a.split is not None else split
     if layout == "c5":
         ids, names = c5_share(rank)
-        return mixed_table(names, a.ratio), ids, split, {"layouts": sorted(set(names)), "clients_per_gpu": len(ids),
+        return mixed_table(names, ratio), ids, split, {"layouts": sorted(set(names)), "clients_per_gpu": len(ids),
                                                          "global_clients": 256, "grouping": "greedy LPT over 8 GPUs"}
-    t = SegmentTable(fp32_sizes(layout), a.ratio, clients)
+    t = SegmentTable(fp32_sizes(layout), ratio, clients)
     ids = list(range(rank * clients, (rank + 1) * clients))
+    _, mode, frozen = cfg_opts(cfg, a)
     return t, ids, split, {"layout": layout, "clients_per_gpu": clients, "elements_per_client": sum(t.sizes),
-                           "segments_per_client": len(t.sizes)}
+                           "segments_per_client": len(t.sizes), "ratio": ratio, "mode": mode,
+                           **({"frozen": "every tensor but the classifier head an exact-zero delta"} if frozen else {})}
 
 
 GRAPH_CONFIGS = ("single", "single_x2", "C5")  # latency-bound plans: step time ~ host launch time
@@ -278,12 +299,17 @@ def setup_workload(cfg, a, dev, rank, headline):
     import torch
 
     from coala_amd.compression import SplitPipeline
-    from coala_amd.workload import synth_batch
+    from coala_amd.workload import freeze_segments, head_only, synth_batch
 
     t, ids, split, desc = build_table(cfg, a, rank, headline)
+    _, mode, frozen = cfg_opts(cfg, a)
     rot = ROTATE if cfg in ROTATE_CONFIGS else 1
     flats = [synth_batch(t, dev, client_ids=[1000 * r + i for i in ids]) for r in range(rot)]
-    base = synth_batch(t, dev, client_ids=[10_000 + i for i in ids]) if a.mode == "delta" else None
+    base = synth_batch(t, dev, client_ids=[10_000 + i for i in ids]) if mode == "delta" else None
+    if frozen:  # trained = w_global + delta with the frozen tensors' deltas exactly zero
+        for f in flats:
+            freeze_segments(f, t, head_only(desc["layout"]))
+            f.add_(base)
     split = max(1, split)
     inflight = max(1, a.inflight) if headline else CONFIG_INFLIGHT.get(cfg, 1)
     slots = []
@@ -292,6 +318,7 @@ def setup_workload(cfg, a, dev, rank, headline):
         slots.append((p, [(p.empty_encoded(), p.empty_flat()) for _ in range(rot)]))
     torch.cuda.synchronize()
     return {"cfg": cfg, "headline": headline, "table": t, "desc": desc, "flats": flats, "base": base, "rot": rot,
+            "mode": mode,
             "slots": slots, "split": slots[0][0].n_parts, "graphs": None, "graph_error": None,
             "fill_ahead": a.fill_ahead == "on"}
 
@@ -435,7 +462,7 @@ def time_workload(W, a, dev, world):
         per = [union([(e[1], e[2]) for e in which[i]]) for i in timed_steps]
         stages[name] = sum(per) / len(per)
     N, K, T = t.n_elements, t.total_k, t.n_segments
-    delta = a.mode == "delta"
+    delta = W["mode"] == "delta"
     vb = 4 if a.bits == 32 else 1
     large_elems = large_elements(pipes[0])
     alg = {  # algorithmic HBM bytes per timed interval

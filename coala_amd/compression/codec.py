@@ -699,6 +699,10 @@ def validate(header, idx, ustart=None):
             while len(_VALIDATED) > 32:
                 _VALIDATED.popitem(last=False)
     _, ns_rep, first, units = hit
+    if header.get("dense"):  # implied indices (0..n-1 per segment): nothing to check beyond the layout
+        if idx.size != 0 or ustart is not None:
+            raise ValueError("COALAQ1: a dense update carries no indices or starts")
+        return
     if idx.size != int(header["total_k"]):
         raise ValueError("COALAQ1: kept-entry count mismatch")
     if ustart is not None and (units is None or int(header.get("n_units", -1)) != units[0].size

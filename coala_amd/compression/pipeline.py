@@ -146,13 +146,14 @@ class SplitPipeline:
     def empty_encoded(self):
         d, vt = self.device, torch.float32 if self.bits == 32 else torch.uint8
         T, K, U = self.table.n_segments, self.table.total_k, self.table.n_units
-        return Encoded(torch.empty(K, dtype=torch.int32, device=d), torch.empty(K, dtype=vt, device=d),
+        implied = all(P["plan"].implied_idx for P in self.parts)  # ratio 1: no idx / starts (dense codec)
+        return Encoded(torch.empty(0 if implied else K, dtype=torch.int32, device=d), torch.empty(K, dtype=vt, device=d),
                        torch.empty(T, dtype=torch.float32, device=d), torch.empty(T, dtype=torch.float32, device=d),
-                       torch.empty(U, dtype=torch.int32, device=d))
+                       None if implied else torch.empty(U, dtype=torch.int32, device=d))
 
     @staticmethod
     def _enc(enc, P):
-        return Encoded(enc.idx[P["k"]], enc.vals[P["k"]], enc.mn[P["t"]], enc.scale[P["t"]],
+        return Encoded(enc.idx[P["k"]] if enc.idx.numel() else enc.idx, enc.vals[P["k"]], enc.mn[P["t"]], enc.scale[P["t"]],
                        None if enc.ustart is None else enc.ustart[P["u"]])
 
 

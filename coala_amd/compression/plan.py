@@ -37,6 +37,11 @@ def _ptr(t):
     return ctypes.c_void_p(t.data_ptr()) if t is not None else ctypes.c_void_p(0)
 
 
+def _idx_ptr(t):
+    """idx of an Encoded: NULL when it holds nothing (a dense plan's implied indices)."""
+    return ctypes.c_void_p(t.data_ptr()) if t is not None and t.numel() else ctypes.c_void_p(0)
+
+
 def _on(stream):
     """Allocation context for buffers a call creates itself: on the stream the kernels run on, so the
     caching allocator never hands their memory to other work before those kernels are done."""
@@ -94,6 +99,12 @@ class CodecPlan:
             raise _lib.CodecError(f"plan total_k {self.total_k} != table {self.table.total_k}")
         if self.n_units != self.table.n_units:
             raise _lib.CodecError(f"plan n_units {self.n_units} != table {self.table.n_units}")
+        # every segment keeps all its elements: the library's dense codec (indices implied, never materialised
+        # unless a caller passes a buffer for them); at ratio 1 (the wire's "dense" updates) the encoded buffers
+        # carry no idx / starts by default
+        segs = self.table.segs
+        self.dense = bool(len(segs)) and bool((segs[:, 1] == segs[:, 2]).all())
+        self.implied_idx = self.dense and getattr(self.table, "ratio", None) is not None and self.table.ratio >= 1.0
 
     @classmethod
     def from_segments(cls, segs, bits=8, device=None):
@@ -128,8 +139,18 @@ class CodecPlan:
     def empty_flat(self):
         return torch.empty(self.span, dtype=torch.float32, device=self.device)
 
-    def empty_encoded(self):
-        """The five output buffers of an encode as views of ONE allocation (16-byte aligned each)."""
+    def empty_encoded(self, with_idx=None):
+        """The five output buffers of an encode as views of ONE allocation (16-byte aligned each). with_idx
+        (default: not implied_idx): False leaves idx empty and ustart None (ratio 1: the indices are implied)."""
+        if with_idx is None:
+            with_idx = not self.implied_idx
+        if not with_idx:
+            vb = 4 if self.bits == RAW_BITS else 1
+            T = self.n_segments
+            buf = torch.empty((vb * self.total_k + 15) // 16 * 16 + 8 * T, dtype=torch.uint8, device=self.device)
+            o = (vb * self.total_k + 15) // 16 * 16
+            return Encoded(torch.empty(0, dtype=torch.int32, device=self.device), buf[:vb * self.total_k].view(self.vals_dtype),
+                           buf[o:o + 4 * T].view(torch.float32), buf[o + 4 * T:o + 8 * T].view(torch.float32), None)
         geo = self.__dict__.get("_enc_geometry")
         if geo is None:
             K, T, U = self.total_k, self.n_segments, self.n_units
@@ -165,7 +186,8 @@ class CodecPlan:
     def _check_encoded(self, e):
         """Dtype, device, contiguity and length of every encoded buffer; returns the ustart pointer to pass (its
         length must be exactly the plan's unit count: a buffer of another layout is an error, not a hint)."""
-        want = ((e.idx, torch.int32, self.total_k), (e.vals, self.vals_dtype, self.total_k),
+        want = ((e.idx, torch.int32, 0 if self.dense and e.idx.numel() == 0 else self.total_k),
+                (e.vals, self.vals_dtype, self.total_k),
                 (e.mn, torch.float32, self.n_segments), (e.scale, torch.float32, self.n_segments))
         if e.ustart is not None:
             want += ((e.ustart, torch.int32, self.n_units),)
@@ -191,7 +213,7 @@ class CodecPlan:
         ust = self._check_encoded(out)
         if ws.device != self.device or ws.numel() * ws.element_size() < self.ws_bytes:
             raise ValueError(f"workspace: need {self.ws_bytes} bytes on {self.device}")
-        args = (self._h, _ptr(flat), _ptr(base), _ptr(out.idx), _ptr(out.vals), _ptr(out.mn),
+        args = (self._h, _ptr(flat), _ptr(base), _idx_ptr(out.idx), _ptr(out.vals), _ptr(out.mn),
                 _ptr(out.scale), ust, _ptr(ws), ctypes.c_uint64(self.ws_bytes), ctypes.c_uint(flags),
                 _stream_handle(stream))
         with torch.cuda.device(self.device):
@@ -257,7 +279,7 @@ class CodecPlan:
         if ws.device != self.device or ws.numel() * ws.element_size() < self.ws_bytes:
             raise ValueError(f"workspace: need {self.ws_bytes} bytes on {self.device}")
         with _device_ctx(self.device):
-            rc = self._lib.coalac_encode_segptr(self._h, _ptr(ptrs), _ptr(base), _ptr(out.idx), _ptr(out.vals),
+            rc = self._lib.coalac_encode_segptr(self._h, _ptr(ptrs), _ptr(base), _idx_ptr(out.idx), _ptr(out.vals),
                                                 _ptr(out.mn), _ptr(out.scale), ust, _ptr(ws),
                                                 ctypes.c_uint64(self.ws_bytes), ctypes.c_uint(flags),
                                                 ctypes.c_void_p(launch.cuda_stream))
@@ -278,7 +300,7 @@ class CodecPlan:
         self._check_flat(out, "output")
         if ws.device != self.device or ws.numel() * ws.element_size() < self.dec_ws_bytes:
             raise ValueError(f"decode workspace: need {self.dec_ws_bytes} bytes on {self.device}")
-        args = (self._h, _ptr(enc.idx), _ptr(enc.vals), _ptr(enc.mn), _ptr(enc.scale), ust, _ptr(base), _ptr(out),
+        args = (self._h, _idx_ptr(enc.idx), _ptr(enc.vals), _ptr(enc.mn), _ptr(enc.scale), ust, _ptr(base), _ptr(out),
                 _ptr(ws), ctypes.c_uint64(self.dec_ws_bytes), _stream_handle(stream))
         with torch.cuda.device(self.device):
             if sched is not None:
@@ -308,6 +330,9 @@ class CodecPlan:
         ust = self._check_encoded(enc)
         if not getattr(self.table, "uniform", False):
             raise ValueError("fused aggregation needs a plan over copies of one layout (a SegmentTable)")
+        if self.dense and enc.idx.numel() == 0:  # (the aggregate kernel reads explicit indices: implied ones made here)
+            with _on(stream):
+                enc = Encoded(self.implied_indices(), enc.vals, enc.mn, enc.scale, enc.ustart)
         C = self.table.clients
         if len(weights) != C:
             raise ValueError(f"need {C} weights, got {len(weights)}")
@@ -342,6 +367,14 @@ class CodecPlan:
                 rc = self._lib.coalac_aggregate_ev(*args, _event_array(events, 3))
         _lib.check(rc, "coalac_aggregate")
         return out  # w / m were allocated on the launch stream: their memory is reused only after the kernel
+
+    def implied_indices(self):
+        """A dense plan's indices (0..n-1 per segment, every client) as a device int32 tensor, made once."""
+        t = self.__dict__.get("_implied")
+        if t is None:
+            one = torch.cat([torch.arange(n, dtype=torch.int32) for n in self.table.segs[:, 1].tolist()])
+            t = self._implied = one.to(self.device)
+        return t
 
     def fallbacks(self, workspace, stream=None):
         """Segments of the last encode with this workspace whose sampled bracket missed (synchronises)."""

@@ -142,17 +142,18 @@ class SegmentTable:
         return SegmentTable(self.sizes, self.ratio, c1 - c0)
 
     def algorithmic_bytes(self, bits=8, delta=False):
-        return algorithmic_bytes(self.n_elements, self.total_k, self.n_segments, bits, delta)
+        return algorithmic_bytes(self.n_elements, self.total_k, self.n_segments, bits, delta, self.ratio >= 1.0)
 
 
-def algorithmic_bytes(N, K, T, bits=8, delta=False):
+def algorithmic_bytes(N, K, T, bits=8, delta=False, implied_idx=False):
     """HBM bytes an ideal encode+decode moves: 8N + 10K + 32T for 8-bit codes.
 
     Encode reads 4N, writes idx (4K) + codes (1K, or 4K raw) + mn/scale/k/off (16T); decode reads
-    those and writes 4N. Delta mode adds a 4N base read on each side.
+    those and writes 4N. Delta mode adds a 4N base read on each side. implied_idx (ratio 1, the dense
+    codec): no idx is written or read — 10N + 32T for 8-bit codes.
     """
     vb = 4 if bits == RAW_BITS else 1
-    b = 8 * N + 2 * (4 + vb) * K + 32 * T
+    b = 8 * N + 2 * ((0 if implied_idx else 4) + vb) * K + 32 * T
     if delta:
         b += 8 * N
     return b

@@ -18,8 +18,9 @@ Layout (little-endian):
     index of the unit's first kept entry — what the encoder's k_select computed anyway, so the decoder (and the
     server's fused aggregate) finds each unit's entries without searching the idx lists. U = "n_units".
     A header with "dense": true (ratio 1: every segment keeps all n elements, idx = 0..n-1 per segment)
-    carries an empty idx section; unpack regenerates it. This is the download-direction default
-    (dense 8-bit weights, ~4x smaller than fp32 instead of 5 B per element with explicit indices).
+    carries an empty idx section, and unpack returns an empty idx: the indices stay implied all the way into
+    the GPU's dense decode (coalac.hip k_dense_deq), never materialised. This is the download-direction
+    default (dense 8-bit weights, ~4x smaller than fp32 instead of 5 B per element with explicit indices).
 """
 import json
 import struct
@@ -35,14 +36,6 @@ VERSION_2 = 2   # ... | vals | ustart | raw
 
 def _pad16(n):
     return (16 - n % 16) % 16
-
-
-def dense_idx(header):
-    """idx of a dense (ratio 1) update: 0..n-1 for every fp32 segment, in segment order."""
-    ns = [int(e["n"]) for e in sorted((e for e in header["entries"] if e["kind"] == "seg"), key=lambda e: e["seg"])]
-    if not ns:
-        return np.zeros(0, dtype=np.int32)
-    return np.concatenate([np.arange(n, dtype=np.int32) for n in ns])
 
 
 def pack(header, mn, scale, idx, vals, raw, header_json=None, ustart=None):
@@ -122,7 +115,7 @@ def sections(blob, header=None):
 
 def unpack(blob):
     """blob -> (header dict, mn, scale, idx, vals, raw bytes, ustart or None). Arrays are read-only views of
-    blob."""
+    blob; a "dense" blob's idx is empty (implied)."""
     mv = memoryview(blob)
     if bytes(mv[:8]) != MAGIC:
         raise ValueError("not a COALAQ1 blob (bad magic)")
@@ -148,9 +141,7 @@ def unpack(blob):
         pos += n * dt.itemsize
     pos += _pad16(pos)
     raw = bytes(mv[pos:])
-    if dense:
-        out[2] = dense_idx(header)
-        if out[2].size != K:
-            raise ValueError("COALAQ1: dense header with k != n")
+    if dense and K != sum(int(e["n"]) for e in header["entries"] if e["kind"] == "seg"):
+        raise ValueError("COALAQ1: dense header with k != n")
     ustart = out[4] if ver == VERSION_2 else None
     return (header, *out[:4], raw, ustart)

@@ -211,6 +211,7 @@ struct Params {
   uint32_t *tstar, *rtie, *status;
   // per large unit
   uint32_t *tlo, *thi, *cntA, *cntC, *gtC, *eqC, *eqpre, *outoff;
+  uint32_t* cntZ;  // per large unit of a segment whose bracket starts at key 0: its zero keys (counted, not recorded)
   uint4* uemit;  // per large unit, from k_select: {T*, tie budget | raw-path flag << 31, mn bits, scale bits}
   uint32_t* cval;  // candidate records, ccap slots per large unit, in index order: the value bits ...
   uint16_t* cpos;  // ... and the position inside the unit (the emit reads both; every select sweep the values only)
@@ -229,6 +230,8 @@ struct Params {
 
   // decode: first kept entry (segment-relative) of every unit — the payload's (wire v2) or k_bounds'
   const uint32_t* ustart;
+  // dense plans (every segment keeps all its elements): per unit the NaN-ignoring {min, max} of its values
+  float* umm;
   // diagnostics: per-block phase timestamps (COALAC_FLAG_STAMPS), NSTAMP per block, 100 MHz ticks
   uint64_t* stamps;
 };
@@ -673,9 +676,17 @@ struct Band {
 // ------------------------------------------------------------------------------------------------
 // CHECK: test each element against the unit's length. A full unit never needs it, nor does a partial one when
 // tlo > 0 (its loads past len return 0, key 0 < tlo): k_scan picks the lean form then (wave-uniform).
-template <bool DELTA, int NB, bool CHECK = true>
-DEV void scan_unit(const Params& P, uint32_t lu, const UnitDev& L, const uint32_t tlo, const uint32_t thi,
+// ZERO (the segment's bracket starts at key 0, tlo == 0: its k-th key may be a zero — a frozen or pruned tensor, an
+// all-zero delta): zero keys are COUNTED per unit (cntZ), not recorded; the candidates are the keys in [1, thi] and
+// above. The select then takes the k-th key as 0 with a tie quota over the zeros (index order) when the nonzero keys
+// number fewer than k, and only the units whose zeros that quota reaches re-read their raw data in k_emit — instead
+// of every element becoming a candidate record, every unit overflowing its slots and the whole segment taking the
+// one-block raw-data path.
+template <bool DELTA, int NB, bool CHECK = true, bool ZERO = false>
+DEV void scan_unit(const Params& P, uint32_t lu, const UnitDev& L, const uint32_t tlo_, const uint32_t thi,
                    uint2* stage) {
+  const uint32_t tlo = ZERO ? 1u : tlo_;  // (ZERO: tlo_ == 0)
+  uint32_t cz = 0;                        // zero keys this lane saw (ZERO)
   constexpr uint32_t IT = UNIT_IT / NB;
   const uint32_t lane = lane_id();
   const uint32_t len = L.len;
@@ -709,7 +720,8 @@ DEV void scan_unit(const Params& P, uint32_t lu, const UnitDev& L, const uint32_
       for (int j = 0; j < 4; ++j) {
         const uint32_t key = fkey(xs[j]);
         fc[j] = (!CHECK || e0 + j < len) && key >= tlo;
-        fa[j] = CHECK ? fc[j] && key > thi : key > thi;  // (thi >= tlo: key > thi implies a candidate)
+        fa[j] = CHECK ? fc[j] && key > thi : key > thi;  // (thi >= tlo or ZERO: key > thi implies a candidate)
+        if (ZERO) cz += ((!CHECK || e0 + j < len) && key == 0u) ? 1u : 0u;
         any = any || fc[j];
       }
       const uint32_t c = (uint32_t)fc[0] + (uint32_t)fc[1] + (uint32_t)fc[2] + (uint32_t)fc[3];
@@ -758,9 +770,14 @@ DEV void scan_unit(const Params& P, uint32_t lu, const UnitDev& L, const uint32_
     wave_fence();
     for (uint32_t i = lane; i < cC && i < STAGE_CAP; i += 64) put(i, stage[i]);
   }
+  if (ZERO) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) cz += (uint32_t)__shfl_xor((int)cz, o, 64);
+  }
   if (lane == 0) {
     P.cntA[lu] = cA;
     P.cntC[lu] = cC;
+    if (ZERO) P.cntZ[lu] = cz;
   }
 }
 
@@ -1118,7 +1135,12 @@ __global__ __launch_bounds__(NTS, WPE) void k_scan(Params P) {
   const UnitDev L = P.lunits[lu];
   // delta: 4 load batches (32 float4 in flight spill)
   const uint32_t tlo = P.tlo[lu], thi = P.thi[lu];
-  if (SCAN_LEAN && (L.len == UNIT || tlo > 0))
+  if (tlo == 0) {  // (wave-uniform: one bracket per segment)
+    if (L.len == UNIT)
+      scan_unit<DELTA, DELTA ? 4 : NB, false, true>(P, lu, L, tlo, thi, stage + wv * STAGE_CAP);
+    else
+      scan_unit<DELTA, DELTA ? 4 : NB, true, true>(P, lu, L, tlo, thi, stage + wv * STAGE_CAP);
+  } else if (SCAN_LEAN && (L.len == UNIT || tlo > 0))
     scan_unit<DELTA, DELTA ? 4 : NB, false>(P, lu, L, tlo, thi, stage + wv * STAGE_CAP);
   else
     scan_unit<DELTA, DELTA ? 4 : NB, true>(P, lu, L, tlo, thi, stage + wv * STAGE_CAP);
@@ -1440,9 +1462,10 @@ DEV uint4 segment_pick(const Params& P, const SegDev& sd, const Band& band, uint
   static_assert(HB2 == 2 * NT || HB2 == NT, "one or two histogram bins per thread");
   constexpr bool TWO = HB2 == 2 * NT;
   constexpr uint32_t GB = 24, CB = 3;
-  uint32_t h0 = 0, h1 = 0, sa = 0, sc = 0, ov = 0;
+  const bool zseg = band.tlo == 0;  // the scan counted this segment's zero keys (cntZ)
+  uint32_t h0 = 0, h1 = 0, sa = 0, sc = 0, ov = 0, sz = 0;
   {
-    uint32_t v0[GB], v1[GB], ca[CB], cc[CB];
+    uint32_t v0[GB], v1[GB], ca[CB], cc[CB], cz[CB];
 #pragma unroll
     for (uint32_t j = 0; j < GB; ++j) {
       const uint64_t row = (uint64_t)(g0 + min(j, ng - 1)) * HB2;
@@ -1454,6 +1477,7 @@ DEV uint4 segment_pick(const Params& P, const SegDev& sd, const Band& band, uint
       const uint32_t i = min(t + j * NT, nu - 1);
       cc[j] = P.cntC[lb + i];
       ca[j] = P.cntA[lb + i];
+      cz[j] = P.cntZ[lb + i];  // (unconditional; used for a zero-bracket segment only)
     }
 #pragma unroll
     for (uint32_t j = 0; j < GB; ++j) {
@@ -1465,6 +1489,7 @@ DEV uint4 segment_pick(const Params& P, const SegDev& sd, const Band& band, uint
       if (t + j * NT < nu) {
         sa += ca[j];
         sc += cc[j];
+        sz += zseg ? cz[j] : 0u;
         ov += cc[j] > P.ccap ? 1u : 0u;
       }
     }
@@ -1487,6 +1512,7 @@ DEV uint4 segment_pick(const Params& P, const SegDev& sd, const Band& band, uint
     const uint32_t c = P.cntC[lb + i];
     sa += P.cntA[lb + i];
     sc += c;
+    sz += zseg ? P.cntZ[lb + i] : 0u;
     ov += c > P.ccap ? 1u : 0u;
   }
   hist[t] = h0;
@@ -1494,9 +1520,13 @@ DEV uint4 segment_pick(const Params& P, const SegDev& sd, const Band& band, uint
   sa = block_sum<NT>(sa, sh);  // barriers inside (also publish hist)
   sc = block_sum<NT>(sc, sh);
   ov = block_sum<NT>(ov, sh);
+  if (zseg) sz = block_sum<NT>(sz, sh);
   // (a unit that overflowed its record slots sends the segment to the raw-data path in segment_select)
-  const bool generic = (P.flags & (COALAC_FLAG_FORCE_EXACT | COALAC_FLAG_GENERIC_SELECT)) || !(sa < k && k <= sc) ||
-                       nu > UCAP || ov != 0;
+  const bool forced = (P.flags & (COALAC_FLAG_FORCE_EXACT | COALAC_FLAG_GENERIC_SELECT)) || nu > UCAP || ov != 0;
+  // the k-th key is a zero: every recorded key (all nonzero) is kept, and the first k - sc zeros by index. The
+  // window [1, 0] is empty: k_gwin counts every record as above it (per-unit kept counts) and takes their min / max
+  if (!forced && zseg && sc < k && k - sc <= sz) return make_uint4(1u, 0u, k - sc, 2u);
+  const bool generic = forced || !(sa < k && k <= sc);
   if (generic) return make_uint4(0u, 0u, 0u, 1u);
   __syncthreads();
   uint32_t r = k - sa;
@@ -1593,7 +1623,7 @@ DEV void group_pick_window(const Params& P, uint32_t gi, GwinSmemT<NT / 64>& W, 
   sw.load(P, G.y, G.z, W.upre, sh);
   const uint4 st = segment_pick<NT>(P, sd, Band(tlo, thi, hh), hist, sh);
   STAMP(P, G.x, 23);
-  if (st.w == 0) group_window<NT>(P, gi, G, st, GS.x, sw, W, sh);
+  if (st.w == 0 || st.w == 2) group_window<NT>(P, gi, G, st, GS.x, sw, W, sh);
   if (threadIdx.x == 0 && G.y == GS.x) {  // the segment's first group
     uint2* ss = reinterpret_cast<uint2*>(P.sstate + G.x);
     pst(P, ss, make_uint2(st.x, st.y));
@@ -1816,7 +1846,24 @@ DEV void segment_select(const Params& P, uint32_t li, SelSmem& S) {
   STAMP(P, li, 0);
   uint32_t T, rt, fp_rank, fn_rank;
   float gmn, gmx;
-  bool done = st.w == 0 && select_from_groups<NT>(P, sd, lb, nu, st, S, T, rt, fp_rank, fn_rank, gmn, gmx);
+  const bool zero_tie = st.w == 2;  // the k-th key is a zero (segment_pick)
+  bool done;
+  if (zero_tie) {
+    // every record kept (k_gwin's per-unit counts above the empty window), the first rt zeros by index; a zero's
+    // sign does not matter to mn / scale (canonicalised + 0.0f below), so one "positive tie" stands for them
+    const uint32_t g0 = sd.g_begin, ng = (nu + GU - 1) / GU;  // ng <= UCAP / GU <= NT
+    gmn = t < ng ? P.gmm[2 * (g0 + t)] : qnan();
+    gmx = t < ng ? P.gmm[2 * (g0 + t) + 1] : qnan();
+    for (uint32_t i = t; i < nu; i += NT) S.ge[i] = P.gtC[lb + i] | (P.cntZ[lb + i] << 16);
+    __syncthreads();
+    T = 0u;
+    rt = st.z;
+    fp_rank = rt > 0 ? 0u : NONE;
+    fn_rank = NONE;
+    done = true;
+  } else {
+    done = st.w == 0 && select_from_groups<NT>(P, sd, lb, nu, st, S, T, rt, fp_rank, fn_rank, gmn, gmx);
+  }
   uint32_t raw_path = 0;
   STAMP(P, li, 1);
   if (!done) {
@@ -1857,27 +1904,6 @@ DEV void segment_select(const Params& P, uint32_t li, SelSmem& S) {
   }
   STAMP(P, li, 10);
 
-  // in-order scan over the units: global tie prefix and output offsets
-  uint32_t carry_e = 0, carry_sel = 0;
-  for (uint32_t c0 = 0; c0 < nu; c0 += NT) {
-    const uint32_t i = c0 + t;
-    const bool valid = i < nu;
-    const uint32_t e = valid ? (done ? S.ge[i] >> 16 : P.eqC[lb + i]) : 0u;  // fast path: counts in LDS
-    uint32_t tot;
-    const uint32_t ex = block_excl_scan<NT>(e, S.sh, tot) + carry_e;
-    carry_e += tot;
-    const uint32_t quota = !valid ? 0u : (ex >= rt ? 0u : min(e, rt - ex));
-    const uint32_t sel = valid ? (done ? S.ge[i] & 0xFFFFu : P.gtC[lb + i]) + quota : 0u;
-    uint32_t tot2;
-    const uint32_t so = block_excl_scan<NT>(sel, S.sh, tot2) + carry_sel;
-    carry_sel += tot2;
-    if (valid) {
-      pst(P, P.eqpre + lb + i, ex);
-      pst(P, P.outoff + lb + i, so);
-      if (P.ustart_out != nullptr) pst(P, P.ustart_out + sd.unit_begin + i, so);  // wire v2: the unit's start
-    }
-  }
-  STAMP(P, li, 11);
   float mn = 0.0f, scale = 0.0f;
   if (!RAW) {
     const float tv = __uint_as_float(T);
@@ -1901,9 +1927,32 @@ DEV void segment_select(const Params& P, uint32_t li, SelSmem& S) {
     pst(P, P.mn + s, mn);
     pst(P, P.scale + s, scale);
   }
-  // the segment's emit parameters per unit: k_emit then loads them with the unit's own words, in one round
-  const uint4 ue = make_uint4(T, rt | (raw_path << 31), __float_as_uint(mn), __float_as_uint(scale));
-  for (uint32_t i = t; i < nu; i += NT) P.uemit[lb + i] = ue;
+  STAMP(P, li, 11);
+
+  // in-order scan over the units: global tie prefix and output offsets; each unit's emit parameters (k_emit loads
+  // them with the unit's own words, in one round): {T*, tie budget | raw-data emit << 31, mn, scale} — raw-data
+  // emit for every unit of a raw-path segment, and for the units of a zero-tie segment whose zeros the quota reaches
+  uint32_t carry_e = 0, carry_sel = 0;
+  for (uint32_t c0 = 0; c0 < nu; c0 += NT) {
+    const uint32_t i = c0 + t;
+    const bool valid = i < nu;
+    const uint32_t e = valid ? (done ? S.ge[i] >> 16 : P.eqC[lb + i]) : 0u;  // fast path: counts in LDS
+    uint32_t tot;
+    const uint32_t ex = block_excl_scan<NT>(e, S.sh, tot) + carry_e;
+    carry_e += tot;
+    const uint32_t quota = !valid ? 0u : (ex >= rt ? 0u : min(e, rt - ex));
+    const uint32_t sel = valid ? (done ? S.ge[i] & 0xFFFFu : P.gtC[lb + i]) + quota : 0u;
+    uint32_t tot2;
+    const uint32_t so = block_excl_scan<NT>(sel, S.sh, tot2) + carry_sel;
+    carry_sel += tot2;
+    if (valid) {
+      pst(P, P.eqpre + lb + i, ex);
+      pst(P, P.outoff + lb + i, so);
+      if (P.ustart_out != nullptr) pst(P, P.ustart_out + sd.unit_begin + i, so);  // wire v2: the unit's start
+      const uint32_t rawu = raw_path | (zero_tie && quota > 0 ? 1u : 0u);
+      P.uemit[lb + i] = make_uint4(T, rt | (rawu << 31), __float_as_uint(mn), __float_as_uint(scale));
+    }
+  }
   STAMP(P, li, 12);
 }
 
@@ -2015,23 +2064,23 @@ DEV void emit_units(const Params& P, uint32_t lu0, uint32_t lu1) {
     nCg = min(nCr, P.ccap);  // stored records (a raw-path unit may have dropped some)
     Tg = ue.x;
     rtg = ue.y & 0x7FFFFFFFu;
-    stg = ue.y >> 31;  // the raw-data path
+    stg = ue.y >> 31;  // raw-data emit (a raw-path segment, or a zero-tie unit whose zeros the quota reaches)
     mng = RAW ? 0.0f : __uint_as_float(ue.z);
     scg = RAW ? 0.0f : __uint_as_float(ue.w);
   } else {
-    // batches: round 1 / 2 — unit, then its segment's parameters; then every unit's first rows of records
-    // (clamped to the count: the one-round form measured slower beside the other sub-batch's streaming)
+    // batches: round 1 — the unit's count, offsets and emit parameters; round 2 — every unit's first rows of
+    // records (clamped to the count: the one-round form measured slower beside the other sub-batch's streaming)
     nCg = min(P.cntC[lug], P.ccap);
-    const uint32_t segg = P.lunits[lug].seg;
     startg = P.lunits[lug].start;
-    stg = P.status[segg];
     sog = P.lunits[lug].out_off;
     eqpg = P.eqpre[lug];
     oog = P.outoff[lug];
-    Tg = P.tstar[segg];
-    rtg = P.rtie[segg];
-    mng = RAW ? 0.0f : P.mn[segg];
-    scg = RAW ? 0.0f : P.scale[segg];
+    const uint4 ue = P.uemit[lug];
+    Tg = ue.x;
+    rtg = ue.y & 0x7FFFFFFFu;
+    stg = ue.y >> 31;  // raw-data emit
+    mng = RAW ? 0.0f : __uint_as_float(ue.z);
+    scg = RAW ? 0.0f : __uint_as_float(ue.w);
 #pragma unroll
     for (uint32_t g = 0; g < UPW; ++g) {
       const uint32_t lu = min(lu0 + g, lu1 - 1), nC = rl(nCg, g);
@@ -2652,6 +2701,191 @@ __global__ __launch_bounds__(BLOCK, AGG_WPE) void k_aggregate(Params P, AggArgs 
     body(std::false_type{});
 }
 
+// ------------------------------------------------------------------------------------------------
+// dense codec: a plan whose every segment keeps all n elements (ratio 1 — the download direction's default,
+// coala/server/base.py:196,397 — or segments too small to drop anything). The index list is implied (0..n-1
+// per segment) and never materialised; a caller that passes idx / ustart buffers still gets them written.
+//   encode: k_dense_minmax (per unit, NaN-ignoring min / max) -> k_dense_seg (per segment: mn, scale) ->
+//           k_dense_quant (per unit: read 4 B, write the 1-B code)         — HBM 4 B + 1 B per element
+//           (the min / max pass reads the update once more; an update that fits the 256 MB Infinity Cache
+//           is re-read from it)
+//   decode: k_dense_deq (per unit: read the 1-B code, write 4 B; + base in delta mode)
+// One wave per 4096-element unit, 16 float4 per lane, XCD-aware unit order in batches.
+// ------------------------------------------------------------------------------------------------
+template <bool DELTA>
+DEV void dense_unit_load(const Params& P, const UnitDev& U, float4 (&v)[UNIT_IT]) {
+  const uint32_t lane = lane_id();
+  const float* xin = P.inptr != nullptr ? P.inptr[U.seg] + U.start : P.in + U.off;
+  const __amdgpu_buffer_rsrc_t rin = unit_rsrc(xin, U.len);
+  const __amdgpu_buffer_rsrc_t rb = unit_rsrc(DELTA ? P.base + U.off : xin, U.len);
+#pragma unroll
+  for (uint32_t it = 0; it < UNIT_IT; ++it) v[it] = unit_load_x4<DELTA>(rin, rb, (it * 64 + lane) * 16);
+}
+
+template <bool DELTA, bool XCD>
+__global__ __launch_bounds__(BLOCK) void k_dense_minmax(Params P) {
+  const uint32_t u = (XCD ? xcd_block(blockIdx.x) : blockIdx.x) * WAVES + (threadIdx.x >> 6);
+  if (u >= P.n_units) return;
+  const UnitDev U = P.units[u];
+  float4 v[UNIT_IT];
+  dense_unit_load<DELTA>(P, U, v);
+  const uint32_t lane = lane_id();
+  float a = qnan(), b = qnan();
+#pragma unroll
+  for (uint32_t it = 0; it < UNIT_IT; ++it) {
+    const uint32_t e0 = (it * 64 + lane) * 4;
+    const float xs[4] = {v[it].x, v[it].y, v[it].z, v[it].w};
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const float x = (U.len == UNIT || e0 + j < U.len) ? xs[j] : qnan();  // (loads past len read 0)
+      a = fmin_nan(a, x);
+      b = fmax_nan(b, x);
+    }
+  }
+  a = wave_min(a);
+  b = wave_max(b);
+  if (lane == 0) {
+    P.umm[2 * u] = a;
+    P.umm[2 * u + 1] = b;
+  }
+}
+
+// one block per segment: its units' partial min / max -> mn, scale (CodecSpec v1: each + 0.0f; scale 0 when
+// they are equal); raw values (bits 32): mn = scale = 0
+template <bool RAW>
+__global__ __launch_bounds__(BLOCK) void k_dense_seg(Params P) {
+  __shared__ float shf[2 * WAVES];
+  const uint32_t s = blockIdx.x;
+  const SegDev sd = P.segs[s];
+  float a = qnan(), b = qnan();
+  if (!RAW)
+    for (uint32_t u = sd.unit_begin + threadIdx.x; u < sd.unit_end; u += BLOCK) {
+      a = fmin_nan(a, P.umm[2 * u]);
+      b = fmax_nan(b, P.umm[2 * u + 1]);
+    }
+  block_minmax<BLOCK>(a, b, shf);
+  if (threadIdx.x == 0) {
+    float mn = 0.0f, scale = 0.0f;
+    if (!RAW && sd.n != 0) {
+      a = a + 0.0f;
+      b = b + 0.0f;
+      mn = a;
+      scale = (b == a) ? 0.0f : (b - a) / P.levels;
+    }
+    P.mn[s] = mn;
+    P.scale[s] = scale;
+  }
+}
+
+template <bool DELTA, bool RAW, bool XCD>
+__global__ __launch_bounds__(BLOCK) void k_dense_quant(Params P) {
+  const uint32_t u = (XCD ? xcd_block(blockIdx.x) : blockIdx.x) * WAVES + (threadIdx.x >> 6);
+  if (u >= P.n_units) return;
+  const UnitDev U = P.units[u];
+  const float mn = RAW ? 0.0f : P.mn[U.seg], scale = RAW ? 0.0f : P.scale[U.seg];
+  float4 v[UNIT_IT];
+  dense_unit_load<DELTA>(P, U, v);
+  const uint32_t lane = lane_id();
+  const uint64_t o = U.out_off + U.start;  // the unit's first entry (k == n: entry e is element e)
+  // whole-dword stores when the unit's codes start 4-byte aligned (16-byte for raw floats) and end on a dword
+  const bool vec = (o & 3u) == 0 && (U.len & 3u) == 0;
+  if (RAW) {
+    float* dst = static_cast<float*>(P.vals) + o;
+    const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(dst, (short)0, (int)(U.len * 4u), 0x00020000);
+#pragma unroll
+    for (uint32_t it = 0; it < UNIT_IT; ++it) {
+      if (vec)
+        unit_store_x4<0>(r, (it * 64 + lane) * 16, v[it]);
+      else
+        unit_store_x1x4<0>(r, (it * 64 + lane) * 16, v[it]);
+    }
+  } else {
+    uint8_t* dst = static_cast<uint8_t*>(P.vals) + o;
+    const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(dst, (short)0, (int)U.len, 0x00020000);
+#pragma unroll
+    for (uint32_t it = 0; it < UNIT_IT; ++it) {
+      const uint32_t q0 = quantize(v[it].x, mn, scale, P.levels), q1 = quantize(v[it].y, mn, scale, P.levels);
+      const uint32_t q2 = quantize(v[it].z, mn, scale, P.levels), q3 = quantize(v[it].w, mn, scale, P.levels);
+      const uint32_t boff = (it * 64 + lane) * 4;
+      if (vec) {
+        __builtin_amdgcn_raw_buffer_store_b32(q0 | (q1 << 8) | (q2 << 16) | (q3 << 24), r, (int)boff, 0, 0);
+      } else {  // (range-checked per byte: the unit's tail past len is dropped)
+        __builtin_amdgcn_raw_buffer_store_b8((uint8_t)q0, r, (int)boff, 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b8((uint8_t)q1, r, (int)boff + 1, 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b8((uint8_t)q2, r, (int)boff + 2, 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b8((uint8_t)q3, r, (int)boff + 3, 0, 0);
+      }
+    }
+  }
+  if (P.idx != nullptr) {  // a caller that asked for the (implied) indices
+    for (uint32_t e = lane; e < U.len; e += 64) P.idx[o + e] = (int32_t)(U.start + e);
+  }
+  if (P.ustart_out != nullptr && lane == 0) P.ustart_out[u] = U.start;
+}
+
+template <bool RAW, bool HASBASE, bool XCD>
+__global__ __launch_bounds__(BLOCK) void k_dense_deq(Params P) {
+  const uint32_t u = (XCD ? xcd_block(blockIdx.x) : blockIdx.x) * WAVES + (threadIdx.x >> 6);
+  if (u >= P.n_units) return;
+  const UnitDev U = P.units[u];
+  const uint32_t lane = lane_id();
+  const float mn = RAW ? 0.0f : P.cmn[U.seg], scale = RAW ? 0.0f : P.cscale[U.seg];
+  const uint64_t o = U.out_off + U.start;
+  const bool vec = (o & 3u) == 0 && (U.len & 3u) == 0;
+  float4 d[UNIT_IT];
+  if (RAW) {
+    const float* src = static_cast<const float*>(P.cvals) + o;
+    const __amdgpu_buffer_rsrc_t r = unit_rsrc(src, U.len);
+#pragma unroll
+    for (uint32_t it = 0; it < UNIT_IT; ++it) {
+      if (vec) {
+        d[it] = unit_load_x4<false>(r, r, (it * 64 + lane) * 16);
+      } else {
+        const uint32_t b = (it * 64 + lane) * 16;
+        d[it] = make_float4(__uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, (int)b, 0, 0)),
+                            __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, (int)b + 4, 0, 0)),
+                            __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, (int)b + 8, 0, 0)),
+                            __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, (int)b + 12, 0, 0)));
+      }
+    }
+  } else {
+    const uint8_t* src = static_cast<const uint8_t*>(P.cvals) + o;
+    const __amdgpu_buffer_rsrc_t r =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(src), (short)0, (int)U.len, 0x00020000);
+    uint32_t w[UNIT_IT];
+#pragma unroll
+    for (uint32_t it = 0; it < UNIT_IT; ++it) {
+      const uint32_t b = (it * 64 + lane) * 4;
+      if (vec) {
+        w[it] = __builtin_amdgcn_raw_buffer_load_b32(r, (int)b, 0, 0);
+      } else {
+        w[it] = (uint32_t)__builtin_amdgcn_raw_buffer_load_b8(r, (int)b, 0, 0) |
+                ((uint32_t)__builtin_amdgcn_raw_buffer_load_b8(r, (int)b + 1, 0, 0) << 8) |
+                ((uint32_t)__builtin_amdgcn_raw_buffer_load_b8(r, (int)b + 2, 0, 0) << 16) |
+                ((uint32_t)__builtin_amdgcn_raw_buffer_load_b8(r, (int)b + 3, 0, 0) << 24);
+      }
+    }
+#pragma unroll
+    for (uint32_t it = 0; it < UNIT_IT; ++it)
+      d[it] = make_float4(dequantize((uint8_t)(w[it] & 0xFFu), mn, scale), dequantize((uint8_t)((w[it] >> 8) & 0xFFu), mn, scale),
+                          dequantize((uint8_t)((w[it] >> 16) & 0xFFu), mn, scale), dequantize((uint8_t)(w[it] >> 24), mn, scale));
+  }
+  const __amdgpu_buffer_rsrc_t rout = unit_rsrc(P.out + U.off, U.len);
+  const __amdgpu_buffer_rsrc_t rb = unit_rsrc(HASBASE ? P.base + U.off : P.out + U.off, U.len);
+#pragma unroll
+  for (uint32_t it = 0; it < UNIT_IT; ++it) {
+    float4 x = d[it];
+    if (HASBASE) {
+      const float4 b = unit_load_x4<false>(rb, rb, (it * 64 + lane) * 16);
+      x = make_float4(b.x + x.x, b.y + x.y, b.z + x.z, b.w + x.w);
+    }
+    if ((U.len & 3u) == 0)
+      unit_store_x4<0>(rout, (it * 64 + lane) * 16, x);
+    else
+      unit_store_x1x4<0>(rout, (it * 64 + lane) * 16, x);
+  }
+}
+
 // k_gather: n scalars of `bytes` each, from their own storage (one device pointer each), into one contiguous
 // buffer — an update's passthrough entries (BatchNorm's int64 num_batches_tracked, one per layer) snapshotted
 // in one launch instead of a stack of tensor copies
@@ -2696,10 +2930,19 @@ size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 struct WsLayout {
   size_t status;
   size_t tstar, rtie;
-  size_t tlo, thi, cntA, cntC, gtC, eqC, eqpre, outoff, uemit;
+  size_t tlo, thi, cntA, cntC, cntZ, gtC, eqC, eqpre, outoff, uemit;
   size_t cval, cpos, stamps, ghist, gcnt, glist, gmm, sstate, shhi;
+  size_t umm;  // dense plans: per-unit min / max
   size_t total;
 };
+
+// a dense plan's encode workspace: the per-unit min / max only
+WsLayout ws_layout_dense(size_t U) {
+  WsLayout L{};
+  L.umm = 0;
+  L.total = std::max<size_t>(align_up(8 * U, 256), 256);
+  return L;
+}
 
 WsLayout ws_layout(size_t S, size_t LU, size_t NG, size_t NL, uint32_t CC) {
   WsLayout L{};
@@ -2716,6 +2959,7 @@ WsLayout ws_layout(size_t S, size_t LU, size_t NG, size_t NL, uint32_t CC) {
   L.thi = take(4 * LU);
   L.cntA = take(4 * LU);
   L.cntC = take(4 * LU);
+  L.cntZ = take(4 * LU);
   L.gtC = take(4 * LU);
   L.eqC = take(4 * LU);
   L.eqpre = take(4 * LU);
@@ -2743,6 +2987,7 @@ struct coalac_plan {
   uint32_t n_small = 0, n_large = 0, n_units = 0, n_lunits = 0;
   uint32_t small_max = SMALL_MAX;  // segments of <= this many elements are "small" (encoded whole by one block)
   uint32_t ccap = UNIT;  // candidate record slots per large unit
+  bool dense = false;    // every segment keeps all its elements: the dense codec (indices implied)
   uint64_t span = 0, total_k = 0;
   void* meta = nullptr;
   SegDev* segs = nullptr;
@@ -2833,6 +3078,47 @@ bool at_boundary(unsigned stages, const int (*span)[2], int nst, int i) {
 
 constexpr int ENC_SPAN[4][2] = {{0, 1}, {1, 2}, {2, 4}, {0, 1}};  // SAMPLE, SCAN, SELECT, SMALL
 constexpr int DEC_SPAN[2][2] = {{0, 1}, {1, 2}};                  // BOUNDS, DECODE
+
+// the dense encode: stage SAMPLE = the min / max pass + the per-segment reduction, stage SCAN = the quantise
+// stream (boundaries 1 / 2 bracket it, as they bracket k_scan); nothing in SELECT
+template <bool DELTA, bool RAW>
+int launch_dense_encode(const Params& P, coalac_plan_t plan, hipStream_t st, const coalac_sched_t* sc) {
+  const unsigned all = COALAC_STAGE_SAMPLE | COALAC_STAGE_SCAN | COALAC_STAGE_SELECT | COALAC_STAGE_SMALL;
+  const unsigned stages = (sc && (sc->stages & all)) ? (sc->stages & all) : all;
+  auto B = [&](int i) { return at_boundary(stages, ENC_SPAN, 4, i) ? boundary(sc, i, st) : COALAC_OK; };
+  const dim3 g((plan->n_units + WAVES - 1) / WAVES);
+  const bool xcd = plan->n_units > LATENCY_PLAN_UNITS;
+  int rc = B(0);
+  if (rc) return rc;
+  if (stages & COALAC_STAGE_SAMPLE) {
+    if (!RAW) {
+      if (xcd)
+        hipLaunchKernelGGL((k_dense_minmax<DELTA, true>), g, dim3(BLOCK), 0, st, P);
+      else
+        hipLaunchKernelGGL((k_dense_minmax<DELTA, false>), g, dim3(BLOCK), 0, st, P);
+    }
+    hipLaunchKernelGGL((k_dense_seg<RAW>), dim3(plan->nseg), dim3(BLOCK), 0, st, P);
+  }
+  if ((rc = B(1))) return rc;
+  if (stages & COALAC_STAGE_SCAN) {
+    if (xcd)
+      hipLaunchKernelGGL((k_dense_quant<DELTA, RAW, true>), g, dim3(BLOCK), 0, st, P);
+    else
+      hipLaunchKernelGGL((k_dense_quant<DELTA, RAW, false>), g, dim3(BLOCK), 0, st, P);
+  }
+  for (int i = 2; i <= 4; ++i)
+    if ((rc = B(i))) return rc;
+  return COALAC_OK;
+}
+
+template <bool RAW, bool HB>
+void launch_dense_decode(const Params& P, coalac_plan_t plan, hipStream_t st) {
+  const dim3 g((plan->n_units + WAVES - 1) / WAVES);
+  if (plan->n_units > LATENCY_PLAN_UNITS)
+    hipLaunchKernelGGL((k_dense_deq<RAW, HB, true>), g, dim3(BLOCK), 0, st, P);
+  else
+    hipLaunchKernelGGL((k_dense_deq<RAW, HB, false>), g, dim3(BLOCK), 0, st, P);
+}
 
 template <bool DELTA, bool RAW>
 void launch_emit(const Params& P, coalac_plan_t plan, hipStream_t st) {
@@ -3040,7 +3326,10 @@ int coalac_plan_create(const coalac_seg_t* h_segs, int nseg, int bits, coalac_pl
   ccap = std::max<uint32_t>(STAGE_CAP, std::min<uint32_t>(UNIT, ccap));
   p->ccap = ccap;
   p->small_max = small_max;
-  p->ws = ws_layout((size_t)nseg, lunits.size(), groups.size(), large_list.size(), ccap);
+  p->dense = true;
+  for (const SegDev& d : segs) p->dense = p->dense && d.k == d.n;
+  p->ws = p->dense ? ws_layout_dense(units.size())
+                   : ws_layout((size_t)nseg, lunits.size(), groups.size(), large_list.size(), ccap);
 
   const size_t o_segs = 0;
   const size_t o_units = align_up(o_segs + sizeof(SegDev) * segs.size(), 256);
@@ -3142,7 +3431,8 @@ int encode_impl(coalac_plan_t plan, const float* d_in, const float* const* d_inp
   if (plan->nseg == 0) return COALAC_OK;
   if (!d_mn || !d_scale) return fail(COALAC_EINVAL, "coalac_encode: mn/scale pointers are NULL");
   if (plan->span && !d_in && !d_inptr) return fail(COALAC_EINVAL, "coalac_encode: input pointer is NULL");
-  if (plan->total_k && (!d_idx || !d_vals)) return fail(COALAC_EINVAL, "coalac_encode: idx/vals pointers are NULL");
+  if (plan->total_k && (!(d_idx || plan->dense) || !d_vals))
+    return fail(COALAC_EINVAL, "coalac_encode: idx/vals pointers are NULL (idx may be NULL for a dense plan only)");
   if ((reinterpret_cast<uintptr_t>(d_in) | reinterpret_cast<uintptr_t>(d_base)) & 15)
     return fail(COALAC_EINVAL, "coalac_encode: input/base must be 16-byte aligned");
   if (reinterpret_cast<uintptr_t>(d_ustart) & 3) return fail(COALAC_EINVAL, "coalac_encode: ustart must be 4-byte aligned");
@@ -3164,6 +3454,22 @@ int encode_impl(coalac_plan_t plan, const float* d_in, const float* const* d_inp
   P.flags = flags;
   uint8_t* w = static_cast<uint8_t*>(d_ws);
   const WsLayout& L = plan->ws;
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  const bool delta = d_base != nullptr, raw = plan->bits == 32;
+  if (plan->dense) {
+    P.umm = reinterpret_cast<float*>(w + L.umm);
+    if (delta && raw)
+      rc = launch_dense_encode<true, true>(P, plan, st, sched);
+    else if (delta)
+      rc = launch_dense_encode<true, false>(P, plan, st, sched);
+    else if (raw)
+      rc = launch_dense_encode<false, true>(P, plan, st, sched);
+    else
+      rc = launch_dense_encode<false, false>(P, plan, st, sched);
+    if (rc) return rc;
+    HIP_CHECK(hipGetLastError());
+    return COALAC_OK;
+  }
   P.tstar = reinterpret_cast<uint32_t*>(w + L.tstar);
   P.rtie = reinterpret_cast<uint32_t*>(w + L.rtie);
   P.status = reinterpret_cast<uint32_t*>(w + L.status);
@@ -3171,6 +3477,7 @@ int encode_impl(coalac_plan_t plan, const float* d_in, const float* const* d_inp
   P.thi = reinterpret_cast<uint32_t*>(w + L.thi);
   P.cntA = reinterpret_cast<uint32_t*>(w + L.cntA);
   P.cntC = reinterpret_cast<uint32_t*>(w + L.cntC);
+  P.cntZ = reinterpret_cast<uint32_t*>(w + L.cntZ);
   P.gtC = reinterpret_cast<uint32_t*>(w + L.gtC);
   P.eqC = reinterpret_cast<uint32_t*>(w + L.eqC);
   P.eqpre = reinterpret_cast<uint32_t*>(w + L.eqpre);
@@ -3185,8 +3492,6 @@ int encode_impl(coalac_plan_t plan, const float* d_in, const float* const* d_inp
   P.gmm = reinterpret_cast<float*>(w + L.gmm);
   P.sstate = reinterpret_cast<uint4*>(w + L.sstate);
   P.shhi = reinterpret_cast<uint32_t*>(w + L.shhi);
-  hipStream_t st = static_cast<hipStream_t>(stream);
-  const bool delta = d_base != nullptr, raw = plan->bits == 32;
   if (delta && raw)
     rc = launch_encode<true, true>(P, plan, st, sched);
   else if (delta)
@@ -3283,14 +3588,14 @@ int coalac_decode_sched(coalac_plan_t plan, const int32_t* d_idx, const void* d_
   // workspace: the kept values then need BOUNDS in this call, or the caller's word (BOUNDS_DONE) that an earlier call
   // enqueued it on this workspace for these arrays, ordered before this one (stale bounds would mis-decode
   // silently); latency-bound plans without starts search their ranges in-kernel (k_fillscatter).
-  if (!d_ustart && !lat && (stages & COALAC_STAGE_SCATTER) && !(stages & COALAC_STAGE_BOUNDS) &&
+  if (!plan->dense && !d_ustart && !lat && (stages & COALAC_STAGE_SCATTER) && !(stages & COALAC_STAGE_BOUNDS) &&
       !(sched && (sched->stages & COALAC_STAGE_BOUNDS_DONE)))
     return fail(COALAC_EINVAL, "coalac_decode: a plan of %u units without per-unit starts decodes its kept values "
                 "from the bounds of COALAC_STAGE_BOUNDS: pass BOUNDS in the same call, or BOUNDS_DONE after a BOUNDS "
                 "call on this workspace", plan->n_units);
   if (!d_out) return fail(COALAC_EINVAL, "coalac_decode: output pointer is NULL");
   const bool payload = (stages & (COALAC_STAGE_BOUNDS | COALAC_STAGE_SCATTER)) != 0;  // reads the encoded arrays
-  if (payload && plan->total_k && (!d_idx || !d_vals))
+  if (payload && plan->total_k && (!(d_idx || plan->dense) || !d_vals))
     return fail(COALAC_EINVAL, "coalac_decode: idx/vals pointers are NULL");
   if (payload && plan->bits != 32 && (!d_mn || !d_scale))
     return fail(COALAC_EINVAL, "coalac_decode: mn/scale pointers are NULL");
@@ -3321,7 +3626,7 @@ int coalac_decode_sched(coalac_plan_t plan, const int32_t* d_idx, const void* d_
     if (rc_) return rc_;      \
   } while (0)
   DEC_BOUNDARY(0);
-  if ((stages & COALAC_STAGE_BOUNDS) && plan->n_bchunks && !lat && !d_ustart)
+  if ((stages & COALAC_STAGE_BOUNDS) && plan->n_bchunks && !lat && !d_ustart && !plan->dense)
     hipLaunchKernelGGL(k_bounds, dim3(plan->n_bchunks), dim3(BLOCK), 0, st, P, plan->bchunks,
                        static_cast<uint32_t*>(d_ws));
   DEC_BOUNDARY(1);
@@ -3333,7 +3638,11 @@ int coalac_decode_sched(coalac_plan_t plan, const int32_t* d_idx, const void* d_
     else if (hb) F<false, true>(__VA_ARGS__);              \
     else F<false, false>(__VA_ARGS__);                     \
   } while (0)
-  if (lat && (!whole || !d_ustart))
+  if (plan->dense) {
+    // every element kept: one dequantise stream, positional (the idx / starts, implied, are not read); its
+    // SCATTER part writes every element (FILL alone has nothing to do)
+    if (stages & COALAC_STAGE_SCATTER) DISPATCH(launch_dense_decode, P, plan, st);
+  } else if (lat && (!whole || !d_ustart))
     // a separately enqueued FILL / SCATTER (the background may go out before the payload exists), or no starts:
     // k_fill / k_scatter, or k_fillscatter (background, in-kernel range search, kept values on top)
     DISPATCH(launch_fillscatter, P, plan, st, stages);
@@ -3367,7 +3676,9 @@ int coalac_aggregate_ev(coalac_plan_t plan, int clients, const int32_t* d_idx, c
     return fail(COALAC_EINVAL, "coalac_aggregate: bad mode %d", mode);
   if (plan->n_units == 0) return COALAC_OK;
   if (!d_out || !d_weights) return fail(COALAC_EINVAL, "coalac_aggregate: output/weights pointer is NULL");
-  if (plan->total_k && (!d_idx || !d_vals)) return fail(COALAC_EINVAL, "coalac_aggregate: idx/vals pointers are NULL");
+  if (plan->total_k && (!d_idx || !d_vals))
+    return fail(COALAC_EINVAL, "coalac_aggregate: idx/vals pointers are NULL (a dense plan's implied indices must be "
+                "passed here)");
   if (plan->bits != 32 && (!d_mn || !d_scale)) return fail(COALAC_EINVAL, "coalac_aggregate: mn/scale pointers are NULL");
   if ((reinterpret_cast<uintptr_t>(d_out) | reinterpret_cast<uintptr_t>(d_base)) & 15)
     return fail(COALAC_EINVAL, "coalac_aggregate: output/base must be 16-byte aligned");
@@ -3466,7 +3777,7 @@ int coalac_gather(const void* const* d_src, int n, int elem_bytes, void* d_out, 
 int coalac_workspace_fallbacks(coalac_plan_t plan, const void* d_ws, void* stream, int* out) {
   if (!plan || !d_ws || !out) return fail(COALAC_EINVAL, "coalac_workspace_fallbacks: NULL argument");
   *out = 0;
-  if (plan->nseg == 0) return COALAC_OK;
+  if (plan->nseg == 0 || plan->dense) return COALAC_OK;
   std::vector<uint32_t> st(plan->nseg);
   std::vector<uint32_t> large(plan->n_large);
   hipStream_t s = static_cast<hipStream_t>(stream);

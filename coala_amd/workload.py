@@ -48,6 +48,36 @@ def synth_batch(table, device, client_ids=None, seed_base=1234):
     return flat
 
 
+def head_only(layout):
+    """Indices (in fp32-segment order) of the tensors a FedPEFT client trains with its backbone frozen: the
+    classifier head. The reference freezes every ViT parameter (application/FedPEFT/lora.py:64, and
+    main.py:62-67 for linear probing) and trains the new head (plus, with LoRA, adapter tensors that the
+    plain ViT-B/16 layout does not hold)."""
+    names = [e["name"] for e in load(layout)["entries"] if e["dtype"] == "float32" and _numel(e["shape"]) > 0]
+    return [i for i, n in enumerate(names) if n.startswith(("fc.", "head."))]
+
+
+def _numel(shape):
+    n = 1
+    for d in shape:
+        n *= d
+    return n
+
+
+def freeze_segments(flat, table, trained):
+    """Zero every fp32 segment of every client except the `trained` ones (segment indices of one client's
+    layout): the delta of a frozen tensor is exactly zero."""
+    keep = set(trained)
+    so = table.client_span_off
+    for c in range(table.clients):
+        sizes = table.client_sizes(c)
+        single = SegmentTable(sizes, table.ratio, 1)
+        for t, (off, n) in enumerate(zip(single.offsets, sizes)):
+            if t not in keep:
+                flat[so[c] + off:so[c] + off + n].zero_()
+    return flat
+
+
 # C5 (SURVEY.md §8(d)): 256 splitFL clients on 8 GPUs; each client draws (seeded) one of the client-side
 # models at cut 1/2/4 or one of the three feature-tensor uploads
 C5_CHOICES = [f"{m}_cut{c}" for m in ("resnet18_split", "resnet50_split", "simple_cnn_split") for c in (1, 2, 4)] + \

@@ -16,18 +16,27 @@ class OraclePlan:
         self.table = SegmentTable(sizes, ratio, clients)
         self.bits = bits
 
+    def _idx(self, enc):
+        """enc.idx, or a dense (ratio 1) update's implied indices (0..n-1 per segment)."""
+        if enc.idx.numel() or not self.table.total_k:
+            return enc.idx.numpy()
+        return np.concatenate([np.arange(int(n), dtype=np.int32) for n in self.table.segs[:, 1]])
+
     def encode(self, flat, base=None, **_):
         x = flat.detach().cpu().numpy()
         b = None if base is None else base.detach().cpu().numpy()
         segs = self.table.segs.astype(np.int64)
         idx, vals, mn, sc = O.encode(x, segs, self.bits, base=b)
+        if self.table.ratio >= 1.0:  # as the HIP plan: a dense update's indices stay implied
+            return Encoded(torch.zeros(0, dtype=torch.int32), torch.from_numpy(vals), torch.from_numpy(mn),
+                           torch.from_numpy(sc), None)
         return Encoded(torch.from_numpy(idx), torch.from_numpy(vals), torch.from_numpy(mn), torch.from_numpy(sc),
                        torch.from_numpy(O.unit_starts(idx, segs)))
 
     def decode(self, enc, base=None, out=None, **_):
         b = None if base is None else base.detach().cpu().numpy()
         res = np.zeros(self.table.span, dtype=np.float32) if b is None else b.copy()
-        O.decode(enc.idx.numpy(), enc.vals.numpy(), enc.mn.numpy(), enc.scale.numpy(),
+        O.decode(self._idx(enc), enc.vals.numpy(), enc.mn.numpy(), enc.scale.numpy(),
                  self.table.segs.astype(np.int64), self.bits, self.table.span, base=b, out=res)
         if out is not None:  # (a recycled decoded module's storage: written in place, as the HIP plan does)
             out[:res.size].copy_(torch.from_numpy(res))
@@ -37,7 +46,7 @@ class OraclePlan:
     def aggregate(self, enc, weights, total=None, base=None, mode="div", avg_mask=None, **_):
         total = float(sum(weights)) if total is None else float(total)
         b = None if base is None else base.detach().cpu().numpy()
-        out = O.aggregate(enc.idx.numpy(), enc.vals.numpy(), enc.mn.numpy(), enc.scale.numpy(),
+        out = O.aggregate(self._idx(enc), enc.vals.numpy(), enc.mn.numpy(), enc.scale.numpy(),
                           self.table.segs.astype(np.int64), self.bits, self.table.clients, weights, total,
                           {"div": O.AGG_DIV, "recip": O.AGG_RECIP, "sum": O.AGG_SUM}[mode], base=b,
                           out_span=self.table.span_per_client, avg_mask=avg_mask)

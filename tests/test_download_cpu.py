@@ -60,7 +60,7 @@ def test_dense_wire_drops_indices_and_round_trips():
     assert len(blob) < 1.01 * n + 4096          # 1 B per element + header, no 4 B indices
     assert up.nbytes < 1.01 * n + 64
     back = CompressedUpdate.from_bytes(blob)
-    assert torch.equal(back.encoded.idx, up.encoded.idx.cpu())
+    assert back.encoded.idx.numel() == 0 and up.encoded.idx.numel() == 0  # implied, never materialised
     for a, b in zip(codec.decode_state(back).values(), codec.decode_state(up).values()):
         _bits_equal(a, b)
 

@@ -20,19 +20,23 @@ import torch
 from coala_amd.compression import SplitPipeline
 from coala_amd.compression.spec import SegmentTable
 from coala_amd.layouts import fp32_sizes
-from coala_amd.workload import c5_share, mixed_table, synth_batch
+from coala_amd.workload import c5_share, freeze_segments, head_only, mixed_table, synth_batch
 from oracle import codec_oracle as O
 from tests.oracle_pool import SharedBatch, oracle_clients
 
 pytestmark = pytest.mark.gpu
 
-# name -> (layout | "c5", clients, sub-batches, mode): bench.py CONFIGS (+ C3 in delta mode)
+# name -> (layout | "c5", clients, sub-batches, mode, ratio, frozen backbone): bench.py CONFIGS
 CASES = {
-    "C2": ("resnet18", 16, 3, "weights"),
-    "C3": ("resnet50_tv", 16, 2, "weights"),
-    "C4": ("vit_b16", 16, 2, "weights"),
-    "C5": ("c5", None, 1, "weights"),
-    "C3-delta": ("resnet50_tv", 16, 2, "delta"),
+    "C2": ("resnet18", 16, 3, "weights", 0.01, False),
+    "C3": ("resnet50_tv", 16, 2, "weights", 0.01, False),
+    "C4": ("vit_b16", 16, 2, "weights", 0.01, False),
+    "C5": ("c5", None, 1, "weights", 0.01, False),
+    "C3-delta": ("resnet50_tv", 16, 2, "delta", 0.01, False),
+    "C3-r0.001": ("resnet50_tv", 16, 2, "weights", 0.001, False),
+    "C3-r0.1": ("resnet50_tv", 16, 2, "weights", 0.1, False),
+    # FedPEFT's frozen backbone (application/FedPEFT/lora.py:64): every tensor but the head an exact-zero delta
+    "C4-frozen": ("vit_b16", 16, 2, "delta", 0.01, True),
 }
 
 
@@ -51,11 +55,14 @@ def _to_shared(t):
 
 @pytest.mark.parametrize("case", list(CASES))
 def test_fullsize_share_bit_exact_vs_oracle(cuda, case):
-    layout, clients, split, mode = CASES[case]
-    ratio, bits = 0.01, 8
+    layout, clients, split, mode, ratio, frozen = CASES[case]
+    bits = 8
     table, ids = _table(layout, clients, ratio)
     flat = synth_batch(table, cuda, client_ids=ids)
     base = synth_batch(table, cuda, client_ids=[10_000 + i for i in ids]) if mode == "delta" else None
+    if frozen:  # as bench.py's C4_frozen: trained = base + delta, the frozen tensors' deltas exactly zero
+        freeze_segments(flat, table, head_only(layout))
+        flat.add_(base)
     # host copies for the oracle (shared memory: the spawned workers map them, nothing is pickled)
     sb = _to_shared(flat)
     bb = _to_shared(base) if base is not None else None

@@ -37,7 +37,9 @@ def run_both(sizes, ratio, bits, xs, bases=None, flags=0, clients=1):
     d_flat = torch.from_numpy(flat).cuda()
     d_base = None if base is None else torch.from_numpy(base).cuda()
     ws = plan.empty_workspace()
-    enc = plan.encode(d_flat, base=d_base, workspace=ws, flags=flags)
+    # (idx and starts asked for even at ratio 1, where a dense plan's are implied: the library writes them when
+    # given buffers; the dense decode reads neither)
+    enc = plan.encode(d_flat, base=d_base, workspace=ws, flags=flags, out=plan.empty_encoded(with_idx=True))
     dec = plan.decode(enc, base=d_base)
     dec_v1 = plan.decode(Encoded(enc.idx, enc.vals, enc.mn, enc.scale), base=d_base)  # no per-unit starts
     torch.cuda.synchronize()
@@ -263,7 +265,7 @@ def test_golden_vectors_bit_exact(cuda, ratio, bits):
     flat = np.zeros(t.span, np.float32)
     for off, x in zip(t.offsets, xs):
         flat[off:off + x.size] = x
-    enc = plan.encode(torch.from_numpy(flat).cuda())
+    enc = plan.encode(torch.from_numpy(flat).cuda(), out=plan.empty_encoded(with_idx=True))
     dec = plan.decode(enc).cpu().numpy()
     idx, vals = enc.idx.cpu().numpy(), enc.vals.cpu().numpy()
     mn, sc = enc.mn.cpu().numpy(), enc.scale.cpu().numpy()
@@ -321,3 +323,84 @@ def test_scan_stage_overflow_in_a_batch(cuda, delta):
     assert plan.n_units > 8192  # a batch plan
     assert_same(plan, g, r)
     assert g["fallbacks"] == 0
+
+
+def frozen_segments(rng, sizes, trained):
+    """Delta-mode inputs of a frozen backbone (FedPEFT freezes every ViT parameter but the head and the LoRA
+    adapters, /root/reference/application/FedPEFT/lora.py:64, main.py:62-67): the trained tensors move, every
+    other one is exactly its base (an all-zero delta)."""
+    bases = gauss(rng, sizes, -2, -1)
+    xs = [b + d if i in trained else b.copy() for i, (b, d) in enumerate(zip(bases, gauss(rng, sizes)))]
+    return xs, bases
+
+
+@pytest.mark.parametrize("ratio", [0.001, 0.01, 0.1])
+@pytest.mark.parametrize("clients", [1, 2])
+def test_frozen_backbone_takes_the_zero_tie_path(cuda, ratio, clients):
+    """An all-zero delta segment brackets at key 0: its zeros are counted, not recorded, and the k-th key is a
+    zero with a tie quota over them (no raw-data fallback). ViT-B/16 with only the head trained: bit-exact,
+    no fallback, in a latency-bound plan (1 client) and a batch plan (2 clients)."""
+    rng = np.random.default_rng(77 + clients)
+    sizes = fp32_sizes("vit_b16")
+    trained = {len(sizes) - 2, len(sizes) - 1}  # fc.weight, fc.bias
+    xs, bases = zip(*[frozen_segments(rng, sizes, trained) for _ in range(clients)])
+    plan, g, r = run_both(sizes, ratio, 8, list(xs), list(bases), clients=clients)
+    assert_same(plan, g, r)
+    assert g["fallbacks"] == 0
+
+
+@pytest.mark.parametrize("nnz_frac", [0.0, 0.002, 0.006, 0.05])
+@pytest.mark.parametrize("bits", [8, 32])
+def test_sparse_segments_zero_tie_path(cuda, nnz_frac, bits):
+    """Weights-mode segments with fewer nonzeros than k (pruned tensors; +0 / -0 mixed) and with more: the k-th
+    key is a zero exactly when nnz < k. Ragged last units, several segment sizes: bit-exact, no fallback."""
+    rng = np.random.default_rng(int(nnz_frac * 1e4) + bits)
+    sizes = [20000, 4096 * 7 + 3, 250000, 1 << 20, 1500]
+    xs = []
+    for n in sizes:
+        x = np.where(rng.random(n) < 0.5, np.float32(0.0), np.float32(-0.0)).astype(np.float32)
+        m = int(nnz_frac * n)
+        pos = rng.choice(n, m, replace=False)
+        x[pos] = (rng.standard_normal(m) * 1e-3).astype(np.float32)
+        xs.append(x)
+    plan, g, r = run_both(sizes, 0.01, bits, [xs])
+    assert_same(plan, g, r)
+    assert g["fallbacks"] == 0
+
+
+@pytest.mark.parametrize("with_idx", [False, True])
+@pytest.mark.parametrize("delta", [False, True])
+@pytest.mark.parametrize("bits", [1, 8, 32])
+def test_dense_plan_implied_indices(cuda, bits, delta, with_idx):
+    """Ratio 1 (the download direction's dense codec): min / max, quantise and dequantise streams with the
+    indices implied — no idx / starts unless asked for. Ragged sizes put segments' codes at odd byte offsets
+    (the byte-store / byte-load paths), NaN / inf / constant / signed-zero segments, a segment of 3 units + 5:
+    bit-exact against the oracle, in a latency-bound and (2 x 20 MB) a batch plan."""
+    rng = np.random.default_rng(bits * 2 + delta)
+    segs = edge_segments(rng) + [gauss(rng, [4096 * 2100 + 3])[0]]
+    sizes = [s.size for s in segs]
+    for clients in (1, 2):
+        plan = CodecPlan(sizes, 1.0, bits, clients=clients)
+        assert plan.dense and plan.implied_idx
+        t = plan.table
+        xs = [segs] * clients
+        flat = to_flat(t, xs)
+        base = to_flat(t, [gauss(rng, sizes, -2, -1)] * clients) if delta else None
+        d_flat = torch.from_numpy(flat).cuda()
+        d_base = None if base is None else torch.from_numpy(base).cuda()
+        out = plan.empty_encoded(with_idx=with_idx)
+        assert (out.idx.numel() == 0 and out.ustart is None) != with_idx
+        enc = plan.encode(d_flat, base=d_base, out=out)
+        dec = plan.decode(enc, base=d_base).cpu().numpy()
+        torch.cuda.synchronize()
+        s64 = t.segs.astype(np.int64)
+        idx, vals, mn, sc = O.encode(flat, s64, bits, base=base)
+        ref = O.decode(idx, vals, mn, sc, s64, bits, t.span, base=base)
+        np.testing.assert_array_equal(enc.vals.cpu().numpy().view(np.uint8), vals.view(np.uint8))
+        np.testing.assert_array_equal(enc.mn.cpu().numpy().view(np.uint32), mn.view(np.uint32))
+        np.testing.assert_array_equal(enc.scale.cpu().numpy().view(np.uint32), sc.view(np.uint32))
+        if with_idx:
+            np.testing.assert_array_equal(enc.idx.cpu().numpy(), idx)
+            np.testing.assert_array_equal(enc.ustart.cpu().numpy(), O.unit_starts(idx, s64))
+        for (off, n, k, oo) in s64:
+            np.testing.assert_array_equal(dec[off:off + n].view(np.uint32), ref[off:off + n].view(np.uint32))
