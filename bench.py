@@ -23,6 +23,9 @@ collective on the data path — torch.distributed only for the barrier and the m
   C4_delta   the C4 share in delta mode
   C4_frozen  the C4 share in delta mode with the backbone frozen as FedPEFT does (application/FedPEFT/lora.py:64,
           main.py:62-67): every tensor but the classifier head is an exact-zero delta
+  download   the download direction: one ResNet-50 global model per step, dense 8-bit codes at
+          ratio 1 (indices implied) — the server's compression() (coala/server/base.py:196) + one client's
+          decode of it (coala/client/base.py:197-201); HBM bytes 10N + 32T
 value = 4 * N * clients * steps / elapsed (GB/s of fp32 update processed, whole job).
 roofline: the dominant kernel's algorithmic bytes per launch / its mean HIP-event duration, vs 8 TB/s.
 cpu_baseline: the numpy oracle (oracle/codec_oracle.py) on a bounded sample of the same workload, on the
@@ -58,12 +61,13 @@ CONFIGS = {  # name -> (layout | "c5", clients per GPU, sub-batches: the best of
     "C5": ("c5", None, 1, {}),  # one latency-bound plan (<= 8192 units): 0.116 ms vs 0.122 as 2 sub-batches
     "single": ("resnet50_tv", 1, "single", {}),
     "single_x2": ("resnet50_tv", 1, "single", {}),
+    "download": ("resnet50_tv", 1, "single", {"ratio": 1.0}),
 }
 # updates in flight per extra config: single_x2 = one update per step, consecutive steps on two streams (a
 # server decodes concurrent uploads from one thread each, coala/server/service.py:71-111)
 CONFIG_INFLIGHT = {"single_x2": 2}
 SINGLE_SPLIT = 1  # segment ranges of the single update run as this many concurrent sub-plans
-DEFAULT_EXTRAS = "C2,C3_delta,C3_r0.001,C3_r0.1,C4,C4_delta,C4_frozen,C5,single,single_x2,plugin"
+DEFAULT_EXTRAS = "C2,C3_delta,C3_r0.001,C3_r0.1,C4,C4_delta,C4_frozen,C5,single,single_x2,download,plugin"
 
 
 def cfg_opts(cfg, a):
@@ -281,7 +285,7 @@ def build_table(cfg, a, rank, headline):
                            **({"frozen": "every tensor but the classifier head an exact-zero delta"} if frozen else {})}
 
 
-GRAPH_CONFIGS = ("single", "single_x2", "C5")  # latency-bound plans: step time ~ host launch time
+GRAPH_CONFIGS = ("single", "single_x2", "C5", "download")  # latency-bound plans: step time ~ host launch time
 
 
 def use_graph(cfg, a):
@@ -290,7 +294,7 @@ def use_graph(cfg, a):
 
 # configs whose timed steps rotate over ROTATE distinct input / output buffer sets (one ResNet-50 update is
 # 102 MB in + 102 MB out: a single set would stay resident in the 256 MB Infinity Cache, step after step)
-ROTATE_CONFIGS = ("single", "single_x2")
+ROTATE_CONFIGS = ("single", "single_x2", "download")
 ROTATE = 3
 
 
@@ -469,20 +473,25 @@ def time_workload(W, a, dev, world):
         "k_scan": 4 * large_elems + (4 * N if delta else 0),
         "k_decode": 4 * N * (2 if delta else 1) + (4 + vb) * K + 8 * T,
     }
+    dense = t.ratio >= 1.0
+    if dense:  # the dense codec: k_dense_quant (read 4 B, write the code) / k_dense_deq (read the code, write 4 B)
+        alg = {"k_scan": 4 * N * (2 if delta else 1) + vb * N, "k_decode": 4 * N * (2 if delta else 1) + vb * N + 8 * T}
     dom = max(alg, key=lambda k: stages[k])
     ach = alg[dom] / (stages[dom] * 1e-3) / 1e9
     step_ms = el / a.steps * 1e3
     step_alg = t.algorithmic_bytes(a.bits, delta)
+    kname = {"k_scan": "k_dense_quant", "k_decode": "k_dense_deq"}[dom] if dense else dom
     res = {
         "value": round(4.0 * N * world * a.steps / el / 1e9, 2), "ms_per_step": round(step_ms, 4),
         "desc": W["desc"], "split": split, "inflight": len(slots), "rotation": W["rot"],
         "elements_per_gpu": N, "segments_per_gpu": T, "kept_per_gpu": K,
-        "roofline": {"bound": "hbm", "kernel": dom if split == 1 else f"{dom} x{split} concurrent launches (union interval)",
+        "roofline": {"bound": "hbm", "kernel": kname if split == 1 else f"{kname} x{split} concurrent launches (union interval)",
                      "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4),
                      "alg_bytes_per_launch": int(alg[dom])},
         "step_roofline": {"alg_bytes_per_step": step_alg, "achieved_GBs": round(step_alg / (step_ms * 1e-3) / 1e9, 1),
                           "frac": round(step_alg / (step_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)},
-        "stages_ms": {k: round(v, 4) for k, v in stages.items()},
+        "stages_ms": {({"k_scan": "k_dense_quant", "k_decode": "k_dense_deq"}[k] if dense else k): round(v, 4)
+                      for k, v in stages.items()},
         "sample_fallbacks": W.get("fallbacks", 0),
         "graph": W["graph_error"] or (graphs is not None and f"{W['gk']} step(s) per graph launch"),
         "fill_ahead": W["fill_ahead"] and all(p.n_parts == 1 for p in pipes),

@@ -2712,14 +2712,36 @@ __global__ __launch_bounds__(BLOCK, AGG_WPE) void k_aggregate(Params P, AggArgs 
 //   decode: k_dense_deq (per unit: read the 1-B code, write 4 B; + base in delta mode)
 // One wave per 4096-element unit, 16 float4 per lane, XCD-aware unit order in batches.
 // ------------------------------------------------------------------------------------------------
-template <bool DELTA>
+#ifndef DENSE_DEQ_SAUX
+#define DENSE_DEQ_SAUX 2  // k_dense_deq store policy (non-temporal: one update's download 0.073 vs 0.088 ms per
+                          // step; a reciprocal-multiply quantise measured no faster: the streams are memory-bound)
+#endif
+#ifndef DENSE_Q_SAUX
+#define DENSE_Q_SAUX 0  // k_dense_quant code store policy
+#endif
+#ifndef DENSE_MM_AUX
+#define DENSE_MM_AUX 0  // k_dense_minmax load policy (0: default, kept in the caches for the quantise pass)
+#endif
+// AUX: the loads' cache policy — the min / max pass reads with the default policy, so an update that fits the
+// Infinity Cache is still there for the quantise pass, whose non-temporal reads are the last use
+template <bool DELTA, int AUX>
 DEV void dense_unit_load(const Params& P, const UnitDev& U, float4 (&v)[UNIT_IT]) {
+  typedef unsigned int u4v __attribute__((ext_vector_type(4)));
   const uint32_t lane = lane_id();
   const float* xin = P.inptr != nullptr ? P.inptr[U.seg] + U.start : P.in + U.off;
   const __amdgpu_buffer_rsrc_t rin = unit_rsrc(xin, U.len);
   const __amdgpu_buffer_rsrc_t rb = unit_rsrc(DELTA ? P.base + U.off : xin, U.len);
 #pragma unroll
-  for (uint32_t it = 0; it < UNIT_IT; ++it) v[it] = unit_load_x4<DELTA>(rin, rb, (it * 64 + lane) * 16);
+  for (uint32_t it = 0; it < UNIT_IT; ++it) {
+    const int boff = (int)((it * 64 + lane) * 16);
+    const u4v a = __builtin_amdgcn_raw_buffer_load_b128(rin, boff, 0, AUX);
+    v[it] = make_float4(__uint_as_float(a.x), __uint_as_float(a.y), __uint_as_float(a.z), __uint_as_float(a.w));
+    if (DELTA) {
+      const u4v b = __builtin_amdgcn_raw_buffer_load_b128(rb, boff, 0, AUX);
+      v[it] = make_float4(v[it].x - __uint_as_float(b.x), v[it].y - __uint_as_float(b.y), v[it].z - __uint_as_float(b.z),
+                          v[it].w - __uint_as_float(b.w));
+    }
+  }
 }
 
 template <bool DELTA, bool XCD>
@@ -2728,7 +2750,7 @@ __global__ __launch_bounds__(BLOCK) void k_dense_minmax(Params P) {
   if (u >= P.n_units) return;
   const UnitDev U = P.units[u];
   float4 v[UNIT_IT];
-  dense_unit_load<DELTA>(P, U, v);
+  dense_unit_load<DELTA, DENSE_MM_AUX>(P, U, v);
   const uint32_t lane = lane_id();
   float a = qnan(), b = qnan();
 #pragma unroll
@@ -2784,7 +2806,7 @@ __global__ __launch_bounds__(BLOCK) void k_dense_quant(Params P) {
   const UnitDev U = P.units[u];
   const float mn = RAW ? 0.0f : P.mn[U.seg], scale = RAW ? 0.0f : P.scale[U.seg];
   float4 v[UNIT_IT];
-  dense_unit_load<DELTA>(P, U, v);
+  dense_unit_load<DELTA, LOAD_AUX>(P, U, v);
   const uint32_t lane = lane_id();
   const uint64_t o = U.out_off + U.start;  // the unit's first entry (k == n: entry e is element e)
   // whole-dword stores when the unit's codes start 4-byte aligned (16-byte for raw floats) and end on a dword
@@ -2808,7 +2830,7 @@ __global__ __launch_bounds__(BLOCK) void k_dense_quant(Params P) {
       const uint32_t q2 = quantize(v[it].z, mn, scale, P.levels), q3 = quantize(v[it].w, mn, scale, P.levels);
       const uint32_t boff = (it * 64 + lane) * 4;
       if (vec) {
-        __builtin_amdgcn_raw_buffer_store_b32(q0 | (q1 << 8) | (q2 << 16) | (q3 << 24), r, (int)boff, 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b32(q0 | (q1 << 8) | (q2 << 16) | (q3 << 24), r, (int)boff, 0, DENSE_Q_SAUX);
       } else {  // (range-checked per byte: the unit's tail past len is dropped)
         __builtin_amdgcn_raw_buffer_store_b8((uint8_t)q0, r, (int)boff, 0, 0);
         __builtin_amdgcn_raw_buffer_store_b8((uint8_t)q1, r, (int)boff + 1, 0, 0);
@@ -2880,9 +2902,9 @@ __global__ __launch_bounds__(BLOCK) void k_dense_deq(Params P) {
       x = make_float4(b.x + x.x, b.y + x.y, b.z + x.z, b.w + x.w);
     }
     if ((U.len & 3u) == 0)
-      unit_store_x4<0>(rout, (it * 64 + lane) * 16, x);
+      unit_store_x4<DENSE_DEQ_SAUX>(rout, (it * 64 + lane) * 16, x);
     else
-      unit_store_x1x4<0>(rout, (it * 64 + lane) * 16, x);
+      unit_store_x1x4<DENSE_DEQ_SAUX>(rout, (it * 64 + lane) * 16, x);
   }
 }
 
