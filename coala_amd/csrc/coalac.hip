@@ -2224,7 +2224,10 @@ DEV void wave_lower_bound(const int32_t* const (&L)[M], const uint32_t (&k)[M], 
 #define DECODE_SAUX_LAT 0  // latency-bound plans: store cache policy (a ~100 MB output: plain stores)
 #endif
 
-template <bool RAW, bool HASBASE, uint32_t WPU, uint32_t QROWS, int SAUX, bool XCD>
+// NCH: 64-entry chunks of the unit's kept entries held in registers across the passes (1 at ratios up to ~1.5 %;
+// plans of higher ratios take 8 — up to 512 entries, ratio ~12 % — so the entry lists are loaded once per unit,
+// not once per pass and again for the zeroing); chunks past NCH are loaded per pass as before
+template <bool RAW, bool HASBASE, uint32_t WPU, uint32_t QROWS, int SAUX, bool XCD, uint32_t NCH = 1>
 __global__ __launch_bounds__(DECODE_NT, HASBASE ? DECODE_LDS_WPE_BASE : DECODE_LDS_WPE) void k_decode_lds(Params P) {
   constexpr uint32_t DW = DECODE_NT / 64, RPW = UNIT_IT / WPU, NPASS = RPW / QROWS;
   constexpr uint32_t QSH = QROWS == 2u ? 9u : QROWS == 4u ? 10u : QROWS == 8u ? 11u : 12u, QM = (1u << QSH) - 1u;
@@ -2249,10 +2252,14 @@ __global__ __launch_bounds__(DECODE_NT, HASBASE ? DECODE_LDS_WPE_BASE : DECODE_L
   lo = min(lo, U.k);
   hi = max(lo, min(min(U.last ? U.k : hi, U.k), lo + U.len));
   const uint32_t cnt = hi - lo;
-  // round 2: the first 64 entries (+ the base rows of the first pass)
-  const uint64_t e1 = U.out_off + min(lo + lane, U.k - 1);
-  const uint32_t q1 = load_code<RAW>(P, e1);
-  const uint32_t pos = (uint32_t)P.cidx[e1] - U.start;
+  // round 2: the first NCH x 64 entries (+ the base rows of the first pass)
+  uint32_t qc[NCH], posc[NCH];
+#pragma unroll
+  for (uint32_t c = 0; c < NCH; ++c) {
+    const uint64_t e1 = U.out_off + min(lo + c * 64 + lane, U.k - 1);
+    qc[c] = load_code<RAW>(P, e1);
+    posc[c] = (uint32_t)P.cidx[e1] - U.start;
+  }
   const uint32_t len = U.len;
   const __amdgpu_buffer_rsrc_t rout = unit_rsrc(P.out + U.off, len);
   const __amdgpu_buffer_rsrc_t rb = unit_rsrc(HASBASE ? P.base + U.off : P.out + U.off, len);
@@ -2261,7 +2268,9 @@ __global__ __launch_bounds__(DECODE_NT, HASBASE ? DECODE_LDS_WPE_BASE : DECODE_L
 #pragma unroll
     for (uint32_t it = 0; it < QROWS; ++it) bn[it] = unit_load_x4<false>(rb, rb, ((pass0 * QROWS + it) * 64 + lane) * 16);
   }
-  const float val = code_value<RAW>(q1, mn, sc);
+  float valc[NCH];
+#pragma unroll
+  for (uint32_t c = 0; c < NCH; ++c) valc[c] = code_value<RAW>(qc[c], mn, sc);
   lds_order();
 #pragma unroll
   for (uint32_t qi = 0; qi < NPASS; ++qi) {
@@ -2275,9 +2284,11 @@ __global__ __launch_bounds__(DECODE_NT, HASBASE ? DECODE_LDS_WPE_BASE : DECODE_L
           bn[it] = unit_load_x4<false>(rb, rb, (((qq + 1) * QROWS + it) * 64 + lane) * 16);
       }
     }
-    // scatter: the first 64 entries are in registers; more (ratio >~ 1.5 %) are loaded chunk by chunk
-    if (lane < min(cnt, 64u) && (pos >> QSH) == qq) tf[pos & QM] = val;
-    for (uint32_t e0 = lo + 64; e0 < hi; e0 += 64) {
+    // scatter: the first NCH x 64 entries are in registers; more are loaded chunk by chunk
+#pragma unroll
+    for (uint32_t c = 0; c < NCH; ++c)
+      if (c * 64 + lane < cnt && (posc[c] >> QSH) == qq) tf[posc[c] & QM] = valc[c];
+    for (uint32_t e0 = lo + NCH * 64; e0 < hi; e0 += 64) {
       const uint64_t e = U.out_off + min(e0 + lane, hi - 1);
       const uint32_t p2 = (uint32_t)P.cidx[e] - U.start;
       if (e0 + lane < hi && (p2 >> QSH) == qq) tf[p2 & QM] = code_value<RAW>(load_code<RAW>(P, e), mn, sc);
@@ -2291,8 +2302,10 @@ __global__ __launch_bounds__(DECODE_NT, HASBASE ? DECODE_LDS_WPE_BASE : DECODE_L
     }
     lds_order();
     if (qi + 1 < NPASS) {  // zero what was written (the same slots), for the next pass
-      if (lane < min(cnt, 64u) && (pos >> QSH) == qq) tf[pos & QM] = 0.0f;
-      for (uint32_t e0 = lo + 64; e0 < hi; e0 += 64) {
+#pragma unroll
+      for (uint32_t c = 0; c < NCH; ++c)
+        if (c * 64 + lane < cnt && (posc[c] >> QSH) == qq) tf[posc[c] & QM] = 0.0f;
+      for (uint32_t e0 = lo + NCH * 64; e0 < hi; e0 += 64) {
         const uint64_t e = U.out_off + min(e0 + lane, hi - 1);
         const uint32_t p2 = (uint32_t)P.cidx[e] - U.start;
         if (e0 + lane < hi && (p2 >> QSH) == qq) tf[p2 & QM] = 0.0f;
@@ -3010,6 +3023,7 @@ struct coalac_plan {
   uint32_t small_max = SMALL_MAX;  // segments of <= this many elements are "small" (encoded whole by one block)
   uint32_t ccap = UNIT;  // candidate record slots per large unit
   bool dense = false;    // every segment keeps all its elements: the dense codec (indices implied)
+  double rmax = 0.0;     // the largest k / n of the plan's segments
   uint64_t span = 0, total_k = 0;
   void* meta = nullptr;
   SegDev* segs = nullptr;
@@ -3343,6 +3357,7 @@ int coalac_plan_create(const coalac_seg_t* h_segs, int nseg, int bits, coalac_pl
   // share + the sampled band + margin), so the workspace is ~1 B/element at ratio 0.01 instead of 8
   double rmax = 0.0;
   for (uint32_t s2 : large_list) rmax = std::max(rmax, (double)segs[s2].k / (double)segs[s2].n);
+  p->rmax = rmax;
   uint32_t ccap = (uint32_t)align_up((size_t)(UNIT * std::min(1.0, 2.0 * rmax + 0.05) + 256.0), 64);
   if (const char* e = getenv("COALAC_CCAP")) ccap = (uint32_t)atoi(e);  // tests: force overflow
   ccap = std::max<uint32_t>(STAGE_CAP, std::min<uint32_t>(UNIT, ccap));
@@ -3566,17 +3581,30 @@ namespace {
 // The write-once decode (k_decode_lds) of a whole plan: batches one wave per unit in two 8-row passes (4-row in
 // delta mode) with non-temporal stores and the XCD-aware order; latency-bound plans DECODE_WPU_LAT waves per unit
 // (one pass each: twice the waves, each with half the work, for a launch of one update's ~6.5 k units).
-template <bool RAW, bool HB>
-void launch_decode_lds(const Params& P, coalac_plan_t plan, hipStream_t st) {
+template <bool RAW, bool HB, uint32_t NCH>
+void launch_decode_lds_n(const Params& P, coalac_plan_t plan, hipStream_t st) {
   constexpr uint32_t DW = DECODE_NT / 64;
   if (plan->n_units <= LATENCY_PLAN_UNITS) {
     constexpr uint32_t W = DECODE_WPU_LAT, Q = HB ? DECODE_QROWS_BASE : UNIT_IT / DECODE_WPU_LAT;
-    hipLaunchKernelGGL((k_decode_lds<RAW, HB, W, (Q < 8u ? Q : 8u), DECODE_SAUX_LAT, false>),
+    hipLaunchKernelGGL((k_decode_lds<RAW, HB, W, (Q < 8u ? Q : 8u), DECODE_SAUX_LAT, false, NCH>),
                        dim3((plan->n_units * W + DW - 1) / DW), dim3(DECODE_NT), 0, st, P);
   } else {
-    hipLaunchKernelGGL((k_decode_lds<RAW, HB, 1u, HB ? DECODE_QROWS_BASE : DECODE_QROWS, STORE_AUX, DECODE_XCD != 0>),
+    hipLaunchKernelGGL((k_decode_lds<RAW, HB, 1u, HB ? DECODE_QROWS_BASE : DECODE_QROWS, STORE_AUX, DECODE_XCD != 0, NCH>),
                        dim3((plan->n_units + DW - 1) / DW), dim3(DECODE_NT), 0, st, P);
   }
+}
+
+// plans whose segments keep more than ~1.5 % (more than 64 entries in a unit on average) hold 8 entry chunks in
+// registers (DECODE_NCH_RATIO: the ratio from which they do)
+#ifndef DECODE_NCH_RATIO
+#define DECODE_NCH_RATIO 0.02
+#endif
+template <bool RAW, bool HB>
+void launch_decode_lds(const Params& P, coalac_plan_t plan, hipStream_t st) {
+  if (plan->rmax > DECODE_NCH_RATIO)
+    launch_decode_lds_n<RAW, HB, 8u>(P, plan, st);
+  else
+    launch_decode_lds_n<RAW, HB, 1u>(P, plan, st);
 }
 
 template <bool RAW, bool HB>
