@@ -112,10 +112,6 @@ def parse():
                    help="at most this many timed steps captured in one graph (--graph; whole input rotations, the "
                         "count that needs the fewest launches): 1 / 4 / 10 steps per launch measured 0.0845 / 0.0803 / "
                         "0.0796 ms per single step (eager 0.080-0.083)")
-    p.add_argument("--fill-ahead", choices=["on", "off"], default="off",
-                   help="one-update configs: write the decode's background on a side stream beside the encode's "
-                        "select chain (SplitPipeline.roundtrip fill_ahead). Off: in a captured graph it measured "
-                        "0.0922 vs 0.0786 ms per single step (the cross-stream edges cost more than the fill)")
     p.add_argument("--cpu-seconds", type=float, default=8.0, help="CPU baseline time budget per leg")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--launch-check", action="store_true",
@@ -322,9 +318,7 @@ def setup_workload(cfg, a, dev, rank, headline):
         slots.append((p, [(p.empty_encoded(), p.empty_flat()) for _ in range(rot)]))
     torch.cuda.synchronize()
     return {"cfg": cfg, "headline": headline, "table": t, "desc": desc, "flats": flats, "base": base, "rot": rot,
-            "mode": mode,
-            "slots": slots, "split": slots[0][0].n_parts, "graphs": None, "graph_error": None,
-            "fill_ahead": a.fill_ahead == "on"}
+            "mode": mode, "slots": slots, "split": slots[0][0].n_parts, "graphs": None, "graph_error": None}
 
 
 def _step(W, i, joined, enc_events=None, dec_events=None):
@@ -334,7 +328,7 @@ def _step(W, i, joined, enc_events=None, dec_events=None):
     r = (i // len(W["slots"])) % W["rot"]
     enc, out = bufs[r]
     p.roundtrip(W["flats"][r], base=W["base"], enc=enc, out=out, enc_events=enc_events, dec_events=dec_events,
-                joined=joined, fill_ahead=W["fill_ahead"] and enc_events is None)
+                joined=joined)
 
 
 def warm_workload(W, a):
@@ -494,7 +488,6 @@ def time_workload(W, a, dev, world):
                       for k, v in stages.items()},
         "sample_fallbacks": W.get("fallbacks", 0),
         "graph": W["graph_error"] or (graphs is not None and f"{W['gk']} step(s) per graph launch"),
-        "fill_ahead": W["fill_ahead"] and all(p.n_parts == 1 for p in pipes),
         "rank_ms_per_step": rank_spread(rank_el, a.steps),
     }
     if headline:
@@ -784,7 +777,7 @@ def main():
             "graph": head["graph"], "rank_ms_per_step": head["rank_ms_per_step"],
             "configs": {k: {f: v[f] for f in ("value", "ms_per_step", "step_roofline", "roofline", "stages_ms", "desc",
                                               "elements_per_gpu", "segments_per_gpu", "split", "inflight", "rotation",
-                                              "graph", "fill_ahead", "sample_fallbacks", "rank_ms_per_step")}
+                                              "graph", "sample_fallbacks", "rank_ms_per_step")}
                         for k, v in results.items()},
         }
         res["box"] = box

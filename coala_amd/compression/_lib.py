@@ -13,10 +13,6 @@ COALAC_FLAG_FORCE_EXACT = 1
 COALAC_FLAG_GENERIC_SELECT = 2
 COALAC_FLAG_STAMPS = 4
 COALAC_FLAG_NO_FORK = 8
-# stages of a split encode / decode (coalac_sched_t.stages; 0 = all)
-COALAC_STAGE_SAMPLE, COALAC_STAGE_SCAN, COALAC_STAGE_SELECT, COALAC_STAGE_SMALL = 1, 2, 4, 8
-COALAC_STAGE_BOUNDS, COALAC_STAGE_DECODE, COALAC_STAGE_FILL, COALAC_STAGE_SCATTER = 1, 2, 4, 8
-COALAC_STAGE_BOUNDS_DONE = 16  # decode: BOUNDS was enqueued by an earlier call on this workspace (batch plans)
 COALAC_AGG_DIV = 0     # acc / total            (torch CPU division by a scalar)
 COALAC_AGG_RECIP = 1   # acc * (1.0f / total)   (torch GPU division by a host scalar)
 COALAC_AGG_SUM = 2     # acc                    (weighted_sum: the multi-GPU per-rank sum)
@@ -40,25 +36,23 @@ SIGNATURES = [
     ("coalac_plan_create", _I, [_P, _I, _I, ctypes.POINTER(_P)]),
     ("coalac_plan_destroy", _I, [_P]),
     ("coalac_plan_query", _I, [_P, ctypes.POINTER(_U64), ctypes.POINTER(_U64), ctypes.POINTER(_U64),
-                               ctypes.POINTER(_U64), ctypes.POINTER(_U64)]),
-    # encode: plan, in / seg pointers, base, idx, vals, mn, scale, ustart, ws, ws_bytes, flags, stream (+ events / sched)
+                               ctypes.POINTER(_U64)]),
+    # encode: plan, in / seg pointers, base, idx, vals, mn, scale, ustart, ws, ws_bytes, flags, stream (+ events)
     ("coalac_encode", _I, [_P, _P, _P, _P, _P, _P, _P, _P, _P, _U64, ctypes.c_uint, _P]),
     ("coalac_encode_segptr", _I, [_P, _P, _P, _P, _P, _P, _P, _P, _P, _U64, ctypes.c_uint, _P]),
-    # decode: plan, idx, vals, mn, scale, ustart, base, out, ws, ws_bytes, stream (+ events / sched)
-    ("coalac_decode", _I, [_P, _P, _P, _P, _P, _P, _P, _P, _P, _U64, _P]),
+    # decode: plan, idx, vals, mn, scale, ustart, base, out, stream (+ events)
+    ("coalac_decode", _I, [_P, _P, _P, _P, _P, _P, _P, _P, _P]),
     ("coalac_encode_ev", _I, [_P, _P, _P, _P, _P, _P, _P, _P, _P, _U64, ctypes.c_uint, _P, _P]),
-    ("coalac_decode_ev", _I, [_P, _P, _P, _P, _P, _P, _P, _P, _P, _U64, _P, _P]),
-    ("coalac_encode_sched", _I, [_P, _P, _P, _P, _P, _P, _P, _P, _P, _U64, ctypes.c_uint, _P, _P]),
-    ("coalac_decode_sched", _I, [_P, _P, _P, _P, _P, _P, _P, _P, _P, _U64, _P, _P]),
-    # aggregate: plan, clients, idx, vals, mn, scale, ustart, weights, total, mode, mask, base, out, ws, ws_bytes, stream
-    ("coalac_aggregate", _I, [_P, _I, _P, _P, _P, _P, _P, _P, ctypes.c_float, _I, _P, _P, _P, _P, _U64, _P]),
-    ("coalac_aggregate_ev", _I, [_P, _I, _P, _P, _P, _P, _P, _P, ctypes.c_float, _I, _P, _P, _P, _P, _U64, _P, _P]),
+    ("coalac_decode_ev", _I, [_P, _P, _P, _P, _P, _P, _P, _P, _P, _P]),
+    # aggregate: plan, clients, idx, vals, mn, scale, ustart, weights, total, mode, mask, base, out, stream (+ events)
+    ("coalac_aggregate", _I, [_P, _I, _P, _P, _P, _P, _P, _P, ctypes.c_float, _I, _P, _P, _P, _P]),
+    ("coalac_aggregate_ev", _I, [_P, _I, _P, _P, _P, _P, _P, _P, ctypes.c_float, _I, _P, _P, _P, _P, _P]),
     ("coalac_gather", _I, [_P, _I, _I, _P, _P]),
     ("coalac_workspace_fallbacks", _I, [_P, _P, _P, ctypes.POINTER(_I)]),
     ("coalac_debug_stamps", _I, [_P, _P, _P, ctypes.POINTER(ctypes.c_uint64), _I]),
 ]
 
-ABI_VERSION = 4
+ABI_VERSION = 5
 
 
 class CodecError(RuntimeError):
@@ -67,11 +61,6 @@ class CodecError(RuntimeError):
 
 class SegDesc(ctypes.Structure):
     _fields_ = [("in_off", _U64), ("n", _U64), ("k", _U64), ("out_off", _U64)]
-
-
-class Sched(ctypes.Structure):
-    """coalac_sched_t: per stage boundary, an event to wait for and an event to record (hipEvent_t)."""
-    _fields_ = [("wait", _P * 5), ("record", _P * 5), ("stages", ctypes.c_uint)]
 
 
 _lock = threading.Lock()

@@ -927,9 +927,9 @@ class UpdateCodec:
 
     WS_CACHE = 16  # encode workspaces kept per codec (one per plan and launch stream in use)
 
-    def _workspace(self, plan, stream=None, decode=False):
-        """The encode (or, decode=True, decode) workspace of `plan` for this thread and `stream` (default: the
-        current one), reused across calls (kernels on
+    def _workspace(self, plan, stream=None):
+        """The encode workspace of `plan` for this thread and `stream` (default: the current one), reused across
+        calls (kernels on
         one stream run in order, so consecutive encodes of one thread can share it). Keyed by thread too: two
         threads encoding on one stream (e.g. both on the default stream) interleave their launches, since the
         ctypes call releases the GIL, and one encode's select would read the other's scan results. A bounded
@@ -939,17 +939,13 @@ class UpdateCodec:
             return None
         if stream is None:
             stream = torch.cuda.current_stream(plan.device) if plan.device.type == "cuda" else None
-        key = (id(plan), threading.get_ident(), None if stream is None else stream.cuda_stream, decode)
+        key = (id(plan), threading.get_ident(), None if stream is None else stream.cuda_stream)
         with self._lock:
             hit = self._ws.get(key)
             if hit is not None and hit[0] is plan:
                 self._ws.move_to_end(key)
                 return hit[1]
-            if decode:
-                with torch.cuda.stream(stream):  # (allocated on the stream that uses it)
-                    ws = plan.empty_decode_workspace()
-            else:
-                ws = plan.empty_workspace()
+            ws = plan.empty_workspace()
             self._ws[key] = (plan, ws)
             self._ws.move_to_end(key)
             while len(self._ws) > self.WS_CACHE:
@@ -1009,8 +1005,7 @@ class UpdateCodec:
                 with torch.cuda.stream(side):
                     enc = update.encoded_to(device, staging=self._staging)
                     self._staged(side)
-                    flat = plan.decode(enc, base=base_flat, out=out, stream=side,
-                                       workspace=self._workspace(plan, side, decode=True))
+                    flat = plan.decode(enc, base=base_flat, out=out, stream=side)
                     if into is not None:
                         for dst, (src, _) in zip(into.raws, raw._groups):
                             dst.copy_(src, non_blocking=True)

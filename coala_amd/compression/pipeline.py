@@ -12,7 +12,7 @@ import torch
 
 from . import _lib
 from .plan import CodecPlan, Encoded
-from .spec import LATENCY_PLAN_UNITS, SegmentTable, units_of
+from .spec import SegmentTable, units_of
 
 _STREAM_POOL = {}  # device index -> streams shared by every SplitPipeline of the process
 
@@ -116,8 +116,7 @@ class SplitPipeline:
                 for c0, c1, st in zip(cuts[:-1], cuts[1:], streams):
                     plan = CodecPlan(None, table.ratio, self.bits, device=self.device, table=table.sub_table(c0, c1))
                     self.parts.append(dict(x=slice(so[c0], so[c1]), k=slice(ko[c0], ko[c1]), t=slice(to[c0], to[c1]),
-                                           u=slice(uo[c0], uo[c1]), plan=plan, ws=plan.empty_workspace(),
-                                           dws=plan.empty_decode_workspace(), stream=st))
+                                           u=slice(uo[c0], uo[c1]), plan=plan, ws=plan.empty_workspace(), stream=st))
             else:
                 # fewer clients than sub-batches (e.g. ONE update): contiguous SEGMENT ranges balanced by
                 # element count, each a plan over absolute segment rows that reads / writes the whole
@@ -129,8 +128,7 @@ class SplitPipeline:
                 for (s0, s1), st in zip(ranges, pooled_streams(self.device, stream_base + len(ranges))[stream_base:]):
                     plan = CodecPlan.from_segments(table.segs[s0:s1], self.bits, device=self.device)
                     self.parts.append(dict(x=slice(None), k=slice(None), t=slice(s0, s1), u=slice(uo[s0], uo[s1]),
-                                           plan=plan, ws=plan.empty_workspace(), dws=plan.empty_decode_workspace(),
-                                           stream=st))
+                                           plan=plan, ws=plan.empty_workspace(), stream=st))
 
     @property
     def n_parts(self):
@@ -178,7 +176,7 @@ class SplitPipeline:
                          flags=self.flags | self.fork_flag, events=None if events is None else events[g])
 
     def _decode_part(self, g, P, enc, base, out, events):
-        P["plan"].decode(self._enc(enc, P), base=self._x(base, P), out=self._x(out, P), workspace=P["dws"],
+        P["plan"].decode(self._enc(enc, P), base=self._x(base, P), out=self._x(out, P),
                          events=None if events is None else events[g])
 
     def encode(self, flat, base=None, out=None, events=None, joined=True):
@@ -197,57 +195,18 @@ class SplitPipeline:
         self._run(lambda g, P: self._decode_part(g, P, enc, base, out, events), joined)
         return out
 
-    def roundtrip(self, flat, base=None, enc=None, out=None, enc_events=None, dec_events=None, joined=True,
-                  fill_ahead=False):
+    def roundtrip(self, flat, base=None, enc=None, out=None, enc_events=None, dec_events=None, joined=True):
         """encode() then decode() with one join each way: sub-batch g's decode follows its own encode on
-        its stream only.
-
-        fill_ahead (one latency-bound part, i.e. one update; meant for captured graphs): the decode's
-        background (COALAC_STAGE_FILL: zeros / base + 0.0f, no payload needed) is written on a side stream
-        beside the encode's select chain (k_ghist, k_gwin, k_select, k_emit: latency-bound, little HBM
-        traffic), forked after k_scan; the kept values (SCATTER) follow once both are done. Eager, each
-        cross-stream wait costs more than the fill it hides; in a graph they are edges."""
+        its stream only."""
         enc = self.empty_encoded() if enc is None else enc
         if out is None:
             out = self.empty_flat() if base is None else torch.empty_like(base)
-        if fill_ahead and self.n_parts == 1 and self.parts[0]["plan"].n_units <= LATENCY_PLAN_UNITS:
-            self._roundtrip_fill_ahead(flat, base, enc, out, joined)
-            return enc, out
 
         def both(g, P):
             self._encode_part(g, P, flat, base, enc, enc_events)
             self._decode_part(g, P, enc, base, out, dec_events)
         self._run(both, joined)
         return enc, out
-
-    def _roundtrip_fill_ahead(self, flat, base, enc, out, joined):
-        P = self.parts[0]
-        plan, st = P["plan"], P["stream"]
-        if "side" not in P:
-            P["side"] = torch.cuda.Stream(self.device)
-            P["scanned"], P["filled"] = torch.cuda.Event(), torch.cuda.Event()
-        side = P["side"]
-        cur = torch.cuda.current_stream(self.device)
-        if joined:
-            st.wait_stream(cur)
-        x, b, e = self._x(flat, P), self._x(base, P), self._enc(enc, P)
-        front = _lib.COALAC_STAGE_SAMPLE | _lib.COALAC_STAGE_SCAN | _lib.COALAC_STAGE_SMALL
-        with torch.cuda.stream(st):
-            plan.encode(x, base=b, out=e, workspace=P["ws"], flags=self.flags | self.fork_flag,
-                        sched=(None, None, front))
-            P["scanned"].record(st)
-        side.wait_event(P["scanned"])
-        with torch.cuda.stream(side):
-            plan.decode(e, base=b, out=self._x(out, P), workspace=P["dws"], sched=(None, None, _lib.COALAC_STAGE_FILL))
-            P["filled"].record(side)
-        with torch.cuda.stream(st):
-            plan.encode(x, base=b, out=e, workspace=P["ws"], flags=self.flags | self.fork_flag,
-                        sched=(None, None, _lib.COALAC_STAGE_SELECT))
-            st.wait_event(P["filled"])
-            plan.decode(e, base=b, out=self._x(out, P), workspace=P["dws"],
-                        sched=(None, None, _lib.COALAC_STAGE_SCATTER))
-        if joined:
-            cur.wait_stream(st)
 
     def fallbacks(self):
         torch.cuda.synchronize(self.device)

@@ -12,7 +12,7 @@ from dataclasses import dataclass
 import torch
 
 from . import _lib
-from .spec import RAW_BITS, VALID_BITS, SegmentTable, SubTable
+from .spec import RAW_BITS, UNIT, VALID_BITS, SegmentTable, SubTable
 
 
 @dataclass
@@ -90,10 +90,10 @@ class CodecPlan:
             _lib.check(self._lib.coalac_plan_create(arr, len(segs), self.bits, ctypes.byref(h)),
                        "coalac_plan_create")
         self._h = h
-        ws, dws, tk, span, nu = (ctypes.c_uint64() for _ in range(5))
-        _lib.check(self._lib.coalac_plan_query(h, ctypes.byref(ws), ctypes.byref(dws), ctypes.byref(tk),
-                                               ctypes.byref(span), ctypes.byref(nu)), "coalac_plan_query")
-        self.ws_bytes, self.dec_ws_bytes = ws.value, dws.value
+        ws, tk, span, nu = (ctypes.c_uint64() for _ in range(4))
+        _lib.check(self._lib.coalac_plan_query(h, ctypes.byref(ws), ctypes.byref(tk), ctypes.byref(span),
+                                               ctypes.byref(nu)), "coalac_plan_query")
+        self.ws_bytes = ws.value
         self.total_k, self.span, self.n_units = tk.value, span.value, nu.value
         if self.total_k != self.table.total_k:
             raise _lib.CodecError(f"plan total_k {self.total_k} != table {self.table.total_k}")
@@ -167,9 +167,6 @@ class CodecPlan:
     def empty_workspace(self):
         return torch.empty(self.ws_bytes, dtype=torch.uint8, device=self.device)
 
-    def empty_decode_workspace(self):
-        return torch.empty(self.dec_ws_bytes, dtype=torch.uint8, device=self.device)
-
     # -- checks -----------------------------------------------------------------------------------
     def _check_flat(self, t, name, need=None):
         if t is None:
@@ -200,11 +197,10 @@ class CodecPlan:
         return _ptr(e.ustart)
 
     # -- codec ------------------------------------------------------------------------------------
-    def encode(self, flat, base=None, out=None, workspace=None, flags=0, stream=None, events=None, sched=None):
+    def encode(self, flat, base=None, out=None, workspace=None, flags=0, stream=None, events=None):
         """Encode flat (fp32[span]) [- base] -> Encoded. Asynchronous on `stream`.
 
-        events: 5 timing events recorded at the stage boundaries (coalac_encode_ev); sched: (wait,
-        record[, stages]) — lists of 5 events (or None) and a COALAC_STAGE_* mask (coalac_encode_sched)."""
+        events: 5 timing events recorded at the kernel boundaries (coalac_encode_ev)."""
         self._check_flat(flat, "input")
         self._check_flat(base, "base")
         with _on(stream):
@@ -217,9 +213,7 @@ class CodecPlan:
                 _ptr(out.scale), ust, _ptr(ws), ctypes.c_uint64(self.ws_bytes), ctypes.c_uint(flags),
                 _stream_handle(stream))
         with torch.cuda.device(self.device):
-            if sched is not None:
-                rc = self._lib.coalac_encode_sched(*args, ctypes.byref(_sched(sched, 5)))
-            elif events is None:
+            if events is None:
                 rc = self._lib.coalac_encode(*args)
             else:
                 rc = self._lib.coalac_encode_ev(*args, _event_array(events, 5))
@@ -286,34 +280,64 @@ class CodecPlan:
         _lib.check(rc, "coalac_encode_segptr")
         return out
 
-    def decode(self, enc, base=None, out=None, workspace=None, stream=None, events=None, sched=None):
+    def unit_starts(self, idx, stream=None):
+        """The per-unit starts (wire v2) of this plan's idx list, computed on the device for a payload that carries
+        none (a version-1 blob, or an Encoded built without them): for unit j of segment s, the number of the
+        segment's kept indices below j * 4096 — one searchsorted over the entries' global unit numbers, which are
+        non-decreasing across the plan (segments in order, indices ascending). An unsorted (untrusted) list gives
+        wrong but in-range starts; the decode kernels clamp them to their unit."""
+        aux = self.__dict__.get("_starts_aux")
+        if aux is None:
+            segs = self.table.segs.astype("int64")
+            n, k, oo = segs[:, 1], segs[:, 2], segs[:, 3]
+            nu = (n + UNIT - 1) // UNIT
+            ubase = torch.from_numpy((nu.cumsum() - nu).astype("int32"))
+            kk, nnu = torch.from_numpy(k), torch.from_numpy(nu)
+            first = torch.from_numpy((k.cumsum() - k).astype("int32"))  # each segment's first entry in the plan's list
+            ents = None
+            if not (oo == (k.cumsum() - k)).all():  # (a SubTable: the segments' entries sit at absolute offsets)
+                ents = torch.cat([torch.arange(int(o), int(o) + int(c), dtype=torch.int64) for o, c in zip(oo, k)])
+            aux = self._starts_aux = (torch.repeat_interleave(ubase, kk).to(self.device),
+                                      torch.repeat_interleave(first, nnu).to(self.device),
+                                      torch.arange(int(nu.sum()), dtype=torch.int32).to(self.device),
+                                      None if ents is None else ents.to(self.device))
+        ubase_rep, first_rep, units, ents = aux
+        with _on(stream):
+            own = idx[:self.total_k] if ents is None else idx[ents]
+            gu = ubase_rep + torch.bitwise_right_shift(own, 12)
+            return (torch.searchsorted(gu, units, out_int32=True) - first_rep).to(torch.int32)
+
+    def _starts_for(self, enc, stream):
+        """enc.ustart, or (no starts, a sparse plan) the device-computed ones."""
+        if enc.ustart is not None or self.dense:
+            return enc
+        return Encoded(enc.idx, enc.vals, enc.mn, enc.scale, self.unit_starts(enc.idx, stream))
+
+    def decode(self, enc, base=None, out=None, stream=None, events=None):
         """Decode Encoded -> dense flat fp32[span] (+ base, fused). Asynchronous on `stream`.
 
-        enc.ustart (wire v2 per-unit starts), when present, saves the decode its search of the idx lists.
-        events / sched: as encode(), 3 boundaries (coalac_decode_ev / coalac_decode_sched)."""
+        enc.ustart: the wire v2 per-unit starts; without them (a v1 payload) they are computed on the device first
+        (unit_starts). events: 3 timing events (coalac_decode_ev: [1] / [2] bracket the decode kernel)."""
+        self._check_encoded(enc)
+        enc = self._starts_for(enc, stream)
         ust = self._check_encoded(enc)
         self._check_flat(base, "base")
         with _on(stream):
             if out is None:
                 out = self.empty_flat() if base is None else torch.empty_like(base)
-            ws = self.empty_decode_workspace() if workspace is None else workspace
         self._check_flat(out, "output")
-        if ws.device != self.device or ws.numel() * ws.element_size() < self.dec_ws_bytes:
-            raise ValueError(f"decode workspace: need {self.dec_ws_bytes} bytes on {self.device}")
         args = (self._h, _idx_ptr(enc.idx), _ptr(enc.vals), _ptr(enc.mn), _ptr(enc.scale), ust, _ptr(base), _ptr(out),
-                _ptr(ws), ctypes.c_uint64(self.dec_ws_bytes), _stream_handle(stream))
+                _stream_handle(stream))
         with torch.cuda.device(self.device):
-            if sched is not None:
-                rc = self._lib.coalac_decode_sched(*args, ctypes.byref(_sched(sched, 3)))
-            elif events is None:
+            if events is None:
                 rc = self._lib.coalac_decode(*args)
             else:
                 rc = self._lib.coalac_decode_ev(*args, _event_array(events, 3))
         _lib.check(rc, "coalac_decode")
         return out
 
-    def aggregate(self, enc, weights, total=None, base=None, out=None, workspace=None, mode="recip", stream=None,
-                  events=None, avg_mask=None):
+    def aggregate(self, enc, weights, total=None, base=None, out=None, mode="recip", stream=None, events=None,
+                  avg_mask=None):
         """Fused decode + FedAvg of the plan's `clients` updates (coalac_aggregate).
 
         enc: the batched Encoded of all clients (client-major, as encode() produces). weights: one
@@ -325,14 +349,17 @@ class CodecPlan:
         strategies.py:57-90: what a multi-GPU server hands to reduce_models, distributed.py:42-57).
         avg_mask: one bool per segment of a client (None: all True); a False segment is not averaged but
         takes client 0's decoded value — aggregation_content "parameters" (strategies.py:32-54, 93-124).
-        enc.ustart (the clients' per-unit starts, concatenated) replaces the k_bounds pass when present.
+        enc.ustart: the clients' per-unit starts, concatenated (computed on the device when absent).
         """
-        ust = self._check_encoded(enc)
+        self._check_encoded(enc)
         if not getattr(self.table, "uniform", False):
             raise ValueError("fused aggregation needs a plan over copies of one layout (a SegmentTable)")
         if self.dense and enc.idx.numel() == 0:  # (the aggregate kernel reads explicit indices: implied ones made here)
             with _on(stream):
-                enc = Encoded(self.implied_indices(), enc.vals, enc.mn, enc.scale, enc.ustart)
+                enc = Encoded(self.implied_indices(), enc.vals, enc.mn, enc.scale, None)
+        if enc.ustart is None:
+            enc = Encoded(enc.idx, enc.vals, enc.mn, enc.scale, self.unit_starts(enc.idx, stream))
+        ust = self._check_encoded(enc)
         C = self.table.clients
         if len(weights) != C:
             raise ValueError(f"need {C} weights, got {len(weights)}")
@@ -344,7 +371,6 @@ class CodecPlan:
             self._check_flat(base, "base", n_out)
         with _on(stream):
             out = torch.empty(n_out, dtype=torch.float32, device=self.device) if out is None else out
-            ws = self.empty_decode_workspace() if workspace is None else workspace
             w = torch.tensor([float(x) for x in weights], dtype=torch.float64).to(torch.float32).to(self.device)
             m = None
             if avg_mask is not None:
@@ -354,12 +380,9 @@ class CodecPlan:
         # (the kernel writes the segments' elements only: an output that ends with the last segment suffices,
         # e.g. a decoded module's buffer, which has no trailing alignment pad)
         self._check_flat(out, "output", self.table.offsets[-1] + self.table.sizes[-1] if self.table.sizes else 0)
-        if ws.device != self.device or ws.numel() * ws.element_size() < self.dec_ws_bytes:
-            raise ValueError(f"aggregate workspace: need {self.dec_ws_bytes} bytes on {self.device}")
         total = float(sum(weights)) if total is None else float(total)
         args = (self._h, C, _ptr(enc.idx), _ptr(enc.vals), _ptr(enc.mn), _ptr(enc.scale), ust, _ptr(w),
-                ctypes.c_float(total), modes[mode], _ptr(m),
-                _ptr(base), _ptr(out), _ptr(ws), ctypes.c_uint64(self.dec_ws_bytes), _stream_handle(stream))
+                ctypes.c_float(total), modes[mode], _ptr(m), _ptr(base), _ptr(out), _stream_handle(stream))
         with torch.cuda.device(self.device):
             if events is None:
                 rc = self._lib.coalac_aggregate(*args)
@@ -393,19 +416,3 @@ def _event_array(events, n):
         if e is not None:
             arr[i] = ctypes.c_void_p(e.cuda_event)
     return arr
-
-
-def _sched(sched, n):
-    """(wait, record[, stages]) — lists of torch.cuda.Event or None, and a COALAC_STAGE_* mask (0 = all)
-    -> coalac_sched_t. Events must exist: recorded once, since torch creates the HIP event lazily."""
-    wait, record = sched[0], sched[1]
-    s = _lib.Sched()
-    s.stages = int(sched[2]) if len(sched) > 2 else 0
-    for i in range(n):
-        for arr, evs in ((s.wait, wait), (s.record, record)):
-            e = evs[i] if evs is not None and i < len(evs) else None
-            if e is not None:
-                if not e.cuda_event:
-                    raise ValueError("sched: event has no HIP event yet (record it once first)")
-                arr[i] = e.cuda_event
-    return s

@@ -37,11 +37,12 @@
 //     k_emit    one wave per 8 large units (1 in latency-bound plans, one load round): kept records ->
 //               ascending idx + codes
 //   Decode: k_decode_lds — every output line written once, the unit's kept values placed through a per-wave
-//   LDS tile; entry ranges from the payload's per-unit starts, or from k_bounds (batches) / an in-kernel
-//   search (k_fillscatter, latency-bound plans) for a payload without them.
+//   LDS tile; entry ranges from the payload's per-unit starts (wire v2; a host that received a v1 blob computes
+//   them, coala_amd/compression/plan.py).
 //   Aggregate (fused decode + FedAvg, server side): k_aggregate — two waves per unit, a per-wave LDS tile
-//   holding the unkept x (base + 0), each client's kept values written in and read back in client order
-//   (+ k_bounds for payloads without per-unit starts).
+//   holding the unkept x (base + 0), each client's kept values written in and read back in client order.
+//   Dense plans (every segment keeps all its elements, ratio 1): k_dense_minmax -> k_dense_seg -> k_dense_quant
+//   encode, k_dense_deq decode — the indices implied, never materialised.
 //
 // Numerics: built with -ffp-contract=off; fp32 sub/div/mul/add are separate IEEE ops, rintf is
 // round-half-even — the same op sequence as the oracle, so decoded values are bit-identical.
@@ -105,9 +106,6 @@ constexpr int SEL_NT_LAT = 512;           // ... in latency-bound plans, where n
 #ifndef SCAN_NB
 #define SCAN_NB 1  // load batches per k_scan unit (weights mode): 1 = all 16 float4 per lane in flight
 #endif
-#ifndef DECODE_XCD
-#define DECODE_XCD 1  // batch k_decode_lds: XCD-aware unit order (xcd_block)
-#endif
 #ifndef SCAN_XCD
 #define SCAN_XCD 1    // k_scan: XCD-aware unit order (128-thread blocks: C3 0.600-0.602 vs 0.604-0.606 ms)
 #endif
@@ -156,7 +154,6 @@ constexpr uint32_t HB2 = 512;             // bins of the per-group band histogra
 constexpr uint32_t GCAP = 256;            // in-window entries a group may hand to k_select
 constexpr uint32_t KEY_MAX = 0x7FFFFFFFu;
 constexpr int HIST_BINS = 2048;
-constexpr uint32_t BCHUNK = 4096;         // idx entries per k_bounds block (aggregate)
 constexpr uint32_t UCAP = 2048;           // units per k_select chunk (8.4 M elements)
 constexpr uint32_t NONE = 0xFFFFFFFFu;
 constexpr int NSTAMP = 32;  // diagnostics slots per segment row (COALAC_FLAG_STAMPS)
@@ -228,7 +225,7 @@ struct Params {
   uint4* sstate;           // [n_large] {wlo, whi, rank inside the window, path: 0 fast / 1 generic}
   uint32_t* shhi;          // [n_large] histogram upper bound: min(T_hi, largest sampled key)
 
-  // decode: first kept entry (segment-relative) of every unit — the payload's (wire v2) or k_bounds'
+  // decode: first kept entry (segment-relative) of every unit — the payload's (wire v2)
   const uint32_t* ustart;
   // dense plans (every segment keeps all its elements): per unit the NaN-ignoring {min, max} of its values
   float* umm;
@@ -2146,52 +2143,6 @@ __global__ __launch_bounds__(BLOCK) void k_emit(Params P) {
 // ------------------------------------------------------------------------------------------------
 // decode
 // ------------------------------------------------------------------------------------------------
-// First entry e of each list L_m[0, k_m) with (uint32)L_m[e] >= target_m (k_m if none), for M lists at once,
-// by one wave: each round probes 64 evenly spaced entries of every remaining interval (all M probe loads
-// in flight together) and keeps the 1/64 of it the answer lies in; ceil(log64 k) rounds (3 for k <= 262k).
-// The lists are segment idx lists (ascending); a corrupt (unsorted) list still gives a result in [0, k]
-// after at most 6 rounds, so decode stays in bounds.
-template <int M>
-DEV void wave_lower_bound(const int32_t* const (&L)[M], const uint32_t (&k)[M], const uint32_t (&target)[M],
-                          uint32_t (&res)[M]) {
-  const uint32_t lane = lane_id();
-  uint32_t a[M], b[M];
-#pragma unroll
-  for (int m = 0; m < M; ++m) {
-    a[m] = 0;
-    b[m] = k[m];
-  }
-  for (int round = 0; round < 6; ++round) {
-    bool more = false;
-#pragma unroll
-    for (int m = 0; m < M; ++m) more = more || a[m] < b[m];
-    if (!more) break;
-    uint32_t v[M], p[M], step[M];
-#pragma unroll
-    for (int m = 0; m < M; ++m) {  // issue every probe load before any is used
-      const uint32_t len = b[m] - a[m];
-      step[m] = len > 64 ? (len + 63) / 64 : 1u;
-      p[m] = a[m] + lane * step[m];
-      v[m] = (uint32_t)L[m][min(p[m], k[m] ? k[m] - 1 : 0u)];
-    }
-#pragma unroll
-    for (int m = 0; m < M; ++m) {
-      if (a[m] >= b[m]) continue;
-      const uint32_t c = (uint32_t)__popcll(__ballot(p[m] < b[m] && v[m] < target[m]));
-      if (c == 0) {
-        b[m] = a[m];
-      } else {
-        const uint32_t lo = a[m] + (c - 1) * step[m] + 1;
-        b[m] = min(b[m], a[m] + c * step[m]);
-        a[m] = min(lo, b[m]);
-        if (step[m] == 1) a[m] = b[m];
-      }
-    }
-  }
-#pragma unroll
-  for (int m = 0; m < M; ++m) res[m] = a[m];
-}
-
 // k_decode_lds: every output line written ONCE (non-temporal float4 stores for batches). WPU waves per unit, each
 // owning RPW = 16 / WPU of its 16 rows, in passes of QROWS rows through a per-wave LDS tile: the pass's kept
 // values are scattered into the zeroed tile (one ds_write per 64 entries), its rows read back (ds_read_b128, + the
@@ -2322,121 +2273,9 @@ __global__ __launch_bounds__(DECODE_NT, HASBASE ? DECODE_LDS_WPE_BASE : DECODE_L
   }
 }
 
-// Latency-bound plans without per-unit starts (a wire v1 payload): the background first (k_fill: every unit's 0 / base + 0.0f, no entry
-// lookup, so the write stream starts at once), then the kept values on top (k_scatter: one thread per entry,
-// per k_bounds chunk; bounds-checked like k_decode). Stream order puts every kept value after the fill.
-// one wave writes unit U's background: 0, or base + 0.0f (-0 -> +0, as the oracle's base + dense)
-#ifndef FILL_AUX
-#define FILL_AUX 0  // k_fill store cache policy (0 plain, 2 non-temporal)
-#endif
-template <bool HASBASE>
-DEV void fill_unit(const Params& P, const UnitDev& U, uint32_t lane) {
-  const __amdgpu_buffer_rsrc_t rout = unit_rsrc(P.out + U.off, U.len);
-  float4 b[UNIT_IT];
-  if (HASBASE) {
-    const __amdgpu_buffer_rsrc_t rb = unit_rsrc(P.base + U.off, U.len);
-#pragma unroll
-    for (uint32_t it = 0; it < UNIT_IT; ++it) {
-      const float4 a = unit_load_x4<false>(rb, rb, (it * 64 + lane) * 16);
-      b[it] = make_float4(a.x + 0.0f, a.y + 0.0f, a.z + 0.0f, a.w + 0.0f);
-    }
-  } else {
-#pragma unroll
-    for (uint32_t it = 0; it < UNIT_IT; ++it) b[it] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-  }
-  if ((U.len & 3u) == 0) {
-#pragma unroll
-    for (uint32_t it = 0; it < UNIT_IT; ++it) unit_store_x4<FILL_AUX>(rout, (it * 64 + lane) * 16, b[it]);
-  } else {
-#pragma unroll
-    for (uint32_t it = 0; it < UNIT_IT; ++it) unit_store_x1x4<FILL_AUX>(rout, (it * 64 + lane) * 16, b[it]);
-  }
-}
-
-template <bool HASBASE>
-__global__ __launch_bounds__(BLOCK) void k_fill(Params P) {
-  const uint32_t u = blockIdx.x * WAVES + (threadIdx.x >> 6);
-  if (u >= P.n_units) return;
-  fill_unit<HASBASE>(P, P.units[u], lane_id());
-}
-
-// k_fillscatter (latency-bound plans decoding a payload without per-unit starts): k_fill and k_scatter as one launch, one wave per unit. The
-// wave stores its unit's background first (nothing to wait for), finds the unit's kept entries [lo, hi) in
-// its segment's sorted idx list in-kernel (wave_lower_bound, while the stores drain), waits until its own
-// stores have completed, and then writes the kept values on top: every output element is written by the
-// wave that owns its unit, background before value. Entries are bounds-checked against the unit (an
-// untrusted list cannot write outside it). Same bytes as k_fill + k_scatter, one launch and no second pass
-// over the payload's chunk list.
-template <bool RAW, bool HASBASE>
-__global__ __launch_bounds__(BLOCK) void k_fillscatter(Params P) {
-  const uint32_t lane = lane_id();
-  const uint32_t u = blockIdx.x * WAVES + (threadIdx.x >> 6);
-  if (u >= P.n_units) return;
-  const UnitDev U = P.units[u];
-  fill_unit<HASBASE>(P, U, lane);
-  const int32_t* L[2] = {P.cidx + U.out_off, P.cidx + U.out_off};
-  const uint32_t kk[2] = {U.k, U.last ? 0u : U.k};  // a segment's last unit ends at k: no search
-  const uint32_t tg[2] = {U.start, U.last ? 0xFFFFFFFFu : U.start + U.len};
-  uint32_t res[2];
-  wave_lower_bound<2>(L, kk, tg, res);
-  const uint32_t lo = min(res[0], U.k), hi = max(lo, min(min(U.last ? U.k : res[1], U.k), lo + U.len));
-  const float mn = RAW ? 0.0f : P.cmn[U.seg];
-  const float sc = RAW ? 0.0f : P.cscale[U.seg];
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the background stores have completed
-  for (uint32_t e0 = lo; e0 < hi; e0 += 64) {
-    const uint32_t e = e0 + lane;
-    if (e < hi) {
-      const uint64_t ge = U.out_off + e;
-      const uint32_t pos = (uint32_t)P.cidx[ge] - U.start;
-      if (pos < U.len) {
-        const float v = code_value<RAW>(load_code<RAW>(P, ge), mn, sc);
-        P.out[U.off + pos] = HASBASE ? P.base[U.off + pos] + v : v;
-      }
-    }
-  }
-}
-
-
 // ------------------------------------------------------------------------------------------------
 // aggregate: fused server-side decode + FedAvg of C client updates of one layout
 // ------------------------------------------------------------------------------------------------
-// k_bounds: ustart[u] = first kept entry whose index falls in unit u or later. One block per chunk of
-// <= BCHUNK entries of one segment's sorted idx list, 16 consecutive entries per thread (loads batched).
-// Indices are range-checked (the list may come from an untrusted blob): a corrupt list can only
-// mis-aggregate, never write out of bounds.
-struct BChunk {
-  uint32_t seg, e0, e1, pad;
-};
-
-__global__ __launch_bounds__(BLOCK) void k_bounds(Params P, const BChunk* chunks, uint32_t* ustart) {
-  constexpr uint32_t EPT = BCHUNK / BLOCK;
-  const BChunk C = chunks[blockIdx.x];
-  const SegDev sd = P.segs[C.seg];
-  const uint32_t nu = sd.unit_end - sd.unit_begin, k = sd.k;
-  const int32_t* L = P.cidx + sd.out_off;
-  uint32_t* us = ustart + sd.unit_begin;
-  const uint32_t e0 = C.e0 + threadIdx.x * EPT;
-  if (e0 >= C.e1) return;
-  uint32_t ix[EPT + 1];
-#pragma unroll
-  for (uint32_t q = 0; q <= EPT; ++q) {
-    // q = 0: the entry before e0; indices clamped so every load is unconditional
-    const uint32_t e = min(e0 + q - (e0 == 0 && q == 0 ? 0u : 1u), C.e1 - 1);
-    ix[q] = (uint32_t)L[e];
-  }
-#pragma unroll
-  for (uint32_t q = 1; q <= EPT; ++q) {
-    const uint32_t e = e0 + q - 1;
-    if (e < C.e1) {
-      const uint32_t u = min(ix[q] >> UNIT_SHIFT, nu - 1);
-      const uint32_t v0 = e == 0 ? 0u : min(ix[q - 1] >> UNIT_SHIFT, nu - 1) + 1;
-      for (uint32_t v = v0; v <= u; ++v) us[v] = e;
-      if (e == k - 1)
-        for (uint32_t v = u + 1; v < nu; ++v) us[v] = k;
-    }
-  }
-}
-
 #ifndef AGG_WPE
 #define AGG_WPE 1  // k_aggregate launch-bounds blocks per CU (register budget)
 #endif
@@ -2447,39 +2286,8 @@ __global__ __launch_bounds__(BLOCK) void k_bounds(Params P, const BChunk* chunks
 #define AGG_DEPTH 16u  // clients whose entries k_aggregate loads together (16 ResNet-50 clients: 4 -> 73.5 us, 8 -> 70.9 us, 16 -> 69.1 us)
 #endif
 
-// k_scatter's work list: one chunk of <= BCHUNK entries of one segment, with the segment's offsets and
-// size inline (the entries, mn and scale then load in one round)
-struct SChunk {
-  uint64_t in_off, out_off;
-  uint32_t seg, n, e0, e1;
-};
-static_assert(sizeof(SChunk) == 32, "SChunk layout");
-
-template <bool RAW, bool HASBASE>
-__global__ __launch_bounds__(BLOCK) void k_scatter(Params P, const SChunk* chunks) {
-  constexpr uint32_t EPT = BCHUNK / BLOCK;
-  const SChunk C = chunks[blockIdx.x];
-  const float mn = RAW ? 0.0f : P.cmn[C.seg];
-  const float sc = RAW ? 0.0f : P.cscale[C.seg];
-  uint32_t ix[EPT], q[EPT];
-#pragma unroll
-  for (uint32_t j = 0; j < EPT; ++j) {  // coalesced: entry C.e0 + j * BLOCK + t (clamped: loads unconditional)
-    const uint64_t e = C.out_off + min(C.e0 + j * BLOCK + threadIdx.x, C.e1 - 1);
-    ix[j] = (uint32_t)P.cidx[e];
-    q[j] = load_code<RAW>(P, e);
-  }
-#pragma unroll
-  for (uint32_t j = 0; j < EPT; ++j) {
-    if (C.e0 + j * BLOCK + threadIdx.x < C.e1 && ix[j] < C.n) {  // an untrusted list stays in its segment
-      const float v = code_value<RAW>(q[j], mn, sc);
-      float* o = P.out + C.in_off + ix[j];
-      *o = HASBASE ? P.base[C.in_off + ix[j]] + v : v;
-    }
-  }
-}
-
 struct AggArgs {
-  const uint32_t* ustart;  // [n_units] from k_bounds
+  const uint32_t* ustart;  // [n_units] the clients' per-unit starts (wire v2)
   const float* weights;    // [clients] fp32 weights (float(w_i), as torch converts a Python scalar)
   uint32_t clients, T, U0; // clients, segments per client, units per client
   uint64_t Kc;             // kept entries per client (out_off stride between clients)
@@ -3036,16 +2844,12 @@ struct coalac_plan {
   uint4* groups = nullptr;
   uint4* gseg = nullptr;
   uint32_t n_groups = 0;
-  BChunk* bchunks = nullptr;  // aggregate: k_bounds work list
-  uint32_t n_bchunks = 0;
-  SChunk* schunks = nullptr;  // latency-bound decode: k_scatter work list (n_bchunks of them)
   std::vector<SegDev> hsegs;  // host copy (aggregate validates the client-copy structure)
   // encode fork/join: k_small runs on `side`, concurrently with k_sample / k_scan on the caller's stream
   hipStream_t side = nullptr;
   hipEvent_t fork = nullptr, join = nullptr;
   std::mutex mu;  // serialises the (asynchronous) enqueue sequences that use side / fork / join
   WsLayout ws{};
-  size_t dec_ws = 0;
 };
 
 namespace {
@@ -3078,72 +2882,50 @@ void fill_meta(Params& P, coalac_plan_t plan) {
   P.ccap = plan->ccap;
 }
 
-// Stage boundary i of an encode / decode enqueue: wait for sc->wait[i], then record sc->record[i].
-int boundary(const coalac_sched_t* sc, int i, hipStream_t st) {
-  if (!sc) return COALAC_OK;
-  if (sc->wait[i]) HIP_CHECK(hipStreamWaitEvent(st, static_cast<hipEvent_t>(sc->wait[i]), 0));
-  if (sc->record[i]) HIP_CHECK(hipEventRecord(static_cast<hipEvent_t>(sc->record[i]), st));
-  return COALAC_OK;
-}
+// Timing events of the _ev variants: hipEventRecord(ev[i], stream) at boundary i of a call (NULL array or entries:
+// nothing recorded). Encode: [0] before k_sample, [1] after it, [2] after k_scan, [3] after the select kernels,
+// [4] after k_emit; decode and aggregate: [0] at the start, [1] before the decode kernel, [2] after it.
+struct Marks {
+  void* const* ev;
+  int n;
+  int at(int i, hipStream_t st) const {
+    if (ev != nullptr && i < n && ev[i] != nullptr) HIP_CHECK(hipEventRecord(static_cast<hipEvent_t>(ev[i]), st));
+    return COALAC_OK;
+  }
+};
 
-#define BOUNDARY(i)                          \
-  do {                                       \
-    const int rc_ = boundary(sc, (i), st);   \
-    if (rc_) return rc_;                     \
+#define MARK(i)                         \
+  do {                                  \
+    const int rc_ = marks.at((i), st);  \
+    if (rc_) return rc_;                \
   } while (0)
-
-// the _ev variants: record-only schedule
-coalac_sched_t record_only(void* const* ev, int n) {
-  coalac_sched_t s{};
-  if (ev)
-    for (int i = 0; i < n; ++i) s.record[i] = ev[i];
-  return s;
-}
 
 // Small segments go beside the large ones' pipeline on a side stream once the batch is big enough for
 // the fork / join (~10-20 us) to pay off (>= 16384 large units, ~3 ResNet-50 updates).
 constexpr uint32_t FORK_MIN_LUNITS = 16384;
 
-// Is stage boundary i of a call adjacent to an enqueued stage? (stage k spans boundaries [lo_k, hi_k])
-bool at_boundary(unsigned stages, const int (*span)[2], int nst, int i) {
-  for (int k = 0; k < nst; ++k)
-    if ((stages >> k) & 1u)
-      if (span[k][0] <= i && i <= span[k][1]) return true;
-  return false;
-}
-
-constexpr int ENC_SPAN[4][2] = {{0, 1}, {1, 2}, {2, 4}, {0, 1}};  // SAMPLE, SCAN, SELECT, SMALL
-constexpr int DEC_SPAN[2][2] = {{0, 1}, {1, 2}};                  // BOUNDS, DECODE
-
-// the dense encode: stage SAMPLE = the min / max pass + the per-segment reduction, stage SCAN = the quantise
-// stream (boundaries 1 / 2 bracket it, as they bracket k_scan); nothing in SELECT
+// the dense encode: the min / max pass and the per-segment reduction between marks 0 and 1, the quantise stream
+// between 1 and 2 (where k_scan sits in a sparse encode)
 template <bool DELTA, bool RAW>
-int launch_dense_encode(const Params& P, coalac_plan_t plan, hipStream_t st, const coalac_sched_t* sc) {
-  const unsigned all = COALAC_STAGE_SAMPLE | COALAC_STAGE_SCAN | COALAC_STAGE_SELECT | COALAC_STAGE_SMALL;
-  const unsigned stages = (sc && (sc->stages & all)) ? (sc->stages & all) : all;
-  auto B = [&](int i) { return at_boundary(stages, ENC_SPAN, 4, i) ? boundary(sc, i, st) : COALAC_OK; };
+int launch_dense_encode(const Params& P, coalac_plan_t plan, hipStream_t st, const Marks& marks) {
   const dim3 g((plan->n_units + WAVES - 1) / WAVES);
   const bool xcd = plan->n_units > LATENCY_PLAN_UNITS;
-  int rc = B(0);
-  if (rc) return rc;
-  if (stages & COALAC_STAGE_SAMPLE) {
-    if (!RAW) {
-      if (xcd)
-        hipLaunchKernelGGL((k_dense_minmax<DELTA, true>), g, dim3(BLOCK), 0, st, P);
-      else
-        hipLaunchKernelGGL((k_dense_minmax<DELTA, false>), g, dim3(BLOCK), 0, st, P);
-    }
-    hipLaunchKernelGGL((k_dense_seg<RAW>), dim3(plan->nseg), dim3(BLOCK), 0, st, P);
-  }
-  if ((rc = B(1))) return rc;
-  if (stages & COALAC_STAGE_SCAN) {
+  MARK(0);
+  if (!RAW) {
     if (xcd)
-      hipLaunchKernelGGL((k_dense_quant<DELTA, RAW, true>), g, dim3(BLOCK), 0, st, P);
+      hipLaunchKernelGGL((k_dense_minmax<DELTA, true>), g, dim3(BLOCK), 0, st, P);
     else
-      hipLaunchKernelGGL((k_dense_quant<DELTA, RAW, false>), g, dim3(BLOCK), 0, st, P);
+      hipLaunchKernelGGL((k_dense_minmax<DELTA, false>), g, dim3(BLOCK), 0, st, P);
   }
-  for (int i = 2; i <= 4; ++i)
-    if ((rc = B(i))) return rc;
+  hipLaunchKernelGGL((k_dense_seg<RAW>), dim3(plan->nseg), dim3(BLOCK), 0, st, P);
+  MARK(1);
+  if (xcd)
+    hipLaunchKernelGGL((k_dense_quant<DELTA, RAW, true>), g, dim3(BLOCK), 0, st, P);
+  else
+    hipLaunchKernelGGL((k_dense_quant<DELTA, RAW, false>), g, dim3(BLOCK), 0, st, P);
+  MARK(2);
+  MARK(3);
+  MARK(4);
   return COALAC_OK;
 }
 
@@ -3168,20 +2950,14 @@ void launch_emit(const Params& P, coalac_plan_t plan, hipStream_t st) {
 }
 
 template <bool DELTA, bool RAW>
-int launch_encode(const Params& P, coalac_plan_t plan, hipStream_t st, const coalac_sched_t* sc) {
+int launch_encode(const Params& P, coalac_plan_t plan, hipStream_t st, const Marks& marks) {
   const uint32_t gu = (plan->n_lunits + WAVES - 1) / WAVES;
-  const unsigned all = COALAC_STAGE_SAMPLE | COALAC_STAGE_SCAN | COALAC_STAGE_SELECT | COALAC_STAGE_SMALL;
-  const unsigned stages = (sc && (sc->stages & all)) ? (sc->stages & all) : all;
-  // whole encode: small segments forked beside k_sample / k_scan (big batches) or inside k_scan;
-  // a call holding SAMPLE + SCAN + SMALL (the encode's front, SELECT maybe in a later call) places them the
-  // same way; any other split: k_small in stage SMALL
-  const bool split = stages != all;
-  const unsigned front = COALAC_STAGE_SAMPLE | COALAC_STAGE_SCAN | COALAC_STAGE_SMALL;
-  const bool fork = plan->n_small && !split && plan->n_lunits >= FORK_MIN_LUNITS && !(P.flags & COALAC_FLAG_NO_FORK);
-  // otherwise the small segments run beside the samplers in k_presel, or (latency-bound plans,
-  // SCAN_SMALL_LAT) in k_scan's first blocks, beside the streaming waves: k_sample alone ahead of it
-  const bool presel = (stages & front) == front && !fork && plan->n_small;
-  const bool small_in_scan = presel && SCAN_SMALL_LAT && plan->n_lunits <= LATENCY_PLAN_UNITS;
+  // small segments: forked beside k_sample / k_scan on the plan's side stream (big batches), beside the samplers in
+  // k_presel (other batches), or in k_scan's first blocks beside the streaming waves (latency-bound plans: k_sample
+  // alone ahead of it)
+  const bool fork = plan->n_small && plan->n_lunits >= FORK_MIN_LUNITS && !(P.flags & COALAC_FLAG_NO_FORK);
+  const bool presel = !fork && plan->n_small;
+  const bool small_in_scan = presel && plan->n_lunits <= LATENCY_PLAN_UNITS;
   Params Q = P;
   Q.scan_small = 0u;
   std::unique_lock<std::mutex> lk(plan->mu, std::defer_lock);
@@ -3195,13 +2971,7 @@ int launch_encode(const Params& P, coalac_plan_t plan, hipStream_t st, const coa
                     hipGetErrorString(hipGetLastError()));
     }
   }
-  auto B = [&](int i) { return at_boundary(stages, ENC_SPAN, 4, i) ? boundary(sc, i, st) : COALAC_OK; };
-#define ENC_BOUNDARY(i)       \
-  do {                        \
-    const int rc_ = B(i);     \
-    if (rc_) return rc_;      \
-  } while (0)
-  ENC_BOUNDARY(0);
+  MARK(0);
   if (fork) {
     HIP_CHECK(hipEventRecord(plan->fork, st));
     HIP_CHECK(hipStreamWaitEvent(plan->side, plan->fork, 0));
@@ -3210,13 +2980,11 @@ int launch_encode(const Params& P, coalac_plan_t plan, hipStream_t st, const coa
   }
   if (presel && !small_in_scan)
     hipLaunchKernelGGL((k_presel<DELTA, RAW>), dim3(plan->n_large + plan->n_small), dim3(BLOCK), 0, st, P);
-  else if ((stages & COALAC_STAGE_SAMPLE) && plan->n_large && plan->n_lunits <= LATENCY_PLAN_UNITS)
+  else if (plan->n_large && plan->n_lunits <= LATENCY_PLAN_UNITS)
     hipLaunchKernelGGL((k_sample<DELTA, RAW, SAMPLE_NT_LAT>), dim3(plan->n_large), dim3(SAMPLE_NT_LAT), 0, st, P);
-  else if ((stages & COALAC_STAGE_SAMPLE) && plan->n_large)
+  else if (plan->n_large)
     hipLaunchKernelGGL((k_sample<DELTA, RAW, BLOCK>), dim3(plan->n_large), dim3(BLOCK), 0, st, P);
-  if ((stages & COALAC_STAGE_SMALL) && plan->n_small && !presel && !fork)
-    hipLaunchKernelGGL((k_small<DELTA, RAW>), dim3(plan->n_small), dim3(BLOCK), 0, st, P);
-  ENC_BOUNDARY(1);
+  MARK(1);
   if (small_in_scan) {
     Q.scan_small = plan->n_small;
     const dim3 gs((plan->n_lunits + SCAN_NT_LAT / 64 - 1) / (SCAN_NT_LAT / 64) + plan->n_small);
@@ -3226,30 +2994,30 @@ int launch_encode(const Params& P, coalac_plan_t plan, hipStream_t st, const coa
     else
       hipLaunchKernelGGL((k_scan<DELTA, RAW, true, SCAN_WPE_LAT, SCAN_NB_LAT, SCAN_NT_LAT>), gs, dim3(SCAN_NT_LAT), 0, st,
                          Q);
-  } else if ((stages & COALAC_STAGE_SCAN) && gu) {
+  } else if (gu) {
     hipLaunchKernelGGL((k_scan<DELTA, RAW, false, SCAN_WPE, SCAN_NB, SCAN_NT>),
                        dim3((plan->n_lunits + SCAN_NT / 64 - 1) / (SCAN_NT / 64)), dim3(SCAN_NT), 0, st, Q);
   }
-  ENC_BOUNDARY(2);
-  if ((stages & COALAC_STAGE_SELECT) && plan->n_large) {
-    if (plan->n_lunits <= LATENCY_PLAN_UNITS)
+  MARK(2);
+  if (plan->n_large) {
+    const bool lat = plan->n_lunits <= LATENCY_PLAN_UNITS;
+    if (lat)
       hipLaunchKernelGGL((k_ghist<GHIST_NT_LAT, true>), dim3(plan->n_groups), dim3(GHIST_NT_LAT), 0, st, P);
     else
       hipLaunchKernelGGL((k_ghist<BLOCK, false>), dim3(plan->n_groups), dim3(BLOCK), 0, st, P);
-    if (plan->n_lunits <= LATENCY_PLAN_UNITS)
+    if (lat)
       hipLaunchKernelGGL((k_gwin<GWIN_NT_LAT, true>), dim3(plan->n_groups), dim3(GWIN_NT_LAT), 0, st, P);
     else
       hipLaunchKernelGGL((k_gwin<BLOCK, false>), dim3(plan->n_groups), dim3(BLOCK), 0, st, P);
-    if (plan->n_lunits <= LATENCY_PLAN_UNITS)
+    if (lat)
       hipLaunchKernelGGL((k_select<DELTA, RAW, SEL_NT_LAT>), dim3(plan->n_large), dim3(SEL_NT_LAT), 0, st, P);
     else
       hipLaunchKernelGGL((k_select<DELTA, RAW>), dim3(plan->n_large), dim3(SEL_NT), 0, st, P);
   }
-  ENC_BOUNDARY(3);
-  if ((stages & COALAC_STAGE_SELECT) && plan->n_large) launch_emit<DELTA, RAW>(P, plan, st);
+  MARK(3);
+  if (plan->n_large) launch_emit<DELTA, RAW>(P, plan, st);
   if (fork) HIP_CHECK(hipStreamWaitEvent(st, plan->join, 0));
-  ENC_BOUNDARY(4);
-#undef ENC_BOUNDARY
+  MARK(4);
   return COALAC_OK;
 }
 
@@ -3271,7 +3039,6 @@ int coalac_plan_create(const coalac_seg_t* h_segs, int nseg, int bits, coalac_pl
   std::vector<UnitDev> units, lunits;
   std::vector<uint4> groups, gseg;
   std::vector<uint32_t> small_list, large_list;
-  std::vector<BChunk> bchunks;
   uint64_t span = 0, total_k = 0;
   std::vector<std::pair<uint64_t, uint64_t>> in_r, out_r;
   uint64_t est_units = 0;
@@ -3317,8 +3084,6 @@ int coalac_plan_create(const coalac_seg_t* h_segs, int nseg, int bits, coalac_pl
       }
     }
     (large ? large_list : small_list).push_back((uint32_t)s);
-    for (uint64_t e0 = 0; e0 < g.k; e0 += BCHUNK)
-      bchunks.push_back(BChunk{(uint32_t)s, (uint32_t)e0, (uint32_t)std::min<uint64_t>(g.k, e0 + BCHUNK), 0u});
     segs[s] = d;
     if (g.n) {
       span = std::max<uint64_t>(span, g.in_off + g.n);
@@ -3350,9 +3115,7 @@ int coalac_plan_create(const coalac_seg_t* h_segs, int nseg, int bits, coalac_pl
   p->n_groups = (uint32_t)groups.size();
   p->span = span;
   p->total_k = total_k;
-  p->n_bchunks = (uint32_t)bchunks.size();
   p->hsegs = segs;
-  p->dec_ws = align_up(4 * (units.size() + 1), 256);  // decode / aggregate: per-unit bounds
   // record slots per large unit: the candidates a unit can expect at the plan's largest ratio (kept
   // share + the sampled band + margin), so the workspace is ~1 B/element at ratio 0.01 instead of 8
   double rmax = 0.0;
@@ -3380,12 +3143,7 @@ int coalac_plan_create(const coalac_seg_t* h_segs, int nseg, int bits, coalac_pl
   const size_t o_ssegs = align_up(o_lsegs + sizeof(SegDev) * lsegs.size(), 256);
   const size_t o_grp = align_up(o_ssegs + sizeof(SegDev) * ssegs.size(), 256);
   const size_t o_gseg = align_up(o_grp + sizeof(uint4) * groups.size(), 256);
-  const size_t o_bch = align_up(o_gseg + sizeof(uint4) * gseg.size(), 256);
-  std::vector<SChunk> schunks;
-  for (const BChunk& c : bchunks)
-    schunks.push_back(SChunk{segs[c.seg].in_off, segs[c.seg].out_off, c.seg, segs[c.seg].n, c.e0, c.e1});
-  const size_t o_sch = align_up(o_bch + sizeof(BChunk) * bchunks.size(), 256);
-  const size_t bytes = align_up(o_sch + sizeof(SChunk) * schunks.size(), 256) + 256;
+  const size_t bytes = align_up(o_gseg + sizeof(uint4) * gseg.size(), 256) + 256;
   std::vector<uint8_t> host(bytes, 0);
   if (!segs.empty()) memcpy(host.data() + o_segs, segs.data(), sizeof(SegDev) * segs.size());
   if (!units.empty()) memcpy(host.data() + o_units, units.data(), sizeof(UnitDev) * units.size());
@@ -3396,8 +3154,6 @@ int coalac_plan_create(const coalac_seg_t* h_segs, int nseg, int bits, coalac_pl
   if (!ssegs.empty()) memcpy(host.data() + o_ssegs, ssegs.data(), sizeof(SegDev) * ssegs.size());
   if (!groups.empty()) memcpy(host.data() + o_grp, groups.data(), sizeof(uint4) * groups.size());
   if (!gseg.empty()) memcpy(host.data() + o_gseg, gseg.data(), sizeof(uint4) * gseg.size());
-  if (!bchunks.empty()) memcpy(host.data() + o_bch, bchunks.data(), sizeof(BChunk) * bchunks.size());
-  if (!schunks.empty()) memcpy(host.data() + o_sch, schunks.data(), sizeof(SChunk) * schunks.size());
   hipError_t e = hipMalloc(&p->meta, bytes);
   if (e != hipSuccess) {
     delete p;
@@ -3419,8 +3175,6 @@ int coalac_plan_create(const coalac_seg_t* h_segs, int nseg, int bits, coalac_pl
   p->ssegs = reinterpret_cast<SegDev*>(m + o_ssegs);
   p->groups = reinterpret_cast<uint4*>(m + o_grp);
   p->gseg = reinterpret_cast<uint4*>(m + o_gseg);
-  p->bchunks = reinterpret_cast<BChunk*>(m + o_bch);
-  p->schunks = reinterpret_cast<SChunk*>(m + o_sch);
   *out = p;
   return COALAC_OK;
 }
@@ -3439,23 +3193,13 @@ int coalac_plan_destroy(coalac_plan_t plan) {
   return COALAC_OK;
 }
 
-int coalac_plan_query(coalac_plan_t plan, uint64_t* ws_bytes, uint64_t* dec_ws_bytes, uint64_t* total_k,
-                      uint64_t* span, uint64_t* n_units) {
+int coalac_plan_query(coalac_plan_t plan, uint64_t* ws_bytes, uint64_t* total_k, uint64_t* span, uint64_t* n_units) {
   if (!plan) return fail(COALAC_EINVAL, "coalac_plan_query: plan is NULL");
   if (ws_bytes) *ws_bytes = plan->ws.total;
-  if (dec_ws_bytes) *dec_ws_bytes = plan->dec_ws;
   if (total_k) *total_k = plan->total_k;
   if (span) *span = plan->span;
   if (n_units) *n_units = plan->n_units;
   return COALAC_OK;
-}
-
-int coalac_encode_ev(coalac_plan_t plan, const float* d_in, const float* d_base, int32_t* d_idx,
-                     void* d_vals, float* d_mn, float* d_scale, uint32_t* d_ustart, void* d_ws, uint64_t ws_bytes,
-                     unsigned flags, void* stream, void* const* events) {
-  const coalac_sched_t s = record_only(events, 5);
-  return coalac_encode_sched(plan, d_in, d_base, d_idx, d_vals, d_mn, d_scale, d_ustart, d_ws, ws_bytes, flags,
-                             stream, events ? &s : nullptr);
 }
 
 }  // extern "C"
@@ -3463,7 +3207,7 @@ int coalac_encode_ev(coalac_plan_t plan, const float* d_in, const float* d_base,
 namespace {
 int encode_impl(coalac_plan_t plan, const float* d_in, const float* const* d_inptr, const float* d_base,
                 int32_t* d_idx, void* d_vals, float* d_mn, float* d_scale, uint32_t* d_ustart, void* d_ws,
-                uint64_t ws_bytes, unsigned flags, void* stream, const coalac_sched_t* sched) {
+                uint64_t ws_bytes, unsigned flags, void* stream, const Marks& marks) {
   if (!plan) return fail(COALAC_EINVAL, "coalac_encode: plan is NULL");
   if (plan->nseg == 0) return COALAC_OK;
   if (!d_mn || !d_scale) return fail(COALAC_EINVAL, "coalac_encode: mn/scale pointers are NULL");
@@ -3496,13 +3240,13 @@ int encode_impl(coalac_plan_t plan, const float* d_in, const float* const* d_inp
   if (plan->dense) {
     P.umm = reinterpret_cast<float*>(w + L.umm);
     if (delta && raw)
-      rc = launch_dense_encode<true, true>(P, plan, st, sched);
+      rc = launch_dense_encode<true, true>(P, plan, st, marks);
     else if (delta)
-      rc = launch_dense_encode<true, false>(P, plan, st, sched);
+      rc = launch_dense_encode<true, false>(P, plan, st, marks);
     else if (raw)
-      rc = launch_dense_encode<false, true>(P, plan, st, sched);
+      rc = launch_dense_encode<false, true>(P, plan, st, marks);
     else
-      rc = launch_dense_encode<false, false>(P, plan, st, sched);
+      rc = launch_dense_encode<false, false>(P, plan, st, marks);
     if (rc) return rc;
     HIP_CHECK(hipGetLastError());
     return COALAC_OK;
@@ -3530,13 +3274,13 @@ int encode_impl(coalac_plan_t plan, const float* d_in, const float* const* d_inp
   P.sstate = reinterpret_cast<uint4*>(w + L.sstate);
   P.shhi = reinterpret_cast<uint32_t*>(w + L.shhi);
   if (delta && raw)
-    rc = launch_encode<true, true>(P, plan, st, sched);
+    rc = launch_encode<true, true>(P, plan, st, marks);
   else if (delta)
-    rc = launch_encode<true, false>(P, plan, st, sched);
+    rc = launch_encode<true, false>(P, plan, st, marks);
   else if (raw)
-    rc = launch_encode<false, true>(P, plan, st, sched);
+    rc = launch_encode<false, true>(P, plan, st, marks);
   else
-    rc = launch_encode<false, false>(P, plan, st, sched);
+    rc = launch_encode<false, false>(P, plan, st, marks);
   if (rc) return rc;
   HIP_CHECK(hipGetLastError());
   return COALAC_OK;
@@ -3545,11 +3289,11 @@ int encode_impl(coalac_plan_t plan, const float* d_in, const float* const* d_inp
 
 extern "C" {
 
-int coalac_encode_sched(coalac_plan_t plan, const float* d_in, const float* d_base, int32_t* d_idx,
-                        void* d_vals, float* d_mn, float* d_scale, uint32_t* d_ustart, void* d_ws, uint64_t ws_bytes,
-                        unsigned flags, void* stream, const coalac_sched_t* sched) {
-  return encode_impl(plan, d_in, nullptr, d_base, d_idx, d_vals, d_mn, d_scale, d_ustart, d_ws, ws_bytes, flags,
-                     stream, sched);
+int coalac_encode_ev(coalac_plan_t plan, const float* d_in, const float* d_base, int32_t* d_idx,
+                     void* d_vals, float* d_mn, float* d_scale, uint32_t* d_ustart, void* d_ws, uint64_t ws_bytes,
+                     unsigned flags, void* stream, void* const* events) {
+  return encode_impl(plan, d_in, nullptr, d_base, d_idx, d_vals, d_mn, d_scale, d_ustart, d_ws, ws_bytes, flags, stream,
+                     Marks{events, 5});
 }
 
 int coalac_encode_segptr(coalac_plan_t plan, const float* const* d_seg_in, const float* d_base, int32_t* d_idx,
@@ -3557,7 +3301,7 @@ int coalac_encode_segptr(coalac_plan_t plan, const float* const* d_seg_in, const
                          unsigned flags, void* stream) {
   if (plan && plan->nseg && !d_seg_in) return fail(COALAC_EINVAL, "coalac_encode_segptr: d_seg_in is NULL");
   return encode_impl(plan, nullptr, d_seg_in, d_base, d_idx, d_vals, d_mn, d_scale, d_ustart, d_ws, ws_bytes, flags,
-                     stream, nullptr);
+                     stream, Marks{nullptr, 0});
 }
 
 int coalac_encode(coalac_plan_t plan, const float* d_in, const float* d_base, int32_t* d_idx, void* d_vals,
@@ -3565,14 +3309,6 @@ int coalac_encode(coalac_plan_t plan, const float* d_in, const float* d_base, in
                   void* stream) {
   return coalac_encode_ev(plan, d_in, d_base, d_idx, d_vals, d_mn, d_scale, d_ustart, d_ws, ws_bytes, flags, stream,
                           nullptr);
-}
-
-int coalac_decode_ev(coalac_plan_t plan, const int32_t* d_idx, const void* d_vals, const float* d_mn,
-                     const float* d_scale, const uint32_t* d_ustart, const float* d_base, float* d_out, void* d_ws,
-                     uint64_t ws_bytes, void* stream, void* const* events) {
-  const coalac_sched_t s = record_only(events, 3);
-  return coalac_decode_sched(plan, d_idx, d_vals, d_mn, d_scale, d_ustart, d_base, d_out, d_ws, ws_bytes, stream,
-                             events ? &s : nullptr);
 }
 
 }  // extern "C"
@@ -3589,16 +3325,14 @@ void launch_decode_lds_n(const Params& P, coalac_plan_t plan, hipStream_t st) {
     hipLaunchKernelGGL((k_decode_lds<RAW, HB, W, (Q < 8u ? Q : 8u), DECODE_SAUX_LAT, false, NCH>),
                        dim3((plan->n_units * W + DW - 1) / DW), dim3(DECODE_NT), 0, st, P);
   } else {
-    hipLaunchKernelGGL((k_decode_lds<RAW, HB, 1u, HB ? DECODE_QROWS_BASE : DECODE_QROWS, STORE_AUX, DECODE_XCD != 0, NCH>),
+    hipLaunchKernelGGL((k_decode_lds<RAW, HB, 1u, HB ? DECODE_QROWS_BASE : DECODE_QROWS, STORE_AUX, true, NCH>),
                        dim3((plan->n_units + DW - 1) / DW), dim3(DECODE_NT), 0, st, P);
   }
 }
 
 // plans whose segments keep more than ~1.5 % (more than 64 entries in a unit on average) hold 8 entry chunks in
-// registers (DECODE_NCH_RATIO: the ratio from which they do)
-#ifndef DECODE_NCH_RATIO
-#define DECODE_NCH_RATIO 0.02
-#endif
+// registers (from ratio 0.02: C3 at ratio 0.1, decode 0.63 -> 0.37 ms)
+constexpr double DECODE_NCH_RATIO = 0.02;
 template <bool RAW, bool HB>
 void launch_decode_lds(const Params& P, coalac_plan_t plan, hipStream_t st) {
   if (plan->rmax > DECODE_NCH_RATIO)
@@ -3606,55 +3340,26 @@ void launch_decode_lds(const Params& P, coalac_plan_t plan, hipStream_t st) {
   else
     launch_decode_lds_n<RAW, HB, 1u>(P, plan, st);
 }
-
-template <bool RAW, bool HB>
-void launch_fillscatter(const Params& P, coalac_plan_t plan, hipStream_t st, unsigned stages) {
-  const dim3 gf((plan->n_units + WAVES - 1) / WAVES);
-  if ((stages & COALAC_STAGE_FILL) && (stages & COALAC_STAGE_SCATTER)) {
-    hipLaunchKernelGGL((k_fillscatter<RAW, HB>), gf, dim3(BLOCK), 0, st, P);
-    return;
-  }
-  if (stages & COALAC_STAGE_FILL) hipLaunchKernelGGL((k_fill<HB>), gf, dim3(BLOCK), 0, st, P);
-  if ((stages & COALAC_STAGE_SCATTER) && plan->n_bchunks)
-    hipLaunchKernelGGL((k_scatter<RAW, HB>), dim3(plan->n_bchunks), dim3(BLOCK), 0, st, P, plan->schunks);
-}
 }  // namespace
 
 extern "C" {
 
-int coalac_decode_sched(coalac_plan_t plan, const int32_t* d_idx, const void* d_vals, const float* d_mn,
-                        const float* d_scale, const uint32_t* d_ustart, const float* d_base, float* d_out, void* d_ws,
-                        uint64_t ws_bytes, void* stream, const coalac_sched_t* sched) {
-  const unsigned all = COALAC_STAGE_BOUNDS | COALAC_STAGE_DECODE;
-  const unsigned known = all | COALAC_STAGE_FILL | COALAC_STAGE_SCATTER;
-  unsigned stages = (sched && (sched->stages & known)) ? (sched->stages & known) : all;
-  // DECODE = FILL + SCATTER: the background and the kept values as separately enqueued parts
-  if (stages & COALAC_STAGE_DECODE) stages |= COALAC_STAGE_FILL | COALAC_STAGE_SCATTER;
-  if (stages & (COALAC_STAGE_FILL | COALAC_STAGE_SCATTER)) stages |= COALAC_STAGE_DECODE;
+int coalac_decode_ev(coalac_plan_t plan, const int32_t* d_idx, const void* d_vals, const float* d_mn,
+                     const float* d_scale, const uint32_t* d_ustart, const float* d_base, float* d_out, void* stream,
+                     void* const* events) {
   if (!plan) return fail(COALAC_EINVAL, "coalac_decode: plan is NULL");
   if (plan->n_units == 0) return COALAC_OK;
-  const bool lat = plan->n_units <= LATENCY_PLAN_UNITS;
-  // Entry ranges per unit: the payload's starts (d_ustart, wire v2), else — batches — the ones k_bounds leaves in the
-  // workspace: the kept values then need BOUNDS in this call, or the caller's word (BOUNDS_DONE) that an earlier call
-  // enqueued it on this workspace for these arrays, ordered before this one (stale bounds would mis-decode
-  // silently); latency-bound plans without starts search their ranges in-kernel (k_fillscatter).
-  if (!plan->dense && !d_ustart && !lat && (stages & COALAC_STAGE_SCATTER) && !(stages & COALAC_STAGE_BOUNDS) &&
-      !(sched && (sched->stages & COALAC_STAGE_BOUNDS_DONE)))
-    return fail(COALAC_EINVAL, "coalac_decode: a plan of %u units without per-unit starts decodes its kept values "
-                "from the bounds of COALAC_STAGE_BOUNDS: pass BOUNDS in the same call, or BOUNDS_DONE after a BOUNDS "
-                "call on this workspace", plan->n_units);
   if (!d_out) return fail(COALAC_EINVAL, "coalac_decode: output pointer is NULL");
-  const bool payload = (stages & (COALAC_STAGE_BOUNDS | COALAC_STAGE_SCATTER)) != 0;  // reads the encoded arrays
-  if (payload && plan->total_k && (!(d_idx || plan->dense) || !d_vals))
-    return fail(COALAC_EINVAL, "coalac_decode: idx/vals pointers are NULL");
-  if (payload && plan->bits != 32 && (!d_mn || !d_scale))
+  // a sparse plan decodes every unit's entry range from the per-unit starts (wire v2; the host computes them for a
+  // v1 payload); a dense plan's indices and starts are implied (neither is read)
+  if (plan->total_k && (!(plan->dense || (d_idx && d_ustart)) || !d_vals))
+    return fail(COALAC_EINVAL, "coalac_decode: idx/vals/ustart pointers are NULL (a sparse plan needs the per-unit "
+                "starts of wire v2)");
+  if (plan->total_k && plan->bits != 32 && (!d_mn || !d_scale))
     return fail(COALAC_EINVAL, "coalac_decode: mn/scale pointers are NULL");
   if ((reinterpret_cast<uintptr_t>(d_out) | reinterpret_cast<uintptr_t>(d_base)) & 15)
     return fail(COALAC_EINVAL, "coalac_decode: output/base must be 16-byte aligned");
   if (reinterpret_cast<uintptr_t>(d_ustart) & 3) return fail(COALAC_EINVAL, "coalac_decode: ustart must be 4-byte aligned");
-  if (!d_ws || ws_bytes < plan->dec_ws)
-    return fail(COALAC_EWORKSPACE, "coalac_decode: workspace %llu < required %llu", (unsigned long long)ws_bytes,
-                (unsigned long long)plan->dec_ws);
   int rc = check_device(plan);
   if (rc) return rc;
   Params P{};
@@ -3665,22 +3370,12 @@ int coalac_decode_sched(coalac_plan_t plan, const int32_t* d_idx, const void* d_
   P.cscale = d_scale;
   P.base = d_base;
   P.out = d_out;
-  P.ustart = d_ustart ? d_ustart : static_cast<const uint32_t*>(d_ws);
+  P.ustart = d_ustart;
   hipStream_t st = static_cast<hipStream_t>(stream);
   const bool raw = plan->bits == 32, hb = d_base != nullptr;
-  const coalac_sched_t* sc = sched;
-  auto B = [&](int i) { return at_boundary(stages, DEC_SPAN, 2, i) ? boundary(sc, i, st) : COALAC_OK; };
-#define DEC_BOUNDARY(i)       \
-  do {                        \
-    const int rc_ = B(i);     \
-    if (rc_) return rc_;      \
-  } while (0)
-  DEC_BOUNDARY(0);
-  if ((stages & COALAC_STAGE_BOUNDS) && plan->n_bchunks && !lat && !d_ustart && !plan->dense)
-    hipLaunchKernelGGL(k_bounds, dim3(plan->n_bchunks), dim3(BLOCK), 0, st, P, plan->bchunks,
-                       static_cast<uint32_t*>(d_ws));
-  DEC_BOUNDARY(1);
-  const bool whole = (stages & COALAC_STAGE_FILL) && (stages & COALAC_STAGE_SCATTER);
+  const Marks marks{events, 3};
+  MARK(0);
+  MARK(1);
 #define DISPATCH(F, ...)                                   \
   do {                                                     \
     if (raw && hb) F<true, true>(__VA_ARGS__);             \
@@ -3688,37 +3383,26 @@ int coalac_decode_sched(coalac_plan_t plan, const int32_t* d_idx, const void* d_
     else if (hb) F<false, true>(__VA_ARGS__);              \
     else F<false, false>(__VA_ARGS__);                     \
   } while (0)
-  if (plan->dense) {
-    // every element kept: one dequantise stream, positional (the idx / starts, implied, are not read); its
-    // SCATTER part writes every element (FILL alone has nothing to do)
-    if (stages & COALAC_STAGE_SCATTER) DISPATCH(launch_dense_decode, P, plan, st);
-  } else if (lat && (!whole || !d_ustart))
-    // a separately enqueued FILL / SCATTER (the background may go out before the payload exists), or no starts:
-    // k_fill / k_scatter, or k_fillscatter (background, in-kernel range search, kept values on top)
-    DISPATCH(launch_fillscatter, P, plan, st, stages);
-  else if (!lat && !(stages & COALAC_STAGE_SCATTER))
-    ;  // FILL alone on a batch plan: k_decode_lds writes the background itself, with the kept values
+  if (plan->dense)
+    DISPATCH(launch_dense_decode, P, plan, st);  // every element kept: one positional dequantise stream
   else
     DISPATCH(launch_decode_lds, P, plan, st);
 #undef DISPATCH
-  DEC_BOUNDARY(2);
-#undef DEC_BOUNDARY
+  MARK(2);
   HIP_CHECK(hipGetLastError());
   return COALAC_OK;
 }
 
 int coalac_decode(coalac_plan_t plan, const int32_t* d_idx, const void* d_vals, const float* d_mn,
-                  const float* d_scale, const uint32_t* d_ustart, const float* d_base, float* d_out, void* d_ws,
-                  uint64_t ws_bytes, void* stream) {
-  return coalac_decode_ev(plan, d_idx, d_vals, d_mn, d_scale, d_ustart, d_base, d_out, d_ws, ws_bytes, stream,
-                          nullptr);
+                  const float* d_scale, const uint32_t* d_ustart, const float* d_base, float* d_out, void* stream) {
+  return coalac_decode_ev(plan, d_idx, d_vals, d_mn, d_scale, d_ustart, d_base, d_out, stream, nullptr);
 }
 
 int coalac_aggregate_ev(coalac_plan_t plan, int clients, const int32_t* d_idx, const void* d_vals,
                         const float* d_mn, const float* d_scale, const uint32_t* d_ustart, const float* d_weights,
                         float total, int mode,
-                        const uint8_t* d_avg_mask, const float* d_base, float* d_out, void* d_ws,
-                        uint64_t ws_bytes, void* stream, void* const* events) {
+                        const uint8_t* d_avg_mask, const float* d_base, float* d_out, void* stream,
+                        void* const* events) {
   if (!plan) return fail(COALAC_EINVAL, "coalac_aggregate: plan is NULL");
   if (clients < 1 || plan->nseg % clients) return fail(COALAC_EINVAL, "coalac_aggregate: %d segments are not %d copies "
                                                        "of one layout", plan->nseg, clients);
@@ -3726,17 +3410,14 @@ int coalac_aggregate_ev(coalac_plan_t plan, int clients, const int32_t* d_idx, c
     return fail(COALAC_EINVAL, "coalac_aggregate: bad mode %d", mode);
   if (plan->n_units == 0) return COALAC_OK;
   if (!d_out || !d_weights) return fail(COALAC_EINVAL, "coalac_aggregate: output/weights pointer is NULL");
-  if (plan->total_k && (!d_idx || !d_vals))
-    return fail(COALAC_EINVAL, "coalac_aggregate: idx/vals pointers are NULL (a dense plan's implied indices must be "
-                "passed here)");
+  if (plan->total_k && (!d_idx || !d_vals || !d_ustart))
+    return fail(COALAC_EINVAL, "coalac_aggregate: idx/vals/ustart pointers are NULL (the per-unit starts of wire v2; a "
+                "dense plan's implied indices and starts must be passed here)");
   if (plan->bits != 32 && (!d_mn || !d_scale)) return fail(COALAC_EINVAL, "coalac_aggregate: mn/scale pointers are NULL");
   if ((reinterpret_cast<uintptr_t>(d_out) | reinterpret_cast<uintptr_t>(d_base)) & 15)
     return fail(COALAC_EINVAL, "coalac_aggregate: output/base must be 16-byte aligned");
   if (reinterpret_cast<uintptr_t>(d_ustart) & 3)
     return fail(COALAC_EINVAL, "coalac_aggregate: ustart must be 4-byte aligned");
-  if (!d_ws || ws_bytes < plan->dec_ws)
-    return fail(COALAC_EWORKSPACE, "coalac_aggregate: workspace %llu < required %llu", (unsigned long long)ws_bytes,
-                (unsigned long long)plan->dec_ws);
   // the table must be `clients` copies of one layout at constant input / output strides
   const uint32_t T = (uint32_t)(plan->nseg / clients);
   const std::vector<SegDev>& H = plan->hsegs;
@@ -3762,7 +3443,7 @@ int coalac_aggregate_ev(coalac_plan_t plan, int clients, const int32_t* d_idx, c
   P.base = d_base;
   P.out = d_out;
   AggArgs A{};
-  A.ustart = d_ustart ? d_ustart : static_cast<const uint32_t*>(d_ws);  // the payloads' starts, or k_bounds'
+  A.ustart = d_ustart;
   A.weights = d_weights;
   A.clients = (uint32_t)clients;
   A.T = T;
@@ -3772,13 +3453,9 @@ int coalac_aggregate_ev(coalac_plan_t plan, int clients, const int32_t* d_idx, c
   A.inv_total = 1.0f / total;
   A.avg_mask = d_avg_mask;
   hipStream_t st = static_cast<hipStream_t>(stream);
-  const coalac_sched_t s = record_only(events, 3);
-  const coalac_sched_t* sc = events ? &s : nullptr;
-  BOUNDARY(0);
-  if (plan->n_bchunks && !d_ustart)
-    hipLaunchKernelGGL(k_bounds, dim3(plan->n_bchunks), dim3(BLOCK), 0, st, P, plan->bchunks,
-                       static_cast<uint32_t*>(d_ws));
-  BOUNDARY(1);
+  const Marks marks{events, 3};
+  MARK(0);
+  MARK(1);
   const uint32_t g = (U0 * AGG_SPLIT + WAVES - 1) / WAVES;
   const bool raw = plan->bits == 32, hb = d_base != nullptr;
 #define AGG(R, H, M) hipLaunchKernelGGL((k_aggregate<R, H, M>), dim3(g), dim3(BLOCK), 0, st, P, A)
@@ -3798,17 +3475,16 @@ int coalac_aggregate_ev(coalac_plan_t plan, int clients, const int32_t* d_idx, c
   }
 #undef AGG_MODES
 #undef AGG
-  BOUNDARY(2);
+  MARK(2);
   HIP_CHECK(hipGetLastError());
   return COALAC_OK;
 }
 
 int coalac_aggregate(coalac_plan_t plan, int clients, const int32_t* d_idx, const void* d_vals, const float* d_mn,
                      const float* d_scale, const uint32_t* d_ustart, const float* d_weights, float total, int mode,
-                     const uint8_t* d_avg_mask, const float* d_base, float* d_out, void* d_ws, uint64_t ws_bytes,
-                     void* stream) {
+                     const uint8_t* d_avg_mask, const float* d_base, float* d_out, void* stream) {
   return coalac_aggregate_ev(plan, clients, d_idx, d_vals, d_mn, d_scale, d_ustart, d_weights, total, mode, d_avg_mask,
-                             d_base, d_out, d_ws, ws_bytes, stream, nullptr);
+                             d_base, d_out, stream, nullptr);
 }
 
 int coalac_gather(const void* const* d_src, int n, int elem_bytes, void* d_out, void* stream) {

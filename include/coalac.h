@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define COALAC_ABI_VERSION 4
+#define COALAC_ABI_VERSION 5
 
 enum {
   COALAC_OK = 0,
@@ -54,7 +54,10 @@ enum {
 };
 /* (ABI 3 dropped ABI 2's COALAC_FLAG_ONE_LAUNCH / FRONT_LAUNCH / ITEM_STAMPS: the one-launch encode variants
  * measured slower than the kernel sequence, DESIGN.md §6c. ABI 4 added the per-unit starts d_ustart to encode,
- * decode and aggregate: wire v2) */
+ * decode and aggregate: wire v2. ABI 5 makes them required by the sparse decode and the aggregate — a host that
+ * receives a version-1 payload computes them (coala_amd/compression/plan.py) — and drops the decode workspace,
+ * the k_bounds / k_fill / k_scatter kernels and the staged (_sched) entry points; plans whose every segment keeps
+ * all its elements run the dense codec, with the indices implied.) */
 
 /* One fp32 segment (= one flattened tensor of the state_dict). Offsets are in ELEMENTS.
  *   in_off : start of the segment in the flat input / dense output buffer; must be a multiple of 4
@@ -78,20 +81,22 @@ const char* coalac_last_error(void);
 int coalac_plan_create(const coalac_seg_t* h_segs, int nseg, int bits, coalac_plan_t* out);
 int coalac_plan_destroy(coalac_plan_t plan);
 
-/* ws_bytes / dec_ws_bytes: workspace coalac_encode / coalac_decode (and coalac_aggregate) need;
+/* ws_bytes: the workspace coalac_encode needs (decode and aggregate need none);
  * total_k: length of idx/vals;
  * span: max(in_off + n) = the minimum length (elements) of the input/output flat buffers;
  * n_units: 4096-element work units (segment by segment: ceil(n / 4096) each) = the length of the per-unit
  * starts array (ustart). Any output pointer may be NULL. */
-int coalac_plan_query(coalac_plan_t plan, uint64_t* ws_bytes, uint64_t* dec_ws_bytes, uint64_t* total_k,
-                      uint64_t* span, uint64_t* n_units);
+int coalac_plan_query(coalac_plan_t plan, uint64_t* ws_bytes, uint64_t* total_k, uint64_t* span, uint64_t* n_units);
 
 /* Encode d_in (fp32[span]) into idx (int32[total_k], segment-relative, ascending per segment),
  * vals (uint8[total_k] codes or fp32[total_k]), mn (fp32[nseg]) and scale (fp32[nseg]).
  * d_ustart (uint32[n_units], or NULL = not written): per 4096-element unit, the index (segment-relative, into
  * the segment's idx list) of its first kept entry — the wire v2 section that lets a decoder find every unit's
  * entries without searching the idx lists (coalac_decode / coalac_aggregate d_ustart).
- * d_base != NULL selects delta mode: the codec encodes (d_in - d_base). */
+ * d_base != NULL selects delta mode: the codec encodes (d_in - d_base).
+ * A DENSE plan (every segment's k == n: ratio 1, the download direction's default) runs the dense codec: a
+ * per-segment min / max pass, then one quantise stream; its indices are implied (0..n-1 per segment) and d_idx /
+ * d_ustart may be NULL (given, they are written too). */
 int coalac_encode(coalac_plan_t plan, const float* d_in, const float* d_base, int32_t* d_idx,
                   void* d_vals, float* d_mn, float* d_scale, uint32_t* d_ustart, void* d_ws, uint64_t ws_bytes,
                   unsigned flags, void* stream);
@@ -106,82 +111,26 @@ int coalac_encode_segptr(coalac_plan_t plan, const float* const* d_seg_in, const
                          unsigned flags, void* stream);
 
 /* Decode into the dense d_out (fp32[span]); only positions inside segments are written.
- * d_ustart: the encoder's per-unit starts (wire v2), or NULL (a v1 payload: batches compute them with k_bounds,
- * latency-bound plans search them in-kernel). d_base != NULL: d_out = d_base + decoded (fused; d_out may alias
- * d_base). The encoded arrays may come from an untrusted blob: out-of-range or unsorted indices, or wrong
- * starts, can mis-decode but never write outside the unit (still, validate blobs on the host; coala_amd/
- * compression/codec.py validate() does). */
+ * d_ustart: the encoder's per-unit starts (wire v2; required unless the plan is dense — a host holding a v1
+ * payload computes them: for unit u of a segment, the number of the segment's kept indices below u * 4096).
+ * d_base != NULL: d_out = d_base + decoded (fused; d_out may alias d_base). The encoded arrays may come from an
+ * untrusted blob: out-of-range or unsorted indices, or wrong starts, can mis-decode but never write outside the
+ * unit (still, validate blobs on the host; coala_amd/compression/codec.py validate() does). A dense plan decodes
+ * positionally (d_idx / d_ustart are not read). */
 int coalac_decode(coalac_plan_t plan, const int32_t* d_idx, const void* d_vals, const float* d_mn,
-                  const float* d_scale, const uint32_t* d_ustart, const float* d_base, float* d_out, void* d_ws,
-                  uint64_t ws_bytes, void* stream);
+                  const float* d_scale, const uint32_t* d_ustart, const float* d_base, float* d_out, void* stream);
 
 /* Profiling variants: identical work, plus hipEventRecord(events[i], stream) between kernels.
  * encode: [0] before k_sample, [1] after k_sample, [2] after k_scan, [3] after the select kernels
  *         (k_ghist, k_gwin, k_select), [4] after k_emit (recorded even if the plan has no large segment);
- * decode: [0] before k_bounds (batches decoding a payload without per-unit starts), [1] before the decode
- *         kernel (k_decode_lds, or k_fillscatter / k_fill), [2] after it (after k_scatter). NULL
- *         array or NULL entries are skipped. */
+ *         dense plans: [1] after the min / max pass, [2] after the quantise stream;
+ * decode: [0] at the start, [1] before the decode kernel, [2] after it. NULL array or NULL entries are skipped. */
 int coalac_encode_ev(coalac_plan_t plan, const float* d_in, const float* d_base, int32_t* d_idx,
                      void* d_vals, float* d_mn, float* d_scale, uint32_t* d_ustart, void* d_ws, uint64_t ws_bytes,
                      unsigned flags, void* stream, void* const* events);
 int coalac_decode_ev(coalac_plan_t plan, const int32_t* d_idx, const void* d_vals, const float* d_mn,
-                     const float* d_scale, const uint32_t* d_ustart, const float* d_base, float* d_out, void* d_ws,
-                     uint64_t ws_bytes, void* stream, void* const* events);
-
-/* Scheduled variants: identical work, split into stages that may be enqueued by separate calls on
- * separate streams. Stages (sched->stages bit mask; 0 = all):
- *   encode  COALAC_STAGE_SAMPLE  k_sample (large segments: sampled bracket)    boundaries 0 .. 1
- *           COALAC_STAGE_SMALL   k_small  (segments of <= 1024 elements, whole) 0 .. 1
- *           COALAC_STAGE_SCAN    k_scan   (the one HBM read of the large segments) 1 .. 2
- *           COALAC_STAGE_SELECT  k_ghist k_gwin k_select k_emit                  2 .. 4
- *   decode  COALAC_STAGE_BOUNDS  k_bounds (plans of > 8192 units decoding a   boundaries 0 .. 1
- *                                 payload without per-unit starts; others
- *                                 need no bounds)
- *           COALAC_STAGE_DECODE  the whole decode: k_decode_lds (every line    1 .. 2
- *                                 written once), or — a plan of <= 8192 units
- *                                 without per-unit starts — k_fillscatter
- *           COALAC_STAGE_FILL    the background only (k_fill: 0, or the base)  1 .. 2
- *                                 of a plan of <= 8192 units; it reads no
- *                                 encoded array, so it may run before the
- *                                 payload exists. Other plans: nothing.
- *           COALAC_STAGE_SCATTER the kept values only (k_scatter), after a     1 .. 2
- *                                 FILL of the same d_out / d_base; other plans:
- *                                 the whole k_decode_lds. FILL + SCATTER = DECODE.
- * SAMPLE, SCAN, SELECT of one encode (and BOUNDS, DECODE of one decode) must run in this order on the
- * same workspace; SMALL is independent of them. A decode call of a plan of > 8192 units without per-unit
- * starts that enqueues the kept values (DECODE or SCATTER) without BOUNDS must set COALAC_STAGE_BOUNDS_DONE:
- * the caller states that an earlier call enqueued BOUNDS for the same arrays on the same workspace, ordered
- * before this one; without it the call returns COALAC_EINVAL (stale bounds would mis-decode silently). The
- * caller orders them, e.g. with the events below.
- * (A whole encode places the small segments itself: beside k_scan on the plan's side stream for big
- * batches, inside k_scan otherwise; so does a call holding SAMPLE + SCAN + SMALL, the encode's front.) At every boundary an enqueued stage starts or ends at, the call first makes
- * `stream` wait for wait[i] (hipStreamWaitEvent; an event another stream recorded) and then records
- * record[i] (hipEventRecord). Boundaries are those of the _ev variants (encode 0..4, decode 0..2).
- * This lets a host pipeline independent batches over two streams: the HBM-streaming kernels (k_scan,
- * k_decode) back to back on one, the latency-bound ones beside them on the other
- * (coala_amd/compression/pipeline.py). NULL entries are skipped; sched == NULL is the plain call. */
-enum {
-  COALAC_STAGE_SAMPLE = 1,
-  COALAC_STAGE_SCAN = 2,
-  COALAC_STAGE_SELECT = 4,
-  COALAC_STAGE_SMALL = 8,
-  COALAC_STAGE_BOUNDS = 1,
-  COALAC_STAGE_DECODE = 2,
-  COALAC_STAGE_FILL = 4,
-  COALAC_STAGE_SCATTER = 8,
-  COALAC_STAGE_BOUNDS_DONE = 16
-};
-typedef struct coalac_sched {
-  void* wait[5];
-  void* record[5];
-  unsigned stages;
-} coalac_sched_t;
-int coalac_encode_sched(coalac_plan_t plan, const float* d_in, const float* d_base, int32_t* d_idx,
-                        void* d_vals, float* d_mn, float* d_scale, uint32_t* d_ustart, void* d_ws, uint64_t ws_bytes,
-                        unsigned flags, void* stream, const coalac_sched_t* sched);
-int coalac_decode_sched(coalac_plan_t plan, const int32_t* d_idx, const void* d_vals, const float* d_mn,
-                        const float* d_scale, const uint32_t* d_ustart, const float* d_base, float* d_out, void* d_ws,
-                        uint64_t ws_bytes, void* stream, const coalac_sched_t* sched);
+                     const float* d_scale, const uint32_t* d_ustart, const float* d_base, float* d_out, void* stream,
+                     void* const* events);
 
 /* Fused server-side decode + FedAvg of the `clients` updates the plan batches.
  * Replaces, on the server, decompression of every upload (coala/server/base.py:558-560, called :376)
@@ -202,17 +151,16 @@ int coalac_decode_sched(coalac_plan_t plan, const int32_t* d_idx, const void* d_
  * average the parameters only and keep models[0]'s buffers (coala/server/strategies.py:32-54, 93-124).
  * d_weights: DEVICE fp32[clients] = float(w_i); total: float(sum of the weights). d_out / d_base are
  * indexed like client 0's segments. d_ustart: the clients' per-unit starts, concatenated in client order
- * (uint32[n_units]), or NULL (then a k_bounds pass computes them). Workspace: dec_ws_bytes of
- * coalac_plan_query. Events (the _ev variant): [0] before the unit-bounds pass, [1] before k_aggregate, [2] after. */
+ * (uint32[n_units]; required). Events (the _ev variant): [0] at the start, [1] before k_aggregate, [2] after. */
 enum { COALAC_AGG_DIV = 0, COALAC_AGG_RECIP = 1, COALAC_AGG_SUM = 2 };
 int coalac_aggregate(coalac_plan_t plan, int clients, const int32_t* d_idx, const void* d_vals,
                      const float* d_mn, const float* d_scale, const uint32_t* d_ustart, const float* d_weights,
-                     float total, int mode, const uint8_t* d_avg_mask, const float* d_base, float* d_out, void* d_ws,
-                     uint64_t ws_bytes, void* stream);
+                     float total, int mode, const uint8_t* d_avg_mask, const float* d_base, float* d_out,
+                     void* stream);
 int coalac_aggregate_ev(coalac_plan_t plan, int clients, const int32_t* d_idx, const void* d_vals,
                         const float* d_mn, const float* d_scale, const uint32_t* d_ustart, const float* d_weights,
                         float total, int mode, const uint8_t* d_avg_mask, const float* d_base, float* d_out,
-                        void* d_ws, uint64_t ws_bytes, void* stream, void* const* events);
+                        void* stream, void* const* events);
 
 /* Snapshot n scalars of elem_bytes (1, 2, 4 or 8) each, read through the DEVICE pointer array d_src (each pointer
  * aligned to elem_bytes), into the contiguous d_out, in one launch on `stream`: the passthrough entries of an

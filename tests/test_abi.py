@@ -70,11 +70,10 @@ def test_binding_argument_counts_match_header():
 
 
 def test_enum_constants_match_header():
-    """Every COALAC_FLAG_* / COALAC_STAGE_* / COALAC_AGG_* value the Python binding uses is the header's."""
+    """Every COALAC_FLAG_* / COALAC_AGG_* value the Python binding uses is the header's (ABI 5: no stage enums)."""
     hdr = open(_build.HDR).read()
     declared = {k: int(v) for k, v in re.findall(r"\b(COALAC_(?:FLAG|STAGE|AGG)_\w+)\s*=\s*(\d+)", hdr)}
-    assert {"COALAC_STAGE_FILL", "COALAC_STAGE_SCATTER", "COALAC_STAGE_DECODE", "COALAC_AGG_SUM"} <= set(declared)
+    assert {"COALAC_FLAG_FORCE_EXACT", "COALAC_FLAG_NO_FORK", "COALAC_AGG_DIV", "COALAC_AGG_SUM"} <= set(declared)
+    assert not any(k.startswith("COALAC_STAGE_") for k in declared)
     for name, value in declared.items():
-        if hasattr(_lib, name):
-            assert getattr(_lib, name) == value, name
-    assert _lib.COALAC_STAGE_FILL | _lib.COALAC_STAGE_SCATTER != _lib.COALAC_STAGE_DECODE  # separate bits
+        assert getattr(_lib, name) == value, name

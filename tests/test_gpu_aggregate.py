@@ -44,7 +44,7 @@ def test_aggregate_matches_oracle_both_modes(cuda, bits, ratio, delta):
     segs = plan.table.segs.astype(np.int64)
     h = [t.cpu().numpy() for t in (enc.idx, enc.vals, enc.mn, enc.scale)]
     b = None if base is None else base.cpu().numpy()
-    v1 = Encoded(enc.idx, enc.vals, enc.mn, enc.scale)  # without the per-unit starts: k_bounds computes them
+    v1 = Encoded(enc.idx, enc.vals, enc.mn, enc.scale)  # without the per-unit starts: computed on the device
     for mode, om in (("recip", O.AGG_RECIP), ("div", O.AGG_DIV)):
         ref = O.aggregate(*h, segs, bits, C, weights, sum(weights), om, base=b, out_span=plan.table.span_per_client)
         for e in (enc, v1):
@@ -149,7 +149,7 @@ def test_aggregate_rejects_non_copy_layouts(cuda):
     plan = CodecPlan([5000, 300, 7000], 0.01, 8, clients=1)
     # 3 segments cannot be 2 copies of one layout: refused before any launch
     rc = plan._lib.coalac_aggregate(plan._h, 2, None, None, None, None, None, None, ctypes.c_float(1.0), 0, None,
-                                    None, None, None, ctypes.c_uint64(0), None)
+                                    None, None, None)
     with pytest.raises(CodecError, match="copies"):
         _lib.check(rc, "coalac_aggregate")
     with pytest.raises(ValueError):

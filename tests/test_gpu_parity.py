@@ -4,7 +4,7 @@ Tolerance (written here as the bar): indices, codes, mn, scale, the wire v2 per-
 must be BIT-IDENTICAL to oracle/codec_oracle.py (both follow the same fp32 op order with no FMA). The spec's
 guaranteed bound, if a rounding-boundary case ever differed, would be one quantisation step (SURVEY.md §8(a));
 we do not use it — any difference fails. Every decode runs twice: from the encoder's per-unit starts (wire v2)
-and without them (a v1 payload: k_bounds / the in-kernel search).
+and without them (a v1 payload: the host computes them on the device, CodecPlan.unit_starts).
 """
 import numpy as np
 import pytest

@@ -8,6 +8,7 @@ import pytest
 import torch
 
 from coala_amd.compression import CodecPlan, SegmentTable, SplitPipeline
+from coala_amd.compression._lib import CodecError
 from coala_amd.layouts import fp32_sizes
 from coala_amd.workload import synth_batch
 from oracle import codec_oracle as O
@@ -181,75 +182,40 @@ def test_split_pipelines_share_pooled_streams(cuda):
         assert torch.equal(d1.view(torch.int32), o.view(torch.int32))
 
 
-def test_decode_fill_scatter_stages(cuda):
-    """COALAC_STAGE_FILL then COALAC_STAGE_SCATTER = COALAC_STAGE_DECODE, for a latency-bound plan (k_fill +
-    k_scatter) and for a batch plan (FILL is nothing, SCATTER the whole k_decode); FILL alone writes the
-    background only."""
-    from coala_amd.compression import _lib
+def test_decode_without_starts_computes_them(cuda):
+    """ABI 5: the sparse decode reads every unit's entry range from the per-unit starts (wire v2). A payload without
+    them (a version-1 blob) has them computed on the device by the host (CodecPlan.unit_starts): equal to the
+    encoder's own, and the decode equal to the one with the shipped starts — for a latency-bound plan, a batch plan
+    and a plan over absolute segment rows (SplitPipeline's ranges of one update). The raw ABI refuses a NULL."""
+    import ctypes
+
+    from coala_amd.compression import Encoded, _lib
     for clients in (1, 4):
         t = SegmentTable(fp32_sizes("resnet50_tv"), 0.01, clients)
         flat = synth_batch(t, cuda, client_ids=range(clients))
         plan = CodecPlan(None, 0.01, 8, table=t, device=cuda)
-        e = plan.encode(flat)
-        ref = plan.decode(e, out=torch.zeros_like(flat))
-        out = torch.full_like(flat, 7.0)
-        plan.decode(e, out=out, sched=(None, None, _lib.COALAC_STAGE_FILL))
+        e2 = plan.encode(flat)
+        e = Encoded(e2.idx, e2.vals, e2.mn, e2.scale)
+        assert torch.equal(plan.unit_starts(e.idx), e2.ustart)
+        ref = plan.decode(e2, out=torch.zeros_like(flat))
+        out = plan.decode(e, out=torch.zeros_like(flat))
         torch.cuda.synchronize()
-        if clients == 1:  # background only: every segment position 0
-            segs = t.segs.astype(np.int64)
-            o = out.cpu().numpy()
-            assert all((o[off:off + n] == 0).all() for off, n, _, _ in segs)
-        else:
-            assert bool((out == 7.0).all())
-        # (a batch plan's k_decode needs its unit bounds: BOUNDS is a stage of its own, as with DECODE)
-        plan.decode(e, out=out, sched=(None, None, _lib.COALAC_STAGE_BOUNDS | _lib.COALAC_STAGE_SCATTER))
-        torch.cuda.synchronize()
-        segs = t.segs.astype(np.int64)
-        o, r = out.cpu().numpy(), ref.cpu().numpy()
-        for off, n, _, _ in segs:
-            np.testing.assert_array_equal(o[off:off + n].view(np.uint32), r[off:off + n].view(np.uint32),
-                                          err_msg=f"clients={clients} segment at {off}")
-
-
-def test_decode_scatter_without_bounds_is_refused(cuda):
-    """A batch plan (> 8192 units) decoding a payload WITHOUT per-unit starts (wire v1) reads the bounds k_bounds
-    leaves in the workspace. SCATTER alone on a fresh workspace would read stale bounds: the ABI refuses it
-    (EINVAL) unless the caller sets BOUNDS_DONE after its own BOUNDS call — which then decodes exactly. With the
-    payload's starts (wire v2) nothing is read from the workspace: SCATTER alone decodes exactly."""
-    from coala_amd.compression import Encoded, _lib
-    t = SegmentTable(fp32_sizes("resnet50_tv"), 0.01, 4)
-    assert CodecPlan(None, 0.01, 8, table=t, device=cuda).n_units > 8192
-    flat = synth_batch(t, cuda, client_ids=range(4))
-    plan = CodecPlan(None, 0.01, 8, table=t, device=cuda)
-    e2 = plan.encode(flat)
-    e = Encoded(e2.idx, e2.vals, e2.mn, e2.scale)  # the same payload without its starts
-    ref = plan.decode(e, out=torch.zeros_like(flat))
-    o2 = torch.zeros_like(flat)
-    garbage = torch.full((plan.dec_ws_bytes,), 0xAB, dtype=torch.uint8, device=cuda)
-    plan.decode(e2, out=o2, workspace=garbage, sched=(None, None, _lib.COALAC_STAGE_SCATTER))
-    torch.cuda.synchronize()
-    assert torch.equal(o2.view(torch.int32), ref.view(torch.int32))
-    ws = torch.full((plan.dec_ws_bytes,), 0xAB, dtype=torch.uint8, device=cuda)  # garbage bounds
-    out = torch.zeros_like(flat)
-    for stages in (_lib.COALAC_STAGE_SCATTER, _lib.COALAC_STAGE_DECODE):
-        with pytest.raises(_lib.CodecError, match="BOUNDS"):
-            plan.decode(e, out=out, workspace=ws, sched=(None, None, stages))
-    plan.decode(e, out=out, workspace=ws, sched=(None, None, _lib.COALAC_STAGE_BOUNDS))
-    plan.decode(e, out=out, workspace=ws, sched=(None, None, _lib.COALAC_STAGE_SCATTER | _lib.COALAC_STAGE_BOUNDS_DONE))
-    torch.cuda.synchronize()
-    assert torch.equal(out.view(torch.int32), ref.view(torch.int32))
-    # a latency-bound plan searches its entry ranges in-kernel: SCATTER alone is fine there
+        assert torch.equal(out.view(torch.int32), ref.view(torch.int32))
+        rc = plan._lib.coalac_decode(plan._h, ctypes.c_void_p(e.idx.data_ptr()), ctypes.c_void_p(e.vals.data_ptr()),
+                                     ctypes.c_void_p(e.mn.data_ptr()), ctypes.c_void_p(e.scale.data_ptr()), None, None,
+                                     ctypes.c_void_p(out.data_ptr()), None)
+        with pytest.raises(CodecError, match="ustart"):
+            _lib.check(rc, "coalac_decode")
     t1 = SegmentTable(fp32_sizes("resnet50_tv"), 0.01, 1)
-    p1 = CodecPlan(None, 0.01, 8, table=t1, device=cuda)
-    f1 = flat[:t1.span]
-    e1 = p1.encode(f1)
-    e1 = Encoded(e1.idx, e1.vals, e1.mn, e1.scale)
-    r1 = p1.decode(e1, out=torch.zeros_like(f1))
-    o1 = torch.zeros_like(f1)
-    p1.decode(e1, out=o1, sched=(None, None, _lib.COALAC_STAGE_FILL))
-    p1.decode(e1, out=o1, sched=(None, None, _lib.COALAC_STAGE_SCATTER))
-    torch.cuda.synchronize()
-    assert torch.equal(o1.view(torch.int32), r1.view(torch.int32))
+    rows = t1.segs[100:180]
+    sub = CodecPlan.from_segments(rows, 8, device=cuda)
+    f1 = synth_batch(t1, cuda, client_ids=[9])
+    full = CodecPlan(None, 0.01, 8, table=t1, device=cuda)
+    ef = full.encode(f1)
+    uo = [0]
+    for n in t1.segs[:, 1].tolist():
+        uo.append(uo[-1] + (int(n) + 4095) // 4096)
+    assert torch.equal(sub.unit_starts(ef.idx), ef.ustart[uo[100]:uo[180]])
 
 
 def test_split_pipelines_in_flight_on_disjoint_streams(cuda):
@@ -334,43 +300,5 @@ def test_split_pipeline_graph_capture_records_every_part(cuda, split):
     e = plan.encode(flat)
     d = plan.decode(e, out=torch.zeros_like(flat))
     torch.cuda.synchronize()
-    assert torch.equal(e.idx, enc.idx) and torch.equal(e.vals, enc.vals)
-    assert torch.equal(d.view(torch.int32), out.view(torch.int32))
-
-
-@pytest.mark.parametrize("delta", [False, True])
-def test_fill_ahead_roundtrip_eager_and_captured(cuda, delta):
-    """fill_ahead: the decode background on a side stream beside the select chain (encode front / select as
-    separate stage calls, decode FILL then SCATTER) — eager and as a captured graph replayed on new data, the
-    result is the plain roundtrip's, bit for bit (and so the oracle's, via the plain path's tests)."""
-    t = SegmentTable(fp32_sizes("resnet50_tv"), 0.01, 1)
-    flat = synth_batch(t, cuda, client_ids=[51])
-    base = synth_batch(t, cuda, client_ids=[52]) if delta else None
-    pipe = SplitPipeline(t, 8, split=1, device=cuda)
-    enc, out = pipe.empty_encoded(), pipe.empty_flat().zero_()
-    pipe.roundtrip(flat, base=base, enc=enc, out=out, fill_ahead=True)
-    torch.cuda.synchronize()
-    plan = CodecPlan(fp32_sizes("resnet50_tv"), 0.01, 8, clients=1, device=cuda)
-
-    def ref():
-        e = plan.encode(flat, base=base)
-        d = plan.decode(e, base=base, out=torch.zeros_like(flat))
-        torch.cuda.synchronize()
-        return e, d
-    e, d = ref()
-    assert torch.equal(e.idx, enc.idx) and torch.equal(e.vals, enc.vals)
-    assert torch.equal(d.view(torch.int32), out.view(torch.int32))
-    g = torch.cuda.CUDAGraph()
-    with torch.cuda.graph(g, stream=pipe.streams[0]):
-        for _ in range(2):
-            pipe.roundtrip(flat, base=base, enc=enc, out=out, joined=False, fill_ahead=True)
-    torch.cuda.synchronize()
-    flat.copy_(synth_batch(t, cuda, client_ids=[53]))
-    out.zero_()
-    torch.cuda.synchronize()
-    with torch.cuda.stream(pipe.streams[0]):
-        g.replay()
-    torch.cuda.synchronize()
-    e, d = ref()
     assert torch.equal(e.idx, enc.idx) and torch.equal(e.vals, enc.vals)
     assert torch.equal(d.view(torch.int32), out.view(torch.int32))

@@ -45,7 +45,6 @@ def main():
     enc = plan.encode(flat, base=base_rep)
     weights = [10 + 3 * i for i in range(C)]
     out = torch.empty(plan.table.span_per_client, dtype=torch.float32, device=dev)
-    ws = plan.empty_decode_workspace()
     evs = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(a.steps)]
     for e in evs:
         for x in e:
@@ -55,11 +54,11 @@ def main():
 
     def timed(e_in):
         for _ in range(a.warmup):
-            plan.aggregate(e_in, weights, base=base, out=out, workspace=ws)
+            plan.aggregate(e_in, weights, base=base, out=out)
         torch.cuda.synchronize()
         t0.record()
         for i in range(a.steps):
-            plan.aggregate(e_in, weights, base=base, out=out, workspace=ws, events=evs[i])
+            plan.aggregate(e_in, weights, base=base, out=out, events=evs[i])
         t1.record()
         torch.cuda.synchronize()
         return (t0.elapsed_time(t1) / a.steps, sum(e[0].elapsed_time(e[1]) for e in evs) / a.steps,

@@ -33,7 +33,7 @@ def run(clients, steps, warmup, layout, ratio, bits):
     flat_d = synth_batch(plan.table, dev, client_ids=range(clients))
     flat_h = flat_d.cpu().pin_memory()
     out_h = torch.empty_like(flat_h).pin_memory()
-    enc_d, ws, dws = plan.empty_encoded(), plan.empty_workspace(), plan.empty_decode_workspace()
+    enc_d, ws = plan.empty_encoded(), plan.empty_workspace()
     out_d = torch.empty_like(flat_d)
     enc_h = [torch.empty_like(t, device="cpu").pin_memory() for t in (enc_d.idx, enc_d.vals, enc_d.mn, enc_d.scale)]
     enc_r = plan.empty_encoded()  # server-side device copy of the received payload
@@ -41,7 +41,7 @@ def run(clients, steps, warmup, layout, ratio, bits):
 
     def device_step():
         plan.encode(in_d, out=enc_d, workspace=ws)
-        plan.decode(enc_d, out=out_d, workspace=dws)
+        plan.decode(enc_d, out=out_d)
 
     def host_step():
         in_d.copy_(flat_h, non_blocking=True)
@@ -50,7 +50,7 @@ def run(clients, steps, warmup, layout, ratio, bits):
             h.copy_(d, non_blocking=True)
         for h, d in zip(enc_h, (enc_r.idx, enc_r.vals, enc_r.mn, enc_r.scale)):
             d.copy_(h, non_blocking=True)
-        plan.decode(enc_r, out=out_d, workspace=dws)
+        plan.decode(enc_r, out=out_d)
         out_h.copy_(out_d, non_blocking=True)
 
     res = {}

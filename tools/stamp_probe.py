@@ -48,11 +48,11 @@ def main():
     n_large = int((n > 4096).sum())
     F = _lib.COALAC_FLAG_STAMPS
     rows = []
-    for mode, sched in (("encode", None), ("small-only", ([None] * 5, [None] * 5, _lib.COALAC_STAGE_SMALL))):
+    for mode in ("encode",):
         acc = []
         for r in range(a.reps):
             ws.zero_()
-            plan.encode(flat, out=enc, workspace=ws, flags=F, sched=sched)
+            plan.encode(flat, out=enc, workspace=ws, flags=F)
             torch.cuda.synchronize()
             buf = (ctypes.c_uint64 * (16 * nseg))()
             got = plan._lib.coalac_debug_stamps(plan._h, _ptr(ws), None, buf, 16 * nseg)
