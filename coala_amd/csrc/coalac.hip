@@ -106,16 +106,6 @@ constexpr int SEL_NT_LAT = 512;           // ... in latency-bound plans, where n
 #ifndef SCAN_NB
 #define SCAN_NB 1  // load batches per k_scan unit (weights mode): 1 = all 16 float4 per lane in flight
 #endif
-#ifndef SCAN_XCD
-#define SCAN_XCD 1    // k_scan: XCD-aware unit order (128-thread blocks: C3 0.600-0.602 vs 0.604-0.606 ms)
-#endif
-#ifndef SCAN_LEAN
-#define SCAN_LEAN 1  // k_scan: no per-element length test on units that cannot need it (scan_unit CHECK)
-#endif
-#ifndef SCAN_SMALL_LAT
-#define SCAN_SMALL_LAT 1  // latency-bound plans: small segments in k_scan's first blocks (k_sample alone ahead;
-                          // batches measured the same either way and keep k_presel)
-#endif
 #ifndef SCAN_WPE_LAT
 #define SCAN_WPE_LAT 6  // latency-bound plans' k_scan: blocks per CU (5 / 1 batch: 24.5 us, 6 / 2: 23.0, 6 / 1
                         // spills: 31.7, 8 / 4: 24.2 on one update; batches keep SCAN_WPE / SCAN_NB)
@@ -127,21 +117,11 @@ constexpr int SEL_NT_LAT = 512;           // ... in latency-bound plans, where n
 #ifndef SCAN_NB_LAT
 #define SCAN_NB_LAT 2   // ... and load batches per unit
 #endif
-#ifndef SAMPLE_PICK2
 #ifndef SAMPLE_NT_LAT
 #define SAMPLE_NT_LAT 256  // latency-bound plans' k_sample block size (1024 threads, 2 load batches each: 0.7 us slower)
 #endif
-#define SAMPLE_PICK2 1  // k_sample: both bracket bins from one block scan of the histogram
-#endif
-#ifndef RANK_SELECT
-#define RANK_SELECT 1  // block_select: rank the <= RANK_MAX keys of the chosen bin instead of more radix passes
-#endif
-#ifndef LOAD_AUX
-#define LOAD_AUX 2   // cache policy of the streaming buffer loads (k_scan): 2 = non-temporal
-#endif
-#ifndef STORE_AUX
-#define STORE_AUX 2  // cache policy of the streaming buffer stores (k_decode): 2 = non-temporal
-#endif
+constexpr int LOAD_AUX = 2;   // cache policy of the streaming buffer loads (k_scan, the quantise stream): non-temporal
+constexpr int STORE_AUX = 2;  // cache policy of the streaming buffer stores (batch k_decode_lds, k_dense_deq): non-temporal
 constexpr uint32_t STAGE_CAP = 512;       // candidate records staged in LDS per k_scan wave
 #ifndef GU_UNITS
 #define GU_UNITS 32
@@ -483,7 +463,7 @@ DEV uint32_t block_select(ForEach&& for_each, uint32_t lo, uint32_t hi, uint32_t
     lo = lo + (b << shift);
     const uint32_t nhi = lo + ((1u << shift) - 1u);
     hi = nhi < hi ? nhi : hi;
-    if (RANK_SELECT && lo < hi && bc <= RANK_MAX && NB >= (int)RANK_MAX)
+    if (lo < hi && bc <= RANK_MAX && NB >= (int)RANK_MAX)
       return rank_select<NT>(for_each, lo, hi, r, hist, sh);
   }
   return lo;
@@ -1054,13 +1034,7 @@ DEV void sample_segment(const Params& P, uint32_t li, uint32_t* hist, uint32_t* 
   __syncthreads();
   uint32_t tlo = 0u, thi = KEY_MAX;
   uint32_t blo = 0, bhi = 0;  // both bracket bins from one scan of the histogram
-  if (SAMPLE_PICK2) {
-    hist_pick2<NT>(hist, rlo < (double)m ? (uint32_t)rlo : 0u, rhi >= 1.0 ? (uint32_t)rhi : 0u, blo, bhi, sh);
-  } else {
-    uint32_t r1 = (uint32_t)rlo, r2 = (uint32_t)rhi;
-    if (rlo < (double)m) blo = hist_pick<NT>(hist, r1, sh);
-    if (rhi >= 1.0) bhi = hist_pick<NT>(hist, r2, sh);
-  }
+  hist_pick2<NT>(hist, rlo < (double)m ? (uint32_t)rlo : 0u, rhi >= 1.0 ? (uint32_t)rhi : 0u, blo, bhi, sh);
   if (rlo < (double)m) tlo = kmin + (blo << shift);
   if (rhi >= 1.0) {
     const uint64_t edge = (uint64_t)kmin + (((uint64_t)bhi + 1) << shift) - 1;
@@ -1127,7 +1101,7 @@ __global__ __launch_bounds__(NTS, WPE) void k_scan(Params P) {
   }
   uint2* stage = reinterpret_cast<uint2*>(arena);
   const uint32_t wv = threadIdx.x >> 6;
-  const uint32_t lu = ((SCAN_XCD && !WITH_SMALL ? xcd_block(blockIdx.x) : blockIdx.x) - P.scan_small) * NWS + wv;
+  const uint32_t lu = ((!WITH_SMALL ? xcd_block(blockIdx.x) : blockIdx.x) - P.scan_small) * NWS + wv;
   if (lu >= P.n_lunits) return;
   const UnitDev L = P.lunits[lu];
   // delta: 4 load batches (32 float4 in flight spill)
@@ -1137,7 +1111,7 @@ __global__ __launch_bounds__(NTS, WPE) void k_scan(Params P) {
       scan_unit<DELTA, DELTA ? 4 : NB, false, true>(P, lu, L, tlo, thi, stage + wv * STAGE_CAP);
     else
       scan_unit<DELTA, DELTA ? 4 : NB, true, true>(P, lu, L, tlo, thi, stage + wv * STAGE_CAP);
-  } else if (SCAN_LEAN && (L.len == UNIT || tlo > 0))
+  } else if (L.len == UNIT || tlo > 0)
     scan_unit<DELTA, DELTA ? 4 : NB, false>(P, lu, L, tlo, thi, stage + wv * STAGE_CAP);
   else
     scan_unit<DELTA, DELTA ? 4 : NB, true>(P, lu, L, tlo, thi, stage + wv * STAGE_CAP);
@@ -1977,9 +1951,6 @@ __global__ __launch_bounds__(NT) void k_select(Params P) {
 #define EMIT_UPW_LAT 1u
 #endif
 constexpr uint32_t EMIT_UPW_LATENCY = EMIT_UPW_LAT;
-#ifndef EMIT_ROWS
-#define EMIT_ROWS 1  // 64-record rows of every unit loaded before the first is classified (1 or 2)
-#endif
 
 DEV uint32_t rl(uint32_t v, uint32_t l) { return (uint32_t)__builtin_amdgcn_readlane((int)v, (int)l); }
 
@@ -2044,7 +2015,7 @@ DEV void emit_units(const Params& P, uint32_t lu0, uint32_t lu1) {
   uint32_t nCg, startg, eqpg, oog, Tg, rtg, stg;
   uint64_t sog;
   float mng, scg;
-  uint2 rec0[UPW], rec1[UPW];  // {position, value bits}
+  uint2 rec0[UPW];  // {position, value bits}: every unit's first 64 records
   if constexpr (UPW == 1) {
     // latency-bound plans — ONE load round: the unit's count, record, offsets and its segment's emit parameters
     // (k_select copies them to every unit), and, before the count is known, the unit's first 64 (128) record
@@ -2057,7 +2028,6 @@ DEV void emit_units(const Params& P, uint32_t lu0, uint32_t lu1) {
     const uint4 ue = P.uemit[lug];
     const uint64_t r0 = (uint64_t)lu0 * P.ccap;
     rec0[0] = make_uint2(P.cpos[r0 + lane], P.cval[r0 + lane]);
-    if (EMIT_ROWS > 1) rec1[0] = make_uint2(P.cpos[r0 + lane + 64], P.cval[r0 + lane + 64]);
     nCg = min(nCr, P.ccap);  // stored records (a raw-path unit may have dropped some)
     Tg = ue.x;
     rtg = ue.y & 0x7FFFFFFFu;
@@ -2084,7 +2054,6 @@ DEV void emit_units(const Params& P, uint32_t lu0, uint32_t lu1) {
       const uint32_t last = nC ? nC - 1 : 0u;
       const uint64_t r0 = (uint64_t)lu * P.ccap;  // unconditional (clamped) loads
       rec0[g] = make_uint2(P.cpos[r0 + min(lane, last)], P.cval[r0 + min(lane, last)]);
-      if (EMIT_ROWS > 1) rec1[g] = make_uint2(P.cpos[r0 + min(lane + 64, last)], P.cval[r0 + min(lane + 64, last)]);
     }
   }
 #pragma unroll
@@ -2108,8 +2077,7 @@ DEV void emit_units(const Params& P, uint32_t lu0, uint32_t lu1) {
         const uint32_t i = i0 + lane;
         const bool valid = i < nC;
         const uint32_t ic = min(i, nC - 1);
-        const uint2 rec = i0 == 0 ? rec0[g] : (EMIT_ROWS > 1 && i0 == 64) ? rec1[g]
-                                                                            : make_uint2(P.cpos[r0 + ic], P.cval[r0 + ic]);
+        const uint2 rec = i0 == 0 ? rec0[g] : make_uint2(P.cpos[r0 + ic], P.cval[r0 + ic]);
         const float x = __uint_as_float(rec.y);
         const uint32_t key = fkey(x);
         const bool e = valid && key == T;
@@ -2533,19 +2501,12 @@ __global__ __launch_bounds__(BLOCK, AGG_WPE) void k_aggregate(Params P, AggArgs 
 //   decode: k_dense_deq (per unit: read the 1-B code, write 4 B; + base in delta mode)
 // One wave per 4096-element unit, 16 float4 per lane, XCD-aware unit order in batches.
 // ------------------------------------------------------------------------------------------------
-#ifndef DENSE_DEQ_SAUX
-#define DENSE_DEQ_SAUX 2  // k_dense_deq store policy (non-temporal: one update's download 0.073 vs 0.088 ms per
-                          // step; a reciprocal-multiply quantise measured no faster: the streams are memory-bound)
-#endif
-#ifndef DENSE_Q_SAUX
-#define DENSE_Q_SAUX 0  // k_dense_quant code store policy
-#endif
-#ifndef DENSE_MM_AUX
-#define DENSE_MM_AUX 0  // k_dense_minmax load policy (0: default, kept in the caches for the quantise pass)
-#endif
-// AUX: the loads' cache policy — the min / max pass reads with the default policy, so an update that fits the
-// Infinity Cache is still there for the quantise pass, whose non-temporal reads are the last use
-template <bool DELTA, int AUX>
+// cache policies: the min / max pass reads with the default policy (an update that fits the Infinity Cache is still
+// there for the quantise pass, which reads non-temporally); the dense decode stores non-temporally (one update's
+// download 0.073 vs 0.088 ms per step with plain stores; a reciprocal-multiply quantise measured no faster: these
+// streams are memory-bound, profiles/r05_ab.txt)
+constexpr int DENSE_MM_AUX = 0;
+template <bool DELTA, int AUX>  // (AUX: the loads' cache policy)
 DEV void dense_unit_load(const Params& P, const UnitDev& U, float4 (&v)[UNIT_IT]) {
   typedef unsigned int u4v __attribute__((ext_vector_type(4)));
   const uint32_t lane = lane_id();
@@ -2651,7 +2612,7 @@ __global__ __launch_bounds__(BLOCK) void k_dense_quant(Params P) {
       const uint32_t q2 = quantize(v[it].z, mn, scale, P.levels), q3 = quantize(v[it].w, mn, scale, P.levels);
       const uint32_t boff = (it * 64 + lane) * 4;
       if (vec) {
-        __builtin_amdgcn_raw_buffer_store_b32(q0 | (q1 << 8) | (q2 << 16) | (q3 << 24), r, (int)boff, 0, DENSE_Q_SAUX);
+        __builtin_amdgcn_raw_buffer_store_b32(q0 | (q1 << 8) | (q2 << 16) | (q3 << 24), r, (int)boff, 0, 0);
       } else {  // (range-checked per byte: the unit's tail past len is dropped)
         __builtin_amdgcn_raw_buffer_store_b8((uint8_t)q0, r, (int)boff, 0, 0);
         __builtin_amdgcn_raw_buffer_store_b8((uint8_t)q1, r, (int)boff + 1, 0, 0);
@@ -2723,9 +2684,9 @@ __global__ __launch_bounds__(BLOCK) void k_dense_deq(Params P) {
       x = make_float4(b.x + x.x, b.y + x.y, b.z + x.z, b.w + x.w);
     }
     if ((U.len & 3u) == 0)
-      unit_store_x4<DENSE_DEQ_SAUX>(rout, (it * 64 + lane) * 16, x);
+      unit_store_x4<STORE_AUX>(rout, (it * 64 + lane) * 16, x);
     else
-      unit_store_x1x4<DENSE_DEQ_SAUX>(rout, (it * 64 + lane) * 16, x);
+      unit_store_x1x4<STORE_AUX>(rout, (it * 64 + lane) * 16, x);
   }
 }
 
