@@ -112,6 +112,9 @@ def parse():
                    help="at most this many timed steps captured in one graph (--graph; whole input rotations, the "
                         "count that needs the fewest launches): 1 / 4 / 10 steps per launch measured 0.0845 / 0.0803 / "
                         "0.0796 ms per single step (eager 0.080-0.083)")
+    p.add_argument("--repeat-windows", type=int, default=5,
+                   help="after the timed region, time the same K steps again this many times and report the min / "
+                        "median / max ms per step beside the line (not part of value)")
     p.add_argument("--cpu-seconds", type=float, default=8.0, help="CPU baseline time budget per leg")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--launch-check", action="store_true",
@@ -401,32 +404,37 @@ def time_workload(W, a, dev, world):
     graphs = W["graphs"]
     # The timed region carries no timing event (each recorded event costs a dispatch gap) and its sub-batch
     # streams are not joined per step, so consecutive steps overlap.
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    if graphs is None:
-        for i in range(a.steps):
-            _step(W, i, a.joined)
-    else:  # per slot: its whole-rotation graphs, then its single steps; slots round-robin
-        gk, S = W["gk"], len(slots)
-        ops = []
-        for j, n in enumerate(W["per_slot"]):
-            big = n // gk
-            ops.append([graphs[gk][j]] * big + [graphs[(1, r % W["rot"])][j] for r in range(n - big * gk)])
-        for q in range(max(len(o) for o in ops)):
-            for o in ops:
-                if q < len(o):
-                    g, st = o[q]
-                    with torch.cuda.stream(st):
-                        g.replay()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    el = time.perf_counter() - t0
+    def timed_region():
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        if graphs is None:
+            for i in range(a.steps):
+                _step(W, i, a.joined)
+        else:  # per slot: its whole-rotation graphs, then its single steps; slots round-robin
+            gk = W["gk"]
+            ops = []
+            for j, n in enumerate(W["per_slot"]):
+                big = n // gk
+                ops.append([graphs[gk][j]] * big + [graphs[(1, r % W["rot"])][j] for r in range(n - big * gk)])
+            for q in range(max(len(o) for o in ops)):
+                for o in ops:
+                    if q < len(o):
+                        g, st = o[q]
+                        with torch.cuda.stream(st):
+                            g.replay()
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        return time.perf_counter() - t0
+    el = timed_region()
     rank_el = gather_elapsed(el, world, dev)
     el = max(rank_el)  # the job's time: the slowest rank
+    # the same K steps timed again in a few more windows (not part of `value`): the spread a single short window
+    # cannot show (box-to-box and run-to-run variance)
+    rep_ms = sorted(timed_region() / a.steps * 1e3 for _ in range(a.repeat_windows))
 
     # Roofline steps (after the timed region, not part of `value`): per sub-batch, HIP events [1] / [2]
     # recorded on its own stream around its streaming kernels, each step joined with the caller's stream
@@ -489,6 +497,9 @@ def time_workload(W, a, dev, world):
         "sample_fallbacks": W.get("fallbacks", 0),
         "graph": W["graph_error"] or (graphs is not None and f"{W['gk']} step(s) per graph launch"),
         "rank_ms_per_step": rank_spread(rank_el, a.steps),
+        "repeat_windows": ({"windows": len(rep_ms), "steps_each": a.steps, "ms_per_step_min": round(rep_ms[0], 4),
+                            "ms_per_step_median": round(rep_ms[len(rep_ms) // 2], 4),
+                            "ms_per_step_max": round(rep_ms[-1], 4)} if rep_ms else None),
     }
     if headline:
         traffic, src = pmc_traffic(dom, W["cfg"], a, split, world)
@@ -775,9 +786,10 @@ def main():
             "roofline": head["roofline"], "step_roofline": head["step_roofline"], "stages_ms": head["stages_ms"],
             "stage_timing": head["stage_timing"], "sample_fallbacks": head["sample_fallbacks"],
             "graph": head["graph"], "rank_ms_per_step": head["rank_ms_per_step"],
+            "repeat_windows": head["repeat_windows"],
             "configs": {k: {f: v[f] for f in ("value", "ms_per_step", "step_roofline", "roofline", "stages_ms", "desc",
                                               "elements_per_gpu", "segments_per_gpu", "split", "inflight", "rotation",
-                                              "graph", "sample_fallbacks", "rank_ms_per_step")}
+                                              "graph", "sample_fallbacks", "rank_ms_per_step", "repeat_windows")}
                         for k, v in results.items()},
         }
         res["box"] = box
