@@ -2,7 +2,8 @@
 
 C client updates of one layout (default 16 x ResNet-50, ratio 0.01, 8-bit, delta mode) are aggregated
 into w_global + FedAvg(decoded deltas) in one launch (k_aggregate, with the payloads' per-unit starts: wire
-v2), and — the "v1" line — from payloads without them (k_bounds + k_aggregate). Reported: GB/s of fp32 update
+v2), and — the "v1" line — from payloads without them (the starts computed on the device first,
+CodecPlan.unit_starts, then k_aggregate). Reported: GB/s of fp32 update
 aggregated (4 * N * C / t), the kernel's algorithmic HBM bytes (base read 4N + output write 4N + C payloads of
 idx/code (5K) + mn/scale (8T) + the per-unit starts (4U)) against 8 TB/s, and the time of the unfused
 reference flow on the same data: C x coalac_decode into dense modules + the restated weighted_sum /
@@ -71,7 +72,6 @@ def main():
     K, T = t.total_k, t.n_segments
     vb = 4 if a.bits == 32 else 1
     alg_agg = 8 * N1 + (4 + vb) * K + 8 * T + 4 * t.n_units
-    alg_bounds = 4 * K
 
     # unfused reference flow: decode every client into a dense buffer, then weighted_sum + div (GPU)
     S = t.span_per_client
@@ -104,8 +104,8 @@ def main():
         "roofline": {"kernel": "k_aggregate", "alg_bytes": alg_agg,
                      "achieved_GBs": round(alg_agg / (k_agg * 1e-3) / 1e9, 1),
                      "frac": round(alg_agg / (k_agg * 1e-3) / 1e9 / 8000.0, 4)},
-        "v1_payloads": {"ms": round(ms1, 4), "k_bounds_ms": round(k_bounds1, 4), "k_aggregate_ms": round(k_agg1, 4),
-                        "bounds_alg_bytes": alg_bounds},
+        "v1_payloads": {"ms": round(ms1, 4), "k_aggregate_ms": round(k_agg1, 4),
+                        "starts": "computed on the device (CodecPlan.unit_starts) before the kernel"},
         "unfused_reference_flow_ms": round(ms_ref, 4), "speedup_vs_unfused": round(ms_ref / ms, 2),
         "bit_identical_to_unfused": bool(same)}), flush=True)
 
