@@ -1139,6 +1139,28 @@ DEV uint32_t chunk_prefix(const uint32_t* cnt, uint32_t cn, uint32_t cap, uint32
 }
 
 
+// The records of a unit past its first two rows (n > 128: plans above ratio ~0.02), TAIL_ROWS rows of 64 per load
+// round instead of one dependent round per row (C3 at ratio 0.1: a ~450-record unit took 6 rounds).
+constexpr uint32_t TAIL_ROWS = 4;
+// (k_emit batches its record rows the same way only in plans above HIGH_RATIO: at ratio 0.01 almost every unit's records
+// fit the preloaded first row, and the batched loop measured 1.5 % slower on C3 — 0.600 vs 0.592 ms per step; C3 at
+// ratio 0.1: 0.922 vs 0.982 ms with it, profiles/r05_ab.txt)
+constexpr double HIGH_RATIO = 0.02;
+template <class F>
+DEV void tail_rows(const uint32_t* R, uint32_t n, uint32_t u, F&& f) {
+  constexpr uint32_t TR = TAIL_ROWS;
+  const uint32_t lane = lane_id();
+  for (uint32_t i0 = 128; i0 < n; i0 += 64 * TR) {
+    uint32_t x[TR];
+#pragma unroll
+    for (uint32_t b = 0; b < TR; ++b)
+      if (i0 + b * 64 < n) x[b] = R[min(i0 + b * 64 + lane, n - 1)];  // (wave-uniform guard)
+#pragma unroll
+    for (uint32_t b = 0; b < TR; ++b)
+      if (i0 + b * 64 < n) f(__uint_as_float(x[b]), i0 + b * 64 + lane < n, u);
+  }
+}
+
 // Wave w owns the units whose first record index (upre[u]) lies in [w*total/NW, (w+1)*total/NW):
 // contiguous unit ranges balanced by record count, so segment order = (wave, unit, lane) order. A wave
 // reads one unit at a time from its contiguous region (coalesced, trivial addressing, the unit is
@@ -1180,10 +1202,7 @@ DEV void unit_sweep(const uint32_t* cand, uint32_t stride, uint32_t lu0, const u
         const uint32_t uu = u + g, n = nn[g];
         f(__uint_as_float(x0[g]), lane < n, uu);
         if (n > 64) f(__uint_as_float(x1[g]), lane + 64 < n, uu);
-        if (n > 128) {
-          const uint32_t* R = cand + (uint64_t)(lu0 + uu) * stride;
-          for (uint32_t i0 = 128; i0 < n; i0 += 64) f(__uint_as_float(R[min(i0 + lane, n - 1)]), i0 + lane < n, uu);
-        }
+        if (n > 128) tail_rows(cand + (uint64_t)(lu0 + uu) * stride, n, uu, f);
         fend(uu);
       }
     }
@@ -1256,10 +1275,7 @@ struct SpecSweep {
         const uint32_t nn = (uint32_t)__builtin_amdgcn_readlane((int)n, (int)g);
         f(__uint_as_float(x0[g]), lane < nn, u);
         if (nn > 64) f(__uint_as_float(x1[g]), lane + 64 < nn, u);
-        if (nn > 128) {
-          const uint32_t* R = P.cval + (uint64_t)(lu0 + u) * P.ccap;
-          for (uint32_t i0 = 128; i0 < nn; i0 += 64) f(__uint_as_float(R[min(i0 + lane, nn - 1)]), i0 + lane < nn, u);
-        }
+        if (nn > 128) tail_rows(P.cval + (uint64_t)(lu0 + u) * P.ccap, nn, u, f);
         fend(u);
       }
     }
@@ -2006,7 +2022,7 @@ DEV void emit_raw_unit(const Params& P, const UnitDev& L, uint32_t T, uint32_t r
 }
 
 // one wave emits the large units [lu0, lu1) (lu1 - lu0 <= UPW)
-template <bool DELTA, bool RAW, uint32_t UPW = EMIT_UPW>
+template <bool DELTA, bool RAW, uint32_t UPW, uint32_t TR>
 DEV void emit_units(const Params& P, uint32_t lu0, uint32_t lu1) {
   const uint32_t lane = lane_id();
   // lane g < UPW holds unit lu0 + g's count, offsets and its segment's T*, tie budget, mn, scale (lanes past
@@ -2073,11 +2089,9 @@ DEV void emit_units(const Params& P, uint32_t lu0, uint32_t lu1) {
       const uint32_t start = rl(startg, g);
       const uint64_t r0 = (uint64_t)lu * P.ccap;
       uint32_t eqc = 0, outc = 0;
-      for (uint32_t i0 = 0; i0 < nC; i0 += 64) {
+      auto row = [&](uint32_t i0, uint2 rec) {
         const uint32_t i = i0 + lane;
         const bool valid = i < nC;
-        const uint32_t ic = min(i, nC - 1);
-        const uint2 rec = i0 == 0 ? rec0[g] : make_uint2(P.cpos[r0 + ic], P.cval[r0 + ic]);
         const float x = __uint_as_float(rec.y);
         const uint32_t key = fkey(x);
         const bool e = valid && key == T;
@@ -2092,19 +2106,32 @@ DEV void emit_units(const Params& P, uint32_t lu0, uint32_t lu1) {
           store_val<RAW>(P, o, x, mn, scale);
         }
         outc += (uint32_t)__popcll(sb);
+      };
+      row(0, rec0[g]);
+      // rows past the first (preloaded) one: TR rows per load round (see tail_rows)
+      for (uint32_t i0 = 64; i0 < nC; i0 += 64 * TR) {
+        uint2 rb[TR];
+#pragma unroll
+        for (uint32_t b = 0; b < TR; ++b) {
+          const uint32_t ic = min(i0 + b * 64 + lane, nC - 1);
+          if (i0 + b * 64 < nC) rb[b] = make_uint2(P.cpos[r0 + ic], P.cval[r0 + ic]);  // (wave-uniform)
+        }
+#pragma unroll
+        for (uint32_t b = 0; b < TR; ++b)
+          if (i0 + b * 64 < nC) row(i0 + b * 64, rb[b]);
       }
     }
   }
 }
 
-template <bool DELTA, bool RAW, uint32_t UPW>
+template <bool DELTA, bool RAW, uint32_t UPW, uint32_t TR>  // TR: record rows per load round past the first
 __global__ __launch_bounds__(BLOCK) void k_emit(Params P) {
   const uint32_t wv = threadIdx.x >> 6;
   const uint32_t lu0 = (blockIdx.x * WAVES + wv) * UPW;
   if (lu0 >= P.n_lunits) return;
   const bool st = blockIdx.x < P.nseg;  // diagnostics rows: block index (slots 13-14)
   if (st) STAMP(P, blockIdx.x, 13);
-  emit_units<DELTA, RAW, UPW>(P, lu0, min(lu0 + UPW, P.n_lunits));
+  emit_units<DELTA, RAW, UPW, TR>(P, lu0, min(lu0 + UPW, P.n_lunits));
   if (st) STAMP(P, blockIdx.x, 14);
 }
 
@@ -2901,12 +2928,21 @@ void launch_dense_decode(const Params& P, coalac_plan_t plan, hipStream_t st) {
 
 template <bool DELTA, bool RAW>
 void launch_emit(const Params& P, coalac_plan_t plan, hipStream_t st) {
+  const bool hi = plan->rmax > HIGH_RATIO;
   if (plan->n_lunits <= LATENCY_PLAN_UNITS) {
     constexpr uint32_t U = EMIT_UPW_LATENCY * WAVES;
-    hipLaunchKernelGGL((k_emit<DELTA, RAW, EMIT_UPW_LATENCY>), dim3((plan->n_lunits + U - 1) / U), dim3(BLOCK), 0, st, P);
+    const dim3 g((plan->n_lunits + U - 1) / U);
+    if (hi)
+      hipLaunchKernelGGL((k_emit<DELTA, RAW, EMIT_UPW_LATENCY, 4u>), g, dim3(BLOCK), 0, st, P);
+    else
+      hipLaunchKernelGGL((k_emit<DELTA, RAW, EMIT_UPW_LATENCY, 1u>), g, dim3(BLOCK), 0, st, P);
   } else {
     constexpr uint32_t U = EMIT_UPW * WAVES;
-    hipLaunchKernelGGL((k_emit<DELTA, RAW, EMIT_UPW>), dim3((plan->n_lunits + U - 1) / U), dim3(BLOCK), 0, st, P);
+    const dim3 g((plan->n_lunits + U - 1) / U);
+    if (hi)
+      hipLaunchKernelGGL((k_emit<DELTA, RAW, EMIT_UPW, 4u>), g, dim3(BLOCK), 0, st, P);
+    else
+      hipLaunchKernelGGL((k_emit<DELTA, RAW, EMIT_UPW, 1u>), g, dim3(BLOCK), 0, st, P);
   }
 }
 
@@ -3293,7 +3329,7 @@ void launch_decode_lds_n(const Params& P, coalac_plan_t plan, hipStream_t st) {
 
 // plans whose segments keep more than ~1.5 % (more than 64 entries in a unit on average) hold 8 entry chunks in
 // registers (from ratio 0.02: C3 at ratio 0.1, decode 0.63 -> 0.37 ms)
-constexpr double DECODE_NCH_RATIO = 0.02;
+constexpr double DECODE_NCH_RATIO = HIGH_RATIO;
 template <bool RAW, bool HB>
 void launch_decode_lds(const Params& P, coalac_plan_t plan, hipStream_t st) {
   if (plan->rmax > DECODE_NCH_RATIO)
