@@ -133,6 +133,7 @@ constexpr uint32_t GU = GU_UNITS;               // units per select group (k_ghi
 constexpr uint32_t HB2 = 512;             // bins of the per-group band histograms
 constexpr uint32_t GCAP = 256;            // in-window entries a group may hand to k_select
 constexpr uint32_t KEY_MAX = 0x7FFFFFFFu;
+constexpr uint32_t TIE_FLAG = 0x80000000u;  // in a unit's T_lo: the sampled k-th key K is a heavy tie (tie mode, k_scan)
 constexpr int HIST_BINS = 2048;
 constexpr uint32_t UCAP = 2048;           // units per k_select chunk (8.4 M elements)
 constexpr uint32_t NONE = 0xFFFFFFFFu;
@@ -188,7 +189,10 @@ struct Params {
   uint32_t *tstar, *rtie, *status;
   // per large unit
   uint32_t *tlo, *thi, *cntA, *cntC, *gtC, *eqC, *eqpre, *outoff;
-  uint32_t* cntZ;  // per large unit of a segment whose bracket starts at key 0: its zero keys (counted, not recorded)
+  uint32_t* cntZ;  // per large unit of a tie-mode segment (T_lo == 0, or flagged): its keys equal to the tie key K
+                   // (0, or T_lo & KEY_MAX) — counted, not recorded
+  uint32_t* tsgn;  // ... and, for K > 0, the in-unit tie rank of its first positive (bits 0-15) and first negative
+                   // (bits 16-31) tie, 0xFFFF = none (a kept +K / -K tie enters mn / scale; a zero's sign does not)
   uint4* uemit;  // per large unit, from k_select: {T*, tie budget | raw-path flag << 31, mn bits, scale bits}
   uint32_t* cval;  // candidate records, ccap slots per large unit, in index order: the value bits ...
   uint16_t* cpos;  // ... and the position inside the unit (the emit reads both; every select sweep the values only)
@@ -653,17 +657,23 @@ struct Band {
 // ------------------------------------------------------------------------------------------------
 // CHECK: test each element against the unit's length. A full unit never needs it, nor does a partial one when
 // tlo > 0 (its loads past len return 0, key 0 < tlo): k_scan picks the lean form then (wave-uniform).
-// ZERO (the segment's bracket starts at key 0, tlo == 0: its k-th key may be a zero — a frozen or pruned tensor, an
-// all-zero delta): zero keys are COUNTED per unit (cntZ), not recorded; the candidates are the keys in [1, thi] and
-// above. The select then takes the k-th key as 0 with a tie quota over the zeros (index order) when the nonzero keys
-// number fewer than k, and only the units whose zeros that quota reaches re-read their raw data in k_emit — instead
-// of every element becoming a candidate record, every unit overflowing its slots and the whole segment taking the
-// one-block raw-data path.
+// ZERO = tie mode, for a segment whose k-th key may be one heavily repeated key K: K = 0 when the bracket starts at
+// key 0 (tlo == 0: a frozen or pruned tensor, an all-zero delta), or the K the sampler flagged (T_lo = K | TIE_FLAG,
+// T_hi = K: its samples around the k-th rank were all K — a sign-SGD or first-Adam-step delta whose |x| are all equal,
+// values clipped at a bound, a quantised tensor). Keys equal to K are COUNTED per unit (cntZ), not recorded; the
+// candidates are the keys above K (in [K + 1, thi], and above). The select then takes the k-th key as K with a tie
+// quota over the K-keys (index order) when the keys above K number fewer than k, and only the units whose K-keys that
+// quota reaches re-read their raw data in k_emit — instead of every element becoming a candidate record, every unit
+// overflowing its slots and the whole segment taking the one-block raw-data path (one ResNet-50 update of equal-|x|
+// values: 9.0 ms per encode + decode on that path, tools/tie_probe.py). For K > 0 the scan also records the in-unit
+// rank of the first positive and first negative K-key (tsgn): whether +K / -K is among the kept values.
 template <bool DELTA, int NB, bool CHECK = true, bool ZERO = false>
 DEV void scan_unit(const Params& P, uint32_t lu, const UnitDev& L, const uint32_t tlo_, const uint32_t thi,
                    uint2* stage) {
-  const uint32_t tlo = ZERO ? 1u : tlo_;  // (ZERO: tlo_ == 0)
-  uint32_t cz = 0;                        // zero keys this lane saw (ZERO)
+  const uint32_t tk = tlo_ & KEY_MAX;     // (ZERO: the tie key K)
+  const uint32_t tlo = ZERO ? tk + 1u : tlo_;
+  uint32_t cz = 0;                        // K-keys this lane saw (ZERO)
+  uint32_t weq = 0, rp = NONE, rn = NONE;  // (ZERO, K > 0: K-keys of the earlier rows; first +K / -K tie rank)
   constexpr uint32_t IT = UNIT_IT / NB;
   const uint32_t lane = lane_id();
   const uint32_t len = L.len;
@@ -698,8 +708,30 @@ DEV void scan_unit(const Params& P, uint32_t lu, const UnitDev& L, const uint32_
         const uint32_t key = fkey(xs[j]);
         fc[j] = (!CHECK || e0 + j < len) && key >= tlo;
         fa[j] = CHECK ? fc[j] && key > thi : key > thi;  // (thi >= tlo or ZERO: key > thi implies a candidate)
-        if (ZERO) cz += ((!CHECK || e0 + j < len) && key == 0u) ? 1u : 0u;
+        if (ZERO) cz += ((!CHECK || e0 + j < len) && key == tk) ? 1u : 0u;
         any = any || fc[j];
+      }
+      if (ZERO && tk != 0u) {  // (wave-uniform) the in-unit ranks of this row's K-keys: index order is (lane, j)
+        uint64_t tb[4];
+        uint32_t pre = 0;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          tb[j] = __ballot((!CHECK || e0 + j < len) && fkey(xs[j]) == tk);
+          pre += mbcnt(tb[j]);
+        }
+        uint32_t mine = 0;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          if ((tb[j] >> lane) & 1ull) {
+            const uint32_t rank = weq + pre + mine;
+            if (__float_as_uint(xs[j]) >> 31)
+              rn = min(rn, rank);
+            else
+              rp = min(rp, rank);
+            ++mine;
+          }
+        }
+        weq += (uint32_t)(__popcll(tb[0]) + __popcll(tb[1]) + __popcll(tb[2]) + __popcll(tb[3]));
       }
       const uint32_t c = (uint32_t)fc[0] + (uint32_t)fc[1] + (uint32_t)fc[2] + (uint32_t)fc[3];
       const uint64_t b1 = __ballot(any);
@@ -750,11 +782,16 @@ DEV void scan_unit(const Params& P, uint32_t lu, const UnitDev& L, const uint32_
   if (ZERO) {
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) cz += (uint32_t)__shfl_xor((int)cz, o, 64);
+    if (tk != 0u) {
+      rp = wave_min_u32(rp);
+      rn = wave_min_u32(rn);
+    }
   }
   if (lane == 0) {
     P.cntA[lu] = cA;
     P.cntC[lu] = cC;
     if (ZERO) P.cntZ[lu] = cz;
+    if (ZERO && tk != 0u) P.tsgn[lu] = min(rp, 0xFFFFu) | (min(rn, 0xFFFFu) << 16);
   }
 }
 
@@ -802,9 +839,11 @@ DEV uint32_t hist_pick(const uint32_t* hist, uint32_t& r, uint32_t* sh) {
 }
 
 // hist_pick for two ranks at once (r1, r2; 0 = not wanted): ONE block scan of the bins instead of two.
-// Returns the bins in b1 / b2 (NONE when not wanted). sh needs >= 64 words (slots 40-43).
+// Returns the bins in b1 / b2 (NONE when not wanted) and the ranks inside them in q1 / q2. sh needs >= 64 words
+// (slots 40-43).
 template <int NT, int NB = HIST_BINS>
-DEV void hist_pick2(const uint32_t* hist, uint32_t r1, uint32_t r2, uint32_t& b1, uint32_t& b2, uint32_t* sh) {
+DEV void hist_pick2(const uint32_t* hist, uint32_t r1, uint32_t r2, uint32_t& b1, uint32_t& b2, uint32_t& q1,
+                    uint32_t& q2, uint32_t* sh) {
   constexpr int BPT = NB / NT;
   const uint32_t t = threadIdx.x;
   uint32_t c[BPT];
@@ -820,6 +859,8 @@ DEV void hist_pick2(const uint32_t* hist, uint32_t r1, uint32_t r2, uint32_t& b1
   if (t == 0) {
     sh[40] = NONE;
     sh[41] = NONE;
+    sh[42] = 0u;
+    sh[43] = 0u;
   }
   __syncthreads();
   const uint32_t rr[2] = {r1, r2};
@@ -838,11 +879,14 @@ DEV void hist_pick2(const uint32_t* hist, uint32_t r1, uint32_t r2, uint32_t& b1
         acc += c[j];
       }
       sh[40 + q] = (uint32_t)b;
+      sh[42 + q] = r - acc;
     }
   }
   __syncthreads();
   b1 = sh[40];
   b2 = sh[41];
+  q1 = sh[42];
+  q2 = sh[43];
   __syncthreads();
 }
 
@@ -1033,16 +1077,72 @@ DEV void sample_segment(const Params& P, uint32_t li, uint32_t* hist, uint32_t* 
   }
   __syncthreads();
   uint32_t tlo = 0u, thi = KEY_MAX;
-  uint32_t blo = 0, bhi = 0;  // both bracket bins from one scan of the histogram
-  hist_pick2<NT>(hist, rlo < (double)m ? (uint32_t)rlo : 0u, rhi >= 1.0 ? (uint32_t)rhi : 0u, blo, bhi, sh);
+  uint32_t blo = 0, bhi = 0, qlo = 0, qhi = 0;  // both bracket bins (and ranks inside) from one scan of the histogram
+  // (a sample too small for an upper margin, rhi < 1, leaves T_hi open; the top sample's bin is still picked, for the
+  // tie test below)
+  hist_pick2<NT>(hist, rlo < (double)m ? (uint32_t)rlo : 0u, rhi >= 1.0 ? (uint32_t)rhi : 1u, blo, bhi, qlo, qhi, sh);
   if (rlo < (double)m) tlo = kmin + (blo << shift);
   if (rhi >= 1.0) {
     const uint64_t edge = (uint64_t)kmin + (((uint64_t)bhi + 1) << shift) - 1;
     thi = (uint32_t)min<uint64_t>(edge, kmax);
   }
+  bool tie = false;
+  const uint32_t mw = rlo < (double)m ? (uint32_t)rlo - (rhi >= 1.0 ? (uint32_t)rhi : 1u) : 0u;  // margin width (ranks)
+  if (rlo < (double)m && (blo == bhi || hist[blo] >= mw)) {
+    // The sampled keys are concentrated where the bracket lies: both bracket ranks in ONE bin, or the lower rank's bin
+    // holding at least the margin's width of samples (continuous data spreads the margin's ~120 ranks over several
+    // bins, each holding a few). Refine inside the bin, 11 bits per pass: while the two ranks share a sub-bin (or for
+    // the lower rank alone), down to single keys. Two ranks that part: the bracket is their sub-bins' outward edges.
+    // Otherwise the lower rank's key K is exact, and a K repeated in the sample (the margin's quarter, >= 8 samples)
+    // is a heavy tie: tie mode (T_lo = K | TIE_FLAG; both ranks on K: T_hi = K too). A K seen fewer times is the
+    // lower edge itself.
+    const bool two = blo == bhi;
+    uint32_t base = kmin + (blo << shift), cK = hist[blo];
+    int sft = shift;
+    bool split = false;
+    __syncthreads();  // (every thread has read hist[blo] before the first refinement clears it)
+    while (sft > 0) {
+      const int ns = sft > 11 ? sft - 11 : 0;
+      const uint32_t top = base + ((1u << sft) - 1u);  // (no wrap: the bin lies inside [kmin, kmax + 2^shift))
+      for (uint32_t i = t; i < HIST_BINS; i += NT) hist[i] = 0;
+      __syncthreads();
+#pragma unroll
+      for (uint32_t it = 0; it < MAXIT; ++it) {
+        if ((okm >> it) & 1u) {
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            if (kk[it][j] >= base && kk[it][j] <= top) atomicAdd(&hist[(kk[it][j] - base) >> ns], 1u);
+        }
+      }
+      __syncthreads();
+      uint32_t b1, b2;
+      hist_pick2<NT>(hist, qlo, two ? qhi : 0u, b1, b2, qlo, qhi, sh);
+      if (two && b1 != b2) {
+        tlo = base + (b1 << ns);
+        if (rhi >= 1.0) thi = min<uint64_t>((uint64_t)base + (((uint64_t)b2 + 1) << ns) - 1, kmax);
+        split = true;
+        break;
+      }
+      cK = hist[b1];
+      __syncthreads();
+      base += b1 << ns;
+      sft = ns;
+    }
+    if (!split) {
+      if (base != 0u && (two || cK >= max(8u, mw / 4u))) {
+        tie = true;
+        tlo = base | TIE_FLAG;
+        if (two) thi = base;
+      } else {
+        tlo = base;  // (base 0: the plain tlo == 0 bracket, tie mode at key 0 already)
+        if (two && rhi >= 1.0) thi = base;
+      }
+    }
+  }
   STAMP(P, li, 18);
   const uint32_t nu = sd.unit_end - sd.unit_begin;
-  const uint32_t hh = max(tlo, min(thi, kmax));  // the band histograms' upper bound (see below)
+  // the band histograms' upper bound (see below)
+  const uint32_t hh = tie ? max(tlo & KEY_MAX, min(thi, kmax)) : max(tlo, min(thi, kmax));
   for (uint32_t i = t; i < nu; i += NT) {
     P.tlo[sd.lu_begin + i] = tlo;
     P.thi[sd.lu_begin + i] = thi;
@@ -1106,8 +1206,8 @@ __global__ __launch_bounds__(NTS, WPE) void k_scan(Params P) {
   const UnitDev L = P.lunits[lu];
   // delta: 4 load batches (32 float4 in flight spill)
   const uint32_t tlo = P.tlo[lu], thi = P.thi[lu];
-  if (tlo == 0) {  // (wave-uniform: one bracket per segment)
-    if (L.len == UNIT)
+  if (tlo == 0 || (tlo & TIE_FLAG)) {  // tie mode (wave-uniform: one bracket per segment)
+    if (L.len == UNIT || tlo != 0)  // (K > 0: a partial unit's loads past len read key 0 < K + 1, never counted)
       scan_unit<DELTA, DELTA ? 4 : NB, false, true>(P, lu, L, tlo, thi, stage + wv * STAGE_CAP);
     else
       scan_unit<DELTA, DELTA ? 4 : NB, true, true>(P, lu, L, tlo, thi, stage + wv * STAGE_CAP);
@@ -1406,7 +1506,7 @@ DEV void group_hist(const Params& P, uint32_t gi, uint32_t* hist, uint32_t* upre
   STAMP(P, G.x, 20);
   // one load round for everything that depends on G only: the band, and every unit's count and first
   // records (the histogram needs no index order, so no count prefix before the record loads)
-  const uint32_t tlo = P.tlo[G.y], thi = P.thi[G.y], hh = P.shhi[G.x];
+  const uint32_t tlo = P.tlo[G.y] & KEY_MAX, thi = P.thi[G.y], hh = P.shhi[G.x];  // (tie mode K: band [K, K], empty)
   GroupSweep<NT, SPEC> sw;
   for (uint32_t i = t; i < HB2; i += NT) hist[i] = 0;
   sw.load(P, G.y, G.z, upre, sh);
@@ -1440,7 +1540,7 @@ __global__ __launch_bounds__(NT) void k_ghist(Params P) {
 // block of the segment computes it (identically) at the start of k_gwin — cheaper than a launch of its
 // own between k_ghist and k_gwin. Returned to every thread.
 template <int NT = BLOCK>
-DEV uint4 segment_pick(const Params& P, const SegDev& sd, const Band& band, uint32_t* hist, uint32_t* sh) {
+DEV uint4 segment_pick(const Params& P, const SegDev& sd, const Band& band, bool tieseg, uint32_t* hist, uint32_t* sh) {
   const uint32_t t = threadIdx.x;
   const uint32_t lb = sd.lu_begin, nu = sd.unit_end - sd.unit_begin, k = sd.k;
   const uint32_t g0 = sd.g_begin, ng = (nu + GU - 1) / GU;
@@ -1449,7 +1549,7 @@ DEV uint4 segment_pick(const Params& P, const SegDev& sd, const Band& band, uint
   static_assert(HB2 == 2 * NT || HB2 == NT, "one or two histogram bins per thread");
   constexpr bool TWO = HB2 == 2 * NT;
   constexpr uint32_t GB = 24, CB = 3;
-  const bool zseg = band.tlo == 0;  // the scan counted this segment's zero keys (cntZ)
+  const bool zseg = tieseg;  // the scan counted this segment's keys equal to its tie key (cntZ; tie mode)
   uint32_t h0 = 0, h1 = 0, sa = 0, sc = 0, ov = 0, sz = 0;
   {
     uint32_t v0[GB], v1[GB], ca[CB], cc[CB], cz[CB];
@@ -1510,7 +1610,7 @@ DEV uint4 segment_pick(const Params& P, const SegDev& sd, const Band& band, uint
   if (zseg) sz = block_sum<NT>(sz, sh);
   // (a unit that overflowed its record slots sends the segment to the raw-data path in segment_select)
   const bool forced = (P.flags & (COALAC_FLAG_FORCE_EXACT | COALAC_FLAG_GENERIC_SELECT)) || nu > UCAP || ov != 0;
-  // the k-th key is a zero: every recorded key (all nonzero) is kept, and the first k - sc zeros by index. The
+  // the k-th key is the tie key K: every recorded key (all above K) is kept, and the first k - sc K-keys by index. The
   // window [1, 0] is empty: k_gwin counts every record as above it (per-unit kept counts) and takes their min / max
   if (!forced && zseg && sc < k && k - sc <= sz) return make_uint4(1u, 0u, k - sc, 2u);
   const bool generic = forced || !(sa < k && k <= sc);
@@ -1608,7 +1708,7 @@ DEV void group_pick_window(const Params& P, uint32_t gi, GwinSmemT<NT / 64>& W, 
   const uint32_t tlo = P.tlo[G.y], thi = P.thi[G.y], hh = P.shhi[G.x];
   GroupSweep<NT, SPEC> sw;
   sw.load(P, G.y, G.z, W.upre, sh);
-  const uint4 st = segment_pick<NT>(P, sd, Band(tlo, thi, hh), hist, sh);
+  const uint4 st = segment_pick<NT>(P, sd, Band(tlo & KEY_MAX, thi, hh), tlo == 0 || (tlo & TIE_FLAG), hist, sh);
   STAMP(P, G.x, 23);
   if (st.w == 0 || st.w == 2) group_window<NT>(P, gi, G, st, GS.x, sw, W, sh);
   if (threadIdx.x == 0 && G.y == GS.x) {  // the segment's first group
@@ -1833,20 +1933,48 @@ DEV void segment_select(const Params& P, uint32_t li, SelSmem& S) {
   STAMP(P, li, 0);
   uint32_t T, rt, fp_rank, fn_rank;
   float gmn, gmx;
-  const bool zero_tie = st.w == 2;  // the k-th key is a zero (segment_pick)
+  const bool zero_tie = st.w == 2;  // the k-th key is the segment's tie key K (segment_pick; tie mode)
   bool done;
   if (zero_tie) {
-    // every record kept (k_gwin's per-unit counts above the empty window), the first rt zeros by index; a zero's
-    // sign does not matter to mn / scale (canonicalised + 0.0f below), so one "positive tie" stands for them
+    // every record kept (k_gwin's per-unit counts above the empty window), the first rt K-keys by index. K = 0: a
+    // zero's sign does not matter to mn / scale (canonicalised + 0.0f below), so one "positive tie" stands for them;
+    // K > 0: the segment-wide ranks of the first +K and -K ties from the units' tie prefixes and in-unit ranks (tsgn)
     const uint32_t g0 = sd.g_begin, ng = (nu + GU - 1) / GU;  // ng <= UCAP / GU <= NT
+    const uint32_t tk = P.tlo[lb] & KEY_MAX;
     gmn = t < ng ? P.gmm[2 * (g0 + t)] : qnan();
     gmx = t < ng ? P.gmm[2 * (g0 + t) + 1] : qnan();
     for (uint32_t i = t; i < nu; i += NT) S.ge[i] = P.gtC[lb + i] | (P.cntZ[lb + i] << 16);
     __syncthreads();
-    T = 0u;
+    T = tk;
     rt = st.z;
     fp_rank = rt > 0 ? 0u : NONE;
     fn_rank = NONE;
+    if (tk != 0u) {  // (block-uniform)
+      uint32_t lp = NONE, ln = NONE, carry = 0;
+      for (uint32_t c0 = 0; c0 < nu; c0 += NT) {
+        const uint32_t i = c0 + t;
+        const uint32_t z = i < nu ? S.ge[i] >> 16 : 0u;
+        uint32_t tot;
+        const uint32_t ex = block_excl_scan<NT>(z, S.sh, tot) + carry;
+        carry += tot;
+        if (i < nu) {
+          const uint32_t sg = P.tsgn[lb + i], fp = sg & 0xFFFFu, fn = sg >> 16;
+          if (fp != 0xFFFFu) lp = min(lp, ex + fp);
+          if (fn != 0xFFFFu) ln = min(ln, ex + fn);
+        }
+      }
+      if (t == 0) {
+        S.sh[42] = NONE;
+        S.sh[43] = NONE;
+      }
+      __syncthreads();
+      if (lp != NONE) atomicMin(&S.sh[42], lp);
+      if (ln != NONE) atomicMin(&S.sh[43], ln);
+      __syncthreads();
+      fp_rank = S.sh[42];
+      fn_rank = S.sh[43];
+      __syncthreads();
+    }
     done = true;
   } else {
     done = st.w == 0 && select_from_groups<NT>(P, sd, lb, nu, st, S, T, rt, fp_rank, fn_rank, gmn, gmx);
@@ -1868,7 +1996,7 @@ DEV void segment_select(const Params& P, uint32_t li, SelSmem& S) {
   __syncthreads();
   for (int i = 0; i < NW; ++i) mc = max(mc, S.wcnt[i]);
   __syncthreads();
-  const uint32_t tlo = P.tlo[lb], thi = P.thi[lb];
+  const uint32_t tlo = P.tlo[lb] & KEY_MAX, thi = P.thi[lb];  // (tie mode K: records are the keys above K)
 
   if ((P.flags & COALAC_FLAG_FORCE_EXACT) || !(sa <= k && k <= sc) || mc > P.ccap) {
     // raw-data path (rare): the exact k-th key of the whole segment, per-unit counts from the raw data;
@@ -2761,7 +2889,7 @@ size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 struct WsLayout {
   size_t status;
   size_t tstar, rtie;
-  size_t tlo, thi, cntA, cntC, cntZ, gtC, eqC, eqpre, outoff, uemit;
+  size_t tlo, thi, cntA, cntC, cntZ, tsgn, gtC, eqC, eqpre, outoff, uemit;
   size_t cval, cpos, stamps, ghist, gcnt, glist, gmm, sstate, shhi;
   size_t umm;  // dense plans: per-unit min / max
   size_t total;
@@ -2791,6 +2919,7 @@ WsLayout ws_layout(size_t S, size_t LU, size_t NG, size_t NL, uint32_t CC) {
   L.cntA = take(4 * LU);
   L.cntC = take(4 * LU);
   L.cntZ = take(4 * LU);
+  L.tsgn = take(4 * LU);
   L.gtC = take(4 * LU);
   L.eqC = take(4 * LU);
   L.eqpre = take(4 * LU);
@@ -3256,6 +3385,7 @@ int encode_impl(coalac_plan_t plan, const float* d_in, const float* const* d_inp
   P.cntA = reinterpret_cast<uint32_t*>(w + L.cntA);
   P.cntC = reinterpret_cast<uint32_t*>(w + L.cntC);
   P.cntZ = reinterpret_cast<uint32_t*>(w + L.cntZ);
+  P.tsgn = reinterpret_cast<uint32_t*>(w + L.tsgn);
   P.gtC = reinterpret_cast<uint32_t*>(w + L.gtC);
   P.eqC = reinterpret_cast<uint32_t*>(w + L.eqC);
   P.eqpre = reinterpret_cast<uint32_t*>(w + L.eqpre);

@@ -368,6 +368,76 @@ def test_sparse_segments_zero_tie_path(cuda, nnz_frac, bits):
     assert g["fallbacks"] == 0
 
 
+def tie_segments(rng, sizes, case):
+    """Segments whose k-th key (ratio 0.01 and 0.1) is one heavily repeated NONZERO key K."""
+    xs = []
+    c = np.float32(1e-3)
+    for n in sizes:
+        sgn = np.where(rng.random(n) < 0.5, -c, c).astype(np.float32)
+        g = (rng.standard_normal(n) * 1e-3).astype(np.float32)
+        if case == "sign":  # sign-SGD / first Adam step: every |x| equal
+            x = sgn
+        elif case == "clipped":  # value clipping at 1.5 sigma: ~13 % of the elements at +-clip
+            x = np.clip(g, -1.5e-3, 1.5e-3).astype(np.float32)
+        elif case == "outliers":  # 0.3 % larger values above a sea of equal |x| (the quota takes the first K-keys)
+            x = sgn.copy()
+            m = max(1, int(0.003 * n))
+            pos = rng.choice(n, m, replace=False)
+            x[pos] = (np.sign(rng.standard_normal(m)) * (2e-3 + np.abs(rng.standard_normal(m)) * 1e-3)).astype(np.float32)
+        elif case == "half_zero":  # +-0 and equal |x| half each
+            x = np.where(rng.random(n) < 0.5, np.float32(0.0), sgn).astype(np.float32)
+            x[rng.random(n) < 0.25] = np.float32(-0.0)
+        else:  # "grid": a 5-level quantised tensor (values in {0, +-c, +-2c}), the k-th key inside the top level
+            x = (np.clip(np.round(g / 7e-4), -2, 2) * c).astype(np.float32)
+        xs.append(x)
+    return xs
+
+
+@pytest.mark.parametrize("case", ["sign", "clipped", "outliers", "half_zero", "grid"])
+@pytest.mark.parametrize("clients", [1, 2])
+def test_heavy_ties_take_the_tie_path(cuda, case, clients):
+    """A segment whose sampled keys around the k-th rank are all one key K > 0 (sign-like deltas, clipped values,
+    quantised tensors) is encoded in tie mode: its K-keys counted per unit, not recorded, the k-th key K with a tie
+    quota in index order, the first +K / -K kept ties in mn / scale (round 4: every unit overflowed its record slots and
+    the segment took the one-block raw-data path, ~100x slower). ResNet-50: a latency-bound plan (1 client) and a batch
+    plan (2 clients); ratios 0.01 and 0.1: bit-exact, no raw-path fallback."""
+    rng = np.random.default_rng(sum(map(ord, case)) + clients)
+    sizes = fp32_sizes("resnet50_tv")
+    xs = [tie_segments(rng, sizes, case) for _ in range(clients)]
+    for ratio in ((0.01, 0.1) if clients == 1 else (0.01,)):
+        plan, g, r = run_both(sizes, ratio, 8, xs, clients=clients)
+        assert_same(plan, g, r)
+        assert g["fallbacks"] == 0, (case, ratio)
+
+
+@pytest.mark.parametrize("bits", [1, 32])
+def test_tie_mode_bits_and_delta(cuda, bits):
+    """Tie mode at 1-bit codes and raw fp32 values, in delta mode: base = multiples of 2^-10, x = base +- 2^-10
+    (exact in fp32, so every x - base is +-2^-10): bit-exact."""
+    rng = np.random.default_rng(40 + bits)
+    sizes = [4096 * 300 + 17, 250000, 1 << 20]
+    q = np.float32(2.0 ** -10)
+    bases = [[(rng.integers(-1000, 1000, n) * q).astype(np.float32) for n in sizes]]
+    xs = [[(b + np.where(rng.random(b.size) < 0.5, -q, q)).astype(np.float32) for b in bases[0]]]
+    plan, g, r = run_both(sizes, 0.01, bits, xs, bases)
+    assert_same(plan, g, r)
+
+
+def test_tie_mode_sample_miss_takes_raw_path(cuda):
+    """Tie mode is the sampler's call: equal |x| everywhere it looks, but 2 % larger values where it does not look
+    put the k-th key above K (the records then hold more than k keys). The segment falls back to the raw-data path:
+    one fallback, bit-exact."""
+    n = 1 << 20
+    rng = np.random.default_rng(9)
+    x = np.where(rng.random(n) < 0.5, np.float32(-1e-3), np.float32(1e-3)).astype(np.float32)
+    unseen = np.flatnonzero(~sampled_positions(n, 0))
+    big = rng.choice(unseen, size=int(0.02 * n), replace=False)
+    x[big] = (rng.standard_normal(big.size) * 1e-2).astype(np.float32)
+    plan, g, r = run_both([n], 0.01, 8, [[x]])
+    assert g["fallbacks"] == 1
+    assert_same(plan, g, r)
+
+
 @pytest.mark.parametrize("with_idx", [False, True])
 @pytest.mark.parametrize("delta", [False, True])
 @pytest.mark.parametrize("bits", [1, 8, 32])
