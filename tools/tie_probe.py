@@ -1,6 +1,7 @@
 """Encode + decode time of one ResNet-50 update (ratio 0.01, 8 bits) for value distributions with heavy ties at a
 NONZERO key — the raw-data path's territory: the §8(d) Gaussian, every |x| equal with random signs (a sign-SGD /
-first-Adam-step delta), and a Gaussian clipped at 1.5 sigma (value clipping: ~13 % of the elements at +-clip).
+first-Adam-step delta), a Gaussian clipped at 1.5 sigma (value clipping: ~13 % of the elements at +-clip), and the
+first-step delta in delta mode, where fp32 rounding of w -+ lr spreads the equal deltas over a few thousand ulps.
 Prints ms per encode+decode (median of 20) and the plan's fallback count.
 
     python tools/tie_probe.py
@@ -26,17 +27,23 @@ def main():
         "sign (all |x| equal)": torch.where(torch.rand(flat.numel(), generator=g, device=dev) < 0.5, -1e-3, 1e-3),
         "clipped at 1.5 sigma": gauss.clamp(-1.5e-3, 1.5e-3),
     }
+    # delta mode: trained = fl(w - lr * sign), so x - w is lr only up to the rounding of w - lr (the deltas cluster
+    # within a few thousand ulps of lr instead of tying exactly)
+    w = torch.randn(flat.numel(), generator=g, device=dev) * 0.05
+    adam = (w - torch.where(torch.rand(flat.numel(), generator=g, device=dev) < 0.5, -1e-3, 1e-3)).float()
     ws = plan.empty_workspace()
     enc = plan.empty_encoded()
     out = plan.empty_flat()
+    cases["first-step delta (fl(w -+ lr) - w)"] = adam
     for name, x in cases.items():
+        base = w if name.startswith("first-step") else None
         flat.copy_(x)
         ts = []
         for i in range(25):
             torch.cuda.synchronize()
             t0 = time.perf_counter()
-            plan.encode(flat, out=enc, workspace=ws)
-            plan.decode(enc, out=out)
+            plan.encode(flat, base=base, out=enc, workspace=ws)
+            plan.decode(enc, base=base, out=out)
             torch.cuda.synchronize()
             ts.append(time.perf_counter() - t0)
         fb = plan.fallbacks(ws)
