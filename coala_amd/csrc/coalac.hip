@@ -1247,10 +1247,10 @@ constexpr uint32_t TAIL_ROWS = 4;
 // ratio 0.1: 0.922 vs 0.982 ms with it, profiles/r05_ab.txt)
 constexpr double HIGH_RATIO = 0.02;
 template <class F>
-DEV void tail_rows(const uint32_t* R, uint32_t n, uint32_t u, F&& f) {
+DEV void tail_rows(const uint32_t* R, uint32_t n, uint32_t u, F&& f, uint32_t from = 128) {
   constexpr uint32_t TR = TAIL_ROWS;
   const uint32_t lane = lane_id();
-  for (uint32_t i0 = 128; i0 < n; i0 += 64 * TR) {
+  for (uint32_t i0 = from; i0 < n; i0 += 64 * TR) {
     uint32_t x[TR];
 #pragma unroll
     for (uint32_t b = 0; b < TR; ++b)
@@ -1266,7 +1266,10 @@ DEV void tail_rows(const uint32_t* R, uint32_t n, uint32_t u, F&& f) {
 // reads one unit at a time from its contiguous region (coalesced, trivial addressing, the unit is
 // wave-uniform so per-unit counts are ballot popcounts), G units per batch with 2 records per lane per
 // unit in flight. f(x, valid, u) is called by ALL lanes (ballots allowed); fend(u) after each unit.
-template <int NW, int G, class F, class FE>
+// RM: record rows per unit in the batch's load round (2; 8 in batch plans above HIGH_RATIO, where a unit holds ~450
+// records: all of them in that one round instead of 1 + 2 rounds per unit — C3 at ratio 0.1: 0.908-0.920 vs
+// 0.925-0.927 ms; the sweeps there are bound by the HBM traffic the other sub-batch's streams leave them)
+template <int NW, int G, int RM = 2, class F, class FE>
 DEV void unit_sweep(const uint32_t* cand, uint32_t stride, uint32_t lu0, const uint32_t* upre, uint32_t cn,
                     uint32_t total, F&& f, FE&& fend) {
   const uint32_t lane = lane_id(), w = threadIdx.x >> 6;
@@ -1285,7 +1288,7 @@ DEV void unit_sweep(const uint32_t* cand, uint32_t stride, uint32_t lu0, const u
   const uint32_t U0 = w == 0 ? 0u : lower(J0);
   const uint32_t U1 = w == NW - 1 ? cn : lower(J1);
   for (uint32_t u = U0; u < U1; u += G) {
-    uint32_t x0[G], x1[G], nn[G];
+    uint32_t x[G][RM], nn[G];
 #pragma unroll
     for (int g = 0; g < G; ++g) {
       const uint32_t uu = min(u + g, U1 - 1);
@@ -1293,16 +1296,19 @@ DEV void unit_sweep(const uint32_t* cand, uint32_t stride, uint32_t lu0, const u
       const uint32_t last = n ? n - 1 : 0u;  // region slot 0 always exists; read it when n == 0
       const uint32_t* R = cand + (uint64_t)(lu0 + uu) * stride;
       nn[g] = n;
-      x0[g] = R[min(lane, last)];
-      x1[g] = R[min(lane + 64, last)];
+#pragma unroll
+      for (int r = 0; r < RM; ++r)
+        if (r < 2 || 64u * r < n) x[g][r] = R[min(lane + 64u * r, last)];  // (rows past 2: wave-uniform guard)
     }
 #pragma unroll
     for (int g = 0; g < G; ++g) {
       if (u + g < U1) {
         const uint32_t uu = u + g, n = nn[g];
-        f(__uint_as_float(x0[g]), lane < n, uu);
-        if (n > 64) f(__uint_as_float(x1[g]), lane + 64 < n, uu);
-        if (n > 128) tail_rows(cand + (uint64_t)(lu0 + uu) * stride, n, uu, f);
+        f(__uint_as_float(x[g][0]), lane < n, uu);
+#pragma unroll
+        for (int r = 1; r < RM; ++r)
+          if (n > 64u * r) f(__uint_as_float(x[g][r]), lane + 64u * r < n, uu);
+        if (n > 64u * RM) tail_rows(cand + (uint64_t)(lu0 + uu) * stride, n, uu, f, 64u * RM);
         fend(uu);
       }
     }
@@ -1325,7 +1331,7 @@ DEV uint32_t reg_prefix(uint32_t c, uint32_t cn, uint32_t* upre, uint32_t* sh) {
 // A group's records swept by the block's waves balanced by record count (unit_sweep): the counts and a block
 // prefix come first, then the record loads — batch plans, where the select kernels run beside the other
 // sub-batch's streaming waves (the speculative sweep below measured slower there: C3 0.617-0.636 vs 0.600-0.604 ms)
-template <int NT>
+template <int NT, int G = GSWEEP, int RM = 2>
 struct BalancedSweep {
   uint32_t* upre;
   uint32_t total, cn;
@@ -1337,7 +1343,7 @@ struct BalancedSweep {
   }
   template <class F, class FE>
   DEV void run(const Params& P, uint32_t lu0, F&& f, FE&& fend) const {
-    unit_sweep<NT / 64, GSWEEP>(P.cval, P.ccap, lu0, upre, cn, total, f, fend);
+    unit_sweep<NT / 64, G, RM>(P.cval, P.ccap, lu0, upre, cn, total, f, fend);
   }
 };
 
@@ -1496,10 +1502,11 @@ DEV void select_generic(const Params& P, uint32_t lb, uint32_t nu, uint32_t tlo,
 // k_ghist: the group's HB2-bin histogram of the band keys [tlo, thi] -> ghist[group]. (A fused variant in
 // which the segment's last-arriving group block ran segment_pick needed an agent-scope release fence in
 // every block — an L2 writeback on gfx950 — and was ~100x slower; kernel boundaries are cheaper.)
-template <int NT, bool SPEC>
-using GroupSweep = std::conditional_t<SPEC, SpecSweep<(GU + NT / 64 - 1) / (NT / 64)>, BalancedSweep<NT>>;
+template <int NT, bool SPEC, bool HR = false>
+using GroupSweep = std::conditional_t<SPEC, SpecSweep<(GU + NT / 64 - 1) / (NT / 64)>,
+                                      std::conditional_t<HR, BalancedSweep<NT, 2, 8>, BalancedSweep<NT>>>;
 
-template <int NT, bool SPEC>
+template <int NT, bool SPEC, bool HR>
 DEV void group_hist(const Params& P, uint32_t gi, uint32_t* hist, uint32_t* upre, uint32_t* sh) {
   const uint4 G = P.groups[gi];  // x: large-segment index, y: first large unit, z: units, w: segment
   const uint32_t t = threadIdx.x;
@@ -1507,7 +1514,7 @@ DEV void group_hist(const Params& P, uint32_t gi, uint32_t* hist, uint32_t* upre
   // one load round for everything that depends on G only: the band, and every unit's count and first
   // records (the histogram needs no index order, so no count prefix before the record loads)
   const uint32_t tlo = P.tlo[G.y] & KEY_MAX, thi = P.thi[G.y], hh = P.shhi[G.x];  // (tie mode K: band [K, K], empty)
-  GroupSweep<NT, SPEC> sw;
+  GroupSweep<NT, SPEC, HR> sw;
   for (uint32_t i = t; i < HB2; i += NT) hist[i] = 0;
   sw.load(P, G.y, G.z, upre, sh);
   __syncthreads();
@@ -1526,12 +1533,12 @@ DEV void group_hist(const Params& P, uint32_t gi, uint32_t* hist, uint32_t* upre
 
 // NT: 256 threads in batches, GHIST_NT_LAT in latency-bound plans (nothing streams beside the block); SPEC: the
 // speculative group sweep (latency-bound plans)
-template <int NT, bool SPEC>
+template <int NT, bool SPEC, bool HR = false>  // HR: batch plans above HIGH_RATIO (8 record rows per unit per round)
 __global__ __launch_bounds__(NT) void k_ghist(Params P) {
   __shared__ uint32_t hist[HB2];
   __shared__ uint32_t upre[GU + 1];
   __shared__ uint32_t sh[64];
-  group_hist<NT, SPEC>(P, blockIdx.x, hist, upre, sh);
+  group_hist<NT, SPEC, HR>(P, blockIdx.x, hist, upre, sh);
 }
 
 // segment_pick: per large segment — validate the sampled bracket, sum the group histograms, pick the bin of
@@ -1692,7 +1699,7 @@ DEV void group_window(const Params& P, uint32_t gi, const uint4 G, const uint4 s
   }
 }
 
-template <int NT, bool SPEC>
+template <int NT, bool SPEC, bool HR>
 DEV void group_pick_window(const Params& P, uint32_t gi, GwinSmemT<NT / 64>& W, uint32_t* hist, uint32_t* sh) {
   // round 1: the group and its segment's geometry (gseg: {first large unit, units, k, first group}, so nothing
   // waits for a segment-table lookup); round 2: the band, the group's unit counts and first records
@@ -1706,7 +1713,7 @@ DEV void group_pick_window(const Params& P, uint32_t gi, GwinSmemT<NT / 64>& W, 
   sd.k = GS.z;
   sd.g_begin = GS.w;
   const uint32_t tlo = P.tlo[G.y], thi = P.thi[G.y], hh = P.shhi[G.x];
-  GroupSweep<NT, SPEC> sw;
+  GroupSweep<NT, SPEC, HR> sw;
   sw.load(P, G.y, G.z, W.upre, sh);
   const uint4 st = segment_pick<NT>(P, sd, Band(tlo & KEY_MAX, thi, hh), tlo == 0 || (tlo & TIE_FLAG), hist, sh);
   STAMP(P, G.x, 23);
@@ -1720,12 +1727,12 @@ DEV void group_pick_window(const Params& P, uint32_t gi, GwinSmemT<NT / 64>& W, 
 }
 
 // NT: 256 threads in batches, GWIN_NT_LAT in latency-bound plans (nothing streams beside the block)
-template <int NT, bool SPEC>
+template <int NT, bool SPEC, bool HR = false>  // HR: as k_ghist
 __global__ __launch_bounds__(NT) void k_gwin(Params P) {
   __shared__ GwinSmemT<NT / 64> W;
   __shared__ uint32_t hist[HB2];
   __shared__ uint32_t sh[64];
-  group_pick_window<NT, SPEC>(P, blockIdx.x, W, hist, sh);
+  group_pick_window<NT, SPEC, HR>(P, blockIdx.x, W, hist, sh);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -3126,13 +3133,17 @@ int launch_encode(const Params& P, coalac_plan_t plan, hipStream_t st, const Mar
   }
   MARK(2);
   if (plan->n_large) {
-    const bool lat = plan->n_lunits <= LATENCY_PLAN_UNITS;
+    const bool lat = plan->n_lunits <= LATENCY_PLAN_UNITS, hr = plan->rmax > HIGH_RATIO;
     if (lat)
       hipLaunchKernelGGL((k_ghist<GHIST_NT_LAT, true>), dim3(plan->n_groups), dim3(GHIST_NT_LAT), 0, st, P);
+    else if (hr)
+      hipLaunchKernelGGL((k_ghist<BLOCK, false, true>), dim3(plan->n_groups), dim3(BLOCK), 0, st, P);
     else
       hipLaunchKernelGGL((k_ghist<BLOCK, false>), dim3(plan->n_groups), dim3(BLOCK), 0, st, P);
     if (lat)
       hipLaunchKernelGGL((k_gwin<GWIN_NT_LAT, true>), dim3(plan->n_groups), dim3(GWIN_NT_LAT), 0, st, P);
+    else if (hr)
+      hipLaunchKernelGGL((k_gwin<BLOCK, false, true>), dim3(plan->n_groups), dim3(BLOCK), 0, st, P);
     else
       hipLaunchKernelGGL((k_gwin<BLOCK, false>), dim3(plan->n_groups), dim3(BLOCK), 0, st, P);
     if (lat)
