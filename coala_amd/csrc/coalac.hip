@@ -80,55 +80,29 @@ constexpr uint32_t SMALL_MAX_LATENCY = 1024;  // ... in latency-bound plans (<= 
                                               // 4096: 14 us, alone on a CU) and the slowest small segment set
                                               // the length of k_presel; bigger segments take the sampled path
 constexpr uint32_t LATENCY_PLAN_UNITS = 8192;  // ~1.3 ResNet-50 updates
-#ifndef SAMPLE_KEYS
-#define SAMPLE_KEYS 8192u
-#endif
+constexpr uint32_t SAMPLE_KEYS = 8192u;
 constexpr uint32_t SAMPLE_MAX = SAMPLE_KEYS;  // sampled keys per large segment
 constexpr int SEL_NT = 256;               // threads of a k_select block in batches (4 waves: one per SIMD, so
                                           // a block finds room beside a streaming kernel's waves)
-#ifndef GWIN_NT_LAT
-#define GWIN_NT_LAT 512  // k_gwin block in latency-bound plans (256 or 512: one or two histogram bins per thread)
-#endif
-#ifndef GHIST_NT_LAT
-#define GHIST_NT_LAT 1024  // k_ghist block in latency-bound plans (256 / 512 / 1024: 6.5 / 5.7 / 5.3 us on one update)
-#endif
+constexpr int GWIN_NT_LAT = 512;  // k_gwin block in latency-bound plans (256 or 512: one or two histogram bins per thread)
+constexpr int GHIST_NT_LAT = 1024;  // k_ghist block in latency-bound plans (256 / 512 / 1024: 6.5 / 5.7 / 5.3 us on one update)
 constexpr int SEL_NT_LAT = 512;           // ... in latency-bound plans, where nothing streams beside it (one
                                           // ResNet-50 update: k_select 11.3 -> 10.2 us; batches measured slower)
-#ifndef SCAN_WPE
-#define SCAN_WPE 5
-#endif
-#ifndef SCAN_NT
-#define SCAN_NT 128  // batch plans' k_scan block size (launch bounds: SCAN_WPE waves per SIMD; C3 0.584 vs 0.616 ms at 256)
-#endif
-#ifndef SCAN_NT_LAT
-#define SCAN_NT_LAT 256  // latency-bound plans' k_scan block size (its first blocks encode the small segments)
-#endif
-#ifndef SCAN_NB
-#define SCAN_NB 1  // load batches per k_scan unit (weights mode): 1 = all 16 float4 per lane in flight
-#endif
-#ifndef SCAN_WPE_LAT
-#define SCAN_WPE_LAT 6  // latency-bound plans' k_scan: blocks per CU (5 / 1 batch: 24.5 us, 6 / 2: 23.0, 6 / 1
-                        // spills: 31.7, 8 / 4: 24.2 on one update; batches keep SCAN_WPE / SCAN_NB)
-#endif
-#ifndef SCAN_WPE_LAT_1K
-#define SCAN_WPE_LAT_1K 7  // ... with the default 1024-element small segments (a 16 KB arena): 7 blocks per CU, so
-                           // one ResNet-50 update's ~1,660 blocks fit one round of the chip's block slots
-#endif
-#ifndef SCAN_NB_LAT
-#define SCAN_NB_LAT 2   // ... and load batches per unit
-#endif
-#ifndef SAMPLE_NT_LAT
-#define SAMPLE_NT_LAT 256  // latency-bound plans' k_sample block size (1024 threads, 2 load batches each: 0.7 us slower)
-#endif
+constexpr int SCAN_WPE = 5;
+constexpr int SCAN_NT = 128;  // batch plans' k_scan block size (launch bounds: SCAN_WPE waves per SIMD; C3 0.584 vs 0.616 ms at 256)
+constexpr int SCAN_NT_LAT = 256;  // latency-bound plans' k_scan block size (its first blocks encode the small segments)
+constexpr int SCAN_NB = 1;  // load batches per k_scan unit (weights mode): 1 = all 16 float4 per lane in flight
+constexpr int SCAN_WPE_LAT = 6;  // latency-bound plans' k_scan: blocks per CU (5 / 1 batch: 24.5 us, 6 / 2: 23.0, 6 / 1
+                                 // spills: 31.7, 8 / 4: 24.2 on one update; batches keep SCAN_WPE / SCAN_NB)
+constexpr int SCAN_WPE_LAT_1K = 7;  // ... with the default 1024-element small segments (a 16 KB arena): 7 blocks per CU, so
+                                    // one ResNet-50 update's ~1,660 blocks fit one round of the chip's block slots
+constexpr int SCAN_NB_LAT = 2;  // ... and load batches per unit
+constexpr int SAMPLE_NT_LAT = 256;  // latency-bound plans' k_sample block size (1024 threads, 2 load batches each: 0.7 us slower)
 constexpr int LOAD_AUX = 2;   // cache policy of the streaming buffer loads (k_scan, the quantise stream): non-temporal
 constexpr int STORE_AUX = 2;  // cache policy of the streaming buffer stores (batch k_decode_lds, k_dense_deq): non-temporal
 constexpr uint32_t STAGE_CAP = 512;       // candidate records staged in LDS per k_scan wave
-#ifndef GU_UNITS
-#define GU_UNITS 32
-#endif
-#ifndef GSWEEP
-#define GSWEEP 4  // units per record-load batch of a balanced group sweep (batch plans)
-#endif
+constexpr int GU_UNITS = 32;
+constexpr int GSWEEP = 4;  // units per record-load batch of a balanced group sweep (batch plans)
 constexpr uint32_t GU = GU_UNITS;               // units per select group (k_ghist / k_gwin block)
 constexpr uint32_t HB2 = 512;             // bins of the per-group band histograms
 constexpr uint32_t GCAP = 256;            // in-window entries a group may hand to k_select
@@ -1391,10 +1365,8 @@ struct SpecSweep {
 // LDS scratch of the segment select (k_select, and the SELECT role of the one-launch encode, whose LDS
 // must stay <= 32 KB so five streaming blocks still fit a CU): 28.3 KB
 constexpr uint32_t WLIST = 1024;  // in-window entries the fast path can hold
-#ifndef SELECT_SPEC
-#define SELECT_SPEC 64u  // k_select: speculatively gathered slots per group window list (one update: 64 -> 0.0811 ms per
-                         // step, 16 -> 0.0830, 8 -> 0.0838: longer lists otherwise cost a dependent round)
-#endif
+constexpr uint32_t SELECT_SPEC = 64u;  // k_select: speculatively gathered slots per group window list (one update: 64 -> 0.0811 ms per
+                                       // step, 16 -> 0.0830, 8 -> 0.0838: longer lists otherwise cost a dependent round)
 constexpr int SEL_HB = 1024;      // bins of the select's radix histograms
 struct SelSmem {
   uint32_t hist[SEL_HB];
@@ -2092,15 +2064,11 @@ __global__ __launch_bounds__(NT) void k_select(Params P) {
 // records: here lane g loads unit g's metadata (two dependent rounds for all units at once) and every
 // unit's first 64 records are in flight before the first one is classified.
 // ------------------------------------------------------------------------------------------------
-#ifndef EMIT_UPW
-#define EMIT_UPW 8u  // large units per k_emit wave in batches (C3 share: +2 % over 2 units per wave)
-#endif
+constexpr uint32_t EMIT_UPW = 8u;  // large units per k_emit wave in batches (C3 share: +2 % over 2 units per wave)
 // ... in latency-bound plans (<= LATENCY_PLAN_UNITS units): a wave's units are handled one after the other,
 // so fewer per wave shortens the launch (one ResNet-50 update: 8 per wave 13.1 us, 2 per wave 6.0, 1 per
 // wave 5.1)
-#ifndef EMIT_UPW_LAT
-#define EMIT_UPW_LAT 1u
-#endif
+constexpr uint32_t EMIT_UPW_LAT = 1u;
 constexpr uint32_t EMIT_UPW_LATENCY = EMIT_UPW_LAT;
 
 DEV uint32_t rl(uint32_t v, uint32_t l) { return (uint32_t)__builtin_amdgcn_readlane((int)v, (int)l); }
@@ -2282,28 +2250,14 @@ __global__ __launch_bounds__(BLOCK) void k_emit(Params P) {
 // over every entry, ~10 VALU each: as much issue time per unit as its stores); round 3 measured one unit per wave in
 // two 8-row passes fastest for batches (C3 0.672 -> 0.622 ms per step, profiles/r03_decode_ab.txt). Entries outside
 // the wave's rows (an untrusted list) never match a pass and are dropped.
-#ifndef DECODE_LDS_WPE
-#define DECODE_LDS_WPE 5
-#endif
-#ifndef DECODE_LDS_WPE_BASE
-#define DECODE_LDS_WPE_BASE 4  // delta mode: two passes of base rows in registers (5 per SIMD spilled)
-#endif
-#ifndef DECODE_QROWS
-#define DECODE_QROWS 8u  // batches, weights mode: rows per tile pass (8: half a unit, 8 KiB of LDS per wave; 4 rows: C3
-                         // 0.671-0.674 ms per step, 8 rows: 0.621-0.623, profiles/r03_decode_ab.txt)
-#endif
-#ifndef DECODE_QROWS_BASE
-#define DECODE_QROWS_BASE 4u  // delta mode: rows per tile pass
-#endif
-#ifndef DECODE_NT
-#define DECODE_NT 256  // k_decode_lds block size (its per-wave LDS tile is QROWS KiB)
-#endif
-#ifndef DECODE_WPU_LAT
-#define DECODE_WPU_LAT 2u  // latency-bound plans: waves per unit (one update: every wave one 8-row pass)
-#endif
-#ifndef DECODE_SAUX_LAT
-#define DECODE_SAUX_LAT 0  // latency-bound plans: store cache policy (a ~100 MB output: plain stores)
-#endif
+constexpr int DECODE_LDS_WPE = 5;
+constexpr int DECODE_LDS_WPE_BASE = 4;  // delta mode: two passes of base rows in registers (5 per SIMD spilled)
+constexpr uint32_t DECODE_QROWS = 8u;  // batches, weights mode: rows per tile pass (8: half a unit, 8 KiB of LDS per wave; 4 rows: C3
+                                       // 0.671-0.674 ms per step, 8 rows: 0.621-0.623, profiles/r03_decode_ab.txt)
+constexpr uint32_t DECODE_QROWS_BASE = 4u;  // delta mode: rows per tile pass
+constexpr int DECODE_NT = 256;  // k_decode_lds block size (its per-wave LDS tile is QROWS KiB)
+constexpr uint32_t DECODE_WPU_LAT = 2u;  // latency-bound plans: waves per unit (one update: every wave one 8-row pass)
+constexpr int DECODE_SAUX_LAT = 0;  // latency-bound plans: store cache policy (a ~100 MB output: plain stores)
 
 // NCH: 64-entry chunks of the unit's kept entries held in registers across the passes (1 at ratios up to ~1.5 %;
 // plans of higher ratios take 8 — up to 512 entries, ratio ~12 % — so the entry lists are loaded once per unit,
@@ -2406,15 +2360,9 @@ __global__ __launch_bounds__(DECODE_NT, HASBASE ? DECODE_LDS_WPE_BASE : DECODE_L
 // ------------------------------------------------------------------------------------------------
 // aggregate: fused server-side decode + FedAvg of C client updates of one layout
 // ------------------------------------------------------------------------------------------------
-#ifndef AGG_WPE
-#define AGG_WPE 1  // k_aggregate launch-bounds blocks per CU (register budget)
-#endif
-#ifndef AGG_SPLIT
-#define AGG_SPLIT 2u  // waves per 4096-element unit in k_aggregate (each owns UNIT_IT / AGG_SPLIT rows)
-#endif
-#ifndef AGG_DEPTH
-#define AGG_DEPTH 16u  // clients whose entries k_aggregate loads together (16 ResNet-50 clients: 4 -> 73.5 us, 8 -> 70.9 us, 16 -> 69.1 us)
-#endif
+constexpr int AGG_WPE = 1;  // k_aggregate launch-bounds blocks per CU (register budget)
+constexpr uint32_t AGG_SPLIT = 2u;  // waves per 4096-element unit in k_aggregate (each owns UNIT_IT / AGG_SPLIT rows)
+constexpr uint32_t AGG_DEPTH = 16u;  // clients whose entries k_aggregate loads together (16 ResNet-50 clients: 4 -> 73.5 us, 8 -> 70.9 us, 16 -> 69.1 us)
 
 struct AggArgs {
   const uint32_t* ustart;  // [n_units] the clients' per-unit starts (wire v2)
