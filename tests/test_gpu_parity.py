@@ -423,6 +423,33 @@ def test_tie_mode_bits_and_delta(cuda, bits):
     assert_same(plan, g, r)
 
 
+@pytest.mark.parametrize("clients", [1, 2])
+def test_tie_mode_nan_inf_and_denormal_ties(cuda, clients):
+    """Large segments whose tie key is a NaN, +-inf or a denormal (all-NaN, NaN beside values, equal-magnitude
+    infinities, a sea of one denormal with both signs): tie mode's K is then a non-finite or subnormal key, the kept
+    +-K values enter mn / scale NaN-ignoring, as the oracle does. Bit-exact against the oracle."""
+    rng = np.random.default_rng(3 + clients)
+    n = 4096 * 5 + 7
+    nan = np.float32(np.nan)
+    segs = [
+        np.full(n, nan, np.float32),
+        np.where(rng.random(n) < 0.3, nan, rng.standard_normal(n).astype(np.float32)).astype(np.float32),
+        np.where(rng.random(n) < 0.5, np.float32(np.inf), np.float32(-np.inf)).astype(np.float32),
+        np.where(rng.random(n) < 0.5, np.float32(1e-40), np.float32(-1e-40)).astype(np.float32),
+        (rng.standard_normal(n) * 1e-3).astype(np.float32),
+    ]
+    sizes = [x.size for x in segs]
+    xs = [[x.copy() for x in segs] for _ in range(clients)]
+    if clients == 2:  # a batch plan (> 8192 units): pad the layout with a large ordinary segment
+        big = 4096 * 8200
+        sizes.append(big)
+        for c in range(clients):
+            xs[c].append((rng.standard_normal(big) * 1e-3).astype(np.float32))
+    for ratio in (0.01, 0.3):
+        plan, g, r = run_both(sizes, ratio, 8, xs, clients=clients)
+        assert_same(plan, g, r)
+
+
 def test_tie_mode_sample_miss_takes_raw_path(cuda):
     """Tie mode is the sampler's call: equal |x| everywhere it looks, but 2 % larger values where it does not look
     put the k-th key above K (the records then hold more than k keys). The segment falls back to the raw-data path:
