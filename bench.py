@@ -23,6 +23,9 @@ collective on the data path — torch.distributed only for the barrier and the m
   C4_delta   the C4 share in delta mode
   C4_frozen  the C4 share in delta mode with the backbone frozen as FedPEFT does (application/FedPEFT/lora.py:64,
           main.py:62-67): every tensor but the classifier head is an exact-zero delta
+  C3_signs   the C3 share in delta mode after one sign-like local step (signSGD, the first Adam step): trained =
+          fl(w_global -+ lr), so every |delta| is lr up to the rounding of the subtraction — heavy near-ties at
+          the k-th key (the tie mode of DESIGN.md §6e; the raw-data path's territory before it)
   download   the download direction: one ResNet-50 global model per step, dense 8-bit codes at
           ratio 1 (indices implied) — the server's compression() (coala/server/base.py:196) + one client's
           decode of it (coala/client/base.py:197-201); HBM bytes 10N + 32T
@@ -58,6 +61,7 @@ CONFIGS = {  # name -> (layout | "c5", clients per GPU, sub-batches: the best of
     "C4": ("vit_b16", 16, SPLIT, {}),
     "C4_delta": ("vit_b16", 16, SPLIT, {"mode": "delta"}),
     "C4_frozen": ("vit_b16", 16, SPLIT, {"mode": "delta", "frozen": True}),
+    "C3_signs": ("resnet50_tv", 16, SPLIT, {"mode": "delta", "signs": True}),
     "C5": ("c5", None, 1, {}),  # one latency-bound plan (<= 8192 units): 0.116 ms vs 0.122 as 2 sub-batches
     "single": ("resnet50_tv", 1, "single", {}),
     "single_x2": ("resnet50_tv", 1, "single", {}),
@@ -67,7 +71,7 @@ CONFIGS = {  # name -> (layout | "c5", clients per GPU, sub-batches: the best of
 # server decodes concurrent uploads from one thread each, coala/server/service.py:71-111)
 CONFIG_INFLIGHT = {"single_x2": 2}
 SINGLE_SPLIT = 1  # segment ranges of the single update run as this many concurrent sub-plans
-DEFAULT_EXTRAS = "C2,C3_delta,C3_r0.001,C3_r0.1,C4,C4_delta,C4_frozen,C5,single,single_x2,download,plugin"
+DEFAULT_EXTRAS = "C2,C3_delta,C3_r0.001,C3_r0.1,C3_signs,C4,C4_delta,C4_frozen,C5,single,single_x2,download,plugin"
 
 
 def cfg_opts(cfg, a):
@@ -281,7 +285,9 @@ def build_table(cfg, a, rank, headline):
     _, mode, frozen = cfg_opts(cfg, a)
     return t, ids, split, {"layout": layout, "clients_per_gpu": clients, "elements_per_client": sum(t.sizes),
                            "segments_per_client": len(t.sizes), "ratio": ratio, "mode": mode,
-                           **({"frozen": "every tensor but the classifier head an exact-zero delta"} if frozen else {})}
+                           **({"frozen": "every tensor but the classifier head an exact-zero delta"} if frozen else {}),
+                           **({"signs": "trained = fl(w_global -+ 1e-3): every |delta| 1e-3 up to rounding"}
+                              if CONFIGS[cfg][3].get("signs") else {})}
 
 
 GRAPH_CONFIGS = ("single", "single_x2", "C5", "download")  # latency-bound plans: step time ~ host launch time
@@ -314,6 +320,10 @@ def setup_workload(cfg, a, dev, rank, headline):
         for f in flats:
             freeze_segments(f, t, head_only(desc["layout"]))
             f.add_(base)
+    if CONFIGS[cfg][3].get("signs"):  # trained = fl(w_global -+ lr): one sign-like step, lr = 1e-3
+        g = torch.Generator(device=dev).manual_seed(4242 + rank)
+        for f in flats:
+            f.copy_(base + torch.where(torch.rand(f.numel(), generator=g, device=dev) < 0.5, -1e-3, 1e-3))
     split = max(1, split)
     inflight = max(1, a.inflight) if headline else CONFIG_INFLIGHT.get(cfg, 1)
     slots = []
