@@ -291,7 +291,7 @@ def build_table(cfg, a, rank, headline):
 
 
 GRAPH_CONFIGS = ("single", "single_x2", "C5", "download")  # latency-bound plans: step time ~ host launch time
-GRAPH_WARM_REPLAYS = 8  # untimed replays of each slot's whole-rotation graph before the timed region
+GRAPH_WARM_REPLAYS = 8  # untimed replays of each slot's whole-rotation graph right before the timed region
 
 
 def use_graph(cfg, a):
@@ -399,15 +399,8 @@ def capture_graphs(W, a):
         for r in range(W["rot"]):  # single steps for the remainder, one per buffer set
             W["graphs"][(1, r)] = capture([r])
         torch.cuda.synchronize()
-        # untimed replays before the timed region: every captured graph once (a graph's first launch uploads it),
-        # then the whole-rotation graphs a few more times (the first window measured 3-6 % slower than the
-        # repeat windows without them: single 0.082 vs 0.078 ms, download 0.078 vs 0.074)
-        for gs in W["graphs"].values():
+        for gs in W["graphs"].values():  # every captured graph once (a graph's first launch uploads it)
             for g, st in gs:
-                with torch.cuda.stream(st):
-                    g.replay()
-        for _ in range(GRAPH_WARM_REPLAYS):
-            for g, st in W["graphs"][gk]:
                 with torch.cuda.stream(st):
                     g.replay()
         torch.cuda.synchronize()
@@ -452,6 +445,15 @@ def time_workload(W, a, dev, world):
         if world > 1:
             dist.barrier()
         return time.perf_counter() - t0
+    if graphs is not None:
+        # the graphs were captured (and replayed once) before the other configs ran: replay them again right before
+        # the timed region, so their buffers are warm again (without this the first window measured a constant
+        # ~0.05-0.1 ms above the repeat windows: C5 0.0911 vs 0.0866 ms per step, download 0.0791 vs 0.0735)
+        for _ in range(GRAPH_WARM_REPLAYS):
+            for g, st in graphs[W["gk"]]:
+                with torch.cuda.stream(st):
+                    g.replay()
+        torch.cuda.synchronize()
     el = timed_region()
     rank_el = gather_elapsed(el, world, dev)
     el = max(rank_el)  # the job's time: the slowest rank
