@@ -309,7 +309,7 @@ def setup_workload(cfg, a, dev, rank, headline):
     import torch
 
     from coala_amd.compression import SplitPipeline
-    from coala_amd.workload import freeze_segments, head_only, synth_batch
+    from coala_amd.workload import freeze_segments, head_only, sign_step, synth_batch
 
     t, ids, split, desc = build_table(cfg, a, rank, headline)
     _, mode, frozen = cfg_opts(cfg, a)
@@ -321,9 +321,8 @@ def setup_workload(cfg, a, dev, rank, headline):
             freeze_segments(f, t, head_only(desc["layout"]))
             f.add_(base)
     if CONFIGS[cfg][3].get("signs"):  # trained = fl(w_global -+ lr): one sign-like step, lr = 1e-3
-        g = torch.Generator(device=dev).manual_seed(4242 + rank)
-        for f in flats:
-            f.copy_(base + torch.where(torch.rand(f.numel(), generator=g, device=dev) < 0.5, -1e-3, 1e-3))
+        for r, f in enumerate(flats):
+            sign_step(f, base, 4242 + 17 * rank + r)
     split = max(1, split)
     inflight = max(1, a.inflight) if headline else CONFIG_INFLIGHT.get(cfg, 1)
     slots = []
@@ -669,6 +668,18 @@ def run_plugin(a, dev, steps):
                     "host-side Python included; flattened = the round-1 path (torch.cat copy first)"}
 
 
+def configs_summary(head, headline, results, plugin):
+    """{config: [GB/s, ms per step, step roofline frac, dominant-kernel roofline frac]} for the headline and every
+    extra (plugin: per client, its hooks' path; kernel frac null) — the line's last key."""
+    out = {headline: [head["value"], head["ms_per_step"], head["step_roofline"]["frac"], head["roofline"]["frac"]]}
+    for k, v in results.items():
+        out[k] = [v["value"], v["ms_per_step"], v["step_roofline"]["frac"], v["roofline"]["frac"]]
+    if plugin is not None:
+        out["plugin"] = [plugin["value"], plugin["ms_per_client"], plugin["step_roofline"]["frac"], None]
+    out["fields"] = "GB/s, ms_per_step, step_roofline_frac, kernel_roofline_frac"
+    return out
+
+
 def launch_ranks(a):
     """`--gpus N` (N > 1) without a launcher: start N rank processes of this script, one per GPU (RANK /
     LOCAL_RANK / WORLD_SIZE / MASTER_* in their environment, as torch.distributed.run sets them), before this
@@ -812,16 +823,21 @@ def main():
             "stage_timing": head["stage_timing"], "sample_fallbacks": head["sample_fallbacks"],
             "graph": head["graph"], "rank_ms_per_step": head["rank_ms_per_step"],
             "repeat_windows": head["repeat_windows"],
-            "configs": {k: {f: v[f] for f in ("value", "ms_per_step", "step_roofline", "roofline", "stages_ms", "desc",
-                                              "elements_per_gpu", "segments_per_gpu", "split", "inflight", "rotation",
-                                              "graph", "sample_fallbacks", "rank_ms_per_step", "repeat_windows")}
-                        for k, v in results.items()},
         }
-        res["box"] = box
-        if plugin is not None:
-            res["configs"]["plugin"] = plugin
+        # cpu_baseline and box BEFORE the per-config details, and a compact summary of every config LAST: the driver
+        # keeps only the tail of stdout, so every config's number must sit in the line's last ~2 KB
         if cpu is not None:
             res["cpu_baseline"] = cpu
+        res["box"] = box
+        res["configs"] = {k: {f: v[f] for f in ("value", "ms_per_step", "step_roofline", "roofline", "stages_ms",
+                                                 "elements_per_gpu", "split", "graph", "sample_fallbacks",
+                                                 "rank_ms_per_step", "repeat_windows")}
+                          for k, v in results.items()}
+        for v in res["configs"].values():  # (the roofline objects without their repeated constant fields)
+            v["roofline"] = {f: v["roofline"][f] for f in ("kernel", "achieved", "frac")}
+        if plugin is not None:
+            res["configs"]["plugin"] = plugin
+        res["configs_summary"] = configs_summary(head, a.config, results, plugin)
         print(json.dumps(res), flush=True)
     if world > 1:
         dist.destroy_process_group()

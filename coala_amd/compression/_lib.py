@@ -50,6 +50,7 @@ SIGNATURES = [
     ("coalac_gather", _I, [_P, _I, _I, _P, _P]),
     ("coalac_workspace_fallbacks", _I, [_P, _P, _P, ctypes.POINTER(_I)]),
     ("coalac_debug_stamps", _I, [_P, _P, _P, ctypes.POINTER(ctypes.c_uint64), _I]),
+    ("coalac_debug_brackets", _I, [_P, _P, _P, ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_uint32), _I]),
 ]
 
 ABI_VERSION = 5

@@ -214,6 +214,9 @@ DEV float qnan() { return __int_as_float(0x7FC00000); }
 
 DEV uint32_t lane_id() { return __lane_id(); }
 
+// lane l's value of v (v_readlane: a wave-uniform result)
+DEV uint32_t rl(uint32_t v, uint32_t l) { return (uint32_t)__builtin_amdgcn_readlane((int)v, (int)l); }
+
 // XCD-aware block order: workgroups are dispatched round-robin over the 8 XCDs (block b on XCD b % 8); the
 // remapped index gives XCD x the x-th contiguous share of [0, gridDim.x) (a bijection for any grid size), so
 // each XCD streams through one region instead of every eighth 64 KiB. NT stores of the unit pattern, 1.5 GiB:
@@ -228,38 +231,61 @@ DEV uint32_t mbcnt(uint64_t m) {
   return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
 }
 
+// Cross-lane steps by DPP (a VALU operand modifier: a few cycles) — __shfl_* lowers to ds_bpermute_b32, an LDS round
+// trip per step (~100+ cycles), and a wave scan is six dependent steps. dpp<CTRL>: lane i reads lane src(i) of v
+// (0 where the source lies outside its row or the row is masked off). CTRL: 0x111 + n - 1 row_shr:n, 0x128 row_ror:8,
+// 0x140 row_mirror, 0x141 row_half_mirror, 0x142 row_bcast:15, 0x143 row_bcast:31, 0xB1 / 0x4E quad_perm xor 1 / xor 2.
+template <int CTRL, int ROWM = 0xF>
+DEV uint32_t dpp(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, ROWM, 0xF, false);
+}
+
+// inclusive prefix sum over the 64 lanes (all lanes active)
 DEV uint32_t wave_incl_scan(uint32_t v) {
-  const uint32_t lane = lane_id();
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    uint32_t t = __shfl_up(v, o, 64);
-    if (lane >= (uint32_t)o) v += t;
-  }
+  v += dpp<0x111>(v);  // row_shr:1, 2, 4, 8: each 16-lane row scanned
+  v += dpp<0x112>(v);
+  v += dpp<0x114>(v);
+  v += dpp<0x118>(v);
+  v += dpp<0x142, 0xA>(v);  // row_bcast:15 into rows 1, 3
+  v += dpp<0x143, 0xC>(v);  // row_bcast:31 into rows 2, 3
   return v;
+}
+
+// reduction over the 64 lanes, the result in every lane: within each row by quad / half-row / row mirrors, then the
+// four rows' values by readlane
+template <class OP>
+DEV uint32_t wave_reduce(uint32_t v, OP op) {
+  v = op(v, dpp<0xB1>(v));
+  v = op(v, dpp<0x4E>(v));
+  v = op(v, dpp<0x141>(v));
+  v = op(v, dpp<0x140>(v));
+  const uint32_t a = (uint32_t)__builtin_amdgcn_readlane((int)v, 0), b = (uint32_t)__builtin_amdgcn_readlane((int)v, 16);
+  const uint32_t c = (uint32_t)__builtin_amdgcn_readlane((int)v, 32), d = (uint32_t)__builtin_amdgcn_readlane((int)v, 48);
+  return op(op(a, b), op(c, d));
 }
 
 DEV float wave_min(float v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v = fmin_nan(v, __shfl_xor(v, o, 64));
-  return v;
+  return __uint_as_float(wave_reduce(__float_as_uint(v), [](uint32_t a, uint32_t b) {
+    return __float_as_uint(fmin_nan(__uint_as_float(a), __uint_as_float(b)));
+  }));
 }
 
 DEV float wave_max(float v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v = fmax_nan(v, __shfl_xor(v, o, 64));
-  return v;
+  return __uint_as_float(wave_reduce(__float_as_uint(v), [](uint32_t a, uint32_t b) {
+    return __float_as_uint(fmax_nan(__uint_as_float(a), __uint_as_float(b)));
+  }));
 }
 
 DEV uint32_t wave_min_u32(uint32_t v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v = min(v, (uint32_t)__shfl_xor((int)v, o, 64));
-  return v;
+  return wave_reduce(v, [](uint32_t a, uint32_t b) { return min(a, b); });
 }
 
 DEV uint32_t wave_max_u32(uint32_t v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v = max(v, (uint32_t)__shfl_xor((int)v, o, 64));
-  return v;
+  return wave_reduce(v, [](uint32_t a, uint32_t b) { return max(a, b); });
+}
+
+DEV uint32_t wave_sum(uint32_t v) {
+  return wave_reduce(v, [](uint32_t a, uint32_t b) { return a + b; });
 }
 
 // Order one wave's own LDS accesses (a scatter, then reads of the same tile by other lanes): the LDS executes a
@@ -357,7 +383,7 @@ DEV uint32_t rank_select(ForEach&& for_each, uint32_t lo, uint32_t hi, uint32_t&
       const uint32_t leader = (uint32_t)__ffsll((long long)m) - 1u;
       uint32_t base = 0;
       if (lane == leader) base = atomicAdd(&sh[39], (uint32_t)__popcll(m));
-      base = (uint32_t)__shfl((int)base, (int)leader, 64);
+      base = (uint32_t)__builtin_amdgcn_readlane((int)base, (int)leader);
       if (in) cand[base + mbcnt(m)] = key;
     }
   });
@@ -754,8 +780,7 @@ DEV void scan_unit(const Params& P, uint32_t lu, const UnitDev& L, const uint32_
     for (uint32_t i = lane; i < cC && i < STAGE_CAP; i += 64) put(i, stage[i]);
   }
   if (ZERO) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) cz += (uint32_t)__shfl_xor((int)cz, o, 64);
+    cz = wave_sum(cz);
     if (tk != 0u) {
       rp = wave_min_u32(rp);
       rn = wave_min_u32(rn);
@@ -1805,6 +1830,10 @@ DEV void raw_counts(const Params& P, uint32_t lb, uint32_t nu, uint32_t T, uint3
   __syncthreads();
 }
 
+template <int NT>
+DEV void window_resolve(SelSmem& S, uint32_t W, uint4 st, float lmn0, float lmx0, uint32_t& T_out, uint32_t& rt_out,
+                        uint32_t& fp, uint32_t& fn, float& gmn, float& gmx);
+
 // Fast-path resolution in k_select: gather the groups' in-window lists (group order = index order),
 // find the exact key inside the window, apply the window entries to the per-unit counts. Returns false
 // if a group's list overflowed (the caller then runs the generic path from scratch).
@@ -1852,6 +1881,18 @@ DEV bool select_from_groups(const Params& P, const SegDev& sd, uint32_t lb, uint
     if (t + j * NT < nu) S.ge[t + j * NT] = gtc[j];
   for (uint32_t i = t + CB * NT; i < nu; i += NT) S.ge[i] = P.gtC[lb + i];
   __syncthreads();
+  window_resolve<NT>(S, W, st, gmn0, gmx0, T_out, rt_out, fp, fn, gmn, gmx);
+  return true;
+}
+
+// The exact k-th key inside the window [st.x, st.y] from the segment's in-window list S.lst[0, W) (index order), rank
+// st.z inside the window; the entries above it and its ties applied to the per-unit counts in S.ge (above | equal << 16);
+// the segment-wide tie ranks of the first positive / negative tie; min / max of the kept window entries folded into
+// this thread's lmn / lmx (the values above the window). Block-level.
+template <int NT>
+DEV void window_resolve(SelSmem& S, uint32_t W, uint4 st, float lmn0, float lmx0, uint32_t& T_out, uint32_t& rt_out,
+                        uint32_t& fp, uint32_t& fn, float& gmn, float& gmx) {
+  const uint32_t t = threadIdx.x;
   uint32_t rt = st.z;
   const uint32_t T = block_select<NT, SEL_HB>(
       [&](auto&& f) {
@@ -1877,8 +1918,8 @@ DEV bool select_from_groups(const Params& P, const SegDev& sd, uint32_t lb, uint
       ++leq;
     }
   }
-  lmn = fmin_nan(lmn, gmn0);  // ng <= NT: thread t < ng holds group t's
-  lmx = fmax_nan(lmx, gmx0);
+  lmn = fmin_nan(lmn, lmn0);  // (select_from_groups: thread t < ng holds group t's)
+  lmx = fmax_nan(lmx, lmx0);
   uint32_t teq;
   const uint32_t ex = block_excl_scan<NT>(leq, S.sh, teq);
   if (t == 0) {
@@ -1896,71 +1937,51 @@ DEV bool select_from_groups(const Params& P, const SegDev& sd, uint32_t lb, uint
   gmn = lmn;
   gmx = lmx;
   __syncthreads();
-  return true;
 }
 
-template <int NT, bool DELTA, bool RAW>
-DEV void segment_select(const Params& P, uint32_t li, SelSmem& S) {
+// Zero-tie ranks (tie mode, the k-th key is the segment's tie key K > 0): the segment-wide ranks of the first +K and
+// -K ties, from the units' tie prefixes (S.ge >> 16 = the unit's K-keys) and in-unit ranks (tsgn). Block-level.
+template <int NT>
+DEV void zero_tie_ranks(const Params& P, uint32_t lb, uint32_t nu, SelSmem& S, uint32_t& fp_rank, uint32_t& fn_rank) {
+  const uint32_t t = threadIdx.x;
+  uint32_t lp = NONE, ln = NONE, carry = 0;
+  for (uint32_t c0 = 0; c0 < nu; c0 += NT) {
+    const uint32_t i = c0 + t;
+    const uint32_t z = i < nu ? S.ge[i] >> 16 : 0u;
+    uint32_t tot;
+    const uint32_t ex = block_excl_scan<NT>(z, S.sh, tot) + carry;
+    carry += tot;
+    if (i < nu) {
+      const uint32_t sg = P.tsgn[lb + i], fp = sg & 0xFFFFu, fn = sg >> 16;
+      if (fp != 0xFFFFu) lp = min(lp, ex + fp);
+      if (fn != 0xFFFFu) ln = min(ln, ex + fn);
+    }
+  }
+  if (t == 0) {
+    S.sh[42] = NONE;
+    S.sh[43] = NONE;
+  }
+  __syncthreads();
+  if (lp != NONE) atomicMin(&S.sh[42], lp);
+  if (ln != NONE) atomicMin(&S.sh[43], ln);
+  __syncthreads();
+  fp_rank = S.sh[42];
+  fn_rank = S.sh[43];
+  __syncthreads();
+}
+
+// The select of a segment that the window path cannot resolve: the generic multi-pass select over the records, or —
+// on a bracket miss, a unit that overflowed its record slots, or COALAC_FLAG_FORCE_EXACT — the raw-data path (exact
+// k-th key of the whole segment from its input, per-unit counts from the raw data, status 1: k_emit re-reads the input).
+// Per-unit counts land in gtC / eqC. Block-level.
+template <int NT, bool DELTA>
+DEV void select_fallback(const Params& P, uint32_t s, const SegDev& sd, SelSmem& S, uint32_t& T, uint32_t& rt,
+                         uint32_t& fp_rank, uint32_t& fn_rank, float& gmn, float& gmx, uint32_t& raw_path) {
   constexpr int NW = NT / 64;
   const uint32_t t = threadIdx.x, wv = t >> 6;
-  const uint32_t s = P.large_list[li];
-  const SegDev sd = P.lsegs[li];  // (same load round as s and the select state)
-  const uint4 st = P.sstate[li];
   const float* xs = seg_in(P, s, sd.in_off);
   const float* bs = DELTA ? P.base + sd.in_off : xs;
   const uint32_t lb = sd.lu_begin, nu = sd.unit_end - sd.unit_begin, k = sd.k;
-  STAMP(P, li, 0);
-  uint32_t T, rt, fp_rank, fn_rank;
-  float gmn, gmx;
-  const bool zero_tie = st.w == 2;  // the k-th key is the segment's tie key K (segment_pick; tie mode)
-  bool done;
-  if (zero_tie) {
-    // every record kept (k_gwin's per-unit counts above the empty window), the first rt K-keys by index. K = 0: a
-    // zero's sign does not matter to mn / scale (canonicalised + 0.0f below), so one "positive tie" stands for them;
-    // K > 0: the segment-wide ranks of the first +K and -K ties from the units' tie prefixes and in-unit ranks (tsgn)
-    const uint32_t g0 = sd.g_begin, ng = (nu + GU - 1) / GU;  // ng <= UCAP / GU <= NT
-    const uint32_t tk = P.tlo[lb] & KEY_MAX;
-    gmn = t < ng ? P.gmm[2 * (g0 + t)] : qnan();
-    gmx = t < ng ? P.gmm[2 * (g0 + t) + 1] : qnan();
-    for (uint32_t i = t; i < nu; i += NT) S.ge[i] = P.gtC[lb + i] | (P.cntZ[lb + i] << 16);
-    __syncthreads();
-    T = tk;
-    rt = st.z;
-    fp_rank = rt > 0 ? 0u : NONE;
-    fn_rank = NONE;
-    if (tk != 0u) {  // (block-uniform)
-      uint32_t lp = NONE, ln = NONE, carry = 0;
-      for (uint32_t c0 = 0; c0 < nu; c0 += NT) {
-        const uint32_t i = c0 + t;
-        const uint32_t z = i < nu ? S.ge[i] >> 16 : 0u;
-        uint32_t tot;
-        const uint32_t ex = block_excl_scan<NT>(z, S.sh, tot) + carry;
-        carry += tot;
-        if (i < nu) {
-          const uint32_t sg = P.tsgn[lb + i], fp = sg & 0xFFFFu, fn = sg >> 16;
-          if (fp != 0xFFFFu) lp = min(lp, ex + fp);
-          if (fn != 0xFFFFu) ln = min(ln, ex + fn);
-        }
-      }
-      if (t == 0) {
-        S.sh[42] = NONE;
-        S.sh[43] = NONE;
-      }
-      __syncthreads();
-      if (lp != NONE) atomicMin(&S.sh[42], lp);
-      if (ln != NONE) atomicMin(&S.sh[43], ln);
-      __syncthreads();
-      fp_rank = S.sh[42];
-      fn_rank = S.sh[43];
-      __syncthreads();
-    }
-    done = true;
-  } else {
-    done = st.w == 0 && select_from_groups<NT>(P, sd, lb, nu, st, S, T, rt, fp_rank, fn_rank, gmn, gmx);
-  }
-  uint32_t raw_path = 0;
-  STAMP(P, li, 1);
-  if (!done) {
   uint32_t sa = 0, sc = 0;
   for (uint32_t i = t; i < nu; i += NT) {
     sa += P.cntA[lb + i];
@@ -1976,7 +1997,7 @@ DEV void segment_select(const Params& P, uint32_t li, SelSmem& S) {
   for (int i = 0; i < NW; ++i) mc = max(mc, S.wcnt[i]);
   __syncthreads();
   const uint32_t tlo = P.tlo[lb] & KEY_MAX, thi = P.thi[lb];  // (tie mode K: records are the keys above K)
-
+  raw_path = 0u;
   if ((P.flags & COALAC_FLAG_FORCE_EXACT) || !(sa <= k && k <= sc) || mc > P.ccap) {
     // raw-data path (rare): the exact k-th key of the whole segment, per-unit counts from the raw data;
     // k_emit re-reads the raw data for this segment (status 1)
@@ -1995,9 +2016,20 @@ DEV void segment_select(const Params& P, uint32_t li, SelSmem& S) {
     // rank of the k-th key among candidates with key <= thi (0: none of them)
     select_generic<NT>(P, lb, nu, tlo, thi, k - sa, S, T, rt, fp_rank, fn_rank, gmn, gmx);
   }
-  }
-  STAMP(P, li, 10);
+}
 
+// The end of every segment select: mn / scale from the kept values' min / max (+ the kept ties' ±T), the segment's
+// T*, tie budget, mn, scale, and the in-order scan over its units — global tie prefix, output offsets (= the wire-v2
+// starts), each unit's emit parameters (k_emit loads them with the unit's own words, in one round): {T*, tie budget |
+// raw-data emit << 31, mn, scale} — raw-data emit for every unit of a raw-path segment, and for the units of a
+// zero-tie segment whose K-keys the quota reaches. done: the per-unit counts are in S.ge (above | equal << 16), else
+// in gtC / eqC. Block-level.
+template <int NT, bool RAW>
+DEV void select_finish(const Params& P, uint32_t s, const SegDev& sd, SelSmem& S, bool done, bool zero_tie,
+                       uint32_t raw_path, uint32_t T, uint32_t rt, uint32_t fp_rank, uint32_t fn_rank, float gmn,
+                       float gmx) {
+  const uint32_t t = threadIdx.x;
+  const uint32_t lb = sd.lu_begin, nu = sd.unit_end - sd.unit_begin;
   float mn = 0.0f, scale = 0.0f;
   if (!RAW) {
     const float tv = __uint_as_float(T);
@@ -2021,11 +2053,6 @@ DEV void segment_select(const Params& P, uint32_t li, SelSmem& S) {
     pst(P, P.mn + s, mn);
     pst(P, P.scale + s, scale);
   }
-  STAMP(P, li, 11);
-
-  // in-order scan over the units: global tie prefix and output offsets; each unit's emit parameters (k_emit loads
-  // them with the unit's own words, in one round): {T*, tie budget | raw-data emit << 31, mn, scale} — raw-data
-  // emit for every unit of a raw-path segment, and for the units of a zero-tie segment whose zeros the quota reaches
   uint32_t carry_e = 0, carry_sel = 0;
   for (uint32_t c0 = 0; c0 < nu; c0 += NT) {
     const uint32_t i = c0 + t;
@@ -2047,6 +2074,43 @@ DEV void segment_select(const Params& P, uint32_t li, SelSmem& S) {
       P.uemit[lb + i] = make_uint4(T, rt | (rawu << 31), __float_as_uint(mn), __float_as_uint(scale));
     }
   }
+}
+
+template <int NT, bool DELTA, bool RAW>
+DEV void segment_select(const Params& P, uint32_t li, SelSmem& S) {
+  const uint32_t t = threadIdx.x;
+  const uint32_t s = P.large_list[li];
+  const SegDev sd = P.lsegs[li];  // (same load round as s and the select state)
+  const uint4 st = P.sstate[li];
+  const uint32_t lb = sd.lu_begin, nu = sd.unit_end - sd.unit_begin;
+  STAMP(P, li, 0);
+  uint32_t T = 0, rt = 0, fp_rank = NONE, fn_rank = NONE;
+  float gmn = qnan(), gmx = qnan();
+  const bool zero_tie = st.w == 2;  // the k-th key is the segment's tie key K (segment_pick; tie mode)
+  bool done;
+  if (zero_tie) {
+    // every record kept (k_gwin's per-unit counts above the empty window), the first rt K-keys by index. K = 0: a
+    // zero's sign does not matter to mn / scale (canonicalised + 0.0f below), so one "positive tie" stands for them;
+    // K > 0: the segment-wide ranks of the first +K and -K ties (zero_tie_ranks)
+    const uint32_t g0 = sd.g_begin, ng = (nu + GU - 1) / GU;  // ng <= UCAP / GU <= NT
+    const uint32_t tk = P.tlo[lb] & KEY_MAX;
+    gmn = t < ng ? P.gmm[2 * (g0 + t)] : qnan();
+    gmx = t < ng ? P.gmm[2 * (g0 + t) + 1] : qnan();
+    for (uint32_t i = t; i < nu; i += NT) S.ge[i] = P.gtC[lb + i] | (P.cntZ[lb + i] << 16);
+    __syncthreads();
+    T = tk;
+    rt = st.z;
+    fp_rank = rt > 0 ? 0u : NONE;
+    if (tk != 0u) zero_tie_ranks<NT>(P, lb, nu, S, fp_rank, fn_rank);  // (block-uniform)
+    done = true;
+  } else {
+    done = st.w == 0 && select_from_groups<NT>(P, sd, lb, nu, st, S, T, rt, fp_rank, fn_rank, gmn, gmx);
+  }
+  uint32_t raw_path = 0;
+  STAMP(P, li, 1);
+  if (!done) select_fallback<NT, DELTA>(P, s, sd, S, T, rt, fp_rank, fn_rank, gmn, gmx, raw_path);
+  STAMP(P, li, 10);
+  select_finish<NT, RAW>(P, s, sd, S, done, zero_tie, raw_path, T, rt, fp_rank, fn_rank, gmn, gmx);
   STAMP(P, li, 12);
 }
 
@@ -2070,8 +2134,6 @@ constexpr uint32_t EMIT_UPW = 8u;  // large units per k_emit wave in batches (C3
 // wave 5.1)
 constexpr uint32_t EMIT_UPW_LAT = 1u;
 constexpr uint32_t EMIT_UPW_LATENCY = EMIT_UPW_LAT;
-
-DEV uint32_t rl(uint32_t v, uint32_t l) { return (uint32_t)__builtin_amdgcn_readlane((int)v, (int)l); }
 
 // the raw-data emit of one large unit (its segment took the raw-data path): re-read the unit, keep key > T
 // and the ties whose segment-wide rank (eqp + ties before them) is < rt, in index order
@@ -3602,6 +3664,20 @@ int coalac_workspace_fallbacks(coalac_plan_t plan, const void* d_ws, void* strea
   for (uint32_t s2 : large) c += st[s2] == 1;
   *out = c;
   return COALAC_OK;
+}
+
+int coalac_debug_brackets(coalac_plan_t plan, const void* d_ws, void* stream, uint32_t* host_tlo, uint32_t* host_thi,
+                          int n) {
+  if (!plan || !d_ws || !host_tlo || !host_thi || n < 0) return fail(COALAC_EINVAL, "coalac_debug_brackets: bad argument");
+  if (plan->dense) return 0;
+  const size_t cnt = std::min<size_t>((size_t)n, plan->n_lunits);
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  if (cnt) {
+    HIP_CHECK(hipMemcpyAsync(host_tlo, static_cast<const uint8_t*>(d_ws) + plan->ws.tlo, 4 * cnt, hipMemcpyDeviceToHost, s));
+    HIP_CHECK(hipMemcpyAsync(host_thi, static_cast<const uint8_t*>(d_ws) + plan->ws.thi, 4 * cnt, hipMemcpyDeviceToHost, s));
+  }
+  HIP_CHECK(hipStreamSynchronize(s));
+  return (int)cnt;
 }
 
 int coalac_debug_stamps(coalac_plan_t plan, const void* d_ws, void* stream, uint64_t* host, int n) {

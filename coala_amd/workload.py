@@ -64,6 +64,15 @@ def _numel(shape):
     return n
 
 
+def sign_step(flat, base, seed, lr=1e-3):
+    """trained = fl(w_global -+ lr) in place of `flat`: one sign-like local step (signSGD, the first Adam step), so
+    every |delta| is lr up to the rounding of the subtraction — heavy near-ties at the k-th key (bench.py C3_signs)."""
+    import torch
+    g = torch.Generator(device=flat.device).manual_seed(seed)
+    flat.copy_(base + torch.where(torch.rand(flat.numel(), generator=g, device=flat.device) < 0.5, -lr, lr))
+    return flat
+
+
 def freeze_segments(flat, table, trained):
     """Zero every fp32 segment of every client except the `trained` ones (segment indices of one client's
     layout): the delta of a frozen tensor is exactly zero."""

@@ -177,6 +177,12 @@ int coalac_workspace_fallbacks(coalac_plan_t plan, const void* d_ws, void* strea
  * `stream`). Returns the count copied or a negative error. */
 int coalac_debug_stamps(coalac_plan_t plan, const void* d_ws, void* stream, uint64_t* host, int n);
 
+/* Diagnostics: copy the sampled brackets {T_lo, T_hi} of the first n large units (plan order: the large segments'
+ * units, segment after segment) of the last encode with d_ws to host (synchronises `stream`). T_lo carries the tie
+ * flag (bit 31) of a tie-mode segment. Returns the count copied or a negative error. */
+int coalac_debug_brackets(coalac_plan_t plan, const void* d_ws, void* stream, uint32_t* host_tlo, uint32_t* host_thi,
+                          int n);
+
 #ifdef __cplusplus
 }
 #endif

@@ -3,7 +3,8 @@
 The configs (BASELINE.json): C2 16 x ResNet-18 (179 M elements, 3 concurrent
 sub-batches), C3 16 x ResNet-50 (410 M, 2 sub-batches; the headline), C4 16 x ViT-B/16 (1.385 G
 elements, 338 k units: the uint32 unit / group indexing at its largest), C5 one GPU's share of the
-heterogeneous splitFL round (MixedTable, one latency-bound plan), and the C3 share in delta mode. Each
+heterogeneous splitFL round (MixedTable, one latency-bound plan), and the C3 share in delta mode, at the other
+ratios, after a sign-like step (near-ties), and C4 with a frozen backbone (zero ties). Each
 batch is synthesised on the GPU exactly as bench.py does (coala_amd/workload.py), encoded and decoded
 with the SplitPipeline the bench times, and compared client by client with oracle/codec_oracle.py run
 over a spawned process pool (tests/oracle_pool.py) on a shared-memory copy of the same batch.
@@ -20,23 +21,26 @@ import torch
 from coala_amd.compression import SplitPipeline
 from coala_amd.compression.spec import SegmentTable
 from coala_amd.layouts import fp32_sizes
-from coala_amd.workload import c5_share, freeze_segments, head_only, mixed_table, synth_batch
+from coala_amd.workload import c5_share, freeze_segments, head_only, mixed_table, sign_step, synth_batch
 from oracle import codec_oracle as O
 from tests.oracle_pool import SharedBatch, oracle_clients
 
 pytestmark = pytest.mark.gpu
 
-# name -> (layout | "c5", clients, sub-batches, mode, ratio, frozen backbone): bench.py CONFIGS
+# name -> (layout | "c5", clients, sub-batches, mode, ratio, trained): bench.py CONFIGS; trained: how the trained
+# weights derive from the base in delta mode (None: synthesised independently)
 CASES = {
-    "C2": ("resnet18", 16, 3, "weights", 0.01, False),
-    "C3": ("resnet50_tv", 16, 2, "weights", 0.01, False),
-    "C4": ("vit_b16", 16, 2, "weights", 0.01, False),
-    "C5": ("c5", None, 1, "weights", 0.01, False),
-    "C3-delta": ("resnet50_tv", 16, 2, "delta", 0.01, False),
-    "C3-r0.001": ("resnet50_tv", 16, 2, "weights", 0.001, False),
-    "C3-r0.1": ("resnet50_tv", 16, 2, "weights", 0.1, False),
+    "C2": ("resnet18", 16, 3, "weights", 0.01, None),
+    "C3": ("resnet50_tv", 16, 2, "weights", 0.01, None),
+    "C4": ("vit_b16", 16, 2, "weights", 0.01, None),
+    "C5": ("c5", None, 1, "weights", 0.01, None),
+    "C3-delta": ("resnet50_tv", 16, 2, "delta", 0.01, None),
+    "C3-r0.001": ("resnet50_tv", 16, 2, "weights", 0.001, None),
+    "C3-r0.1": ("resnet50_tv", 16, 2, "weights", 0.1, None),
     # FedPEFT's frozen backbone (application/FedPEFT/lora.py:64): every tensor but the head an exact-zero delta
-    "C4-frozen": ("vit_b16", 16, 2, "delta", 0.01, True),
+    "C4-frozen": ("vit_b16", 16, 2, "delta", 0.01, "frozen"),
+    # one sign-like local step: trained = fl(w_global -+ 1e-3), near-ties at the k-th key (bench.py C3_signs)
+    "C3-signs": ("resnet50_tv", 16, 2, "delta", 0.01, "signs"),
 }
 
 
@@ -55,14 +59,16 @@ def _to_shared(t):
 
 @pytest.mark.parametrize("case", list(CASES))
 def test_fullsize_share_bit_exact_vs_oracle(cuda, case):
-    layout, clients, split, mode, ratio, frozen = CASES[case]
+    layout, clients, split, mode, ratio, trained = CASES[case]
     bits = 8
     table, ids = _table(layout, clients, ratio)
     flat = synth_batch(table, cuda, client_ids=ids)
     base = synth_batch(table, cuda, client_ids=[10_000 + i for i in ids]) if mode == "delta" else None
-    if frozen:  # as bench.py's C4_frozen: trained = base + delta, the frozen tensors' deltas exactly zero
+    if trained == "frozen":  # as bench.py's C4_frozen: trained = base + delta, the frozen tensors' deltas exactly zero
         freeze_segments(flat, table, head_only(layout))
         flat.add_(base)
+    elif trained == "signs":  # as bench.py's C3_signs
+        sign_step(flat, base, 4242)
     # host copies for the oracle (shared memory: the spawned workers map them, nothing is pickled)
     sb = _to_shared(flat)
     bb = _to_shared(base) if base is not None else None

@@ -29,7 +29,7 @@ def to_flat(table, xs):
     return flat
 
 
-def run_both(sizes, ratio, bits, xs, bases=None, flags=0, clients=1):
+def run_both(sizes, ratio, bits, xs, bases=None, flags=0, clients=1, brackets=False):
     plan = CodecPlan(sizes, ratio, bits, clients=clients)
     table = plan.table
     flat = to_flat(table, xs)
@@ -46,6 +46,13 @@ def run_both(sizes, ratio, bits, xs, bases=None, flags=0, clients=1):
     g = dict(idx=enc.idx.cpu().numpy(), vals=enc.vals.cpu().numpy(), mn=enc.mn.cpu().numpy(),
              scale=enc.scale.cpu().numpy(), ustart=enc.ustart.cpu().numpy(), dec=dec.cpu().numpy(),
              dec_v1=dec_v1.cpu().numpy(), fallbacks=plan.fallbacks(ws))
+    if brackets:  # the sampled {T_lo, T_hi} of every large unit (coalac_debug_brackets)
+        import ctypes
+        nl = sum((int(n) + 4095) // 4096 for n in table.segs[:, 1] if n > small_limit(table.segs[:, 1]))
+        lo, hi = (ctypes.c_uint32 * max(nl, 1))(), (ctypes.c_uint32 * max(nl, 1))()
+        got = plan._lib.coalac_debug_brackets(plan._h, ctypes.c_void_p(ws.data_ptr()), None, lo, hi, nl)
+        assert got == nl, (got, nl)
+        g["tlo"], g["thi"] = np.frombuffer(lo, np.uint32)[:nl].copy(), np.frombuffer(hi, np.uint32)[:nl].copy()
     segs = table.segs.astype(np.int64)
     idx, vals, mn, sc = O.encode(flat, segs, bits, base=base)
     ref_dec = O.decode(idx, vals, mn, sc, segs, bits, table.span, base=base)
@@ -448,6 +455,53 @@ def test_tie_mode_nan_inf_and_denormal_ties(cuda, clients):
     for ratio in (0.01, 0.3):
         plan, g, r = run_both(sizes, ratio, 8, xs, clients=clients)
         assert_same(plan, g, r)
+
+
+@pytest.mark.parametrize("plan_kind", ["latency", "batch"])
+@pytest.mark.parametrize("delta", [False, True])
+def test_near_tie_refinement(cuda, plan_kind, delta):
+    """Near-tied values at the k-th key (tests/sampler_model.py near_tie_layout: 16 near-tied levels, a continuous band
+    of near-ties, equal |x|, plain Gaussian — the neighbourhood of a sign-like update's k-th key), ratios 0.01 / 0.1:
+    the sampler's concentrated-bin refinement ends in each of its outcomes (a split bracket, tie mode, a lower edge K
+    seen too rarely for tie mode, no refinement; tests/test_sampler_model.py asserts they all occur). The kernel's
+    bracket of every large segment equals the model's (tests/sampler_model.py restates sample_segment), the codec
+    is bit-exact against the oracle, and exactly the segments the model predicts take the raw-data path. Delta mode: base = N(0, 1e-6) (x - base keeps the
+    near-tie structure); batch: two clients + a 33.6 M-element segment (> 8192 units)."""
+    from tests.sampler_model import bracket, ccap_for, near_tie_layout, takes_raw_path
+    rng = np.random.default_rng(77)
+    clients = 2 if plan_kind == "batch" else 1
+    xs = [near_tie_layout(rng) for _ in range(clients)]
+    if plan_kind == "batch":
+        for c in range(clients):
+            xs[c].append((rng.standard_normal(4096 * 8200) * 1e-3).astype(np.float32))
+    sizes = [x.size for x in xs[0]]
+    bases = None
+    if delta:
+        bases = [[(rng.standard_normal(n) * 1e-6).astype(np.float32) for n in sizes] for _ in range(clients)]
+        xs = [[(x + b).astype(np.float32) for x, b in zip(xc, bc)] for xc, bc in zip(xs, bases)]
+    T = len(sizes)
+    outcomes = set()
+    for ratio in (0.01, 0.1):
+        plan, g, r = run_both(sizes, ratio, 8, xs, bases, clients=clients, brackets=True)
+        assert_same(plan, g, r)
+        lim = small_limit(plan.table.segs[:, 1])
+        lu, raw = 0, 0
+        for c in range(clients):
+            for t in range(T):
+                n = sizes[t]
+                if n <= lim:
+                    continue
+                d = xs[c][t] if bases is None else (xs[c][t] - bases[c][t]).astype(np.float32)
+                k = int(plan.table.segs[c * T + t, 2])
+                tlo, thi, o = bracket(d, k, c * T + t)
+                outcomes.add(o)
+                assert (int(g["tlo"][lu]), int(g["thi"][lu])) == (tlo, thi), (ratio, c, t, n, o)
+                raw += takes_raw_path(d, k, tlo, thi, ccap_for([ratio]))
+                lu += (n + 4095) // 4096
+        # the segments the model sends to the raw-data path (a split bracket of the 16-level input at ratio 0.1
+        # holds more candidates than a unit's record slots), and no other
+        assert g["fallbacks"] == raw, (ratio, g["fallbacks"], raw)
+    assert {"split", "tie", "edge"} <= outcomes, outcomes
 
 
 def test_tie_mode_sample_miss_takes_raw_path(cuda):
