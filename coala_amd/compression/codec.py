@@ -1459,8 +1459,8 @@ class _TreeRecipe:
         every module's tables unchanged) and its root — (None, None) if there is none. The root is taken
         while the pool lock is held, so the moment a tree is chosen it is no longer idle for any other
         thread (the remote server decodes from one thread per upload, coala/server/service.py:74).
-        Trees not handed out for a while (2 x the pool size + EVICT_SLACK calls: more than a round needs)
-        are dropped from the pool."""
+        Idle trees not handed out for a while (2 x the pool size + EVICT_SLACK calls: more than a round needs)
+        are dropped from the pool; held ones stay."""
         if not self.pool or not isinstance(raw, RawState):
             return None, None
         self._current()
@@ -1474,9 +1474,12 @@ class _TreeRecipe:
                     sk.generation += 1
                     sk.last = self.tick
                     break
+            # only IDLE trees go: a tree still held (a server keeps round r's uploads until round r + 1 replaces them,
+            # coala/server/base.py:377-381) becomes reusable when its holder lets go, however long that takes
             horizon = 2 * len(self.pool) + self.EVICT_SLACK
             if any(self.tick - sk.last > horizon for sk in self.pool):
-                self.pool[:] = [sk for sk in self.pool if self.tick - sk.last <= horizon]
+                self.pool[:] = [sk for sk in self.pool
+                                if self.tick - sk.last <= horizon or sk is found or sk.counts() != sk.base]
             return found, root
 
     def refresh(self, sk):

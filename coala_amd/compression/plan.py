@@ -354,9 +354,10 @@ class CodecPlan:
         self._check_encoded(enc)
         if not getattr(self.table, "uniform", False):
             raise ValueError("fused aggregation needs a plan over copies of one layout (a SegmentTable)")
-        if self.dense and enc.idx.numel() == 0:  # (the aggregate kernel reads explicit indices: implied ones made here)
-            with _on(stream):
-                enc = Encoded(self.implied_indices(), enc.vals, enc.mn, enc.scale, None)
+        if self.dense and enc.idx.numel() == 0:  # (the aggregate kernel reads explicit indices: the implied ones and
+            with _on(stream):                      # the implied starts, both made once per plan)
+                enc = Encoded(self.implied_indices(), enc.vals, enc.mn, enc.scale,
+                              self.implied_starts() if enc.ustart is None else enc.ustart)
         if enc.ustart is None:
             enc = Encoded(enc.idx, enc.vals, enc.mn, enc.scale, self.unit_starts(enc.idx, stream))
         ust = self._check_encoded(enc)
@@ -397,6 +398,15 @@ class CodecPlan:
         if t is None:
             one = torch.cat([torch.arange(n, dtype=torch.int32) for n in self.table.segs[:, 1].tolist()])
             t = self._implied = one.to(self.device)
+        return t
+
+    def implied_starts(self):
+        """A dense plan's per-unit starts (unit j of a segment starts at entry 4096 j: every element is kept), every
+        client, as a device int32 tensor, made once (recomputed by a device searchsorted per call)."""
+        t = self.__dict__.get("_implied_starts")
+        if t is None:
+            one = torch.cat([torch.arange(0, n, UNIT, dtype=torch.int32) for n in self.table.segs[:, 1].tolist()])
+            t = self._implied_starts = one.to(self.device)
         return t
 
     def fallbacks(self, workspace, stream=None):

@@ -235,6 +235,16 @@ DEV uint32_t mbcnt(uint64_t m) {
 // trip per step (~100+ cycles), and a wave scan is six dependent steps. dpp<CTRL>: lane i reads lane src(i) of v
 // (0 where the source lies outside its row or the row is masked off). CTRL: 0x111 + n - 1 row_shr:n, 0x128 row_ror:8,
 // 0x140 row_mirror, 0x141 row_half_mirror, 0x142 row_bcast:15, 0x143 row_bcast:31, 0xB1 / 0x4E quad_perm xor 1 / xor 2.
+// min(a, b) kept out of the optimiser's reach: next to min(r, x), the tie quota `x >= r ? 0 : min(c, r - x)` was folded
+// into a saturating subtract whose clamp the gfx950 build then dropped — min(r, x) came out as x and a unit reserved a
+// slot for a tie it did not keep (k_select, round 6: tools/dbg_encode.py, resnet18 ratio 0.1 delta). With qp = this,
+// the quota is min(c, r - qp): r - qp never wraps.
+DEV uint32_t umin_opaque(uint32_t a, uint32_t b) {
+  uint32_t r;
+  asm("v_min_u32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+
 template <int CTRL, int ROWM = 0xF>
 DEV uint32_t dpp(uint32_t v) {
   return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, ROWM, 0xF, false);
@@ -325,6 +335,36 @@ DEV uint32_t block_excl_scan(uint32_t v, uint32_t* sh, uint32_t& total) {
   }
   total = tot;
   return off + inc - v;
+}
+
+// Two block-wide exclusive scans sharing one pair of barriers (sh needs >= 2 * NT/64 words). Call from all threads.
+template <int NT>
+DEV void block_excl_scan2(uint32_t a, uint32_t b, uint32_t* sh, uint32_t& ea, uint32_t& eb, uint32_t& ta,
+                          uint32_t& tb) {
+  constexpr int NW = NT / 64;
+  const uint32_t lane = lane_id(), w = threadIdx.x >> 6;
+  const uint32_t ia = wave_incl_scan(a), ib = wave_incl_scan(b);
+  __syncthreads();
+  if (lane == 63) {
+    sh[w] = ia;
+    sh[NW + w] = ib;
+  }
+  __syncthreads();
+  uint32_t oa = 0, ob = 0, sa = 0, sb = 0;
+#pragma unroll
+  for (int i = 0; i < NW; ++i) {
+    const uint32_t x = sh[i], y = sh[NW + i];
+    if ((uint32_t)i < w) {
+      oa += x;
+      ob += y;
+    }
+    sa += x;
+    sb += y;
+  }
+  ea = oa + ia - a;
+  eb = ob + ib - b;
+  ta = sa;
+  tb = sb;
 }
 
 template <int NT>
@@ -942,7 +982,7 @@ DEV void small_encode(const Params& P, uint32_t si, float* vals, uint32_t* hist,
   }
   uint32_t eqtot;
   const uint32_t eqpre = block_excl_scan<NT>(eq, sh, eqtot);
-  const uint32_t quota = eqpre >= rt ? 0u : min(eq, rt - eqpre);
+  const uint32_t quota = min(eq, rt - umin_opaque(rt, eqpre));
   uint32_t seltot;
   const uint32_t opre = block_excl_scan<NT>(gt + quota, sh, seltot);
   STAMP(P, s, 5);
@@ -1737,6 +1777,7 @@ __global__ __launch_bounds__(NT) void k_gwin(Params P) {
 // its ccap record slots): T* from the raw keys (segment_select), per-unit counts from the raw data here,
 // and the emit re-reads the raw data (emit_raw_unit). No candidate record is used.
 // ------------------------------------------------------------------------------------------------
+constexpr uint32_t RAW_NB = 2u;  // load rounds per unit of a raw-data pass (round 5: 4 rounds of 4 float4 per lane)
 // One wave's pass over a unit's raw data (row by row, index order): per element whether key > T and
 // whether key == T, handed to f(row, j, x, gt, tie) for every lane (ballots allowed inside f).
 template <bool DELTA, class F>
@@ -1745,12 +1786,13 @@ DEV void raw_unit_rows(const Params& P, const UnitDev& L, F&& f) {
   const float* xin = P.inptr != nullptr ? P.inptr[L.seg] + L.start : P.in + L.off;
   const __amdgpu_buffer_rsrc_t rin = unit_rsrc(xin, L.len);
   const __amdgpu_buffer_rsrc_t rbase = unit_rsrc(DELTA ? P.base + L.off : xin, L.len);
-  for (uint32_t nb = 0; nb < 4; ++nb) {  // 4 float4 per lane in flight (register-lean)
-    float4 v[4];
+  for (uint32_t nb = 0; nb < RAW_NB; ++nb) {  // UNIT_IT / RAW_NB float4 per lane in flight
+    constexpr uint32_t IT = UNIT_IT / RAW_NB;
+    float4 v[IT];
 #pragma unroll
-    for (uint32_t i = 0; i < 4; ++i) v[i] = unit_load_x4<DELTA>(rin, rbase, ((nb * 4 + i) * 64 + lane) * 16);
+    for (uint32_t i = 0; i < IT; ++i) v[i] = unit_load_x4<DELTA>(rin, rbase, ((nb * IT + i) * 64 + lane) * 16);
 #pragma unroll
-    for (uint32_t i = 0; i < 4; ++i) f(nb * 4 + i, v[i]);
+    for (uint32_t i = 0; i < IT; ++i) f(nb * IT + i, v[i]);
   }
 }
 
@@ -1759,7 +1801,7 @@ DEV void raw_unit_rows(const Params& P, const UnitDev& L, F&& f) {
 // unit ranges in order. Block-level: call from all threads.
 template <int NT, bool DELTA>
 DEV void raw_counts(const Params& P, uint32_t lb, uint32_t nu, uint32_t T, uint32_t* sh, uint32_t* wcnt,
-                    uint32_t& fp, uint32_t& fn, float& gmn, float& gmx) {
+                    uint32_t& fp, uint32_t& fn, float& gmn, float& gmx, uint32_t* ge) {
   constexpr int NW = NT / 64;
   const uint32_t lane = lane_id(), wv = threadIdx.x >> 6;
   const uint32_t u0 = (uint32_t)((uint64_t)nu * wv / NW), u1 = (uint32_t)((uint64_t)nu * (wv + 1) / NW);
@@ -1809,6 +1851,7 @@ DEV void raw_counts(const Params& P, uint32_t lb, uint32_t nu, uint32_t T, uint3
     if (lane == 0) {
       pst(P, P.gtC + lb + u, ug);
       pst(P, P.eqC + lb + u, ue);
+      if (u < UCAP) ge[u] = ug | (ue << 16);  // (select_finish reads LDS: other threads own the unit there)
     }
   }
   // wave prefixes of the tie counts -> segment-wide ranks of the first positive / negative tie
@@ -1939,22 +1982,55 @@ DEV void window_resolve(SelSmem& S, uint32_t W, uint4 st, float lmn0, float lmx0
   __syncthreads();
 }
 
-// Zero-tie ranks (tie mode, the k-th key is the segment's tie key K > 0): the segment-wide ranks of the first +K and
-// -K ties, from the units' tie prefixes (S.ge >> 16 = the unit's K-keys) and in-unit ranks (tsgn). Block-level.
+// Units per thread when a block's threads own contiguous unit ranges (select_finish, the zero-tie select): nu <= UCAP
+// units in one pass
 template <int NT>
-DEV void zero_tie_ranks(const Params& P, uint32_t lb, uint32_t nu, SelSmem& S, uint32_t& fp_rank, uint32_t& fn_rank) {
+constexpr uint32_t unit_span() { return (UCAP + NT - 1) / NT; }
+
+// The zero-tie select (tie mode, the k-th key is the segment's tie key K): every record is kept and the first rt K-keys
+// by index. Thread t owns the contiguous units [t * E, t * E + E) (nu <= UCAP) and loads their above-K record counts,
+// K-key counts and (K > 0) first +-K tie ranks in ONE round; S.ge gets above | K-keys << 16. K > 0: the segment-wide
+// ranks of the first +K and -K ties, from one block scan of the units' K-key counts and their in-unit ranks (tsgn).
+// (Round 5 loaded each 256-unit chunk after the previous one's scan: three dependent global rounds per 576-unit
+// segment, each behind the other sub-batch's streaming — k_select 185 vs 38 us per 8-client launch on C3_signs.)
+template <int NT>
+DEV void zero_tie_select(const Params& P, uint32_t lb, uint32_t nu, uint32_t tk, SelSmem& S, uint32_t& fp_rank,
+                         uint32_t& fn_rank) {
+  constexpr uint32_t E = unit_span<NT>();
   const uint32_t t = threadIdx.x;
-  uint32_t lp = NONE, ln = NONE, carry = 0;
-  for (uint32_t c0 = 0; c0 < nu; c0 += NT) {
-    const uint32_t i = c0 + t;
-    const uint32_t z = i < nu ? S.ge[i] >> 16 : 0u;
-    uint32_t tot;
-    const uint32_t ex = block_excl_scan<NT>(z, S.sh, tot) + carry;
-    carry += tot;
-    if (i < nu) {
-      const uint32_t sg = P.tsgn[lb + i], fp = sg & 0xFFFFu, fn = sg >> 16;
+  const uint32_t u0 = min(nu, t * E);
+  uint32_t zg[E], zc[E], zs[E];
+#pragma unroll
+  for (uint32_t j = 0; j < E; ++j) {
+    const uint32_t u = min(u0 + j, nu - 1);  // (clamped: one round, every load unconditional)
+    zg[j] = P.gtC[lb + u];
+    zc[j] = P.cntZ[lb + u];
+    zs[j] = tk != 0u ? P.tsgn[lb + u] : 0xFFFFFFFFu;
+  }
+  uint32_t z = 0;
+#pragma unroll
+  for (uint32_t j = 0; j < E; ++j) {
+    if (u0 + j < nu) {
+      S.ge[u0 + j] = zg[j] | (zc[j] << 16);
+      z += zc[j];
+    }
+  }
+  fp_rank = NONE;
+  fn_rank = NONE;
+  if (tk == 0u) {  // (block-uniform) K = 0: a zero's sign does not matter to mn / scale
+    __syncthreads();
+    return;
+  }
+  uint32_t tot;
+  uint32_t ex = block_excl_scan<NT>(z, S.sh, tot);  // (barriers inside: S.ge complete after them)
+  uint32_t lp = NONE, ln = NONE;
+#pragma unroll
+  for (uint32_t j = 0; j < E; ++j) {
+    if (u0 + j < nu) {
+      const uint32_t fp = zs[j] & 0xFFFFu, fn = zs[j] >> 16;
       if (fp != 0xFFFFu) lp = min(lp, ex + fp);
       if (fn != 0xFFFFu) ln = min(ln, ex + fn);
+      ex += zc[j];
     }
   }
   if (t == 0) {
@@ -2009,7 +2085,7 @@ DEV void select_fallback(const Params& P, uint32_t s, const SegDev& sd, SelSmem&
         },
         0u, KEY_MAX, rk, S.hist, S.sh);
     rt = rk;
-    raw_counts<NT, DELTA>(P, lb, nu, T, S.sh, S.wcnt, fp_rank, fn_rank, gmn, gmx);
+    raw_counts<NT, DELTA>(P, lb, nu, T, S.sh, S.wcnt, fp_rank, fn_rank, gmn, gmx, S.ge);
     raw_path = 1u;
     if (t == 0) pst(P, P.status + s, 1u);
   } else {
@@ -2053,26 +2129,49 @@ DEV void select_finish(const Params& P, uint32_t s, const SegDev& sd, SelSmem& S
     pst(P, P.mn + s, mn);
     pst(P, P.scale + s, scale);
   }
-  uint32_t carry_e = 0, carry_sel = 0;
-  for (uint32_t c0 = 0; c0 < nu; c0 += NT) {
-    const uint32_t i = c0 + t;
-    const bool valid = i < nu;
-    const uint32_t e = valid ? (done ? S.ge[i] >> 16 : P.eqC[lb + i]) : 0u;  // fast path: counts in LDS
-    uint32_t tot;
-    const uint32_t ex = block_excl_scan<NT>(e, S.sh, tot) + carry_e;
-    carry_e += tot;
-    const uint32_t quota = !valid ? 0u : (ex >= rt ? 0u : min(e, rt - ex));
-    const uint32_t sel = valid ? (done ? S.ge[i] & 0xFFFFu : P.gtC[lb + i]) + quota : 0u;
-    uint32_t tot2;
-    const uint32_t so = block_excl_scan<NT>(sel, S.sh, tot2) + carry_sel;
-    carry_sel += tot2;
-    if (valid) {
-      pst(P, P.eqpre + lb + i, ex);
-      pst(P, P.outoff + lb + i, so);
-      if (P.ustart_out != nullptr) pst(P, P.ustart_out + sd.unit_begin + i, so);  // wire v2: the unit's start
-      const uint32_t rawu = raw_path | (zero_tie && quota > 0 ? 1u : 0u);
-      P.uemit[lb + i] = make_uint4(T, rt | (rawu << 31), __float_as_uint(mn), __float_as_uint(scale));
+  // thread t owns the contiguous units [t * E, t * E + E) of each UCAP-unit chunk: ONE paired scan of the tie and
+  // above-T* counts per chunk (the quotas of the units before u sum to min(rt, ties before u), so u's output offset is
+  // its above-T* prefix + that). The counts are in LDS (S.ge: every path leaves them there for nu <= UCAP); a segment
+  // of more units (the generic path, chunk by chunk) reads gtC / eqC with L1-bypassing loads — other threads of this
+  // block wrote them, and a plain load may hit a line this CU's L1 cached before (cdna_hip_programming.md §6 G16)
+  constexpr uint32_t E = unit_span<NT>();
+  const bool lds = done || nu <= UCAP;
+  uint32_t carry_e = 0, carry_g = 0;
+  for (uint32_t c0 = 0; c0 < nu; c0 += E * NT) {
+    const uint32_t u0 = min(nu, c0 + t * E), u1 = min(nu, u0 + E);
+    uint32_t ce[E], cg[E], se = 0, sg = 0;
+#pragma unroll
+    for (uint32_t j = 0; j < E; ++j) {
+      const uint32_t u = min(u0 + j, nu - 1);
+      const uint32_t v = lds ? S.ge[u] : 0u;
+      ce[j] = u0 + j < u1 ? (lds ? v >> 16 : __builtin_nontemporal_load(P.eqC + lb + u)) : 0u;
+      cg[j] = u0 + j < u1 ? (lds ? v & 0xFFFFu : __builtin_nontemporal_load(P.gtC + lb + u)) : 0u;
+      se += ce[j];
+      sg += cg[j];
     }
+    uint32_t ex_e, ex_g, te, tg;
+    block_excl_scan2<NT>(se, sg, S.sh, ex_e, ex_g, te, tg);
+    ex_e += carry_e;
+    ex_g += carry_g;
+    carry_e += te;
+    carry_g += tg;
+#pragma unroll
+    for (uint32_t j = 0; j < E; ++j) {
+      const uint32_t u = u0 + j;
+      if (u < u1) {
+        const uint32_t qp = umin_opaque(rt, ex_e);  // ties kept before u (see umin_opaque)
+        const uint32_t quota = min(ce[j], rt - qp);
+        const uint32_t so = ex_g + qp;
+        pst(P, P.eqpre + lb + u, ex_e);
+        pst(P, P.outoff + lb + u, so);
+        if (P.ustart_out != nullptr) pst(P, P.ustart_out + sd.unit_begin + u, so);  // wire v2: the unit's start
+        const uint32_t rawu = raw_path | (zero_tie && quota > 0 ? 1u : 0u);
+        P.uemit[lb + u] = make_uint4(T, rt | (rawu << 31), __float_as_uint(mn), __float_as_uint(scale));
+        ex_e += ce[j];
+        ex_g += cg[j];
+      }
+    }
+    if (c0 + E * NT < nu) __syncthreads();  // (S.sh reused by the next chunk's scan)
   }
 }
 
@@ -2089,19 +2188,17 @@ DEV void segment_select(const Params& P, uint32_t li, SelSmem& S) {
   const bool zero_tie = st.w == 2;  // the k-th key is the segment's tie key K (segment_pick; tie mode)
   bool done;
   if (zero_tie) {
-    // every record kept (k_gwin's per-unit counts above the empty window), the first rt K-keys by index. K = 0: a
-    // zero's sign does not matter to mn / scale (canonicalised + 0.0f below), so one "positive tie" stands for them;
-    // K > 0: the segment-wide ranks of the first +K and -K ties (zero_tie_ranks)
+    // every record kept (k_gwin's per-unit counts above the empty window), the first rt K-keys by index
+    // (zero_tie_select). K = 0: a zero's sign does not matter to mn / scale (canonicalised + 0.0f below), so one
+    // "positive tie" stands for them
     const uint32_t g0 = sd.g_begin, ng = (nu + GU - 1) / GU;  // ng <= UCAP / GU <= NT
     const uint32_t tk = P.tlo[lb] & KEY_MAX;
     gmn = t < ng ? P.gmm[2 * (g0 + t)] : qnan();
     gmx = t < ng ? P.gmm[2 * (g0 + t) + 1] : qnan();
-    for (uint32_t i = t; i < nu; i += NT) S.ge[i] = P.gtC[lb + i] | (P.cntZ[lb + i] << 16);
-    __syncthreads();
     T = tk;
     rt = st.z;
-    fp_rank = rt > 0 ? 0u : NONE;
-    if (tk != 0u) zero_tie_ranks<NT>(P, lb, nu, S, fp_rank, fn_rank);  // (block-uniform)
+    zero_tie_select<NT>(P, lb, nu, tk, S, fp_rank, fn_rank);
+    if (tk == 0u) fp_rank = rt > 0 ? 0u : NONE;
     done = true;
   } else {
     done = st.w == 0 && select_from_groups<NT>(P, sd, lb, nu, st, S, T, rt, fp_rank, fn_rank, gmn, gmx);
@@ -2186,13 +2283,17 @@ DEV void emit_raw_unit(const Params& P, const UnitDev& L, uint32_t T, uint32_t r
   });
 }
 
-// one wave emits the large units [lu0, lu1) (lu1 - lu0 <= UPW)
+// one wave emits the large units lu0 + g * stride, g < UPW, below lu1 (batches: stride = the number of emit waves, so a
+// wave's units lie across the plan — the units that take the raw-data emit, a tie-mode segment's first ones, spread
+// over many waves instead of filling a few with 8 raw units each: C3_signs k_emit 416 us per 8-client launch at HEAD)
 template <bool DELTA, bool RAW, uint32_t UPW, uint32_t TR>
-DEV void emit_units(const Params& P, uint32_t lu0, uint32_t lu1) {
+DEV void emit_units(const Params& P, uint32_t lu0, uint32_t lu1, uint32_t stride) {
   const uint32_t lane = lane_id();
-  // lane g < UPW holds unit lu0 + g's count, offsets and its segment's T*, tie budget, mn, scale (lanes past
-  // UPW or past the last unit repeat a valid unit; never used)
-  const uint32_t lug = min(lu0 + min(lane, UPW - 1), lu1 - 1);
+  auto unit = [&](uint32_t g) { return lu0 + g * stride; };
+  const uint32_t ng = lu0 < lu1 ? min(UPW, (lu1 - lu0 + stride - 1) / stride) : 0u;  // this wave's units
+  // lane g < UPW holds unit g's count, offsets and its segment's T*, tie budget, mn, scale (lanes past the wave's
+  // units repeat its last one; never used)
+  const uint32_t lug = unit(min(lane, ng - 1));
   uint32_t nCg, startg, eqpg, oog, Tg, rtg, stg;
   uint64_t sog;
   float mng, scg;
@@ -2231,7 +2332,7 @@ DEV void emit_units(const Params& P, uint32_t lu0, uint32_t lu1) {
     scg = RAW ? 0.0f : __uint_as_float(ue.w);
 #pragma unroll
     for (uint32_t g = 0; g < UPW; ++g) {
-      const uint32_t lu = min(lu0 + g, lu1 - 1), nC = rl(nCg, g);
+      const uint32_t lu = unit(min(g, ng - 1)), nC = rl(nCg, g);
       const uint32_t last = nC ? nC - 1 : 0u;
       const uint64_t r0 = (uint64_t)lu * P.ccap;  // unconditional (clamped) loads
       rec0[g] = make_uint2(P.cpos[r0 + min(lane, last)], P.cval[r0 + min(lane, last)]);
@@ -2240,12 +2341,12 @@ DEV void emit_units(const Params& P, uint32_t lu0, uint32_t lu1) {
 #pragma unroll
   for (uint32_t g = 0; g < UPW; ++g) {
     const uint32_t nC = rl(nCg, g);
-    if (lu0 + g < lu1 && rl(stg, g) != 0) {
+    if (g < ng && rl(stg, g) != 0) {
       const uint64_t so = ((uint64_t)rl((uint32_t)(sog >> 32), g) << 32) | rl((uint32_t)sog, g);
-      emit_raw_unit<DELTA, RAW>(P, P.lunits[lu0 + g], rl(Tg, g), rl(rtg, g), rl(eqpg, g), so + rl(oog, g),
+      emit_raw_unit<DELTA, RAW>(P, P.lunits[unit(g)], rl(Tg, g), rl(rtg, g), rl(eqpg, g), so + rl(oog, g),
                                 __uint_as_float(rl(__float_as_uint(mng), g)), __uint_as_float(rl(__float_as_uint(scg), g)));
-    } else if (lu0 + g < lu1 && nC != 0) {
-      const uint32_t lu = lu0 + g;
+    } else if (g < ng && nC != 0) {
+      const uint32_t lu = unit(g);
       const uint32_t T = rl(Tg, g), rt = rl(rtg, g), eqp = rl(eqpg, g);
       const float mn = __uint_as_float(rl(__float_as_uint(mng), g));
       const float scale = __uint_as_float(rl(__float_as_uint(scg), g));
@@ -2292,11 +2393,11 @@ DEV void emit_units(const Params& P, uint32_t lu0, uint32_t lu1) {
 template <bool DELTA, bool RAW, uint32_t UPW, uint32_t TR>  // TR: record rows per load round past the first
 __global__ __launch_bounds__(BLOCK) void k_emit(Params P) {
   const uint32_t wv = threadIdx.x >> 6;
-  const uint32_t lu0 = (blockIdx.x * WAVES + wv) * UPW;
-  if (lu0 >= P.n_lunits) return;
+  const uint32_t gw = blockIdx.x * WAVES + wv, nw = gridDim.x * WAVES;  // (UPW == 1: one unit per wave)
+  if (gw >= P.n_lunits) return;
   const bool st = blockIdx.x < P.nseg;  // diagnostics rows: block index (slots 13-14)
   if (st) STAMP(P, blockIdx.x, 13);
-  emit_units<DELTA, RAW, UPW, TR>(P, lu0, min(lu0 + UPW, P.n_lunits));
+  emit_units<DELTA, RAW, UPW, TR>(P, gw, P.n_lunits, UPW == 1 ? 1u : nw);
   if (st) STAMP(P, blockIdx.x, 14);
 }
 

@@ -29,9 +29,11 @@ def fill_client(flat, table, client_id, seed_base=1234, zero_frac=0.005, tie_fra
         zi = torch.randint(0, span, (m0,), generator=g, device=flat.device)
         flat[:span].index_fill_(0, zi, 0.0)
     if m1:
-        ti = torch.randint(0, span, (m1,), generator=g, device=flat.device)
-        tj = torch.randint(0, span, (m1,), generator=g, device=flat.device)
-        sgn = torch.randint(0, 2, (m1,), generator=g, device=flat.device).to(torch.float32) * 2.0 - 1.0
+        # distinct targets: index_copy_ with a repeated index keeps whichever write lands last on the GPU, so
+        # the data (and a test's k-th key) would change from run to run
+        ti = torch.unique(torch.randint(0, span, (m1,), generator=g, device=flat.device))
+        tj = torch.randint(0, span, (m1,), generator=g, device=flat.device)[:ti.numel()]
+        sgn = torch.randint(0, 2, (m1,), generator=g, device=flat.device)[:ti.numel()].to(torch.float32) * 2.0 - 1.0
         flat[:span].index_copy_(0, ti, flat[:span][tj].abs() * sgn)
     return flat
 

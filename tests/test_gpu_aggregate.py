@@ -55,6 +55,34 @@ def test_aggregate_matches_oracle_both_modes(cuda, bits, ratio, delta):
                 np.testing.assert_array_equal(g[off:off + n].view(np.uint32), ref[off:off + n].view(np.uint32))
 
 
+@pytest.mark.parametrize("bits", [8, 32])
+@pytest.mark.parametrize("delta", [True, False])
+def test_aggregate_dense_plan_matches_oracle(cuda, bits, delta):
+    """A dense plan (ratio 1: every element kept, indices and starts implied — the download direction's codec):
+    the fused aggregate from the implied indices and the plan's cached implied starts (made once, not per call) and
+    from the device-computed starts, bit-identical to the oracle over the same implied indices."""
+    C = 3
+    plan, one, enc, base = setup("lenet", 1.0, bits, C, delta, seed=3 + bits)
+    assert plan.dense and enc.idx.numel() == 0 and enc.ustart is None
+    weights = [4, 1, 7]
+    segs = plan.table.segs.astype(np.int64)
+    idx = plan.implied_indices()
+    h = [idx.cpu().numpy()] + [t.cpu().numpy() for t in (enc.vals, enc.mn, enc.scale)]
+    b = None if base is None else base.cpu().numpy()
+    starts = plan.implied_starts()
+    assert starts is plan.implied_starts()  # cached
+    np.testing.assert_array_equal(starts.cpu().numpy(), plan.unit_starts(idx).cpu().numpy())
+    explicit = Encoded(idx, enc.vals, enc.mn, enc.scale)  # explicit indices, starts computed on the device
+    for mode, om in (("recip", O.AGG_RECIP), ("div", O.AGG_DIV)):
+        ref = O.aggregate(*h, segs, bits, C, weights, sum(weights), om, base=b, out_span=plan.table.span_per_client)
+        for e in (enc, explicit):
+            out = plan.aggregate(e, weights, base=base, mode=mode)
+            torch.cuda.synchronize()
+            g = out.cpu().numpy()
+            for off, n in zip(plan.table.offsets, plan.table.sizes):
+                np.testing.assert_array_equal(g[off:off + n].view(np.uint32), ref[off:off + n].view(np.uint32))
+
+
 @pytest.mark.parametrize("delta", [True, False])
 def test_aggregate_matches_torch_gpu_fedavg_on_decoded(cuda, delta):
     """The reference flow on the GPU: decode each client, then weighted_sum + torch.div on cuda."""

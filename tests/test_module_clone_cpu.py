@@ -299,6 +299,29 @@ def test_recycled_storage_bumps_the_version_counter():
     assert ids
 
 
+def test_recycling_with_more_clients_per_round_than_half_the_pool():
+    """A server with more uploads per round than POOL_MAX / 2: each round's decoded module of client
+    j replaces client j's module of the previous round (coala/server/base.py:377-381), so the trees of round r stay held
+    while round r + 1 decodes. From the third round on every decode reuses a pooled tree (none is evicted while held,
+    none built anew beyond the pool's capacity), and every module holds its own update."""
+    from coala_amd.compression.codec import _TreeRecipe, _recipe
+    codec, g, base, ups, fresh = _codec_round(seed_global=7)
+    C = _TreeRecipe.POOL_MAX // 2 + 8
+    held, seen, built = {}, set(), []
+    for rnd in range(4):
+        new_ids = 0
+        for j in range(C):
+            m = codec.decode_module(ups[j % 3], g, base=base)
+            new_ids += id(m) not in seen
+            seen.add(id(m))
+            held[j] = m  # replaces client j's module of the previous round
+            del m
+        built.append(new_ids)
+    assert built[0] == C and built[2] == 0 and built[3] == 0, built
+    assert len(_recipe(g).pool) <= C + 1
+    assert all(_equal_state(held[j], fresh[j % 3]) for j in range(C))
+
+
 def test_pool_release_eviction_and_opt_out():
     """release_pool() empties the pool; trees not handed out for a while are evicted; recycle=False never
     pools or reuses a module."""
@@ -311,15 +334,22 @@ def test_pool_release_eviction_and_opt_out():
     assert len(rec.pool) == 3
     codec.release_pool()
     assert not rec.pool
-    # eviction: with the pool of 3, trees 1 and 2 stay held while tree 0 is reused again and again
+    # eviction: with the pool of 3, trees 1 and 2 stay HELD while tree 0 is reused again and again: kept past the
+    # horizon (a held tree becomes reusable when its holder lets go); released, they are idle and stale: dropped
     ms = [codec.decode_module(u, g, base=base) for u in ups]
     keep = ms[1:]
     del ms
-    for i in range(2 * 3 + _TreeRecipe.EVICT_SLACK + 3):
+    horizon = 2 * 3 + _TreeRecipe.EVICT_SLACK
+    for i in range(horizon + 3):
         m = codec.decode_module(ups[i % 3], g, base=base)
         del m
-    assert len(rec.pool) == 1  # the held trees were not handed out for longer than the horizon
-    assert all(_equal_state(k, fresh[1 + j]) for j, k in enumerate(keep))  # (evicted, not overwritten)
+    assert len(rec.pool) == 3  # held trees are not evicted
+    assert all(_equal_state(k, fresh[1 + j]) for j, k in enumerate(keep))  # (nor overwritten)
+    keep = None
+    for i in range(2):
+        m = codec.decode_module(ups[i % 3], g, base=base)
+        del m
+    assert len(rec.pool) == 1  # idle and not handed out for longer than the horizon: dropped
     # opt-out
     off = UpdateCodec(0.05, 8, "delta", OracleBackend(), recycle=False)
     codec.release_pool()
