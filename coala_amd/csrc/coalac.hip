@@ -1982,55 +1982,22 @@ DEV void window_resolve(SelSmem& S, uint32_t W, uint4 st, float lmn0, float lmx0
   __syncthreads();
 }
 
-// Units per thread when a block's threads own contiguous unit ranges (select_finish, the zero-tie select): nu <= UCAP
-// units in one pass
+// Zero-tie ranks (tie mode, the k-th key is the segment's tie key K > 0): the segment-wide ranks of the first +K and
+// -K ties, from the units' tie prefixes (S.ge >> 16 = the unit's K-keys) and in-unit ranks (tsgn). Block-level.
 template <int NT>
-constexpr uint32_t unit_span() { return (UCAP + NT - 1) / NT; }
-
-// The zero-tie select (tie mode, the k-th key is the segment's tie key K): every record is kept and the first rt K-keys
-// by index. Thread t owns the contiguous units [t * E, t * E + E) (nu <= UCAP) and loads their above-K record counts,
-// K-key counts and (K > 0) first +-K tie ranks in ONE round; S.ge gets above | K-keys << 16. K > 0: the segment-wide
-// ranks of the first +K and -K ties, from one block scan of the units' K-key counts and their in-unit ranks (tsgn).
-// (Round 5 loaded each 256-unit chunk after the previous one's scan: three dependent global rounds per 576-unit
-// segment, each behind the other sub-batch's streaming — k_select 185 vs 38 us per 8-client launch on C3_signs.)
-template <int NT>
-DEV void zero_tie_select(const Params& P, uint32_t lb, uint32_t nu, uint32_t tk, SelSmem& S, uint32_t& fp_rank,
-                         uint32_t& fn_rank) {
-  constexpr uint32_t E = unit_span<NT>();
+DEV void zero_tie_ranks(const Params& P, uint32_t lb, uint32_t nu, SelSmem& S, uint32_t& fp_rank, uint32_t& fn_rank) {
   const uint32_t t = threadIdx.x;
-  const uint32_t u0 = min(nu, t * E);
-  uint32_t zg[E], zc[E], zs[E];
-#pragma unroll
-  for (uint32_t j = 0; j < E; ++j) {
-    const uint32_t u = min(u0 + j, nu - 1);  // (clamped: one round, every load unconditional)
-    zg[j] = P.gtC[lb + u];
-    zc[j] = P.cntZ[lb + u];
-    zs[j] = tk != 0u ? P.tsgn[lb + u] : 0xFFFFFFFFu;
-  }
-  uint32_t z = 0;
-#pragma unroll
-  for (uint32_t j = 0; j < E; ++j) {
-    if (u0 + j < nu) {
-      S.ge[u0 + j] = zg[j] | (zc[j] << 16);
-      z += zc[j];
-    }
-  }
-  fp_rank = NONE;
-  fn_rank = NONE;
-  if (tk == 0u) {  // (block-uniform) K = 0: a zero's sign does not matter to mn / scale
-    __syncthreads();
-    return;
-  }
-  uint32_t tot;
-  uint32_t ex = block_excl_scan<NT>(z, S.sh, tot);  // (barriers inside: S.ge complete after them)
-  uint32_t lp = NONE, ln = NONE;
-#pragma unroll
-  for (uint32_t j = 0; j < E; ++j) {
-    if (u0 + j < nu) {
-      const uint32_t fp = zs[j] & 0xFFFFu, fn = zs[j] >> 16;
+  uint32_t lp = NONE, ln = NONE, carry = 0;
+  for (uint32_t c0 = 0; c0 < nu; c0 += NT) {
+    const uint32_t i = c0 + t;
+    const uint32_t z = i < nu ? S.ge[i] >> 16 : 0u;
+    uint32_t tot;
+    const uint32_t ex = block_excl_scan<NT>(z, S.sh, tot) + carry;
+    carry += tot;
+    if (i < nu) {
+      const uint32_t sg = P.tsgn[lb + i], fp = sg & 0xFFFFu, fn = sg >> 16;
       if (fp != 0xFFFFu) lp = min(lp, ex + fp);
       if (fn != 0xFFFFu) ln = min(ln, ex + fn);
-      ex += zc[j];
     }
   }
   if (t == 0) {
@@ -2129,49 +2096,43 @@ DEV void select_finish(const Params& P, uint32_t s, const SegDev& sd, SelSmem& S
     pst(P, P.mn + s, mn);
     pst(P, P.scale + s, scale);
   }
-  // thread t owns the contiguous units [t * E, t * E + E) of each UCAP-unit chunk: ONE paired scan of the tie and
-  // above-T* counts per chunk (the quotas of the units before u sum to min(rt, ties before u), so u's output offset is
-  // its above-T* prefix + that). The counts are in LDS (S.ge: every path leaves them there for nu <= UCAP); a segment
-  // of more units (the generic path, chunk by chunk) reads gtC / eqC with L1-bypassing loads — other threads of this
-  // block wrote them, and a plain load may hit a line this CU's L1 cached before (cdna_hip_programming.md §6 G16)
-  constexpr uint32_t E = unit_span<NT>();
+  // thread t takes unit c0 + t of each NT-unit chunk (coalesced loads and stores): ONE paired block scan of the tie and
+  // above-T* counts per chunk — the quotas of the units before u sum to min(rt, ties before u), so u's output offset is
+  // its above-T* prefix + that. The counts are in LDS (S.ge) whenever nu <= UCAP (every path leaves them there); a
+  // segment of more units (the generic path, chunk by chunk) reads gtC / eqC with L1-bypassing loads — this block
+  // wrote them, and a plain load may hit a line this CU's L1 cached before (cdna_hip_programming.md §6 G16)
   const bool lds = done || nu <= UCAP;
   uint32_t carry_e = 0, carry_g = 0;
-  for (uint32_t c0 = 0; c0 < nu; c0 += E * NT) {
-    const uint32_t u0 = min(nu, c0 + t * E), u1 = min(nu, u0 + E);
-    uint32_t ce[E], cg[E], se = 0, sg = 0;
-#pragma unroll
-    for (uint32_t j = 0; j < E; ++j) {
-      const uint32_t u = min(u0 + j, nu - 1);
-      const uint32_t v = lds ? S.ge[u] : 0u;
-      ce[j] = u0 + j < u1 ? (lds ? v >> 16 : __builtin_nontemporal_load(P.eqC + lb + u)) : 0u;
-      cg[j] = u0 + j < u1 ? (lds ? v & 0xFFFFu : __builtin_nontemporal_load(P.gtC + lb + u)) : 0u;
-      se += ce[j];
-      sg += cg[j];
-    }
-    uint32_t ex_e, ex_g, te, tg;
-    block_excl_scan2<NT>(se, sg, S.sh, ex_e, ex_g, te, tg);
-    ex_e += carry_e;
-    ex_g += carry_g;
-    carry_e += te;
-    carry_g += tg;
-#pragma unroll
-    for (uint32_t j = 0; j < E; ++j) {
-      const uint32_t u = u0 + j;
-      if (u < u1) {
-        const uint32_t qp = umin_opaque(rt, ex_e);  // ties kept before u (see umin_opaque)
-        const uint32_t quota = min(ce[j], rt - qp);
-        const uint32_t so = ex_g + qp;
-        pst(P, P.eqpre + lb + u, ex_e);
-        pst(P, P.outoff + lb + u, so);
-        if (P.ustart_out != nullptr) pst(P, P.ustart_out + sd.unit_begin + u, so);  // wire v2: the unit's start
-        const uint32_t rawu = raw_path | (zero_tie && quota > 0 ? 1u : 0u);
-        P.uemit[lb + u] = make_uint4(T, rt | (rawu << 31), __float_as_uint(mn), __float_as_uint(scale));
-        ex_e += ce[j];
-        ex_g += cg[j];
+  for (uint32_t c0 = 0; c0 < nu; c0 += NT) {  // (block_excl_scan2 opens with a barrier: S.sh free again)
+    const uint32_t i = c0 + t;
+    const bool valid = i < nu;
+    uint32_t e = 0, g = 0;
+    if (valid) {
+      if (lds) {
+        const uint32_t v = S.ge[i];
+        e = v >> 16;
+        g = v & 0xFFFFu;
+      } else {
+        e = __builtin_nontemporal_load(P.eqC + lb + i);
+        g = __builtin_nontemporal_load(P.gtC + lb + i);
       }
     }
-    if (c0 + E * NT < nu) __syncthreads();  // (S.sh reused by the next chunk's scan)
+    uint32_t ex, gx, te, tg;
+    block_excl_scan2<NT>(e, g, S.sh, ex, gx, te, tg);
+    ex += carry_e;
+    gx += carry_g;
+    carry_e += te;
+    carry_g += tg;
+    const uint32_t qp = umin_opaque(rt, ex);  // ties kept before unit i (see umin_opaque)
+    const uint32_t quota = min(e, rt - qp);
+    const uint32_t so = gx + qp;
+    if (valid) {
+      pst(P, P.eqpre + lb + i, ex);
+      pst(P, P.outoff + lb + i, so);
+      if (P.ustart_out != nullptr) pst(P, P.ustart_out + sd.unit_begin + i, so);  // wire v2: the unit's start
+      const uint32_t rawu = raw_path | (zero_tie && quota > 0 ? 1u : 0u);
+      P.uemit[lb + i] = make_uint4(T, rt | (rawu << 31), __float_as_uint(mn), __float_as_uint(scale));
+    }
   }
 }
 
@@ -2188,17 +2149,19 @@ DEV void segment_select(const Params& P, uint32_t li, SelSmem& S) {
   const bool zero_tie = st.w == 2;  // the k-th key is the segment's tie key K (segment_pick; tie mode)
   bool done;
   if (zero_tie) {
-    // every record kept (k_gwin's per-unit counts above the empty window), the first rt K-keys by index
-    // (zero_tie_select). K = 0: a zero's sign does not matter to mn / scale (canonicalised + 0.0f below), so one
-    // "positive tie" stands for them
+    // every record kept (k_gwin's per-unit counts above the empty window), the first rt K-keys by index. K = 0: a
+    // zero's sign does not matter to mn / scale (canonicalised + 0.0f below), so one "positive tie" stands for them;
+    // K > 0: the segment-wide ranks of the first +K and -K ties (zero_tie_ranks)
     const uint32_t g0 = sd.g_begin, ng = (nu + GU - 1) / GU;  // ng <= UCAP / GU <= NT
     const uint32_t tk = P.tlo[lb] & KEY_MAX;
     gmn = t < ng ? P.gmm[2 * (g0 + t)] : qnan();
     gmx = t < ng ? P.gmm[2 * (g0 + t) + 1] : qnan();
+    for (uint32_t i = t; i < nu; i += NT) S.ge[i] = P.gtC[lb + i] | (P.cntZ[lb + i] << 16);
+    __syncthreads();
     T = tk;
     rt = st.z;
-    zero_tie_select<NT>(P, lb, nu, tk, S, fp_rank, fn_rank);
-    if (tk == 0u) fp_rank = rt > 0 ? 0u : NONE;
+    fp_rank = rt > 0 ? 0u : NONE;
+    if (tk != 0u) zero_tie_ranks<NT>(P, lb, nu, S, fp_rank, fn_rank);  // (block-uniform)
     done = true;
   } else {
     done = st.w == 0 && select_from_groups<NT>(P, sd, lb, nu, st, S, T, rt, fp_rank, fn_rank, gmn, gmx);
@@ -2283,9 +2246,11 @@ DEV void emit_raw_unit(const Params& P, const UnitDev& L, uint32_t T, uint32_t r
   });
 }
 
-// one wave emits the large units lu0 + g * stride, g < UPW, below lu1 (batches: stride = the number of emit waves, so a
-// wave's units lie across the plan — the units that take the raw-data emit, a tie-mode segment's first ones, spread
-// over many waves instead of filling a few with 8 raw units each: C3_signs k_emit 416 us per 8-client launch at HEAD)
+// one wave emits the large units lu0 + g * stride, g < UPW, below lu1. Batches: a block takes a tile of WAVES * UPW
+// consecutive units and its waves interleave them (stride WAVES), so the units that take the raw-data emit — a tie-mode
+// segment's first ones, consecutive — are shared by the block's waves instead of filling one wave with 8 raw passes in
+// series, while a wave's metadata loads stay within a few lines. (Striding by the whole grid spread them further but
+// scattered every wave's metadata loads over 8 lines per array: C2 +2-10 %, C3 +1-6 % by box, profiles/r06_ab.txt.)
 template <bool DELTA, bool RAW, uint32_t UPW, uint32_t TR>
 DEV void emit_units(const Params& P, uint32_t lu0, uint32_t lu1, uint32_t stride) {
   const uint32_t lane = lane_id();
@@ -2393,11 +2358,11 @@ DEV void emit_units(const Params& P, uint32_t lu0, uint32_t lu1, uint32_t stride
 template <bool DELTA, bool RAW, uint32_t UPW, uint32_t TR>  // TR: record rows per load round past the first
 __global__ __launch_bounds__(BLOCK) void k_emit(Params P) {
   const uint32_t wv = threadIdx.x >> 6;
-  const uint32_t gw = blockIdx.x * WAVES + wv, nw = gridDim.x * WAVES;  // (UPW == 1: one unit per wave)
-  if (gw >= P.n_lunits) return;
+  const uint32_t t0 = blockIdx.x * WAVES * UPW;  // the block's tile of WAVES * UPW consecutive units
+  if (t0 + wv >= P.n_lunits) return;
   const bool st = blockIdx.x < P.nseg;  // diagnostics rows: block index (slots 13-14)
   if (st) STAMP(P, blockIdx.x, 13);
-  emit_units<DELTA, RAW, UPW, TR>(P, gw, P.n_lunits, UPW == 1 ? 1u : nw);
+  emit_units<DELTA, RAW, UPW, TR>(P, t0 + wv, min(t0 + WAVES * UPW, P.n_lunits), WAVES);
   if (st) STAMP(P, blockIdx.x, 14);
 }
 
