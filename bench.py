@@ -809,15 +809,16 @@ def main():
 
     if rank == 0:
         d = head["desc"]
+        h_ratio, h_mode, _ = cfg_opts(a.config, a)  # (the headline config's own ratio / mode, else the command line's)
         res = {
             "metric": METRIC, "value": head["value"], "unit": "GB/s", "n_gpus": world, "steps": a.steps,
             "warmup": a.warmup, "ms_per_step": head["ms_per_step"], "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
             "config": {"workload": f"{a.config}-per-GPU: {d.get('clients_per_gpu')} x {d.get('layout', 'mixed')} "
-                                   f"fp32 updates per GPU, top-k {a.ratio}, {a.bits}-bit codes, {a.mode} mode, "
+                                   f"fp32 updates per GPU, top-k {h_ratio}, {a.bits}-bit codes, {h_mode} mode, "
                                    f"encode+decode batched as {head['split']} concurrent sub-batches",
-                       **d, "global_clients": d.get("clients_per_gpu", 0) * world, "ratio": a.ratio, "bits": a.bits,
-                       "mode": a.mode, "sub_batches_per_step": head["split"], "inflight_steps": head["inflight"],
+                       **d, "global_clients": d.get("clients_per_gpu", 0) * world, "ratio": h_ratio, "bits": a.bits,
+                       "mode": h_mode, "sub_batches_per_step": head["split"], "inflight_steps": head["inflight"],
                        "parallelism": f"replicas{world}"},
             "roofline": head["roofline"], "step_roofline": head["step_roofline"], "stages_ms": head["stages_ms"],
             "stage_timing": head["stage_timing"], "sample_fallbacks": head["sample_fallbacks"],
