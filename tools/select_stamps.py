@@ -14,13 +14,19 @@ from coala_amd.layouts import fp32_sizes  # noqa: E402
 from coala_amd.workload import synth_batch  # noqa: E402
 
 clients = int(sys.argv[1]) if len(sys.argv) > 1 else 1
+signs = len(sys.argv) > 2 and sys.argv[2] == "signs"  # C3_signs data: delta mode after one sign-like step
 sizes = fp32_sizes("resnet50_tv")
 plan = CodecPlan(sizes, 0.01, 8, clients=clients)
 flat = synth_batch(plan.table, torch.device("cuda", 0))
+base = None
+if signs:
+    from coala_amd.workload import sign_step  # noqa: E402
+    base = synth_batch(plan.table, torch.device("cuda", 0), client_ids=[10_000 + i for i in range(clients)])
+    sign_step(flat, base, 4242)
 ws = plan.empty_workspace()
 enc = plan.empty_encoded()
 for _ in range(3):
-    plan.encode(flat, out=enc, workspace=ws, flags=COALAC_FLAG_STAMPS)
+    plan.encode(flat, base=base, out=enc, workspace=ws, flags=COALAC_FLAG_STAMPS)
 torch.cuda.synchronize()
 nseg = plan.n_segments
 buf = (ctypes.c_uint64 * (16 * nseg))()
