@@ -15,6 +15,8 @@ collective on the data path — torch.distributed only for the barrier and the m
           1 GPU"; latency-bound)
   single_x2  ONE ResNet-50 update per step, two steps in flight on two streams (a server decoding
           concurrent uploads, one thread each: coala/server/service.py:71-111)
+  single_x4  the same with four steps in flight (the reference's gRPC server runs up to 10 worker threads,
+          coala/communication/grpc_wrapper.py:51)
   plugin  the hooks' own path per ResNet-50 client, delta mode: client compression() encoding the trained
           module's parameters in place + server decompression(model) into a new module on w_global
   C3_delta   the C3 share in delta mode (what the plugin runs by default: w_local - w_global on encode, + w_global
@@ -65,13 +67,14 @@ CONFIGS = {  # name -> (layout | "c5", clients per GPU, sub-batches: the best of
     "C5": ("c5", None, 1, {}),  # one latency-bound plan (<= 8192 units): 0.116 ms vs 0.122 as 2 sub-batches
     "single": ("resnet50_tv", 1, "single", {}),
     "single_x2": ("resnet50_tv", 1, "single", {}),
+    "single_x4": ("resnet50_tv", 1, "single", {}),
     "download": ("resnet50_tv", 1, "single", {"ratio": 1.0}),
 }
 # updates in flight per extra config: single_x2 = one update per step, consecutive steps on two streams (a
 # server decodes concurrent uploads from one thread each, coala/server/service.py:71-111)
-CONFIG_INFLIGHT = {"single_x2": 2}
+CONFIG_INFLIGHT = {"single_x2": 2, "single_x4": 4}
 SINGLE_SPLIT = 1  # segment ranges of the single update run as this many concurrent sub-plans
-DEFAULT_EXTRAS = "C2,C3_delta,C3_r0.001,C3_r0.1,C3_signs,C4,C4_delta,C4_frozen,C5,single,single_x2,download,plugin"
+DEFAULT_EXTRAS = "C2,C3_delta,C3_r0.001,C3_r0.1,C3_signs,C4,C4_delta,C4_frozen,C5,single,single_x2,single_x4,download,plugin"
 
 
 def cfg_opts(cfg, a):
@@ -290,7 +293,7 @@ def build_table(cfg, a, rank, headline):
                               if CONFIGS[cfg][3].get("signs") else {})}
 
 
-GRAPH_CONFIGS = ("single", "single_x2", "C5", "download")  # latency-bound plans: step time ~ host launch time
+GRAPH_CONFIGS = ("single", "single_x2", "single_x4", "C5", "download")  # latency-bound plans: step time ~ host launch time
 GRAPH_WARM_REPLAYS = 8  # untimed replays of each slot's whole-rotation graph right before the timed region
 
 
@@ -300,7 +303,7 @@ def use_graph(cfg, a):
 
 # configs whose timed steps rotate over ROTATE distinct input / output buffer sets (one ResNet-50 update is
 # 102 MB in + 102 MB out: a single set would stay resident in the 256 MB Infinity Cache, step after step)
-ROTATE_CONFIGS = ("single", "single_x2", "download")
+ROTATE_CONFIGS = ("single", "single_x2", "single_x4", "download")
 ROTATE = 3
 
 
