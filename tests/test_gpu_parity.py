@@ -555,3 +555,51 @@ def test_dense_plan_implied_indices(cuda, bits, delta, with_idx):
             np.testing.assert_array_equal(enc.ustart.cpu().numpy(), O.unit_starts(idx, s64))
         for (off, n, k, oo) in s64:
             np.testing.assert_array_equal(dec[off:off + n].view(np.uint32), ref[off:off + n].view(np.uint32))
+
+
+# -- the tie quota across units (round 6: a folded saturating subtract lost its clamp) -------------------------------
+def tie_quota_segment(rng, n, k, tie_units, extra_kept_ties=0):
+    """n distinct keys, except the k-th largest key T repeated once in each of `tie_units` (in that order), so the
+    quota keeps only the first 1 + extra_kept_ties of them by index: every later tie unit must reserve no slot."""
+    keys = np.unique(rng.integers(0x30000000, 0x3F000000, int(n * 1.05), dtype=np.int64))
+    assert keys.size >= n
+    keys = rng.permutation(keys[:n]).astype(np.uint32)
+    order = np.argsort(-keys.astype(np.int64), kind="stable")
+    kth = k - 1 - extra_kept_ties  # the key at this rank becomes T; the ranks above it up to k - 1 become ties too
+    T = keys[order[kth]]
+    extra = [int(p) for p in order[kth - extra_kept_ties:kth]]
+    keys[extra] = T
+    first = True
+    for u in tie_units:
+        lo, hi = u * 4096, min(n, u * 4096 + 4096)
+        cand = lo + np.flatnonzero(keys[lo:hi] < T)
+        q = int(cand[rng.integers(0, cand.size)])
+        if first:  # move the original T element into the first tie unit
+            p0 = int(order[kth])
+            keys[p0], keys[q] = keys[q], keys[p0]
+            first = False
+        else:
+            keys[q] = T
+    sign = np.where(rng.random(n) < 0.5, 0x80000000, 0).astype(np.uint32)
+    return (keys | sign).view(np.float32)
+
+
+@pytest.mark.parametrize("clients", [1, 16])  # latency plan (k_select 512 threads), batch plan (256 threads)
+@pytest.mark.parametrize("tie_units,extra", [((37, 222), 0), ((255, 256), 0), ((63, 64, 575), 1), ((0, 300, 301), 0),
+                                             ((127, 128, 129, 511), 2)])
+def test_tie_quota_across_units(cuda, clients, tie_units, extra):
+    """One 576-unit segment (ResNet-50's largest) whose k-th key repeats in several units, only the first few of them
+    kept, followed by a small segment that a reserved-but-unwritten slot would spill into. Bit-exact idx / starts /
+    decode; the output offsets were off by one from the first unit after a skipped tie in round 6's first select
+    finish."""
+    sizes = [2359296, 512]
+    ratio = 0.1
+    k = int(np.ceil(sizes[0] * ratio))
+    rng = np.random.default_rng(600 + sum(tie_units) + extra)
+    xs = []
+    for c in range(clients):
+        xs.append([tie_quota_segment(rng, sizes[0], k, tie_units, extra),
+                   rng.standard_normal(sizes[1]).astype(np.float32)])
+    plan, g, r = run_both(sizes, ratio, 8, xs, clients=clients)
+    assert_same(plan, g, r)
+    assert g["fallbacks"] == 0
