@@ -2744,6 +2744,7 @@ __global__ __launch_bounds__(BLOCK, AGG_WPE) void k_aggregate(Params P, AggArgs 
 // download 0.073 vs 0.088 ms per step with plain stores; a reciprocal-multiply quantise measured no faster: these
 // streams are memory-bound, profiles/r05_ab.txt)
 constexpr int DENSE_MM_AUX = 0;
+constexpr int DENSE_Q_AUX = 2;  // the quantise stream's loads (non-temporal)
 template <bool DELTA, int AUX>  // (AUX: the loads' cache policy)
 DEV void dense_unit_load(const Params& P, const UnitDev& U, float4 (&v)[UNIT_IT]) {
   typedef unsigned int u4v __attribute__((ext_vector_type(4)));
@@ -2819,15 +2820,60 @@ __global__ __launch_bounds__(BLOCK) void k_dense_seg(Params P) {
   }
 }
 
-template <bool DELTA, bool RAW, bool XCD>
+// SEGRED: every wave reduces its segment's per-unit min / max itself (k_dense_seg folded in: the unit's loads are in
+// flight meanwhile, the ~50 KB of pairs are L2-resident, and one launch boundary goes); the segment's first unit
+// writes its mn / scale. Used when every segment has a unit (an empty segment has no wave to write its zeros).
+template <bool DELTA, bool RAW, bool XCD, bool SEGRED>
 __global__ __launch_bounds__(BLOCK) void k_dense_quant(Params P) {
   const uint32_t u = (XCD ? xcd_block(blockIdx.x) : blockIdx.x) * WAVES + (threadIdx.x >> 6);
   if (u >= P.n_units) return;
   const UnitDev U = P.units[u];
-  const float mn = RAW ? 0.0f : P.mn[U.seg], scale = RAW ? 0.0f : P.scale[U.seg];
-  float4 v[UNIT_IT];
-  dense_unit_load<DELTA, LOAD_AUX>(P, U, v);
   const uint32_t lane = lane_id();
+  // SEGRED: the first SEGRED_PAIRS x 64 units' min / max pairs are loaded ahead of the unit's own loads (straight-line
+  // code: the reduce waits for them alone, the unit's loads still in flight); a longer segment's remainder afterwards
+  constexpr uint32_t SEGRED_PAIRS = 8;
+  SegDev sd{};
+  float2 m[SEGRED_PAIRS];
+  const float2* umm2 = reinterpret_cast<const float2*>(P.umm);
+  if (SEGRED) {
+    sd = P.segs[U.seg];
+    if (!RAW) {
+#pragma unroll
+      for (uint32_t j = 0; j < SEGRED_PAIRS; ++j) {
+        const uint32_t w = sd.unit_begin + j * 64 + lane;
+        m[j] = w < sd.unit_end ? umm2[w] : make_float2(qnan(), qnan());
+      }
+    }
+  }
+  float4 v[UNIT_IT];
+  dense_unit_load<DELTA, DENSE_Q_AUX>(P, U, v);
+  float mn = 0.0f, scale = 0.0f;
+  if (SEGRED) {
+    if (!RAW) {  // (same NaN-ignoring min / max and + 0.0f as k_dense_seg: order-independent, bit-identical)
+      float a = qnan(), b = qnan();
+#pragma unroll
+      for (uint32_t j = 0; j < SEGRED_PAIRS; ++j) {
+        a = fmin_nan(a, m[j].x);
+        b = fmax_nan(b, m[j].y);
+      }
+      for (uint32_t w = sd.unit_begin + SEGRED_PAIRS * 64 + lane; w < sd.unit_end; w += 64) {
+        const float2 t = umm2[w];
+        a = fmin_nan(a, t.x);
+        b = fmax_nan(b, t.y);
+      }
+      a = wave_min(a) + 0.0f;
+      b = wave_max(b) + 0.0f;
+      mn = a;
+      scale = (b == a) ? 0.0f : (b - a) / P.levels;
+    }
+    if (u == sd.unit_begin && lane == 0) {
+      P.mn[U.seg] = mn;
+      P.scale[U.seg] = scale;
+    }
+  } else if (!RAW) {
+    mn = P.mn[U.seg];
+    scale = P.scale[U.seg];
+  }
   const uint64_t o = U.out_off + U.start;  // the unit's first entry (k == n: entry e is element e)
   // whole-dword stores when the unit's codes start 4-byte aligned (16-byte for raw floats) and end on a dword
   const bool vec = (o & 3u) == 0 && (U.len & 3u) == 0;
@@ -3031,6 +3077,7 @@ struct coalac_plan {
   uint32_t small_max = SMALL_MAX;  // segments of <= this many elements are "small" (encoded whole by one block)
   uint32_t ccap = UNIT;  // candidate record slots per large unit
   bool dense = false;    // every segment keeps all its elements: the dense codec (indices implied)
+  bool dense_empty = false;  // a dense plan with a 0-element segment (keeps the separate k_dense_seg)
   double rmax = 0.0;     // the largest k / n of the plan's segments
   uint64_t span = 0, total_k = 0;
   void* meta = nullptr;
@@ -3117,12 +3164,20 @@ int launch_dense_encode(const Params& P, coalac_plan_t plan, hipStream_t st, con
     else
       hipLaunchKernelGGL((k_dense_minmax<DELTA, false>), g, dim3(BLOCK), 0, st, P);
   }
-  hipLaunchKernelGGL((k_dense_seg<RAW>), dim3(plan->nseg), dim3(BLOCK), 0, st, P);
-  MARK(1);
-  if (xcd)
-    hipLaunchKernelGGL((k_dense_quant<DELTA, RAW, true>), g, dim3(BLOCK), 0, st, P);
-  else
-    hipLaunchKernelGGL((k_dense_quant<DELTA, RAW, false>), g, dim3(BLOCK), 0, st, P);
+  if (plan->dense_empty) {  // a segment without units: k_dense_seg writes every segment's mn / scale
+    hipLaunchKernelGGL((k_dense_seg<RAW>), dim3(plan->nseg), dim3(BLOCK), 0, st, P);
+    MARK(1);
+    if (xcd)
+      hipLaunchKernelGGL((k_dense_quant<DELTA, RAW, true, false>), g, dim3(BLOCK), 0, st, P);
+    else
+      hipLaunchKernelGGL((k_dense_quant<DELTA, RAW, false, false>), g, dim3(BLOCK), 0, st, P);
+  } else {
+    MARK(1);
+    if (xcd)
+      hipLaunchKernelGGL((k_dense_quant<DELTA, RAW, true, true>), g, dim3(BLOCK), 0, st, P);
+    else
+      hipLaunchKernelGGL((k_dense_quant<DELTA, RAW, false, true>), g, dim3(BLOCK), 0, st, P);
+  }
   MARK(2);
   MARK(3);
   MARK(4);
@@ -3341,6 +3396,7 @@ int coalac_plan_create(const coalac_seg_t* h_segs, int nseg, int bits, coalac_pl
   p->small_max = small_max;
   p->dense = true;
   for (const SegDev& d : segs) p->dense = p->dense && d.k == d.n;
+  for (const SegDev& d : segs) p->dense_empty = p->dense_empty || d.unit_begin == d.unit_end;
   p->ws = p->dense ? ws_layout_dense(units.size())
                    : ws_layout((size_t)nseg, lunits.size(), groups.size(), large_list.size(), ccap);
 

@@ -519,16 +519,20 @@ def test_tie_mode_sample_miss_takes_raw_path(cuda):
     assert_same(plan, g, r)
 
 
+@pytest.mark.parametrize("with_empty", [False, True])
 @pytest.mark.parametrize("with_idx", [False, True])
 @pytest.mark.parametrize("delta", [False, True])
 @pytest.mark.parametrize("bits", [1, 8, 32])
-def test_dense_plan_implied_indices(cuda, bits, delta, with_idx):
+def test_dense_plan_implied_indices(cuda, bits, delta, with_idx, with_empty):
     """Ratio 1 (the download direction's dense codec): min / max, quantise and dequantise streams with the
     indices implied — no idx / starts unless asked for. Ragged sizes put segments' codes at odd byte offsets
     (the byte-store / byte-load paths), NaN / inf / constant / signed-zero segments, a segment of 3 units + 5:
-    bit-exact against the oracle, in a latency-bound and (2 x 20 MB) a batch plan."""
+    bit-exact against the oracle, in a latency-bound and (2 x 20 MB) a batch plan. Without a 0-element segment
+    the quantise waves reduce their segment's min / max themselves (round 6); with one, k_dense_seg runs."""
     rng = np.random.default_rng(bits * 2 + delta)
     segs = edge_segments(rng) + [gauss(rng, [4096 * 2100 + 3])[0]]
+    if with_empty:
+        segs = segs[:3] + [np.zeros(0, np.float32)] + segs[3:] + [np.zeros(0, np.float32)]
     sizes = [s.size for s in segs]
     for clients in (1, 2):
         plan = CodecPlan(sizes, 1.0, bits, clients=clients)
