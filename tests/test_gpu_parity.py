@@ -607,3 +607,39 @@ def test_tie_quota_across_units(cuda, clients, tie_units, extra):
     plan, g, r = run_both(sizes, ratio, 8, xs, clients=clients)
     assert_same(plan, g, r)
     assert g["fallbacks"] == 0
+
+
+@pytest.mark.parametrize("bits", [4, 8])
+def test_dense_quantise_near_code_boundaries(cuda, bits):
+    """The dense quantise divides by the reciprocal with an FMA correction (round 6); the code must equal the
+    oracle's IEEE (x - mn) / scale + rint wherever the quotient sits a few ulps off a half-integer or an integer,
+    for scales of every mantissa shape (all ones, a power of two, random) and far-apart exponents."""
+    rng = np.random.default_rng(40 + bits)
+    levels = (1 << bits) - 1
+    segs = []
+    for mant in (0x7FFFFF, 0x0, 0x7FFF00, 0x3A5A5A, int(rng.integers(0, 1 << 23))):
+        for e in (-100, -80, -20, -3, 0, 7, 60, 95):  # (-100, 95: outside [2^-90, 2^90], the division)
+            sc = np.array([((127 + e) << 23) | mant], np.uint32).view(np.float32)[0]
+            mn = np.float32(rng.standard_normal()) * np.float32(2.0 ** e)
+            mx = np.float32(mn + np.float32(levels) * sc)
+            sc = np.float32((mx - mn) / np.float32(levels))  # the scale the codec derives (CodecSpec v1)
+            ks = rng.integers(0, levels, 6000).astype(np.float32)
+            half = (ks + np.float32(0.5)) * sc
+            whole = ks * sc
+            base = np.where(rng.random(6000) < 0.5, half, whole).astype(np.float32)
+            x = (mn + base).astype(np.float32)
+            x = (x.view(np.int32) + rng.integers(-3, 4, 6000).astype(np.int32)).view(np.float32)
+            x = np.clip(x, mn, mx).astype(np.float32)
+            segs.append(np.concatenate([[mn, mx], x]).astype(np.float32))
+    sizes = [s.size for s in segs]
+    plan = CodecPlan(sizes, 1.0, bits)
+    assert plan.dense
+    t = plan.table
+    flat = to_flat(t, [segs])
+    enc = plan.encode(torch.from_numpy(flat).cuda())
+    torch.cuda.synchronize()
+    s64 = t.segs.astype(np.int64)
+    idx, vals, mn, sc = O.encode(flat, s64, bits)
+    np.testing.assert_array_equal(enc.mn.cpu().numpy().view(np.uint32), mn.view(np.uint32))
+    np.testing.assert_array_equal(enc.scale.cpu().numpy().view(np.uint32), sc.view(np.uint32))
+    np.testing.assert_array_equal(enc.vals.cpu().numpy().view(np.uint8), vals.view(np.uint8))
