@@ -1,3 +1,9 @@
+/* Host check of the dense quantise's division (coalac.hip k_dense_quant):
+ * t1 = fma(fma(-q, b, a), y, q) with q = a * y, y = 1 / b  against  t0 = a / b, on random and boundary-targeted
+ * (a, b): scale exponents in [2^-90, 2^89] (mantissas all ones / zero / random), a uniform in [0, levels * b], within
+ * 4 ulps of half-integer and integer quotients, or any float. Counts differing quotients (a >= 2^-100) and differing
+ * rint codes. Build: gcc -O2 -mfma -o /tmp/rcp_div_check tools/rcp_div_check.c -lm; run: /tmp/rcp_div_check 1000000000
+ * (round 6: bad=0 bad_rint=0). */
 #include <stdio.h>
 #include <stdint.h>
 #include <string.h>
