@@ -2188,7 +2188,9 @@ __global__ __launch_bounds__(NT) void k_select(Params P) {
 // records: here lane g loads unit g's metadata (two dependent rounds for all units at once) and every
 // unit's first 64 records are in flight before the first one is classified.
 // ------------------------------------------------------------------------------------------------
-constexpr uint32_t EMIT_UPW = 8u;  // large units per k_emit wave in batches (C3 share: +2 % over 2 units per wave)
+constexpr uint32_t EMIT_UPW = 4u;  // large units per k_emit wave in batches (round 6, with the interleaved tile: 4 vs 8
+                                   // C3 0.586-0.595 vs 0.608-0.639 ms, C2 0.271 vs 0.275-0.278, C3_signs 1.427-1.436 vs
+                                   // 1.471-1.543, C4 2.205 vs 2.155-2.202; 2 units: C3 0.624; profiles/r06_ab_emit_upw.txt)
 // ... in latency-bound plans (<= LATENCY_PLAN_UNITS units): a wave's units are handled one after the other,
 // so fewer per wave shortens the launch (one ResNet-50 update: 8 per wave 13.1 us, 2 per wave 6.0, 1 per
 // wave 5.1)
